@@ -1,0 +1,107 @@
+"""ctypes binding of ``libfjagg.so`` — the C ABI declared in ``include/fjagg.h``.
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950) into
+``fedjax_amd/_build/libfjagg.so``. It links against the HIP runtime by soname
+(``libamdhip64.so.7``); ``torch`` is imported first so that the library binds to
+the HIP runtime torch already loaded (one runtime per process, so torch's
+streams and device pointers are valid inside the library). ``load()`` verifies
+that exactly one HIP runtime is mapped.
+
+There is no fallback: if the library is missing or fails to load, every entry
+point raises :class:`FjaggError`.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FJAGG_LIB", os.path.join(_HERE, "_build", "libfjagg.so"))
+
+# enum fjagg_dtype
+F32, BF16, I32 = 0, 1, 2
+# enum fjagg_flags
+SCALE, ACCUMULATE, NONTEMPORAL, UNALIGNED = 1, 2, 4, 8
+# enum fjagg_mode
+MODE_EXACT, MODE_SPLIT = 0, 1
+ABI_VERSION = 1
+
+# every symbol include/fjagg.h declares: (name, restype, argtypes)
+_i64, _i32, _f32, _vp, _u64 = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint64
+_SIGNATURES = {
+    "fjagg_last_error": (ctypes.c_char_p, []),
+    "fjagg_abi_version": (_i32, []),
+    "fjagg_wsum_dense": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _i32, _i32, _vp, _i64, _vp]),
+    "fjagg_split_workspace_bytes": (_i64, [_i64, _i64]),
+    "fjagg_ptrs_plan": (_i64, [_i32, _i32, _vp, _i32, _vp, _i64]),
+    "fjagg_wsum_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _i32, _vp]),
+    "fjagg_l2sq_workspace_bytes": (_i64, [_i64, _i64]),
+    "fjagg_l2sq_dense": (_i32, [_i32, _vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp]),
+    "fjagg_fill_synth": (_i32, [_i32, _vp, _i64, _i64, _i64, _i64, _u64, _f32, _vp]),
+}
+SYMBOLS = tuple(_SIGNATURES)
+
+
+class FjaggError(RuntimeError):
+    """A libfjagg call failed (message from ``fjagg_last_error``) or the library
+    could not be loaded."""
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def hip_runtimes_mapped() -> list:
+    """Distinct libamdhip64 files mapped into this process."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})
+    except OSError:  # pragma: no cover
+        return []
+
+
+def load() -> ctypes.CDLL:
+    """Load libfjagg.so once; raise FjaggError if it is missing or inconsistent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise FjaggError(
+                f"{LIB_PATH} is missing: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` from the repo root")
+        try:
+            lib = ctypes.CDLL(LIB_PATH)
+        except OSError as e:
+            raise FjaggError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                raise FjaggError(f"{LIB_PATH} does not export {name}")
+            fn.restype, fn.argtypes = res, args
+        if lib.fjagg_abi_version() != ABI_VERSION:
+            raise FjaggError(f"ABI mismatch: library {lib.fjagg_abi_version()} != {ABI_VERSION}")
+        runtimes = hip_runtimes_mapped()
+        if len(runtimes) > 1:
+            raise FjaggError(f"two HIP runtimes mapped into one process: {runtimes}")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().fjagg_last_error().decode(errors="replace")
+        raise FjaggError(f"{what} failed ({rc}): {msg}")
+
+
+def call(name: str, *args):
+    """Call an int-returning entry point and raise on a non-zero status."""
+    rc = getattr(load(), name)(*args)
+    check(rc, name)
+    return rc

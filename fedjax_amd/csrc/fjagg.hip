@@ -1,0 +1,803 @@
+// fjagg.hip — MI355X (gfx950) kernels and C ABI for FedJAX's client-delta aggregation.
+//
+// The hot path is the weighted fold of tree_mean (fedjax/core/tree_util.py:76-96):
+// for every parameter element p, s = sum_k fl(x_k[p] * w_k) in client order, then
+// y[p] = fl(s * f32(1/W)). It is a streaming reduction over K*P input bytes with
+// 2 flops per element read: HBM-bound, no MFMA. Design:
+//
+//   * one lane owns E "units" of 16 bytes (4 f32 / 8 bf16) of the parameter axis and
+//     walks all K clients in order, so the fold is the reference's exact sequence
+//     (no cross-lane reduction, no FMA: compiled with -ffp-contract=off);
+//   * the row base of client k is wave-uniform (an SGPR), the lane offset is a
+//     32-bit VGPR constant, so each load is one global_load_dwordx4 with saddr;
+//   * U clients are loaded before they are folded, giving U*E*16 B in flight per
+//     lane (latency hiding through MLP, not through LDS: there is no reuse);
+//   * element tails and unaligned leaves use the same body with 1-element units;
+//   * the pytree path walks a device-resident (client, leaf) pointer table with
+//     a block table, so ONE launch covers every leaf of every client;
+//   * FJAGG_MODE_SPLIT splits the client axis over blockIdx.y for shapes whose
+//     parameter axis cannot fill 256 CUs, and combines the range sums in order.
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <type_traits>
+
+#include "fjagg.h"
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(FJAGG_EHIP, "%s: %s", what, hipGetErrorString(e));
+  return FJAGG_OK;
+}
+
+constexpr int kThreads = 256;   // 4 waves of 64
+constexpr int kPtrsE = 2;       // units per lane of the pytree kernel (fixed by the plan)
+constexpr int kSplitMax = 64;   // max client ranges in FJAGG_MODE_SPLIT
+constexpr int64_t kSplitHeader = 256;  // bytes of ones at the head of the split workspace
+
+// ---------------------------------------------------------------- element types
+template <int DT> struct Elem;
+template <> struct Elem<FJAGG_F32> { static constexpr int B = 4; };
+template <> struct Elem<FJAGG_BF16> { static constexpr int B = 2; };
+template <> struct Elem<FJAGG_I32> { static constexpr int B = 4; };
+
+template <int IN> constexpr int vec_width() { return 16 / Elem<IN>::B; }
+
+struct AccF {
+  using T = float;
+  static constexpr int DT = FJAGG_F32;
+  static __device__ __forceinline__ T mul(T x, T w) { return __fmul_rn(x, w); }
+  static __device__ __forceinline__ T add(T a, T b) { return __fadd_rn(a, b); }
+};
+struct AccI {  // XLA int32 arithmetic wraps
+  using T = int;
+  static constexpr int DT = FJAGG_I32;
+  static __device__ __forceinline__ T mul(T x, T w) { return (int)((unsigned)x * (unsigned)w); }
+  static __device__ __forceinline__ T add(T a, T b) { return (int)((unsigned)a + (unsigned)b); }
+};
+
+__device__ __forceinline__ float bf16_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ unsigned f32_to_bf16(float f) {  // RNE, NaN stays NaN
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return ((u >> 16) | 0x40u) & 0xffffu;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+// A "unit" is what one lane loads per client: 16 bytes (V = vec_width) or one
+// element (V = 1).
+template <int IN, int V> struct Unit {
+  static constexpr int BYTES = V * Elem<IN>::B;
+  using Raw = typename std::conditional<(BYTES == 16), u32x4, unsigned>::type;
+};
+
+template <int IN, int V, bool NT>
+__device__ __forceinline__ typename Unit<IN, V>::Raw load_unit(const uint8_t* p) {
+  if constexpr (Unit<IN, V>::BYTES == 16) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+  } else if constexpr (Elem<IN>::B == 4) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p));
+    else return *reinterpret_cast<const unsigned*>(p);
+  } else {
+    if constexpr (NT) return (unsigned)__builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(p));
+    else return (unsigned)*reinterpret_cast<const unsigned short*>(p);
+  }
+}
+
+template <int IN, class ACC, int V>
+__device__ __forceinline__ void decode(typename Unit<IN, V>::Raw r, typename ACC::T (&o)[V]) {
+  if constexpr (V == 1) {
+    if constexpr (IN == FJAGG_BF16) o[0] = bf16_lo(r);
+    else if constexpr (IN == FJAGG_F32) o[0] = __uint_as_float(r);
+    else if constexpr (ACC::DT == FJAGG_F32) o[0] = (float)(int)r;
+    else o[0] = (int)r;
+  } else if constexpr (IN == FJAGG_BF16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = bf16_lo(r[i]);
+      o[2 * i + 1] = bf16_hi(r[i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (IN == FJAGG_F32) o[i] = __uint_as_float(r[i]);
+      else if constexpr (ACC::DT == FJAGG_F32) o[i] = (float)(int)r[i];
+      else o[i] = (int)r[i];
+    }
+  }
+}
+
+// fold state -> output element bits
+template <int OUT, class ACC>
+__device__ __forceinline__ unsigned finish(typename ACC::T s, bool do_scale, float scale) {
+  if constexpr (ACC::DT == FJAGG_F32) {
+    float f = do_scale ? __fmul_rn(s, scale) : s;
+    if constexpr (OUT == FJAGG_BF16) return f32_to_bf16(f);
+    else return __float_as_uint(f);
+  } else {
+    if constexpr (OUT == FJAGG_I32) return (unsigned)s;  // scale rejected on the host
+    else return __float_as_uint(do_scale ? __fmul_rn((float)s, scale) : (float)s);
+  }
+}
+
+// output element bits -> fold state (FJAGG_ACCUMULATE)
+template <int OUT, class ACC>
+__device__ __forceinline__ typename ACC::T init_from(unsigned bits) {
+  if constexpr (ACC::DT == FJAGG_F32) {
+    if constexpr (OUT == FJAGG_BF16) return __uint_as_float(bits << 16);
+    else return __uint_as_float(bits);
+  } else {
+    return (int)bits;
+  }
+}
+
+template <int OUT, int V>
+__device__ __forceinline__ void store_unit(uint8_t* p, const unsigned (&b)[V]) {
+  constexpr int OB = Elem<OUT>::B;
+  if constexpr (V == 1) {
+    if constexpr (OB == 4) *reinterpret_cast<unsigned*>(p) = b[0];
+    else *reinterpret_cast<unsigned short*>(p) = (unsigned short)b[0];
+  } else if constexpr (OB == 2) {  // V == 8 bf16 -> 16 B
+    u32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = b[2 * i] | (b[2 * i + 1] << 16);
+    *reinterpret_cast<u32x4*>(p) = v;
+  } else {  // V*4 bytes, V in {4, 8}
+#pragma unroll
+    for (int c = 0; c < V / 4; ++c) {
+      u32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = b[4 * c + i];
+      reinterpret_cast<u32x4*>(p)[c] = v;
+    }
+  }
+}
+
+template <int OUT, int V>
+__device__ __forceinline__ void load_out_unit(const uint8_t* p, unsigned (&b)[V]) {
+  constexpr int OB = Elem<OUT>::B;
+  if constexpr (V == 1) {
+    if constexpr (OB == 4) b[0] = *reinterpret_cast<const unsigned*>(p);
+    else b[0] = *reinterpret_cast<const unsigned short*>(p);
+  } else if constexpr (OB == 2) {
+    u32x4 v = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      b[2 * i] = v[i] & 0xffffu;
+      b[2 * i + 1] = v[i] >> 16;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < V / 4; ++c) {
+      u32x4 v = reinterpret_cast<const u32x4*>(p)[c];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[4 * c + i] = v[i];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ fold body
+// Each lane folds E units; unit j of this lane sits at byte offset off[j] of every
+// client row (a 32-bit lane constant) and is written to outp[j]. row(k) returns the
+// wave-uniform base address of client k. Clients are folded in order 0..K-1.
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, class RowFn>
+__device__ __forceinline__ void fold(RowFn row, int64_t K, const uint32_t (&off)[E],
+                                     uint8_t* const (&outp)[E], const bool (&valid)[E],
+                                     const typename ACC::T* __restrict__ w, bool do_scale,
+                                     float scale, bool accumulate) {
+  using T = typename ACC::T;
+  using Raw = typename Unit<IN, V>::Raw;
+  T acc[E][V];
+  {  // client 0: s_0 = t_0 (tree_util.py:89-91) or out + t_0 (running sum)
+    const uint8_t* r = row(0);
+    Raw v[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) v[j] = load_unit<IN, V, NT>(r + off[j]);
+    const T w0 = w[0];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      T t[V];
+      decode<IN, ACC, V>(v[j], t);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[j][i] = ACC::mul(t[i], w0);
+    }
+    if (accumulate) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        unsigned b[V];
+        load_out_unit<OUT, V>(outp[j], b);
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(init_from<OUT, ACC>(b[i]), acc[j][i]);
+      }
+    }
+  }
+  int64_t k = 1;
+  for (; k + U <= K; k += U) {
+    Raw v[U][E];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint8_t* r = row(k + u);
+#pragma unroll
+      for (int j = 0; j < E; ++j) v[u][j] = load_unit<IN, V, NT>(r + off[j]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const T wk = w[k + u];
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        T t[V];
+        decode<IN, ACC, V>(v[u][j], t);
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(acc[j][i], ACC::mul(t[i], wk));
+      }
+    }
+  }
+  for (; k < K; ++k) {
+    const uint8_t* r = row(k);
+    const T wk = w[k];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      T t[V];
+      decode<IN, ACC, V>(load_unit<IN, V, NT>(r + off[j]), t);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(acc[j][i], ACC::mul(t[i], wk));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    if (!valid[j]) continue;
+    unsigned b[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) b[i] = finish<OUT, ACC>(acc[j][i], do_scale, scale);
+    store_unit<OUT, V>(outp[j], b);
+  }
+}
+
+// Dense slab: client k at x + k*ld_bytes; P = nunits*V + tail_n elements.
+// Block 0 folds the tail (if any) with 1-element units; the rest cover the units.
+// blockIdx.y selects a client range [y*kchunk, min(K, (y+1)*kchunk)) and writes to
+// out + y*out_ystride_bytes (FJAGG_MODE_SPLIT); exact mode has gridDim.y == 1.
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT>
+__global__ __launch_bounds__(kThreads) void k_dense(
+    const uint8_t* __restrict__ x, int64_t ld_bytes, int64_t K, int64_t nunits, int tail_n,
+    const typename ACC::T* __restrict__ w, float scale, int do_scale, int accumulate,
+    uint8_t* __restrict__ out, int64_t kchunk, int64_t out_ystride_bytes) {
+  constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
+  const int tid = threadIdx.x;
+  const int64_t k0 = (int64_t)blockIdx.y * kchunk;
+  const int64_t kn = (K - k0 < kchunk) ? (K - k0) : kchunk;
+  const uint8_t* xb = x + k0 * ld_bytes;
+  const typename ACC::T* wb = w + k0;
+  uint8_t* ob = out + (int64_t)blockIdx.y * out_ystride_bytes;
+  auto row = [=](int64_t k) { return xb + k * ld_bytes; };
+  int64_t b = blockIdx.x;
+  if (tail_n > 0) {
+    if (b == 0) {
+      if (tid < tail_n) {
+        const int64_t e = nunits * V + tid;
+        const uint32_t off[1] = {(uint32_t)(e * IB)};
+        uint8_t* const op[1] = {ob + e * OB};
+        const bool valid[1] = {true};
+        fold<IN, ACC, OUT, 1, 1, U, NT>(row, kn, off, op, valid, wb, do_scale != 0, scale,
+                                        accumulate != 0);
+      }
+      return;
+    }
+    b -= 1;
+  }
+  uint32_t off[E];
+  uint8_t* op[E];
+  bool valid[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    int64_t u = b * (kThreads * E) + j * kThreads + tid;
+    valid[j] = u < nunits;
+    if (!valid[j]) u = nunits - 1;  // keep the load in bounds; the store is skipped
+    off[j] = (uint32_t)(u * (V * IB));
+    op[j] = ob + u * (V * OB);
+  }
+  fold<IN, ACC, OUT, V, E, U, NT>(row, kn, off, op, valid, wb, do_scale != 0, scale,
+                                  accumulate != 0);
+}
+
+// Pytree path. image = in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[nblk].
+// block word: bits 0..39 first unit, 40..61 leaf, 62 tail flag.
+template <int IN, class ACC, int OUT, int V, int U, bool NT>
+__global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ img, int L,
+                                                   int64_t K,
+                                                   const typename ACC::T* __restrict__ w,
+                                                   float scale, int do_scale, int accumulate) {
+  constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
+  constexpr int E = kPtrsE;
+  const int tid = threadIdx.x;
+  const int64_t* in_ptrs = img;
+  const int64_t* out_ptrs = img + K * L;
+  const int64_t* leaf_n = out_ptrs + L;
+  const int64_t be = leaf_n[L + blockIdx.x];
+  const int leaf = (int)((be >> 40) & 0x3fffff);
+  const bool tail = (be >> 62) & 1;
+  const int64_t u0 = be & ((1ll << 40) - 1);
+  const int64_t n = leaf_n[leaf];
+  const int64_t nunits = n / V;
+  uint8_t* ob = reinterpret_cast<uint8_t*>(out_ptrs[leaf]);
+  auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]); };
+  if (tail) {
+    if (tid < n - nunits * V) {
+      const int64_t e = nunits * V + tid;
+      const uint32_t off[1] = {(uint32_t)(e * IB)};
+      uint8_t* const op[1] = {ob + e * OB};
+      const bool valid[1] = {true};
+      fold<IN, ACC, OUT, 1, 1, U, NT>(row, K, off, op, valid, w, do_scale != 0, scale,
+                                      accumulate != 0);
+    }
+    return;
+  }
+  uint32_t off[E];
+  uint8_t* op[E];
+  bool valid[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    int64_t u = u0 + j * kThreads + tid;
+    valid[j] = u < nunits;
+    if (!valid[j]) u = nunits - 1;
+    off[j] = (uint32_t)(u * (V * IB));
+    op[j] = ob + u * (V * OB);
+  }
+  fold<IN, ACC, OUT, V, E, U, NT>(row, K, off, op, valid, w, do_scale != 0, scale,
+                                  accumulate != 0);
+}
+
+// Per-client sum of squares: grid (nb, K); ws[k*nb + b] = block partial (f32),
+// then k_l2sq_combine sums the nb partials of each client in block order.
+template <int IN>
+__global__ __launch_bounds__(kThreads) void k_l2sq_partial(const uint8_t* __restrict__ x,
+                                                          int64_t ld_bytes, int64_t P,
+                                                          int64_t per_block,
+                                                          float* __restrict__ ws) {
+  constexpr int IB = Elem<IN>::B;
+  constexpr int VW = vec_width<IN>();
+  const int64_t k = blockIdx.y;
+  const uint8_t* r = x + k * ld_bytes;
+  const int64_t e0 = (int64_t)blockIdx.x * per_block;
+  const int64_t e1 = (e0 + per_block < P) ? e0 + per_block : P;
+  float s = 0.f;
+  const bool vec = ((reinterpret_cast<uintptr_t>(r) & 15) == 0) && (per_block % VW == 0);
+  if (vec) {
+    const int64_t nfull = (e1 - e0) / VW;
+    for (int64_t u = threadIdx.x; u < nfull; u += kThreads) {
+      float t[VW];
+      decode<IN, AccF, VW>(load_unit<IN, VW, true>(r + (e0 + u * VW) * IB), t);
+#pragma unroll
+      for (int i = 0; i < VW; ++i) s = __fadd_rn(s, __fmul_rn(t[i], t[i]));
+    }
+    for (int64_t e = e0 + nfull * VW + threadIdx.x; e < e1; e += kThreads) {
+      float t[1];
+      decode<IN, AccF, 1>(load_unit<IN, 1, false>(r + e * IB), t);
+      s = __fadd_rn(s, __fmul_rn(t[0], t[0]));
+    }
+  } else {
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += kThreads) {
+      float t[1];
+      decode<IN, AccF, 1>(load_unit<IN, 1, false>(r + e * IB), t);
+      s = __fadd_rn(s, __fmul_rn(t[0], t[0]));
+    }
+  }
+  // wave reduction (fixed shuffle tree) then the 4 wave sums in order
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s = __fadd_rn(s, __shfl_xor(s, o, 64));
+  __shared__ float red[kThreads / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = red[0];
+#pragma unroll
+    for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, red[i]);
+    ws[k * gridDim.x + blockIdx.x] = t;
+  }
+}
+
+__global__ void k_l2sq_combine(const float* __restrict__ ws, int64_t nb, int64_t K,
+                               float* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < nb; ++b) s = __fadd_rn(s, ws[k * nb + b]);
+  out[k] = s;
+}
+
+// Synthetic deltas (tests/bench only): bit-identical to oracle/fold_ref.c.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+template <int DT>
+__global__ __launch_bounds__(kThreads) void k_fill(uint8_t* __restrict__ x, int64_t ld, int64_t K,
+                                                  int64_t P, int64_t k0, uint64_t seed,
+                                                  float amp) {
+  const int64_t total = K * P;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kThreads) {
+    const int64_t k = i / P, p = i - k * P;
+    const uint64_t h = mix64(seed ^ mix64(((uint64_t)(k0 + k) << 32) | ((uint64_t)p & 0xffffffffull)));
+    const float u = __fsub_rn(__fmul_rn((float)(uint32_t)(h >> 40), 1.0f / 8388608.0f), 1.0f);
+    const float v = __fmul_rn(amp, u);
+    if constexpr (DT == FJAGG_BF16)
+      reinterpret_cast<unsigned short*>(x)[k * ld + p] = (unsigned short)f32_to_bf16(v);
+    else
+      reinterpret_cast<float*>(x)[k * ld + p] = v;
+  }
+}
+
+// ------------------------------------------------------------------ host side
+struct Combo {
+  int in, acc, out;
+};
+bool combo_ok(int in, int acc, int out) {
+  static const Combo ok[] = {{FJAGG_F32, FJAGG_F32, FJAGG_F32},  {FJAGG_BF16, FJAGG_F32, FJAGG_BF16},
+                             {FJAGG_BF16, FJAGG_F32, FJAGG_F32}, {FJAGG_I32, FJAGG_F32, FJAGG_F32},
+                             {FJAGG_I32, FJAGG_I32, FJAGG_I32},  {FJAGG_I32, FJAGG_I32, FJAGG_F32}};
+  for (const Combo& c : ok)
+    if (c.in == in && c.acc == acc && c.out == out) return true;
+  return false;
+}
+int elem_bytes(int dt) { return dt == FJAGG_BF16 ? 2 : 4; }
+int vwidth(int dt) { return 16 / elem_bytes(dt); }
+
+// Kernel variants of the dense path: (E units per lane, U clients in flight).
+// Variant 0 is the default chosen from the measurements in profiles/.
+struct DenseArgs {
+  const uint8_t* x;
+  int64_t ld_bytes, K, nunits;
+  int tail_n;
+  const void* w;
+  float scale;
+  int do_scale, accumulate;
+  uint8_t* out;
+  int64_t kchunk, out_ystride;
+};
+
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT>
+void launch_dense_t(const DenseArgs& a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((k_dense<IN, ACC, OUT, V, E, U, NT>), grid, dim3(kThreads), 0, s, a.x,
+                     a.ld_bytes, a.K, a.nunits, a.tail_n,
+                     reinterpret_cast<const typename ACC::T*>(a.w), a.scale, a.do_scale,
+                     a.accumulate, a.out, a.kchunk, a.out_ystride);
+}
+
+struct VariantShape {
+  int E, U;
+};
+constexpr VariantShape kVariants[] = {{2, 8}, {1, 8}, {1, 16}, {2, 16}, {4, 4}, {4, 8}, {1, 32}};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+template <int IN, class ACC, int OUT, int V, bool NT>
+int launch_dense_v(int variant, const DenseArgs& a, int64_t nblk_units, int64_t gy,
+                   hipStream_t s) {
+  const int E = kVariants[variant].E;
+  dim3 grid((unsigned)(nblk_units + (a.tail_n > 0 ? 1 : 0)), (unsigned)gy);
+  switch (variant) {
+    case 0: launch_dense_t<IN, ACC, OUT, V, 2, 8, NT>(a, grid, s); break;
+    case 1: launch_dense_t<IN, ACC, OUT, V, 1, 8, NT>(a, grid, s); break;
+    case 2: launch_dense_t<IN, ACC, OUT, V, 1, 16, NT>(a, grid, s); break;
+    case 3: launch_dense_t<IN, ACC, OUT, V, 2, 16, NT>(a, grid, s); break;
+    case 4: launch_dense_t<IN, ACC, OUT, V, 4, 4, NT>(a, grid, s); break;
+    case 5: launch_dense_t<IN, ACC, OUT, V, 4, 8, NT>(a, grid, s); break;
+    case 6: launch_dense_t<IN, ACC, OUT, V, 1, 32, NT>(a, grid, s); break;
+    default: return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
+  }
+  (void)E;
+  return check_launch("k_dense");
+}
+
+template <int IN, class ACC, int OUT>
+int launch_dense_io(bool vec, bool nt, int variant, const DenseArgs& a, int64_t nblk_units,
+                    int64_t gy, hipStream_t s) {
+  constexpr int VW = vec_width<IN>();
+  if (vec) {
+    return nt ? launch_dense_v<IN, ACC, OUT, VW, true>(variant, a, nblk_units, gy, s)
+              : launch_dense_v<IN, ACC, OUT, VW, false>(variant, a, nblk_units, gy, s);
+  }
+  return nt ? launch_dense_v<IN, ACC, OUT, 1, true>(variant, a, nblk_units, gy, s)
+            : launch_dense_v<IN, ACC, OUT, 1, false>(variant, a, nblk_units, gy, s);
+}
+
+int launch_dense_dispatch(int in, int acc, int out, bool vec, bool nt, int variant,
+                          const DenseArgs& a, int64_t nblk_units, int64_t gy, hipStream_t s) {
+#define FJ_CASE(I, A, O, ACCT)                                                          \
+  if (in == I && acc == A && out == O)                                                  \
+    return launch_dense_io<I, ACCT, O>(vec, nt, variant, a, nblk_units, gy, s);
+  FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_BF16, AccF)
+  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
+  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
+#undef FJ_CASE
+  return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination (%d,%d,%d)", in, acc, out);
+}
+
+int64_t split_count(int64_t K, int64_t P) {
+  // enough workgroups to give every one of the 256 CUs ~8 of them, each range
+  // keeping >= 8 clients
+  const int64_t nb = (P / 4 + kThreads * 2 - 1) / (kThreads * 2) + 1;
+  int64_t s = (2048 + nb - 1) / nb;
+  if (s > K / 8) s = K / 8;
+  if (s > kSplitMax) s = kSplitMax;
+  return s < 1 ? 1 : s;
+}
+
+int validate_common(int in, int acc, int out, int64_t K, int flags, float scale) {
+  if (!combo_ok(in, acc, out))
+    return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination (in=%d, acc=%d, out=%d)", in,
+                acc, out);
+  if (K < 1) return fail(FJAGG_EINVAL, "K must be >= 1 (got %lld)", (long long)K);
+  if (acc == FJAGG_I32 && out == FJAGG_I32 && (flags & FJAGG_SCALE))
+    return fail(FJAGG_EINVAL, "FJAGG_SCALE needs a float output");
+  if ((flags & FJAGG_ACCUMULATE) && !((acc == FJAGG_F32 && out != FJAGG_I32) ||
+                                      (acc == FJAGG_I32 && out == FJAGG_I32)))
+    return fail(FJAGG_EINVAL, "FJAGG_ACCUMULATE needs the output in the fold's type");
+  (void)scale;
+  return FJAGG_OK;
+}
+
+// One dense launch over elements [0, P) of rows that start at x (row stride ld_bytes).
+int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, int64_t K,
+                int64_t P, const void* w, float scale, uint8_t* y, int flags, hipStream_t s,
+                int64_t kchunk, int64_t gy, int64_t y_ystride) {
+  const int ib = elem_bytes(in), ob = elem_bytes(out), vw = vwidth(in);
+  const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) % 16 == 0) &&
+                   (ld_bytes % 16 == 0) && (y_ystride % 16 == 0) && P >= vw;
+  const int variant = (flags >> 8) & 0xff;
+  if (variant >= kNumVariants) return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
+  const int E = kVariants[variant].E;
+  const int V = vec ? vw : 1;
+  DenseArgs a;
+  a.x = x;
+  a.ld_bytes = ld_bytes;
+  a.K = K;
+  a.nunits = P / V;
+  a.tail_n = (int)(P - a.nunits * V);
+  a.w = w;
+  a.scale = scale;
+  a.do_scale = (flags & FJAGG_SCALE) ? 1 : 0;
+  a.accumulate = (flags & FJAGG_ACCUMULATE) ? 1 : 0;
+  a.out = y;
+  a.kchunk = kchunk;
+  a.out_ystride = y_ystride;
+  const int64_t nblk = (a.nunits + (int64_t)kThreads * E - 1) / ((int64_t)kThreads * E);
+  (void)ob;
+  (void)ib;
+  return launch_dense_dispatch(in, acc, out, vec, (flags & FJAGG_NONTEMPORAL) != 0, variant, a,
+                               nblk, gy, s);
+}
+
+// Row bytes are addressed with 32-bit lane offsets: launch column chunks of <= 1 GiB.
+constexpr int64_t kMaxRowBytes = 1ll << 30;
+
+int dense_exact_chunked(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, int64_t K,
+                        int64_t P, const void* w, float scale, uint8_t* y, int flags,
+                        hipStream_t s, int64_t kchunk, int64_t gy, int64_t y_ystride) {
+  const int64_t ib = elem_bytes(in), ob = elem_bytes(out);
+  const int64_t chunk = kMaxRowBytes / ib;
+  for (int64_t p0 = 0; p0 < P; p0 += chunk) {
+    const int64_t n = (P - p0 < chunk) ? (P - p0) : chunk;
+    int rc = dense_exact(in, acc, out, x + p0 * ib, ld_bytes, K, n, w, scale, y + p0 * ob, flags,
+                         s, kchunk, gy, y_ystride);
+    if (rc) return rc;
+  }
+  return FJAGG_OK;
+}
+
+template <int IN, class ACC, int OUT, int V>
+int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w,
+                  float scale, int do_scale, int accumulate, hipStream_t s) {
+  const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
+  if (nt)
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, 8, true>), dim3((unsigned)nblk), dim3(kThreads), 0,
+                       s, img, L, K, wt, scale, do_scale, accumulate);
+  else
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, 8, false>), dim3((unsigned)nblk), dim3(kThreads),
+                       0, s, img, L, K, wt, scale, do_scale, accumulate);
+  return check_launch("k_ptrs");
+}
+
+template <int IN, class ACC, int OUT>
+int launch_ptrs_io(bool vec, bool nt, const int64_t* img, int L, int64_t K, int64_t nblk,
+                   const void* w, float scale, int do_scale, int accumulate, hipStream_t s) {
+  if (vec)
+    return launch_ptrs_t<IN, ACC, OUT, vec_width<IN>()>(nt, img, L, K, nblk, w, scale, do_scale,
+                                                        accumulate, s);
+  return launch_ptrs_t<IN, ACC, OUT, 1>(nt, img, L, K, nblk, w, scale, do_scale, accumulate, s);
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char* fjagg_last_error(void) { return g_err; }
+
+int fjagg_abi_version(void) { return FJAGG_ABI_VERSION; }
+
+int64_t fjagg_split_workspace_bytes(int64_t K, int64_t P) {
+  if (K < 1 || P < 1) return 0;
+  const int64_t s = split_count(K, P);
+  if (s <= 1) return 0;
+  return kSplitHeader + s * ((P * 4 + 255) / 256 * 256);
+}
+
+int fjagg_wsum_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_dev, int64_t ld,
+                     int64_t K, int64_t P, const void* w_dev, float scale, void* out_dev,
+                     int flags, int mode, void* ws_dev, int64_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  int rc = validate_common(in_dtype, acc_dtype, out_dtype, K, flags, scale);
+  if (rc) return rc;
+  if (P < 0 || ld < P) return fail(FJAGG_EINVAL, "need 0 <= P <= ld (P=%lld ld=%lld)", (long long)P, (long long)ld);
+  if (P == 0) return FJAGG_OK;
+  if (!x_dev || !w_dev || !out_dev) return fail(FJAGG_EINVAL, "null pointer argument");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint8_t* x = reinterpret_cast<const uint8_t*>(x_dev);
+  uint8_t* y = reinterpret_cast<uint8_t*>(out_dev);
+  const int64_t ib = elem_bytes(in_dtype);
+  if (mode == FJAGG_MODE_EXACT)
+    return dense_exact_chunked(in_dtype, acc_dtype, out_dtype, x, ld * ib, K, P, w_dev, scale, y,
+                               flags, s, K, 1, 0);
+  if (mode != FJAGG_MODE_SPLIT) return fail(FJAGG_EINVAL, "unknown mode %d", mode);
+  const int64_t S = split_count(K, P);
+  if (S <= 1)  // nothing to split: the exact path already fills the chip
+    return dense_exact_chunked(in_dtype, acc_dtype, out_dtype, x, ld * ib, K, P, w_dev, scale, y,
+                               flags, s, K, 1, 0);
+  const int64_t need = fjagg_split_workspace_bytes(K, P);
+  if (!ws_dev || ws_bytes < need)
+    return fail(FJAGG_EINVAL, "split mode needs %lld workspace bytes (got %lld)", (long long)need,
+                (long long)ws_bytes);
+  uint8_t* ws = reinterpret_cast<uint8_t*>(ws_dev);
+  const int64_t pstride = (P * 4 + 255) / 256 * 256;  // bytes per range partial
+  const int64_t kchunk = (K + S - 1) / S;
+  const int64_t gy = (K + kchunk - 1) / kchunk;
+  // 1) each client range folds into its own partial (fold type, no scale)
+  const int flags1 = flags & ~(FJAGG_SCALE | FJAGG_ACCUMULATE);
+  rc = dense_exact_chunked(in_dtype, acc_dtype, acc_dtype, x, ld * ib, K, P, w_dev, 1.0f,
+                           ws + kSplitHeader, flags1, s, kchunk, gy, pstride);
+  if (rc) return rc;
+  // 2) ordered combine of the gy partials = unit-weight fold (x*1 is exact)
+  const unsigned one_bits = acc_dtype == FJAGG_F32 ? 0x3f800000u : 1u;
+  if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws), (int)one_bits, kSplitMax, s) != hipSuccess)
+    return check_launch("hipMemsetD32Async");
+  const int flags2 = flags & (FJAGG_SCALE | FJAGG_ACCUMULATE);
+  return dense_exact_chunked(acc_dtype, acc_dtype, out_dtype, ws + kSplitHeader, pstride, gy, P,
+                             ws, scale, y, flags2, s, gy, 1, 0);
+}
+
+int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, int64_t* blocks,
+                        int64_t blocks_cap) {
+  g_err[0] = 0;
+  if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16 && in_dtype != FJAGG_I32)
+    return fail(FJAGG_EINVAL, "bad dtype %d", in_dtype);
+  if (L < 0 || L >= (1 << 22)) return fail(FJAGG_EINVAL, "bad leaf count %d", L);
+  const int64_t V = (flags & FJAGG_UNALIGNED) ? 1 : vwidth(in_dtype);
+  const int64_t per = (int64_t)kThreads * kPtrsE;
+  int64_t nblk = 0;
+  for (int l = 0; l < L; ++l) {  // tails first: they are latency-bound, start them early
+    const int64_t n = leaf_n[l];
+    if (n < 0 || n * elem_bytes(in_dtype) > kMaxRowBytes)
+      return fail(FJAGG_EINVAL, "leaf %d: %lld elements unsupported", l, (long long)n);
+    if (n % V) {
+      if (nblk < blocks_cap) blocks[nblk] = ((int64_t)l << 40) | (1ll << 62);
+      ++nblk;
+    }
+  }
+  for (int l = 0; l < L; ++l) {
+    const int64_t nunits = leaf_n[l] / V;
+    for (int64_t u = 0; u < nunits; u += per) {
+      if (nblk < blocks_cap) blocks[nblk] = ((int64_t)l << 40) | u;
+      ++nblk;
+    }
+  }
+  return nblk;
+}
+
+int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,
+                    int64_t K, int64_t nblk, const void* w_dev, float scale, int flags,
+                    void* stream) {
+  g_err[0] = 0;
+  int rc = validate_common(in_dtype, acc_dtype, out_dtype, K, flags, scale);
+  if (rc) return rc;
+  if (nblk == 0) return FJAGG_OK;
+  if (nblk < 0 || nblk > 0x7fffffff || !image_dev || !w_dev || L < 1)
+    return fail(FJAGG_EINVAL, "bad plan (nblk=%lld, L=%d)", (long long)nblk, L);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool vec = !(flags & FJAGG_UNALIGNED);
+  const bool nt = (flags & FJAGG_NONTEMPORAL) != 0;
+  const int ds = (flags & FJAGG_SCALE) ? 1 : 0, ac = (flags & FJAGG_ACCUMULATE) ? 1 : 0;
+#define FJ_CASE(I, A, O, ACCT)                                                                 \
+  if (in_dtype == I && acc_dtype == A && out_dtype == O)                                       \
+    return launch_ptrs_io<I, ACCT, O>(vec, nt, image_dev, L, K, nblk, w_dev, scale, ds, ac, s);
+  FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_BF16, AccF)
+  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
+  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
+#undef FJ_CASE
+  return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination");
+}
+
+int64_t fjagg_l2sq_workspace_bytes(int64_t K, int64_t P) {
+  if (K < 1 || P < 1) return 0;
+  const int64_t per = 64 * 1024;  // elements per workgroup
+  const int64_t nb = (P + per - 1) / per;
+  return K * nb * 4;
+}
+
+int fjagg_l2sq_dense(int in_dtype, const void* x_dev, int64_t ld, int64_t K, int64_t P,
+                     float* out_dev, void* ws_dev, int64_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16)
+    return fail(FJAGG_EUNSUPPORTED, "l2sq supports f32 and bf16 inputs");
+  if (K < 1 || P < 1 || ld < P) return fail(FJAGG_EINVAL, "bad shape");
+  if (K > 65535) return fail(FJAGG_EINVAL, "l2sq: K > 65535 unsupported");
+  const int64_t need = fjagg_l2sq_workspace_bytes(K, P);
+  if (!ws_dev || ws_bytes < need)
+    return fail(FJAGG_EINVAL, "l2sq needs %lld workspace bytes", (long long)need);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t per = 64 * 1024, nb = (P + per - 1) / per;
+  const int64_t ldb = ld * elem_bytes(in_dtype);
+  float* ws = reinterpret_cast<float*>(ws_dev);
+  const uint8_t* x = reinterpret_cast<const uint8_t*>(x_dev);
+  dim3 grid((unsigned)nb, (unsigned)K);
+  if (in_dtype == FJAGG_F32)
+    hipLaunchKernelGGL(k_l2sq_partial<FJAGG_F32>, grid, dim3(kThreads), 0, s, x, ldb, P, per, ws);
+  else
+    hipLaunchKernelGGL(k_l2sq_partial<FJAGG_BF16>, grid, dim3(kThreads), 0, s, x, ldb, P, per, ws);
+  int rc = check_launch("k_l2sq_partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_l2sq_combine, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, ws, nb, K,
+                     out_dev);
+  return check_launch("k_l2sq_combine");
+}
+
+int fjagg_fill_synth(int dtype, void* x_dev, int64_t ld, int64_t K, int64_t P, int64_t k0,
+                     uint64_t seed, float amp, void* stream) {
+  g_err[0] = 0;
+  if (K < 0 || P < 0 || ld < P) return fail(FJAGG_EINVAL, "bad shape");
+  if (K == 0 || P == 0) return FJAGG_OK;
+  if (!x_dev) return fail(FJAGG_EINVAL, "null pointer");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t total = K * P;
+  int64_t nb = (total + kThreads - 1) / kThreads;
+  if (nb > 65536) nb = 65536;
+  uint8_t* x = reinterpret_cast<uint8_t*>(x_dev);
+  if (dtype == FJAGG_F32)
+    hipLaunchKernelGGL(k_fill<FJAGG_F32>, dim3((unsigned)nb), dim3(kThreads), 0, s, x, ld, K, P, k0,
+                       seed, amp);
+  else if (dtype == FJAGG_BF16)
+    hipLaunchKernelGGL(k_fill<FJAGG_BF16>, dim3((unsigned)nb), dim3(kThreads), 0, s, x, ld, K, P, k0,
+                       seed, amp);
+  else
+    return fail(FJAGG_EUNSUPPORTED, "fill supports f32 and bf16");
+  return check_launch("k_fill");
+}
+
+}  // extern "C"

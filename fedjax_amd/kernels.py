@@ -1,0 +1,149 @@
+"""Tensor-level wrappers over the C ABI (include/fjagg.h).
+
+Every function here takes device-resident ``torch`` tensors, launches on torch's
+current HIP stream and returns without synchronising (like a JAX dispatch).
+They are the only route from Python to the kernels; there is no CPU or PyTorch
+fallback: a host tensor, an unsupported dtype or a missing library raises.
+"""
+
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from fedjax_amd import _lib
+
+_CODES = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.int32: _lib.I32}
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    try:
+        return _CODES[dt]
+    except KeyError:
+        raise TypeError(f"fedjax_amd kernels support float32, bfloat16 and int32, not {dt}") from None
+
+
+def _stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require_device(*ts: torch.Tensor) -> torch.device:
+    dev = None
+    for t in ts:
+        if not t.is_cuda:
+            raise ValueError("fedjax_amd kernels need device tensors (got a host tensor); "
+                             "move client deltas to the GPU first")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"tensors on different devices: {dev} and {t.device}")
+    return dev
+
+
+def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[float] = None,
+                       out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None,
+                       accumulate: bool = False, mode: str = "exact",
+                       workspace: Optional[torch.Tensor] = None, nontemporal: bool = False,
+                       variant: int = 0) -> torch.Tensor:
+    """Fold a client-major slab ``x[K, P]`` (row stride ``x.stride(0)``, unit column
+    stride) with per-client weights ``w[K]`` into ``out[P]``.
+
+    ``w`` is float32 (float fold) or int32 (integer fold; int32 ``x`` only).
+    ``scale`` multiplies the fold at the end (tree_mean's f32(1/W)).
+    ``accumulate`` starts the fold from ``out``'s current contents.
+    """
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("x must be a [K, P] tensor with unit column stride")
+    K, P = x.shape
+    if w.shape != (K,):
+        raise ValueError(f"w must have shape ({K},), got {tuple(w.shape)}")
+    acc = _lib.I32 if w.dtype == torch.int32 else _lib.F32
+    if w.dtype not in (torch.float32, torch.int32) or not w.is_contiguous():
+        raise TypeError("w must be a contiguous float32 or int32 tensor")
+    if out is None:
+        if out_dtype is None:
+            if acc == _lib.F32:  # int32 leaves * float weights promote to float32
+                out_dtype = torch.float32 if x.dtype == torch.int32 else x.dtype
+            else:
+                out_dtype = torch.float32 if scale is not None else torch.int32
+        out = torch.empty(P, dtype=out_dtype, device=x.device)
+    if out.numel() != P or not out.is_contiguous():
+        raise ValueError("out must be a contiguous tensor of P elements")
+    dev = _require_device(x, w, out)
+    flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
+    flags |= (_lib.NONTEMPORAL if nontemporal else 0) | ((variant & 0xFF) << 8)
+    m = {"exact": _lib.MODE_EXACT, "split": _lib.MODE_SPLIT}[mode]
+    ws_ptr, ws_bytes = None, 0
+    if m == _lib.MODE_SPLIT:
+        need = split_workspace_bytes(K, P)
+        if need:
+            if workspace is None:
+                workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+            ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+    ld = x.stride(0) if K > 1 else P
+    _lib.call("fjagg_wsum_dense", dtype_code(x.dtype), acc, dtype_code(out.dtype), x.data_ptr(), ld,
+              K, P, w.data_ptr(), float(scale if scale is not None else 1.0), out.data_ptr(), flags,
+              m, ws_ptr, ws_bytes, _stream_handle(dev))
+    return out
+
+
+def split_workspace_bytes(K: int, P: int) -> int:
+    return int(_lib.load().fjagg_split_workspace_bytes(K, P))
+
+
+def ptrs_plan(in_code: int, leaf_n: Sequence[int], unaligned: bool) -> np.ndarray:
+    """Block table of the pytree kernel (host int64 array)."""
+    lib = _lib.load()
+    n = np.ascontiguousarray(leaf_n, dtype=np.int64)
+    flags = _lib.UNALIGNED if unaligned else 0
+    need = lib.fjagg_ptrs_plan(in_code, flags, n.ctypes.data, len(n), None, 0)
+    _lib.check(0 if need >= 0 else int(need), "fjagg_ptrs_plan")
+    blocks = np.empty(max(need, 1), dtype=np.int64)
+    got = lib.fjagg_ptrs_plan(in_code, flags, n.ctypes.data, len(n), blocks.ctypes.data, need)
+    _lib.check(0 if got >= 0 else int(got), "fjagg_ptrs_plan")
+    return blocks[:need]
+
+
+def weighted_sum_ptrs(in_code: int, acc_code: int, out_code: int, image_dev: torch.Tensor,
+                      L: int, K: int, nblk: int, w_dev: torch.Tensor, scale: Optional[float],
+                      accumulate: bool = False, unaligned: bool = False,
+                      nontemporal: bool = False) -> None:
+    """Launch the pytree kernel over a device plan image (see include/fjagg.h)."""
+    dev = _require_device(image_dev, w_dev)
+    flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
+    flags |= (_lib.UNALIGNED if unaligned else 0) | (_lib.NONTEMPORAL if nontemporal else 0)
+    _lib.call("fjagg_wsum_ptrs", in_code, acc_code, out_code, image_dev.data_ptr(), L, K, nblk,
+              w_dev.data_ptr(), float(scale if scale is not None else 1.0), flags,
+              _stream_handle(dev))
+
+
+def l2_squared_dense(x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                     workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-client sum of squares of a [K, P] slab -> float32[K] (tree_util.py:105-108)."""
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("x must be a [K, P] tensor with unit column stride")
+    K, P = x.shape
+    dev = _require_device(x)
+    if out is None:
+        out = torch.empty(K, dtype=torch.float32, device=dev)
+    need = int(_lib.load().fjagg_l2sq_workspace_bytes(K, P))
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty(max(need, 4), dtype=torch.uint8, device=dev)
+    ld = x.stride(0) if K > 1 else P
+    _lib.call("fjagg_l2sq_dense", dtype_code(x.dtype), x.data_ptr(), ld, K, P, out.data_ptr(),
+              workspace.data_ptr(), workspace.numel() * workspace.element_size(), _stream_handle(dev))
+    return out
+
+
+def fill_synth(x: torch.Tensor, *, k0: int = 0, seed: int = 0, amp: float = 0.01) -> torch.Tensor:
+    """Synthetic deltas x[k, p] = amp * u(seed, k0 + k, p) (tests/bench only)."""
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("x must be a [K, P] tensor with unit column stride")
+    dev = _require_device(x)
+    K, P = x.shape
+    ld = x.stride(0) if K > 1 else P
+    _lib.call("fjagg_fill_synth", dtype_code(x.dtype), x.data_ptr(), ld, K, P, k0, seed, amp,
+              _stream_handle(dev))
+    return x

@@ -1,0 +1,146 @@
+/*
+ * fjagg.h — C ABI of the MI355X-native FedJAX aggregation library (libfjagg.so).
+ *
+ * This library replaces the arithmetic of FedJAX's server-side client-update
+ * aggregation, i.e. the weighted fold that `fedjax.tree_util.tree_mean` performs
+ * over K client-delta pytrees:
+ *
+ *     reference                                   replaced by
+ *     ------------------------------------------  ---------------------------------
+ *     tree_weight   fedjax/core/tree_util.py:29-32  fjagg_wsum_* (per-client multiply)
+ *     _tree_add_eq  fedjax/core/tree_util.py:47-54  fjagg_wsum_* (fused running add)
+ *     _tree_inverse_weight_eq  tree_util.py:58-61   fjagg_wsum_* with FJAGG_SCALE
+ *     tree_mean loop tree_util.py:76-96             one fjagg_wsum_* launch per bucket
+ *     tree_sum       tree_util.py:64-73             fjagg_wsum_* with unit weights
+ *     tree_add       tree_util.py:47-50             fjagg_wsum_* K=2, unit weights
+ *     tree_l2_squared tree_util.py:105-108          fjagg_l2sq_*
+ *
+ * The reference has no native code: each of those rows is a `jax.jit` dispatch
+ * into XLA. The Python mirror of the reference's API
+ * (fedjax_amd/tree_util.py, fedjax_amd/aggregators/) is the only caller inside
+ * this repository; INTEGRATION.md shows the ctypes binding a FedJAX maintainer
+ * would add.
+ *
+ * Conventions
+ *   - every entry point returns 0 on success or a negative FJAGG_E* code; the
+ *     message of the last failure on the calling thread is fjagg_last_error().
+ *   - every launch is asynchronous on the given hipStream_t (passed as void*;
+ *     NULL = the null stream). No entry point allocates, frees or synchronises,
+ *     so launches may be captured into a hipGraph.
+ *   - pointers named *_dev are device pointers; everything else is host memory.
+ *   - inputs are never written (reference ownership rule, tree_util_test.py:50-51).
+ *
+ * Arithmetic contract (FJAGG_MODE_EXACT, the default): for every element p
+ *     t_k = fl(x_k[p] * w_k)            (IEEE single, round to nearest, no FMA)
+ *     s_0 = t_0                          (s_0 = fl(out[p] + t_0) with FJAGG_ACCUMULATE)
+ *     s_k = fl(s_{k-1} + t_k)            k = 1 .. K-1, in client order
+ *     out[p] = fl(s_{K-1} * scale)       with FJAGG_SCALE, else s_{K-1}
+ * which is bit-for-bit the sequence XLA executes for tree_mean.
+ * FJAGG_MODE_SPLIT folds contiguous client ranges independently and combines
+ * the range sums in range order: not bitwise, within the bound in DESIGN.md.
+ */
+#ifndef FJAGG_H_
+#define FJAGG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FJAGG_ABI_VERSION 1
+
+/* element types */
+enum fjagg_dtype {
+  FJAGG_F32 = 0,   /* IEEE binary32 */
+  FJAGG_BF16 = 1,  /* bfloat16 (stored as uint16) */
+  FJAGG_I32 = 2,   /* two's complement int32, wrapping arithmetic like XLA */
+};
+
+/* flags (bitwise OR) */
+enum fjagg_flags {
+  FJAGG_SCALE = 1 << 0,       /* multiply the fold by `scale` (tree_mean's f32(1/W)) */
+  FJAGG_ACCUMULATE = 1 << 1,  /* fold starts from the current contents of the output */
+  FJAGG_NONTEMPORAL = 1 << 2, /* non-temporal (streaming) loads of the client deltas */
+  FJAGG_UNALIGNED = 1 << 3,   /* ptrs path: some pointer is not 16-byte aligned */
+};
+/* bits 8..15 of flags select a kernel variant (0 = default); used by tuning only */
+#define FJAGG_VARIANT(v) (((v)&0xff) << 8)
+
+enum fjagg_mode {
+  FJAGG_MODE_EXACT = 0, /* sequential per-element fold: bitwise equal to the reference */
+  FJAGG_MODE_SPLIT = 1, /* client axis split over workgroups, ordered combine */
+};
+
+/* error codes */
+#define FJAGG_OK 0
+#define FJAGG_EINVAL (-1)
+#define FJAGG_EHIP (-2)
+#define FJAGG_EUNSUPPORTED (-3)
+
+/* Message of the last failed call on this thread ("" if none). */
+const char* fjagg_last_error(void);
+/* FJAGG_ABI_VERSION of the loaded library. */
+int fjagg_abi_version(void);
+
+/*
+ * Dense client-major slab: client k's delta is x_dev + k*ld elements, P
+ * contiguous elements each. acc_dtype is FJAGG_F32 (w_dev is float[K]) or
+ * FJAGG_I32 (integer fold, w_dev is int32[K]). Supported (in, acc, out):
+ *   (F32,F32,F32) (BF16,F32,BF16) (BF16,F32,F32) (I32,F32,F32) (I32,I32,I32) (I32,I32,F32)
+ * mode FJAGG_MODE_SPLIT needs ws_dev of fjagg_split_workspace_bytes(K, P) bytes
+ * (ws may be NULL in exact mode).
+ * Replaces: the per-client loop of tree_mean, fedjax/core/tree_util.py:85-96.
+ */
+int fjagg_wsum_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_dev,
+                     int64_t ld, int64_t K, int64_t P, const void* w_dev, float scale,
+                     void* out_dev, int flags, int mode, void* ws_dev, int64_t ws_bytes,
+                     void* stream);
+
+/* Workspace bytes FJAGG_MODE_SPLIT needs for a K x P fold (0 if split is not used). */
+int64_t fjagg_split_workspace_bytes(int64_t K, int64_t P);
+
+/*
+ * Pytree path: K clients x L leaves, each leaf a separate allocation.
+ * Launches ONE kernel over every leaf. The plan image is an int64 array in
+ * device memory laid out as
+ *     in_ptrs [K*L]   client k, leaf l at k*L + l (device addresses)
+ *     out_ptrs[L]
+ *     leaf_n  [L]     elements per leaf
+ *     blocks  [nblk]  from fjagg_ptrs_plan()
+ * Replaces: jax.tree.map over leaves inside tree_weight/tree_add,
+ * fedjax/core/tree_util.py:32,50, for the whole tree_mean loop :85-96.
+ */
+/* Fills blocks[] (up to blocks_cap entries) for leaves of leaf_n[l] elements and
+ * returns the number of blocks the plan needs (negative FJAGG_E* on error); call
+ * with blocks_cap = 0 to size the array. flags: FJAGG_UNALIGNED if any client or
+ * output pointer is not 16-byte aligned (the same flag must go to the launch). */
+int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, int64_t* blocks,
+                        int64_t blocks_cap);
+int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev,
+                    int L, int64_t K, int64_t nblk, const void* w_dev, float scale,
+                    int flags, void* stream);
+
+/*
+ * Squared L2 norm of each of K client deltas (the per-client diagnostic of
+ * examples/fed_avg.py:79-81 -> tree_util.py:105-108), accumulated in f32 per
+ * workgroup and combined in a fixed order: deterministic, not bitwise equal to
+ * XLA's reduction tree. out_dev is float[K]; ws_dev needs
+ * fjagg_l2sq_workspace_bytes(K, P) bytes.
+ */
+int64_t fjagg_l2sq_workspace_bytes(int64_t K, int64_t P);
+int fjagg_l2sq_dense(int in_dtype, const void* x_dev, int64_t ld, int64_t K, int64_t P,
+                     float* out_dev, void* ws_dev, int64_t ws_bytes, void* stream);
+
+/*
+ * Synthetic client deltas for tests and benchmarks (never on the product path):
+ *   x[k][p] = amp * u(seed, k0 + k, p),  u = uniform in [-1, 1) with 2^-23 steps,
+ * from a counter-based hash shared bit-for-bit with oracle/fold_ref.c.
+ */
+int fjagg_fill_synth(int dtype, void* x_dev, int64_t ld, int64_t K, int64_t P, int64_t k0,
+                     uint64_t seed, float amp, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FJAGG_H_ */
