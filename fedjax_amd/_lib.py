@@ -41,6 +41,8 @@ _SIGNATURES = {
     "fjagg_wsum_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _i32, _vp]),
     "fjagg_l2sq_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_l2sq_dense": (_i32, [_i32, _vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp]),
+    "fjagg_l2sq_rows_workspace_bytes": (_i64, [_i64, _i64]),
+    "fjagg_l2sq_rows": (_i32, [_i32, _vp, _i64, _i64, _i64, _i32, _vp, _vp, _i64, _vp]),
     "fjagg_fill_synth": (_i32, [_i32, _vp, _i64, _i64, _i64, _i64, _u64, _f32, _vp]),
 }
 SYMBOLS = tuple(_SIGNATURES)

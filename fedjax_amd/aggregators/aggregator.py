@@ -1,0 +1,62 @@
+"""Aggregator interface and the weighted-mean aggregator.
+
+Mirror of google/fedjax 0.0.17 ``fedjax/aggregators/aggregator.py``:
+
+* :class:`Aggregator` — frozen pytree dataclass of ``init`` / ``apply`` (:53-80);
+* :class:`MeanAggregatorState` — empty state (:83-85);
+* :func:`mean_aggregator` — ``apply`` lazily drops client ids and calls
+  :func:`fedjax_amd.tree_util.tree_mean` (:88-102), which folds all K clients on
+  the GPU in one kernel launch per leaf-dtype group.
+"""
+
+from typing import Any, Callable, Iterable, Tuple
+
+from fedjax_amd import dataclasses
+from fedjax_amd import tree_util
+from fedjax_amd.typing import ClientId, Params
+
+PyTree = Any
+AggregatorState = PyTree
+
+
+@dataclasses.dataclass
+class Aggregator:
+    """Interface for algorithms to aggregate (aggregator.py:53-80).
+
+    Usage, as in the reference::
+
+      aggregator = mean_aggregator()
+      state = aggregator.init()
+      for i in range(num_rounds):
+        clients_params_and_weights = compute_client_outputs(i)
+        aggregated_params, state = aggregator.apply(clients_params_and_weights, state)
+
+    Attributes:
+      init: Returns initial state of aggregator.
+      apply: Returns the new aggregator state and aggregated params.
+    """
+    init: Callable[[], AggregatorState]
+    apply: Callable[[Iterable[Tuple[ClientId, Params, float]], AggregatorState],
+                    Tuple[Params, AggregatorState]]
+
+
+@dataclasses.dataclass
+class MeanAggregatorState:
+    """Mean aggregator is stateless."""
+
+
+def mean_aggregator() -> Aggregator:
+    """Builds (weighted) mean aggregator."""
+
+    def init():
+        return MeanAggregatorState()
+
+    def apply(clients_params_and_weights, state):
+        def extract_params_and_weight(clients_params_and_weight):
+            _, param, weight = clients_params_and_weight
+            return param, weight
+
+        params_and_weights = map(extract_params_and_weight, clients_params_and_weights)
+        return tree_util.tree_mean(params_and_weights), state
+
+    return Aggregator(init, apply)

@@ -424,6 +424,47 @@ __global__ void k_l2sq_combine(const float* __restrict__ ws, int64_t nb, int64_t
   out[k] = s;
 }
 
+// Pytree form: rows r = 0..R-1 at arbitrary addresses (image = ptrs[R] | n[R]);
+// grid (nbx, R); block b of row r sums elements [b*per, (b+1)*per) of that row.
+template <int IN>
+__global__ __launch_bounds__(kThreads) void k_l2sq_rows(const int64_t* __restrict__ img, int64_t R,
+                                                       int64_t per, float* __restrict__ ws) {
+  constexpr int IB = Elem<IN>::B;
+  const int64_t r = blockIdx.y;
+  const uint8_t* x = reinterpret_cast<const uint8_t*>(img[r]);
+  const int64_t n = img[R + r];
+  const int64_t e0 = (int64_t)blockIdx.x * per;
+  const int64_t e1 = (e0 + per < n) ? e0 + per : n;
+  float s = 0.f;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kThreads) {
+    float t[1];
+    decode<IN, AccF, 1>(load_unit<IN, 1, false>(x + e * IB), t);
+    s = __fadd_rn(s, __fmul_rn(t[0], t[0]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s = __fadd_rn(s, __shfl_xor(s, o, 64));
+  __shared__ float red[kThreads / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = red[0];
+#pragma unroll
+    for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, red[i]);
+    ws[r * gridDim.x + blockIdx.x] = t;
+  }
+}
+
+// out[g] = sum over rows [g*rows_per_group, (g+1)*rows_per_group) and their nb partials,
+// in order; sqrt of it when take_sqrt.
+__global__ void k_l2sq_groups(const float* __restrict__ ws, int64_t nb, int64_t G,
+                              int64_t rows_per_group, int take_sqrt, float* __restrict__ out) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  float s = 0.f;
+  for (int64_t i = 0; i < rows_per_group * nb; ++i) s = __fadd_rn(s, ws[g * rows_per_group * nb + i]);
+  out[g] = take_sqrt ? __fsqrt_rn(s) : s;
+}
+
 // Synthetic deltas (tests/bench only): bit-identical to oracle/fold_ref.c.
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -454,7 +495,8 @@ struct Combo {
   int in, acc, out;
 };
 bool combo_ok(int in, int acc, int out) {
-  static const Combo ok[] = {{FJAGG_F32, FJAGG_F32, FJAGG_F32},  {FJAGG_BF16, FJAGG_F32, FJAGG_BF16},
+  static const Combo ok[] = {{FJAGG_F32, FJAGG_F32, FJAGG_F32},  {FJAGG_F32, FJAGG_F32, FJAGG_BF16},
+                             {FJAGG_BF16, FJAGG_F32, FJAGG_BF16},
                              {FJAGG_BF16, FJAGG_F32, FJAGG_F32}, {FJAGG_I32, FJAGG_F32, FJAGG_F32},
                              {FJAGG_I32, FJAGG_I32, FJAGG_I32},  {FJAGG_I32, FJAGG_I32, FJAGG_F32}};
   for (const Combo& c : ok)
@@ -528,6 +570,7 @@ int launch_dense_dispatch(int in, int acc, int out, bool vec, bool nt, int varia
   if (in == I && acc == A && out == O)                                                  \
     return launch_dense_io<I, ACCT, O>(vec, nt, variant, a, nblk_units, gy, s);
   FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_BF16, AccF)
   FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_BF16, AccF)
   FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_F32, AccF)
   FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
@@ -776,6 +819,40 @@ int fjagg_l2sq_dense(int in_dtype, const void* x_dev, int64_t ld, int64_t K, int
   hipLaunchKernelGGL(k_l2sq_combine, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, ws, nb, K,
                      out_dev);
   return check_launch("k_l2sq_combine");
+}
+
+int64_t fjagg_l2sq_rows_workspace_bytes(int64_t R, int64_t max_n) {
+  if (R < 1 || max_n < 1) return 0;
+  const int64_t per = 64 * 1024;
+  return R * ((max_n + per - 1) / per) * 4;
+}
+
+int fjagg_l2sq_rows(int in_dtype, const int64_t* image_dev, int64_t R, int64_t max_n,
+                    int64_t rows_per_group, int take_sqrt, float* out_dev, void* ws_dev,
+                    int64_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16)
+    return fail(FJAGG_EUNSUPPORTED, "l2sq supports f32 and bf16 inputs");
+  if (R < 1 || max_n < 0 || rows_per_group < 1 || R % rows_per_group || R > 65535)
+    return fail(FJAGG_EINVAL, "bad row grouping (R=%lld, rows_per_group=%lld)", (long long)R,
+                (long long)rows_per_group);
+  const int64_t per = 64 * 1024, nb = max_n > 0 ? (max_n + per - 1) / per : 1;
+  const int64_t need = R * nb * 4;
+  if (!ws_dev || ws_bytes < need || !image_dev || !out_dev)
+    return fail(FJAGG_EINVAL, "l2sq_rows needs %lld workspace bytes", (long long)need);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* ws = reinterpret_cast<float*>(ws_dev);
+  dim3 grid((unsigned)nb, (unsigned)R);
+  if (in_dtype == FJAGG_F32)
+    hipLaunchKernelGGL(k_l2sq_rows<FJAGG_F32>, grid, dim3(kThreads), 0, s, image_dev, R, per, ws);
+  else
+    hipLaunchKernelGGL(k_l2sq_rows<FJAGG_BF16>, grid, dim3(kThreads), 0, s, image_dev, R, per, ws);
+  int rc = check_launch("k_l2sq_rows");
+  if (rc) return rc;
+  const int64_t G = R / rows_per_group;
+  hipLaunchKernelGGL(k_l2sq_groups, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, ws, nb, G,
+                     rows_per_group, take_sqrt, out_dev);
+  return check_launch("k_l2sq_groups");
 }
 
 int fjagg_fill_synth(int dtype, void* x_dev, int64_t ld, int64_t K, int64_t P, int64_t k0,

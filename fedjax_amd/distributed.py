@@ -1,0 +1,129 @@
+"""Client-sharded aggregation over the GPUs of one node.
+
+The reference has no device-side reduction: its only multi-device mechanism,
+``ForEachClientPmapBackend`` (fedjax/core/for_each_client.py:266-357), spreads
+client *training* over ``jax.local_devices()`` and copies every client output
+back to ``devices[0]`` (:351-353), where ``tree_mean`` runs on one device.
+
+Here every rank (one process per GPU, ``torch.distributed`` over RCCL/xGMI)
+owns a contiguous range of clients, folds them with the HIP kernel into a
+float32 partial that is already multiplied by f32(1/W), and the partials are
+summed by ``reduce`` (or ``all_reduce``) over xGMI — the only exchange step.
+The parameter axis is cut into buckets so the reduce of bucket b overlaps the
+fold of bucket b+1 (the collective runs on RCCL's own stream).
+
+Numerics: the result differs from the single-GPU exact fold only by the G-way
+combine and the per-rank scaling; tests/test_distributed.py and the GPU tests
+check it against the per-element bound in DESIGN.md §4.
+"""
+
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from fedjax_amd import kernels, tree_util
+
+# bucket edges are multiples of this many elements (keeps 16-byte alignment)
+BUCKET_ALIGN = 1024
+
+
+def shard_range(num_clients: int, rank: int, world_size: int) -> Tuple[int, int]:
+    """Contiguous client range [k0, k1) of ``rank`` (sizes differ by at most 1)."""
+    base, extra = divmod(num_clients, world_size)
+    k0 = rank * base + min(rank, extra)
+    return k0, k0 + base + (1 if rank < extra else 0)
+
+
+def bucket_edges(P: int, buckets: int) -> List[Tuple[int, int]]:
+    buckets = max(1, int(buckets))
+    step = -(-P // buckets)
+    step = max(BUCKET_ALIGN, -(-step // BUCKET_ALIGN) * BUCKET_ALIGN)
+    return [(p0, min(P, p0 + step)) for p0 in range(0, P, step)]
+
+
+def total_weight(local_weights: Sequence, group=None, device=None):
+    """W over all ranks' clients when no rank knows every weight: the local sums
+    (reference accumulation, Python float) are summed in float64 across ranks."""
+    W = 0.0
+    for w in local_weights:
+        W += tree_util._host_weight(w)
+    t = torch.tensor([float(W)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, group=group)
+    return float(t.item())
+
+
+def _default_partial(x: torch.Tensor, w: torch.Tensor, scale: float, out: torch.Tensor) -> None:
+    nbytes = x.numel() * x.element_size()
+    kernels.weighted_sum_dense(x, w, scale=scale, out=out,
+                               nontemporal=nbytes >= tree_util.NONTEMPORAL_MIN_BYTES)
+
+
+def sharded_weighted_mean(x_local: torch.Tensor, w_local: torch.Tensor, W_total, *, group=None,
+                          dst: int = 0, all_ranks: bool = False, buckets: int = 4,
+                          out: Optional[torch.Tensor] = None,
+                          partial_fn: Optional[Callable] = None) -> torch.Tensor:
+    """Weighted mean over all ranks' client rows.
+
+    x_local: this rank's client deltas [K_g, P] (unit column stride, may be K_g = 0
+    only if partial_fn handles it); w_local: their float32 weights [K_g] on the same
+    device; W_total: sum of ALL clients' weights (reference semantics, host scalar).
+    Returns the float32 mean [P] — valid on ``dst`` (every rank with ``all_ranks``).
+    partial_fn(x, w, scale, out) computes ``out = fl(sum_k x_k w_k) * scale`` for one
+    bucket; the default is the HIP kernel (tests inject the oracle to run on gloo).
+    """
+    P = x_local.shape[1]
+    scale = float(np.float32(tree_util._inverse(W_total)))
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=x_local.device)
+    fn = partial_fn or _default_partial
+    works = []
+    for p0, p1 in bucket_edges(P, buckets):
+        seg = out[p0:p1]
+        fn(x_local[:, p0:p1], w_local, scale, seg)
+        if all_ranks:
+            works.append(dist.all_reduce(seg, op=dist.ReduceOp.SUM, group=group, async_op=True))
+        else:
+            works.append(dist.reduce(seg, dst=dst, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    for wk in works:
+        wk.wait()
+    return out
+
+
+def sharded_tree_mean(local_pytrees_and_weights, *, W_total=None, group=None, dst: int = 0,
+                      all_ranks: bool = False):
+    """``tree_mean`` over the union of every rank's clients.
+
+    Each rank folds its own (pytree, weight) pairs in one pytree-kernel launch
+    (already scaled by f32(1/W)); the float32 partial leaves are packed into one
+    buffer and summed across ranks. Returns the mean pytree (float32 leaves) on
+    ``dst`` (on every rank with ``all_ranks``), ``None`` elsewhere or when no rank
+    has a client.
+    """
+    pairs = list(local_pytrees_and_weights)
+    trees = [t for t, _ in pairs]
+    weights = [tree_util._host_weight(w) for _, w in pairs]
+    if W_total is None:
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else None
+        W_total = total_weight(weights, group=group, device=dev)
+    if not trees:
+        raise ValueError("every rank needs at least one client (use shard_range)")
+    td, rows = tree_util._client_rows(trees)
+    sizes = [x.numel() for x in rows[0]]
+    flat = torch.empty(sum(sizes), dtype=torch.float32, device=rows[0][0].device)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    views = [flat[o:o + n].view(x.shape) for o, n, x in zip(offs[:-1], sizes, rows[0])]
+    if any(x.dtype != torch.float32 for x in rows[0]):
+        raise TypeError("sharded_tree_mean needs float32 leaves")
+    tree_util._fold(rows, weights, scale=tree_util._inverse(W_total), out=views, accumulate=False)
+    if all_ranks:
+        dist.all_reduce(flat, group=group)
+    else:
+        dist.reduce(flat, dst=dst, group=group)
+    if all_ranks or dist.get_rank(group) == dst:
+        from fedjax_amd import pytree
+        return pytree.unflatten(td, views)
+    return None

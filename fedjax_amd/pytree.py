@@ -1,0 +1,162 @@
+"""Minimal pytree flattening with ``jax.tree_util``'s leaf order.
+
+The reference relies on ``jax.tree_util`` (a third-party dependency, SURVEY.md
+§8a row A11) to walk parameter trees. This module restates the part of it the
+aggregation path needs, over trees whose leaves are tensors / arrays / scalars:
+
+* ``dict``: children in **sorted key order** (jax sorts dict keys);
+* ``collections.OrderedDict`` / ``defaultdict``: insertion order / sorted order,
+  as jax registers them;
+* ``list``, ``tuple``, ``namedtuple``: positional;
+* ``None``: an empty subtree (no leaves);
+* classes registered with :func:`register_pytree_node` (``fedjax_amd.dataclass``
+  registers its data fields, fedjax/core/dataclasses.py:23-53);
+* anything else is a leaf.
+
+Structure mismatches raise ``ValueError`` (``jax.tree.map`` does too).
+"""
+
+from __future__ import annotations
+
+import collections
+from typing import Any, Callable, Dict, List, Tuple
+
+_REGISTRY: Dict[type, Tuple[Callable, Callable]] = {}
+
+
+def register_pytree_node(cls: type, flatten_fn: Callable, unflatten_fn: Callable) -> None:
+    """flatten_fn(x) -> (children, aux); unflatten_fn(aux, children) -> x."""
+    _REGISTRY[cls] = (flatten_fn, unflatten_fn)
+
+
+class TreeDef:
+    """Hashable structure of a pytree (node kind, aux data, children)."""
+
+    __slots__ = ("kind", "aux", "children", "num_leaves", "_hash")
+
+    def __init__(self, kind, aux, children):
+        self.kind = kind
+        self.aux = aux
+        self.children = children
+        self.num_leaves = 1 if kind == "leaf" else sum(c.num_leaves for c in children)
+        self._hash = None
+
+    def _key(self):
+        return (self.kind, self.aux, self.children)
+
+    def __eq__(self, other):
+        return isinstance(other, TreeDef) and (self is other or self._key() == other._key())
+
+    def __hash__(self):
+        if self._hash is None:
+            self._hash = hash(self._key())
+        return self._hash
+
+    def __repr__(self):
+        if self.kind == "leaf":
+            return "*"
+        return f"{self.kind}{'' if self.aux is None else self.aux!r}({', '.join(map(repr, self.children))})"
+
+
+_LEAF = TreeDef("leaf", None, ())
+_NONE = TreeDef("none", None, ())
+
+
+def _is_namedtuple(x) -> bool:
+    return isinstance(x, tuple) and hasattr(type(x), "_fields")
+
+
+def _node(tree) -> Tuple[str, Any, List[Any]]:
+    """(kind, aux, children) of one node, or ('leaf', None, []) for a leaf."""
+    t = type(tree)
+    if tree is None:
+        return "none", None, []
+    if t in _REGISTRY:
+        children, aux = _REGISTRY[t][0](tree)
+        return "custom", (t, aux), list(children)
+    if t is dict or t is collections.defaultdict:
+        keys = tuple(sorted(tree))
+        aux = keys if t is dict else (keys, tree.default_factory)
+        return ("dict" if t is dict else "defaultdict"), aux, [tree[k] for k in keys]
+    if t is collections.OrderedDict:
+        keys = tuple(tree)
+        return "odict", keys, [tree[k] for k in keys]
+    if t is list:
+        return "list", len(tree), list(tree)
+    if t is tuple:
+        return "tuple", len(tree), list(tree)
+    if _is_namedtuple(tree):
+        return "namedtuple", t, list(tree)
+    return "leaf", None, []
+
+
+def flatten(tree) -> Tuple[List[Any], TreeDef]:
+    leaves: List[Any] = []
+
+    def rec(x) -> TreeDef:
+        kind, aux, children = _node(x)
+        if kind == "leaf":
+            leaves.append(x)
+            return _LEAF
+        if kind == "none":
+            return _NONE
+        return TreeDef(kind, aux, tuple(rec(c) for c in children))
+
+    td = rec(tree)
+    return leaves, td
+
+
+def leaves_of(tree) -> List[Any]:
+    return flatten(tree)[0]
+
+
+def flatten_as(treedef: TreeDef, tree) -> List[Any]:
+    """Leaves of ``tree``, which must have structure ``treedef`` (ValueError if not)."""
+    leaves, td = flatten(tree)
+    if td != treedef:
+        raise ValueError(f"pytree structure mismatch: expected {treedef!r}, got {td!r}")
+    return leaves
+
+
+def unflatten(treedef: TreeDef, leaves) -> Any:
+    it = iter(leaves)
+
+    def rec(td: TreeDef):
+        k = td.kind
+        if k == "leaf":
+            return next(it)
+        if k == "none":
+            return None
+        vals = [rec(c) for c in td.children]
+        if k == "dict":
+            return dict(zip(td.aux, vals))
+        if k == "defaultdict":
+            d = collections.defaultdict(td.aux[1])
+            d.update(zip(td.aux[0], vals))
+            return d
+        if k == "odict":
+            return collections.OrderedDict(zip(td.aux, vals))
+        if k == "list":
+            return vals
+        if k == "tuple":
+            return tuple(vals)
+        if k == "namedtuple":
+            return td.aux(*vals)
+        if k == "custom":
+            cls, aux = td.aux
+            return _REGISTRY[cls][1](aux, vals)
+        raise AssertionError(k)
+
+    out = rec(treedef)
+    if next(it, _SENTINEL) is not _SENTINEL:
+        raise ValueError("too many leaves for treedef")
+    return out
+
+
+_SENTINEL = object()
+
+
+def tree_map(fn: Callable, tree, *rest) -> Any:
+    leaves, td = flatten(tree)
+    others = [flatten_as(td, r) for r in rest]
+    return unflatten(td, [fn(*xs) for xs in zip(leaves, *others)])

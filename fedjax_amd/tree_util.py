@@ -1,0 +1,350 @@
+"""``fedjax.tree_util`` for device-resident torch pytrees, computed by HIP kernels.
+
+Drop-in for google/fedjax 0.0.17 ``fedjax/core/tree_util.py`` (re-exported as
+``fedjax.tree_util``, fedjax/__init__.py:22). Same names, arguments, return
+structure and error behaviour; leaves are ``torch`` tensors on a ROCm device
+(host tensors, numpy arrays and Python scalars are copied to the device first —
+the host-resident deployment path).
+
+Every arithmetic op goes through ``libfjagg.so`` (``fedjax_amd.kernels``). There
+is no CPU / PyTorch fallback: without the library or a GPU these raise.
+
+Semantics follow the reference under JAX's defaults (x64 disabled):
+
+* the fold of :func:`tree_mean` is the reference's exact op sequence —
+  ``t_k = fl(x_k * f32(w_k))``, ``s_0 = t_0``, ``s_k = fl(s_{k-1} + t_k)``,
+  ``y = fl(s * f32(1/W))`` with ``W`` summed on the host exactly as
+  tree_util.py:86,95 does — so float32 results are bitwise equal to FedJAX's;
+* Python numbers are weakly typed (take the leaf's dtype), int64/float64 leaves
+  canonicalise to int32/float32, int32 leaves with Python-int weights fold in
+  wrapping int32 and become float32 only at the final ``1/W`` scale;
+* bfloat16 leaves are folded in float32 and rounded once (the reference rounds
+  every op to bfloat16; DESIGN.md §4 states the bound against an f64 oracle).
+"""
+
+from __future__ import annotations
+
+import numbers
+from typing import Any, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from fedjax_amd import _lib, kernels, pytree
+from fedjax_amd.typing import PyTree
+
+__all__ = [
+    "tree_weight", "tree_inverse_weight", "tree_zeros_like", "tree_add", "tree_sum",
+    "tree_mean", "tree_size", "tree_l2_squared", "tree_l2_norm", "tree_clip_by_global_norm",
+    "tree_l2_norms",
+]
+
+# Non-temporal loads pay off once the deltas cannot stay in the 256 MiB Infinity
+# Cache between rounds (profiles/r01_probe.txt: +10 % at 17 GB, -7 % at 0.6 GB).
+NONTEMPORAL_MIN_BYTES = 1 << 30
+
+_CANONICAL = {
+    torch.float32: torch.float32, torch.bfloat16: torch.bfloat16, torch.int32: torch.int32,
+    torch.int64: torch.int32, torch.float64: torch.float32,
+}
+
+
+# --------------------------------------------------------------------------- leaves
+def _default_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise _lib.FjaggError("fedjax_amd aggregates on a ROCm GPU; torch.cuda.is_available() is False")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _find_device(leaves: Iterable[Any]) -> torch.device:
+    for x in leaves:
+        if isinstance(x, torch.Tensor) and x.is_cuda:
+            return x.device
+    return _default_device()
+
+
+def _to_tensor(x) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x
+    if isinstance(x, (bool, np.bool_)):
+        raise TypeError("boolean leaves are not supported")
+    if isinstance(x, numbers.Integral) and not isinstance(x, np.generic):
+        return torch.tensor(x, dtype=torch.int32)
+    if isinstance(x, numbers.Real) and not isinstance(x, np.generic):
+        return torch.tensor(x, dtype=torch.float32)
+    a = np.asarray(x)
+    if not a.flags.writeable or not a.flags.c_contiguous:
+        a = np.ascontiguousarray(a).copy()
+    return torch.from_numpy(a)
+
+
+def _device_leaf(x, device: torch.device) -> torch.Tensor:
+    """Leaf as a contiguous device tensor of a canonical dtype (jnp.asarray rules)."""
+    t = _to_tensor(x)
+    dt = _CANONICAL.get(t.dtype)
+    if dt is None:
+        raise TypeError(f"leaf dtype {t.dtype} is not supported (float32, bfloat16, int32; "
+                        "int64/float64 canonicalise to 32 bits)")
+    if t.device != device:
+        t = t.to(device, non_blocking=t.is_pinned())
+    if t.dtype != dt:
+        t = t.to(dt)
+    if not t.is_contiguous():
+        t = t.contiguous()
+    return t
+
+
+# -------------------------------------------------------------------------- weights
+_WEAK_INT, _WEAK_FLOAT, _STRONG_INT, _STRONG_FLOAT = range(4)
+
+
+def _host_weight(w):
+    """A weight as the host value the reference would compute with: Python numbers
+    stay Python numbers (weakly typed); arrays/tensors become numpy scalars."""
+    if isinstance(w, torch.Tensor):
+        if w.numel() != 1:
+            raise ValueError("weights must be scalars")
+        a = w.detach().reshape(()).cpu().numpy()
+        return a[()]
+    if isinstance(w, np.ndarray):
+        if w.size != 1:
+            raise ValueError("weights must be scalars")
+        return w.reshape(())[()]
+    return w
+
+
+def _weight_kind(w) -> int:
+    if isinstance(w, np.generic):
+        if isinstance(w, np.bool_):
+            return _STRONG_INT
+        return _STRONG_INT if isinstance(w, np.integer) else _STRONG_FLOAT
+    if isinstance(w, numbers.Integral):  # includes bool
+        return _WEAK_INT
+    if isinstance(w, numbers.Real):
+        return _WEAK_FLOAT
+    raise TypeError(f"weight {w!r} is not a real scalar")
+
+
+def _inverse(W):
+    """tree_util.py:37,60: ``(1. / weight) if weight > 0. else 0.`` on the host."""
+    return (1.0 / W) if W > 0.0 else 0.0
+
+
+# ----------------------------------------------------------------------- fold engine
+def _leaf_rule(dt: torch.dtype, kinds: Sequence[int], scaled_kind: Optional[int]):
+    """(in_code, acc_code, out_dtype) of one leaf position under JAX promotion."""
+    strong_float = any(k == _STRONG_FLOAT for k in kinds) or scaled_kind == _STRONG_FLOAT
+    if dt == torch.float32:
+        return _lib.F32, _lib.F32, torch.float32
+    if dt == torch.bfloat16:
+        return _lib.BF16, _lib.F32, (torch.float32 if strong_float else torch.bfloat16)
+    # int32 leaves: int * int folds in int32; int * float promotes to float32
+    if all(k in (_WEAK_INT, _STRONG_INT) for k in kinds):
+        return _lib.I32, _lib.I32, (torch.int32 if scaled_kind is None else torch.float32)
+    return _lib.I32, _lib.F32, torch.float32
+
+
+def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
+          out: Optional[List[torch.Tensor]] = None, accumulate: bool = False,
+          nontemporal: Optional[bool] = None) -> List[torch.Tensor]:
+    """y_l = [out_l +] sum_k fl(rows[k][l] * w_k) [* scale] for every leaf l, one
+    kernel launch per (input, fold, output) dtype group. ``out`` gives the
+    destination tensors (fresh ones otherwise); ``accumulate`` folds into them."""
+    if accumulate and out is None:
+        raise ValueError("accumulate needs out")
+    K, L = len(rows), len(rows[0])
+    kinds = [_weight_kind(w) for w in weights]
+    scaled_kind = None if scale is None else _weight_kind(scale)
+    device = rows[0][0].device if L else None
+    outs: List[Optional[torch.Tensor]] = [None] * L
+    groups = {}
+    for l in range(L):
+        x0 = rows[0][l]
+        for k in range(1, K):
+            xk = rows[k][l]
+            if xk.shape != x0.shape:
+                raise ValueError(f"leaf {l}: client {k} has shape {tuple(xk.shape)}, "
+                                 f"client 0 has {tuple(x0.shape)}")
+            if xk.dtype != x0.dtype:
+                raise TypeError(f"leaf {l}: client {k} has dtype {xk.dtype}, client 0 has {x0.dtype}")
+            if xk.device != device:
+                raise ValueError(f"leaf {l}: client {k} is on {xk.device}, expected {device}")
+        in_c, acc_c, out_dt = _leaf_rule(x0.dtype, kinds, scaled_kind)
+        if out is not None:
+            o = out[l]
+            if o.dtype != out_dt or o.shape != x0.shape or not o.is_contiguous() or o.device != device:
+                raise ValueError(f"leaf {l}: destination must be a contiguous {out_dt} tensor "
+                                 f"of shape {tuple(x0.shape)} on {device}")
+        else:
+            o = torch.empty(x0.shape, dtype=out_dt, device=device)
+        outs[l] = o
+        groups.setdefault((in_c, acc_c, kernels.dtype_code(out_dt)), []).append(l)
+
+    for (in_c, acc_c, out_c), ls in groups.items():
+        leaf_n = np.array([rows[0][l].numel() for l in ls], dtype=np.int64)
+        if not leaf_n.any():
+            continue
+        in_ptrs = np.array([[rows[k][l].data_ptr() for l in ls] for k in range(K)], dtype=np.int64)
+        out_ptrs = np.array([outs[l].data_ptr() for l in ls], dtype=np.int64)
+        unaligned = bool((in_ptrs % 16).any() or (out_ptrs % 16).any())
+        blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)
+        if acc_c == _lib.F32:
+            w_host = np.array([np.float32(w) for w in weights], dtype=np.float32)
+        else:
+            w_host = np.array([np.int64(w) for w in weights], dtype=np.int64).astype(np.int32)
+        w_words = np.zeros((K + 1) // 2, dtype=np.int64)
+        w_words.view(np.uint8)[: 4 * K] = w_host.view(np.uint8)
+        image = np.concatenate([in_ptrs.ravel(), out_ptrs, leaf_n, blocks, w_words])
+        image_dev = torch.from_numpy(image).pin_memory().to(device, non_blocking=True)
+        w_dev_ptr = image_dev.data_ptr() + 8 * (image.size - w_words.size)
+        total_bytes = int(leaf_n.sum()) * K * (2 if in_c == _lib.BF16 else 4)
+        nt = (total_bytes >= NONTEMPORAL_MIN_BYTES) if nontemporal is None else nontemporal
+        flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
+        flags |= (_lib.UNALIGNED if unaligned else 0) | (_lib.NONTEMPORAL if nt else 0)
+        _lib.call("fjagg_wsum_ptrs", in_c, acc_c, out_c, image_dev.data_ptr(), len(ls), K,
+                  len(blocks), w_dev_ptr, float(np.float32(scale) if scale is not None else 1.0),
+                  flags, torch.cuda.current_stream(device).cuda_stream)
+    return outs
+
+
+def _client_rows(trees: Sequence[PyTree]) -> Tuple[pytree.TreeDef, List[List[torch.Tensor]]]:
+    leaves0, td = pytree.flatten(trees[0])
+    device = _find_device(leaves0)
+    rows = [[_device_leaf(x, device) for x in leaves0]]
+    for t in trees[1:]:
+        rows.append([_device_leaf(x, device) for x in pytree.flatten_as(td, t)])
+    return td, rows
+
+
+# ------------------------------------------------------------------------ public API
+def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
+    """Weights tree leaves by weight (tree_util.py:29-32)."""
+    td, rows = _client_rows([pytree_])
+    if not rows[0]:
+        return pytree.unflatten(td, [])
+    return pytree.unflatten(td, _fold(rows, [_host_weight(weight)]))
+
+
+def tree_inverse_weight(pytree_: PyTree, weight: float) -> PyTree:
+    """Weights tree leaves by ``1 / weight`` (tree_util.py:35-38)."""
+    return tree_weight(pytree_, _inverse(_host_weight(weight)))
+
+
+def tree_zeros_like(pytree_: PyTree) -> PyTree:
+    """Creates a tree with zeros with same structure as the input (tree_util.py:41-44)."""
+    leaves, td = pytree.flatten(pytree_)
+    device = _find_device(leaves)
+    out = []
+    for x in leaves:
+        t = _to_tensor(x)
+        dt = _CANONICAL.get(t.dtype)
+        if dt is None:
+            raise TypeError(f"leaf dtype {t.dtype} is not supported")
+        out.append(torch.zeros(t.shape, dtype=dt, device=device))
+    return pytree.unflatten(td, out)
+
+
+def tree_add(left: PyTree, right: PyTree) -> PyTree:
+    """Adds two trees together (tree_util.py:47-50): x*1 is exact, so a K=2 fold
+    with unit weights is the reference's ``jnp.add``."""
+    td, rows = _client_rows([left, right])
+    if not rows[0]:
+        return pytree.unflatten(td, [])
+    return pytree.unflatten(td, _fold(rows, [1, 1]))
+
+
+def tree_sum(pytrees: Iterable[PyTree]) -> PyTree:
+    """Sums multiple trees together (tree_util.py:64-73); ``None`` if empty."""
+    trees = list(pytrees)
+    if not trees:
+        return None
+    td, rows = _client_rows(trees)
+    if not rows[0]:
+        return pytree.unflatten(td, [])
+    return pytree.unflatten(td, _fold(rows, [1] * len(trees)))
+
+
+def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
+    """Returns (weighted) mean of input trees and weights (tree_util.py:76-96).
+
+    All K clients are folded by ONE kernel launch per leaf-dtype group; the result
+    is bitwise equal to the reference's sequential jit fold for float32 leaves.
+    The iterable is consumed once (it may be a generator, compression.py:191).
+    """
+    trees, weights = [], []
+    sum_weight = 0.0
+    for tree, weight in pytrees_and_weights:
+        w = _host_weight(weight)
+        trees.append(tree)
+        weights.append(w)
+        sum_weight += w  # tree_util.py:95 (Python float; numpy scalars keep their type)
+    if not trees:
+        return None  # tree_util.py:96 maps over None
+    td, rows = _client_rows(trees)
+    if not rows[0]:
+        return pytree.unflatten(td, [])
+    inv = _inverse(sum_weight)
+    return pytree.unflatten(td, _fold(rows, weights, scale=inv))
+
+
+def tree_size(pytree_: PyTree) -> int:
+    """Returns total size of all tree leaves (tree_util.py:99-102)."""
+    return int(sum(_to_tensor(x).numel() for x in pytree.leaves_of(pytree_)))
+
+
+def _l2_rows(rows: List[List[torch.Tensor]], take_sqrt: bool) -> torch.Tensor:
+    K, L = len(rows), len(rows[0])
+    device = rows[0][0].device
+    out = torch.empty(K, dtype=torch.float32, device=device)
+    for row in rows:
+        for x in row:
+            if x.dtype not in (torch.float32, torch.bfloat16):
+                raise TypeError(f"l2 norms support float32/bfloat16 leaves, not {x.dtype}")
+    if any(x.dtype != rows[0][0].dtype for row in rows for x in row):
+        raise TypeError("l2 norms need one leaf dtype across the tree")
+    ptrs = np.array([x.data_ptr() for row in rows for x in row], dtype=np.int64)
+    ns = np.array([x.numel() for row in rows for x in row], dtype=np.int64)
+    image_dev = torch.from_numpy(np.concatenate([ptrs, ns])).pin_memory().to(device, non_blocking=True)
+    max_n = int(ns.max()) if ns.size else 0
+    need = int(_lib.load().fjagg_l2sq_rows_workspace_bytes(K * L, max_n))
+    ws = torch.empty(max(need, 4), dtype=torch.uint8, device=device)
+    _lib.call("fjagg_l2sq_rows", kernels.dtype_code(rows[0][0].dtype), image_dev.data_ptr(), K * L,
+              max_n, L, 1 if take_sqrt else 0, out.data_ptr(), ws.data_ptr(), ws.numel(),
+              torch.cuda.current_stream(device).cuda_stream)
+    return out
+
+
+def tree_l2_squared(pytree_: PyTree) -> torch.Tensor:
+    """Returns squared l2 norm of tree (tree_util.py:105-108), a 0-d float32 tensor."""
+    _, rows = _client_rows([pytree_])
+    if not rows[0]:
+        return torch.zeros((), dtype=torch.float32, device=_default_device())
+    return _l2_rows(rows, take_sqrt=False).reshape(())
+
+
+def tree_l2_norm(pytree_: PyTree) -> torch.Tensor:
+    """Returns l2 norm of tree (tree_util.py:111-114), a 0-d float32 tensor."""
+    _, rows = _client_rows([pytree_])
+    if not rows[0]:
+        return torch.zeros((), dtype=torch.float32, device=_default_device())
+    return _l2_rows(rows, take_sqrt=True).reshape(())
+
+
+def tree_l2_norms(pytrees: Sequence[PyTree]) -> torch.Tensor:
+    """l2 norm of each of K trees in ONE launch (float32[K]) — the per-client
+    ``delta_l2_norm`` diagnostic of examples/fed_avg.py:79-81 batched."""
+    trees = list(pytrees)
+    _, rows = _client_rows(trees)
+    return _l2_rows(rows, take_sqrt=True)
+
+
+def tree_clip_by_global_norm(pytree_: PyTree, max_norm: float) -> PyTree:
+    """Clips a pytree of arrays using their global norm (tree_util.py:117-133).
+
+    ``scale = min(1, max_norm / norm)`` is formed in float32 as the reference does;
+    it is read back to the host to parameterise the weighting launch.
+    """
+    norm = np.float32(tree_l2_norm(pytree_).item())
+    with np.errstate(divide="ignore", invalid="ignore"):
+        scale = np.minimum(np.float32(1), np.float32(max_norm) / norm)
+    return tree_weight(pytree_, np.float32(scale))

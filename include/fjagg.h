@@ -87,7 +87,8 @@ int fjagg_abi_version(void);
  * Dense client-major slab: client k's delta is x_dev + k*ld elements, P
  * contiguous elements each. acc_dtype is FJAGG_F32 (w_dev is float[K]) or
  * FJAGG_I32 (integer fold, w_dev is int32[K]). Supported (in, acc, out):
- *   (F32,F32,F32) (BF16,F32,BF16) (BF16,F32,F32) (I32,F32,F32) (I32,I32,I32) (I32,I32,F32)
+ *   (F32,F32,F32) (F32,F32,BF16) (BF16,F32,BF16) (BF16,F32,F32) (I32,F32,F32) (I32,I32,I32)
+ *   (I32,I32,F32); the pytree path supports the same set except (F32,F32,BF16).
  * mode FJAGG_MODE_SPLIT needs ws_dev of fjagg_split_workspace_bytes(K, P) bytes
  * (ws may be NULL in exact mode).
  * Replaces: the per-client loop of tree_mean, fedjax/core/tree_util.py:85-96.
@@ -131,6 +132,18 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
 int64_t fjagg_l2sq_workspace_bytes(int64_t K, int64_t P);
 int fjagg_l2sq_dense(int in_dtype, const void* x_dev, int64_t ld, int64_t K, int64_t P,
                      float* out_dev, void* ws_dev, int64_t ws_bytes, void* stream);
+
+/*
+ * Pytree form of the squared norm: R rows at arbitrary device addresses, the
+ * image is int64 [ptrs[R] | n[R]]; rows are grouped in consecutive runs of
+ * rows_per_group (one client's leaves), out_dev[g] = sum of the group's squares
+ * (sqrt of it when take_sqrt != 0: tree_l2_norm, tree_util.py:111-114). Each row
+ * is summed in 64 Ki-element blocks and the partials are added in row/block order.
+ */
+int64_t fjagg_l2sq_rows_workspace_bytes(int64_t R, int64_t max_n);
+int fjagg_l2sq_rows(int in_dtype, const int64_t* image_dev, int64_t R, int64_t max_n,
+                    int64_t rows_per_group, int take_sqrt, float* out_dev, void* ws_dev,
+                    int64_t ws_bytes, void* stream);
 
 /*
  * Synthetic client deltas for tests and benchmarks (never on the product path):

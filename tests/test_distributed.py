@@ -1,0 +1,78 @@
+"""Client-sharded aggregation over world_size 2 with the gloo backend (CPU).
+
+The per-rank fold is injected (``partial_fn``) with the oracle restatement so
+the sharding, bucketing, W handling and reduce/all_reduce logic of
+fedjax_amd.distributed run without a GPU; the GPU test runs the same function
+with the HIP kernel.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import tree_util_ref as ref
+
+K, P = 24, 5000
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _oracle_partial(x, w, scale, out):
+    y = ref.wsum_dense(x.numpy(), w.numpy(), scale=np.float32(scale))
+    out.copy_(torch.from_numpy(y))
+
+
+def _worker(rank, world, port, all_ranks, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fedjax_amd import distributed as fd
+        weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
+        W = 0.0
+        for w in weights:
+            W += w
+        k0, k1 = fd.shard_range(K, rank, world)
+        x = torch.from_numpy(ref.synth(k1 - k0, P, seed=9, k0=k0))
+        wl = torch.tensor(np.float32(weights[k0:k1]))
+        out = fd.sharded_weighted_mean(x, wl, W, buckets=3, all_ranks=all_ranks, partial_fn=_oracle_partial)
+        W2 = fd.total_weight(weights[k0:k1])
+        q.put((rank, out.numpy().copy(), W2))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("all_ranks", [False, True])
+def test_sharded_mean_world2_gloo(all_ranks, coracle):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, all_ranks, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (y, W2)) for r, y, W2 in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
+    x = ref.synth(K, P, seed=9)
+    r = ref.mean_scale(weights)
+    want = ref.wsum_dense(x, np.float32(weights), scale=r)
+    bound = coracle.bound_f32(x, np.float32(weights), r, want)
+    G = 2
+    # sequential-sum bound with G extra roundings
+    bound = bound * (K + G + 2) / (K + 2)
+    for rank in ([0, 1] if all_ranks else [0]):
+        y = res[rank][0]
+        assert np.all(np.abs(y.astype(np.float64) - want) <= bound), rank
+        assert res[rank][1] == float(sum(weights))

@@ -1,0 +1,105 @@
+"""Host logic of the product path that needs no GPU: weight semantics, dtype
+rules, block planning, sharding and bucketing."""
+import numpy as np
+import pytest
+import torch
+
+from fedjax_amd import _lib, distributed, kernels, tree_util as tu
+from oracle import tree_util_ref as ref
+
+
+def test_total_weight_follows_reference_types():
+    # Python numbers: f64 accumulation (tree_util.py:86,95)
+    W = 0.0
+    for w in [1, 2.5, 3]:
+        W += tu._host_weight(w)
+    assert type(W) is float and W == 6.5
+    # float32 tensors/arrays: stays float32 (NEP 50 == jax weak typing)
+    W = 0.0
+    for w in [torch.tensor(0.1), np.float32(0.2)]:
+        W += tu._host_weight(w)
+    assert isinstance(W, np.float32)
+    assert tu._inverse(W) == np.float32(1) / W and isinstance(tu._inverse(W), np.float32)
+    assert tu._inverse(0.0) == 0.0 and tu._inverse(-3.0) == 0.0
+
+
+def test_inverse_matches_oracle_mean_scale():
+    for ws in ([3, 4, 5], [0.1, 0.7, 1e-3], [500] * 1024):
+        W = 0.0
+        for w in ws:
+            W += w
+        assert np.float32(tu._inverse(W)) == ref.mean_scale(ws)
+
+
+def test_weight_kinds_and_leaf_rules():
+    K = tu._weight_kind
+    assert [K(1), K(1.0), K(np.int32(1)), K(np.float32(1))] == [0, 1, 2, 3]
+    with pytest.raises(TypeError):
+        K("1")
+    R = tu._leaf_rule
+    assert R(torch.float32, [0, 1], None) == (_lib.F32, _lib.F32, torch.float32)
+    assert R(torch.bfloat16, [0, 1], 1) == (_lib.BF16, _lib.F32, torch.bfloat16)
+    assert R(torch.bfloat16, [3], 1) == (_lib.BF16, _lib.F32, torch.float32)  # bf16 * strong f32
+    assert R(torch.int32, [0, 2], None) == (_lib.I32, _lib.I32, torch.int32)  # tree_sum of ints
+    assert R(torch.int32, [0, 0], 1) == (_lib.I32, _lib.I32, torch.float32)  # tree_mean of ints
+    assert R(torch.int32, [1], None) == (_lib.I32, _lib.F32, torch.float32)  # int * 2.0
+
+
+def test_leaf_canonicalisation_rules():
+    assert tu._to_tensor(3).dtype == torch.int32
+    assert tu._to_tensor(2.5).dtype == torch.float32
+    assert tu._CANONICAL[torch.int64] == torch.int32 and tu._CANONICAL[torch.float64] == torch.float32
+    with pytest.raises(TypeError):
+        tu._to_tensor(True)
+
+
+def _decode(blocks):
+    return [((b >> 40) & 0x3FFFFF, bool((b >> 62) & 1), b & ((1 << 40) - 1)) for b in blocks.tolist()]
+
+
+@pytest.mark.parametrize("unaligned", [False, True])
+def test_ptrs_plan_covers_every_unit_once(unaligned):
+    leaf_n = [32, 288, 64, 18432, 128, 1179648, 62, 7936, 0, 3, 1]
+    V = 1 if unaligned else 4
+    per = 256 * 2
+    blocks = kernels.ptrs_plan(_lib.F32, leaf_n, unaligned)
+    seen = {l: [] for l in range(len(leaf_n))}
+    tails = set()
+    dec = _decode(blocks)
+    # tails come first (latency-bound blocks start early)
+    first_main = next((i for i, d in enumerate(dec) if not d[1]), len(dec))
+    assert all(d[1] for d in dec[:first_main]) and not any(d[1] for d in dec[first_main:])
+    for leaf, tail, u0 in dec:
+        if tail:
+            tails.add(leaf)
+        else:
+            seen[leaf].append(u0)
+    for l, n in enumerate(leaf_n):
+        nunits = n // V
+        assert sorted(seen[l]) == list(range(0, nunits, per))
+        assert (l in tails) == (n % V != 0)
+
+
+def test_ptrs_plan_bf16_units():
+    blocks = kernels.ptrs_plan(_lib.BF16, [17], False)
+    dec = _decode(blocks)
+    assert dec == [(0, True, 0), (0, False, 0)]  # 2 units of 8 + a 1-element tail
+
+
+def test_shard_range_partitions_clients():
+    for K in (1, 7, 1024, 1025):
+        for G in (1, 2, 3, 8):
+            ranges = [distributed.shard_range(K, g, G) for g in range(G)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == K
+            assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+            sizes = [b - a for a, b in ranges]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_bucket_edges_are_aligned_and_cover():
+    for P in (1, 1000, 1206590, 4194304):
+        for nb in (1, 4, 7):
+            e = distributed.bucket_edges(P, nb)
+            assert e[0][0] == 0 and e[-1][1] == P
+            assert all(a[1] == b[0] for a, b in zip(e, e[1:]))
+            assert all(p0 % distributed.BUCKET_ALIGN == 0 for p0, _ in e)
