@@ -1,0 +1,232 @@
+"""Benchmark of the aggregation hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2] [--e2e]
+
+One step = one weighted mean of the round's client deltas, already resident in
+HBM: host W and f32 weights (4 KiB pinned H2D) + the fold kernel, exactly what
+``ClientDeltaSlab.mean`` / ``sharded_weighted_mean`` do per round.
+
+* N = 1: BASELINE configs[2], 1024 clients x 4,194,304 fp32 params (17.2 GB) on
+  one MI355X — the configuration the north-star target is quoted on.
+* N > 1 (torchrun, one rank per GPU): the same 1024 clients sharded N ways
+  (configs[3]); each rank folds its 1024/N clients, already scaled by f32(1/W),
+  and the partials are summed by a bucketed RCCL reduce to rank 0 that overlaps
+  the next bucket's fold. Strong scaling: total work is fixed.
+
+value = K*P*4 bytes of client deltas / wall time of the K timed steps (max over
+ranks). roofline.achieved = the same algorithmic bytes per fold launch / the
+launch's mean duration from HIP events on the launch stream. cpu_baseline =
+the oracle's C restatement of the reference op sequence (oracle/fold_ref.c,
+``oracle_tree_mean_refseq_f32``) on a bounded sample, rank 0, N = 1 only.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "device-resident aggregated client-delta GB/s, K clients × P fp32 params"
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+WORKLOADS = {
+    "c3": (1024, 4 * 1024 * 1024, "configs[2]: mean aggregator, 1024 clients x 4 M-param (4,194,304) fp32 deltas"),
+    "c2": (128, 1206590, "configs[1]: mean aggregator, 128 clients x 1,206,590-param EMNIST-CNN fp32 deltas"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def fedavg_weights(K, seed=1):
+    return np.random.RandomState(seed).randint(1, 501, size=K).tolist()
+
+
+def cpu_baseline(K, seconds=8.0):
+    """Reference op sequence (per client: fresh w*x buffer, in-place add; final
+    scale) on the host, 1 thread and all usable cores, bounded sample."""
+    import ctypes
+
+    from tests import coracle as co
+
+    lib_path = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(lib_path):
+        import __graft_entry__
+        __graft_entry__.build()
+    o = co.load(lib_path)
+    Ps = 1 << 18  # sample: all K clients x 262,144 params (1 GiB for K = 1024)
+    x = o.synth_f32(K, Ps, seed=0)
+    w = np.float32(fedavg_weights(K))
+    r = np.float32(1.0 / float(sum(fedavg_weights(K))))
+    cores = min(16, len(os.sched_getaffinity(0)))
+    res = {}
+    for nt in sorted({1, cores}):
+        reps, t = 0, 0.0
+        while t < seconds / 2 or reps < 2:
+            t0 = time.perf_counter()
+            o.refseq_f32(x, w, r, nthreads=nt)
+            t += time.perf_counter() - t0
+            reps += 1
+        res[nt] = K * Ps * 4 * reps / t / 1e9
+    del ctypes
+    return {"value": round(res[cores], 2), "unit": "GB/s", "cores": cores, "kind": "port",
+            "single_thread_value": round(res[1], 2),
+            "sample": f"{K} clients x {Ps} params fp32 ({K * Ps * 4 / 2**30:.2f} GiB), reference op "
+                      f"sequence (tree_util.py:85-96) restated in C, oracle/fold_ref.c; "
+                      f"{os.uname().machine} host, {cores} of {len(os.sched_getaffinity(0))} visible cores"}
+
+
+def load_traffic(workload):
+    p = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--buckets", type=int, default=4)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--nontemporal", type=int, default=-1, help="-1 auto, 0 off, 1 on")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also time host-resident deltas (H2D + fold + D2H)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("launch N>1 with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    import fedjax_amd  # noqa: F401
+    from fedjax_amd import distributed as fd, kernels, tree_util as tu
+
+    K, P, desc = WORKLOADS[args.workload]
+    weights = fedavg_weights(K)
+    W = 0.0
+    for w in weights:
+        W += w  # tree_util.py:95
+    k0, k1 = fd.shard_range(K, rank, world)
+    Kl = k1 - k0
+    x = torch.empty(Kl, P, dtype=torch.float32, device=dev)
+    kernels.fill_synth(x, seed=0, k0=k0)  # the same global client k on every N
+    w_local = [weights[k] for k in range(k0, k1)]
+    out = torch.empty(P, dtype=torch.float32, device=dev)
+    nbytes_local = Kl * P * 4
+    nt = (nbytes_local >= tu.NONTEMPORAL_MIN_BYTES) if args.nontemporal < 0 else bool(args.nontemporal)
+    scale = float(np.float32(tu._inverse(W)))
+    stream = torch.cuda.current_stream(dev)
+    kernel_ms = []
+
+    def fold(xs, wd, o, events):
+        if events is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        kernels.weighted_sum_dense(xs, wd, scale=scale, out=o, nontemporal=nt, variant=args.variant)
+        if events is not None:
+            e1.record(stream)
+            events.append((e0, e1, xs.shape[0] * xs.shape[1] * 4))
+
+    def step(events=None):
+        wd = torch.from_numpy(np.float32(w_local)).pin_memory().to(dev, non_blocking=True)
+        if world == 1:
+            fold(x, wd, out, events)
+        else:
+            fd.sharded_weighted_mean(x, wd, W, buckets=args.buckets, out=out,
+                                     partial_fn=lambda xs, wdd, sc, o: fold(xs, wdd, o, events))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(events)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = [e0.elapsed_time(e1) for e0, e1, _ in events]
+    bytes_per_launch = float(np.mean([b for _, _, b in events]))
+    mean_kernel_s = float(np.mean(kernel_ms)) / 1e3
+    achieved = bytes_per_launch / mean_kernel_s / 1e9
+
+    e2e = None
+    if args.e2e and world == 1:
+        xh = torch.empty(K, P, dtype=torch.float32).pin_memory()
+        xh.copy_(x.cpu())
+        yh = torch.empty(P, dtype=torch.float32).pin_memory()
+        wd = torch.from_numpy(np.float32(w_local)).to(dev)
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(3):
+            x.copy_(xh, non_blocking=True)
+            kernels.weighted_sum_dense(x, wd, scale=scale, out=out, nontemporal=nt)
+            yh.copy_(out, non_blocking=True)
+        torch.cuda.synchronize()
+        e2e = K * P * 4 * 3 / (time.perf_counter() - ts) / 1e9
+        del xh
+
+    if rank == 0:
+        value = K * P * 4 * args.steps / elapsed / 1e9
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: counter-hash client deltas 0.01*u[-1,1), integer weights in [1,500]",
+            "config": {"workload": desc, "clients": K, "params": P, "clients_per_gpu": Kl,
+                       "parallelism": f"client-sharded x{world}" + (" + RCCL reduce" if world > 1 else ""),
+                       "buckets": args.buckets if world > 1 else 1, "nontemporal": nt,
+                       "variant": args.variant},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": load_traffic(args.workload),
+                         "kernel": "k_dense<f32> weighted fold", "bytes_per_launch": bytes_per_launch,
+                         "mean_launch_ms": round(mean_kernel_s * 1e3, 4)},
+        }
+        if e2e is not None:
+            res["e2e_host_resident_GBs"] = round(e2e, 2)
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(K)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,72 @@
+"""Client-sharded aggregation with the HIP kernel on the GPU, world_size 2.
+
+Both ranks share the box's single GPU, so the exchange uses gloo (RCCL refuses
+two ranks on one device); the RCCL path itself runs in bench.py --gpus N.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import tree_util_ref as ref
+
+pytestmark = pytest.mark.gpu
+K, P = 48, 70001
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import fedjax_amd
+        from fedjax_amd import distributed as fd, kernels
+        dev = torch.device("cuda:0")
+        weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
+        W = 0.0
+        for w in weights:
+            W += w
+        k0, k1 = fd.shard_range(K, rank, world)
+        x = torch.empty(k1 - k0, P, dtype=torch.float32, device=dev)
+        kernels.fill_synth(x, seed=9, k0=k0)
+        wl = torch.tensor(np.float32(weights[k0:k1]), device=dev)
+        y = fd.sharded_weighted_mean(x, wl, W, buckets=3, all_ranks=True)
+        trees = [({"a": x[i, :1000], "b": x[i, 1000:]}, weights[k0 + i]) for i in range(k1 - k0)]
+        m = fd.sharded_tree_mean(trees, all_ranks=True)
+        torch.cuda.synchronize()
+        q.put((rank, y.cpu().numpy(), torch.cat([m["a"], m["b"]]).cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_mean_world2_on_gpu(cuda, coracle):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (y, m) for r, y, m in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
+    x = coracle.synth_f32(K, P, seed=9)
+    r = ref.mean_scale(weights)
+    want = coracle.wsum_f32(x, np.float32(weights), scale=r)
+    bound = coracle.bound_f32(x, np.float32(weights), r, want) * (K + 4) / (K + 2)
+    for rank in (0, 1):
+        for got in res[rank]:
+            assert np.all(np.abs(got.astype(np.float64) - want) <= bound)

@@ -1,0 +1,314 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Bar: float32 / int32 exact mode bitwise equal to the reference
+restatement; split mode and multi-rank within the sequential-summation bound
+|y - y_ref| <= (K + G + 2) * 2^-24 * |r| * sum_k |fl(x_k w_k)| + 2^-24 |y_ref|;
+bfloat16 within one bf16 rounding of the f64 oracle plus that bound.
+"""
+import numpy as np
+import numpy.testing as npt
+import pytest
+import torch
+
+import fedjax_amd
+from fedjax_amd import _lib, kernels, tree_util as tu
+from oracle import tree_util_ref as ref
+from tests import fedavg_restated as fr
+from tests import golden_cases as gc
+from tests.coracle import bf16_to_f32
+
+pytestmark = pytest.mark.gpu
+U = 2.0 ** -24
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32 if a.dtype.itemsize == 4 else np.uint16)
+
+
+def host(t):
+    t = t.detach().cpu()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16)
+    return t.numpy()
+
+
+# ------------------------------------------------------------------ golden fixtures
+@pytest.mark.parametrize("name", gc.NAMES)
+def test_golden_fixture_on_gpu(name, cuda, coracle):
+    c = gc.load(name)
+    x, shapes = c["x"], c["shapes"]
+    if name.startswith("bf16"):
+        xt = torch.from_numpy(x.view(np.int16)).view(torch.bfloat16).to(cuda)
+    else:
+        xt = torch.from_numpy(x).to(cuda)
+    trees = [gc.split_leaves(xt[k], shapes) for k in range(x.shape[0])]
+    m = tu.tree_mean(zip(trees, c["weight_list"]))
+    got = np.concatenate([host(v).ravel() for v in m])
+    if name.startswith("bf16"):
+        y = bf16_to_f32(got).astype(np.float64)
+        y64 = c["y_f64"]
+        w = np.float32(c["weight_list"])
+        r = np.float32(1.0 / sum(c["weight_list"]))
+        xf = bf16_to_f32(x)
+        tsum = np.abs(xf.astype(np.float64) * w[:, None]).sum(0)
+        tol = 2.0 ** -8 * np.abs(y64) + (x.shape[0] + 3) * U * r * tsum
+        assert np.all(np.abs(y - y64) <= tol)
+        # and far closer than the reference's own bf16 arithmetic
+        err_ref = np.abs(bf16_to_f32(c["y_refsem"]) - y64).max()
+        assert np.abs(y - y64).max() <= err_ref
+    else:
+        assert np.array_equal(bits(got), bits(c["y"])), name
+
+
+# ------------------------------------------------------------- reference KATs on GPU
+def test_mean_aggregator_kat(cuda):
+    # fedjax/aggregators/aggregator_test.py:24-37
+    d = [("a", {"w": torch.tensor([1., 2., 3.], device=cuda)}, 2.),
+         ("b", {"w": torch.tensor([2., 4., 6.], device=cuda)}, 4.),
+         ("c", {"w": torch.tensor([1., 3., 5.], device=cuda)}, 2.)]
+    agg = fedjax_amd.aggregators.mean_aggregator()
+    state = agg.init()
+    mean, new_state = agg.apply(d, state)
+    npt.assert_array_equal(host(mean["w"]), [1.5, 3.25, 5.])
+    assert new_state is state
+
+
+def test_aggregator_consumes_generator_once(cuda):
+    gen = ((str(k), {"w": torch.full((5,), float(k), device=cuda)}, 1) for k in range(4))
+    mean, _ = fedjax_amd.aggregators.mean_aggregator().apply(gen, None)
+    npt.assert_array_equal(host(mean["w"]), np.full(5, 1.5, np.float32))
+
+
+def test_tree_weight_sum_mean_kats(cuda):
+    # fedjax/core/tree_util_test.py:27-62
+    p1 = {"x": torch.tensor([[[4, 5]], [[1, 1]]], device=cuda), "y": torch.tensor([[3], [1]], device=cuda)}
+    p2 = {"x": torch.tensor([[[2, 3]], [[4, 5]]], device=cuda), "y": torch.tensor([[6], [7]], device=cuda)}
+    w = tu.tree_weight(p1, 2.0)
+    npt.assert_array_equal(host(w["x"]), [[[8.0, 10.0]], [[2.0, 2.0]]])
+    npt.assert_array_equal(host(w["y"]), [[6.0], [2.0]])
+    assert w["x"].dtype == torch.float32
+    before = [t.clone() for t in (p1["x"], p1["y"], p2["x"], p2["y"])]
+    s = tu.tree_sum([p1, p2])
+    npt.assert_array_equal(host(s["x"]), [[[6, 8]], [[5, 6]]])
+    npt.assert_array_equal(host(s["y"]), [[9], [8]])
+    assert s["x"].dtype == torch.int32
+    for a, b in zip(before, (p1["x"], p1["y"], p2["x"], p2["y"])):
+        assert torch.equal(a, b)  # inputs are never written (tree_util_test.py:50-51)
+    trees = [(torch.tensor(0, device=cuda), torch.tensor(1, device=cuda)),
+             (torch.tensor(2, device=cuda), torch.tensor(3, device=cuda)),
+             (torch.tensor(4, device=cuda), torch.tensor(5, device=cuda))]
+    m = tu.tree_mean(zip(trees, [6., 7., 8.]))
+    npt.assert_array_almost_equal([host(v) for v in m], (2.1904761904761907, 3.1904761904761907))
+    assert tu.tree_mean([]) is None and tu.tree_sum([]) is None
+    assert tu.tree_size(p1) == 6
+
+
+def test_tree_clip_and_norm_kats(cuda):
+    # fedjax/core/tree_util_test.py:64-73
+    p = {"x": torch.tensor([[[4., 5.]], [[1., 1.]]], device=cuda), "y": torch.tensor([[3.], [1.]], device=cuda)}
+    npt.assert_allclose(host(tu.tree_l2_norm(p)), 7.28011, rtol=1e-6)
+    npt.assert_allclose(host(tu.tree_l2_squared(p)), 53.0, rtol=1e-7)
+    c = tu.tree_clip_by_global_norm(p, 3.640055)
+    npt.assert_array_almost_equal(host(c["x"]), [[[2, 2.5]], [[0.5, 0.5]]])
+    npt.assert_array_almost_equal(host(c["y"]), [[1.5], [0.5]])
+
+
+@pytest.mark.parametrize("name,round_fn,bs,epochs,want,want_norms", fr.KATS)
+def test_fedavg_round_kats_on_gpu(name, round_fn, bs, epochs, want, want_norms, cuda):
+    new, norms = round_fn(tu, lambda a: torch.from_numpy(np.asarray(a)).to(cuda), host,
+                          fr.SERVER_PARAMS, fr.CLIENTS, bs, epochs, 0)
+    npt.assert_allclose(new["w"], want, err_msg=name)
+    for cid, v in want_norms.items():
+        npt.assert_allclose(norms[cid], v, rtol=1e-6, err_msg=name)
+
+
+def test_host_resident_leaves_are_copied(cuda):
+    trees = [({"w": np.full(3, float(k), np.float32)}, 1) for k in range(3)]
+    m = tu.tree_mean(trees)
+    assert m["w"].is_cuda
+    npt.assert_array_equal(host(m["w"]), [1., 1., 1.])
+
+
+def test_tree_add_zeros_inverse(cuda):
+    a = {"p": torch.arange(10, dtype=torch.float32, device=cuda)}
+    z = tu.tree_zeros_like(a)
+    s = tu.tree_add(z, tu.tree_weight(a, 3))
+    s = tu.tree_inverse_weight(s, 3.0)
+    want = ref.tree_inverse_weight(ref.tree_add(np.zeros(10, np.float32), np.arange(10, dtype=np.float32) * 3), 3.0)
+    assert np.array_equal(bits(host(s["p"])), bits(want))
+
+
+def test_error_behaviour(cuda):
+    with pytest.raises(ValueError):
+        tu.tree_mean([({"a": torch.ones(3, device=cuda)}, 1), ({"b": torch.ones(3, device=cuda)}, 1)])
+    with pytest.raises(ValueError):
+        tu.tree_mean([({"a": torch.ones(3, device=cuda)}, 1), ({"a": torch.ones(4, device=cuda)}, 1)])
+    with pytest.raises(TypeError):
+        tu.tree_mean([({"a": torch.ones(3, dtype=torch.float16, device=cuda)}, 1)])
+    with pytest.raises(ValueError):
+        kernels.weighted_sum_dense(torch.ones(2, 8), torch.ones(2))
+
+
+# ------------------------------------------------------------------- dense kernel
+SHAPES = [(1, 1), (1, 5), (2, 4), (3, 7), (37, 10007), (130, 12291), (9, 2 ** 16 + 3), (1000, 333)]
+
+
+@pytest.mark.parametrize("K,P", SHAPES)
+def test_dense_all_variants_bitwise(K, P, cuda, coracle):
+    x = torch.empty(K, P, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(x, seed=K * 7 + P)
+    xh = coracle.synth_f32(K, P, seed=K * 7 + P)
+    assert np.array_equal(bits(host(x)), bits(xh))
+    wi = [int(v) for v in ref.fedavg_weights(K, seed=P)]
+    r = ref.mean_scale(wi)
+    want = coracle.wsum_f32(xh, np.float32(wi), scale=r)
+    w = torch.tensor(np.float32(wi), device=cuda)
+    for variant in range(7):
+        for nt in (False, True):
+            y = kernels.weighted_sum_dense(x, w, scale=float(r), variant=variant, nontemporal=nt)
+            assert np.array_equal(bits(host(y)), bits(want)), (variant, nt)
+
+
+def test_dense_accumulate_and_strided_rows(cuda, coracle):
+    K, P, ld = 17, 3001, 3072
+    base = torch.empty(K, ld, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(base, seed=1)
+    x = base[:, :P]
+    xh = coracle.synth_f32(K, ld, seed=1)[:, :P]
+    w = np.float32(ref.fedavg_weights(K, seed=2))
+    init = coracle.synth_f32(1, P, seed=3)[0]
+    out = torch.from_numpy(init.copy()).to(cuda)
+    kernels.weighted_sum_dense(x, torch.from_numpy(w).to(cuda), out=out, accumulate=True)
+    want = coracle.wsum_f32(xh, w, init=init)
+    assert np.array_equal(bits(host(out)), bits(want))
+
+
+def test_dense_unaligned_views_take_scalar_path(cuda, coracle):
+    K, P = 5, 1001
+    base = torch.empty(K, P + 1, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(base, seed=4)
+    x = base[:, 1:]  # 4-byte offset: not 16-byte aligned
+    xh = coracle.synth_f32(K, P + 1, seed=4)[:, 1:]
+    w = np.float32([1, 2, 3, 4, 5])
+    y = kernels.weighted_sum_dense(x, torch.from_numpy(w).to(cuda), scale=0.25)
+    assert np.array_equal(bits(host(y)), bits(coracle.wsum_f32(xh, w, scale=np.float32(0.25))))
+
+
+def test_int_fold_wraps_like_xla(cuda):
+    x = torch.tensor([[2 ** 30, -(2 ** 30), 7, 1], [2 ** 30, -(2 ** 30), 9, 1]], dtype=torch.int32, device=cuda)
+    w = torch.tensor([3, 2], dtype=torch.int32, device=cuda)
+    y = kernels.weighted_sum_dense(x, w)
+    assert y.dtype == torch.int32
+    npt.assert_array_equal(host(y), np.array([2 ** 30, -(2 ** 30), 39, 5], np.int32))
+
+
+def _bound(coracle, xh, w, r, want, G=1):
+    K = xh.shape[0]
+    return coracle.bound_f32(xh, w, r, want) * (K + G + 2) / (K + 2)
+
+
+@pytest.mark.parametrize("K,P", [(1024, 16384), (512, 1000), (64, 4097)])
+def test_split_mode_within_bound(K, P, cuda, coracle):
+    x = torch.empty(K, P, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(x, seed=5)
+    xh = coracle.synth_f32(K, P, seed=5)
+    wi = [int(v) for v in ref.fedavg_weights(K)]
+    r = ref.mean_scale(wi)
+    w = np.float32(wi)
+    want = coracle.wsum_f32(xh, w, scale=r)
+    y = host(kernels.weighted_sum_dense(x, torch.from_numpy(w).to(cuda), scale=float(r), mode="split"))
+    # at most 64 client ranges are combined (kSplitMax in fjagg.hip)
+    assert np.all(np.abs(y.astype(np.float64) - want) <= _bound(coracle, xh, w, r, want, G=64))
+
+
+def test_bf16_dense_vs_f64_oracle(cuda, coracle):
+    K, P = 64, 20000
+    x = torch.empty(K, P, dtype=torch.bfloat16, device=cuda)
+    kernels.fill_synth(x, seed=6)
+    xb = coracle.synth_bf16(K, P, seed=6)
+    assert np.array_equal(host(x), xb)
+    wi = ref.fedavg_weights(K)
+    r = 1.0 / wi.sum()
+    y64 = coracle.wsum_bf16_f64(xb, np.float64(wi), r)
+    w = torch.tensor(np.float32(wi), device=cuda)
+    yb = bf16_to_f32(host(kernels.weighted_sum_dense(x, w, scale=float(np.float32(r)))))
+    yf = host(kernels.weighted_sum_dense(x, w, scale=float(np.float32(r)), out_dtype=torch.float32))
+    tsum = np.abs(bf16_to_f32(xb).astype(np.float64) * np.float32(wi)[:, None]).sum(0)
+    fbound = (K + 3) * U * r * tsum + U * np.abs(y64)
+    assert np.all(np.abs(yf - y64) <= fbound)
+    assert np.all(np.abs(yb - y64) <= 2.0 ** -8 * np.abs(y64) + fbound)
+
+
+# ------------------------------------------------------------------- pytree kernel
+def test_pytree_unaligned_and_mixed_leaves(cuda, coracle):
+    K = 6
+    P = 4 * 1000 + 11
+    base = torch.empty(K, P, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(base, seed=8)
+    xh = coracle.synth_f32(K, P, seed=8)
+    cuts = [0, 1, 33, 1000, 3003, P]  # odd offsets: unaligned leaf views
+    trees = [{f"l{i}": base[k, cuts[i]:cuts[i + 1]] for i in range(len(cuts) - 1)} for k in range(K)]
+    wi = [3, 1, 4, 1, 5, 9]
+    m = tu.tree_mean(zip(trees, wi))
+    got = np.concatenate([host(m[f"l{i}"]) for i in range(len(cuts) - 1)])
+    want = coracle.wsum_f32(xh, np.float32(wi), scale=ref.mean_scale(wi))
+    assert np.array_equal(bits(got), bits(want))
+
+
+def test_slab_mean_equals_tree_mean_equals_oracle(cuda, coracle):
+    shapes = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "linear": {"b": (128,), "w": (100, 128)}}
+    template = pytree_map(lambda s: np.zeros(s, np.float32), shapes)
+    K = 20
+    slab = fedjax_amd.ClientDeltaSlab(template, K, device=cuda).fill_synthetic(seed=10)
+    P = slab.num_params
+    xh = coracle.synth_f32(K, P, seed=10)
+    wi = [int(v) for v in ref.fedavg_weights(K, seed=11)]
+    want = coracle.wsum_f32(xh, np.float32(wi), scale=ref.mean_scale(wi))
+    m1 = slab.mean(wi)
+    m2 = tu.tree_mean((slab.client(k), wi[k]) for k in range(K))
+    for m in (m1, m2):
+        flat = np.concatenate([host(v).ravel() for v in fedjax_amd.pytree.leaves_of(m)])
+        assert np.array_equal(bits(flat), bits(want))
+    norms = host(slab.l2_norms())
+    npt.assert_allclose(norms, np.sqrt((xh.astype(np.float64) ** 2).sum(1)), rtol=2e-6)
+    norms2 = host(tu.tree_l2_norms([slab.client(k) for k in range(K)]))
+    npt.assert_allclose(norms2, norms, rtol=2e-6)
+
+
+def pytree_map(fn, shapes):
+    if isinstance(shapes, dict):
+        return {k: pytree_map(fn, v) for k, v in shapes.items()}
+    return fn(shapes)
+
+
+# -------------------------------------------------------------- full-size properties
+def synth_cols(K, cols, seed, amp=0.01):
+    """oracle synth restricted to some columns (same hash)."""
+    k = (np.arange(K, dtype=np.uint64) << np.uint64(32))[:, None]
+    p = np.asarray(cols, np.uint64)[None, :]
+    h = ref._mix64(np.uint64(seed) ^ ref._mix64(k | p))
+    u = (h >> np.uint64(40)).astype(np.uint32).astype(np.float32) * np.float32(1 / 8388608) - np.float32(1)
+    return np.float32(amp) * u
+
+
+@pytest.mark.parametrize("K,P", [(128, 1206590), (1024, 4 * 1024 * 1024)])
+def test_full_size_configs(K, P, cuda):
+    """BASELINE configs 2 and 3 at full size: sampled columns bitwise vs the oracle,
+    weight-scaling invariance (2w gives the identical bits) over every element."""
+    x = torch.empty(K, P, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(x, seed=0)
+    wi = [int(v) for v in ref.fedavg_weights(K)]
+    r = ref.mean_scale(wi)
+    w = torch.tensor(np.float32(wi), device=cuda)
+    y = kernels.weighted_sum_dense(x, w, scale=float(r), nontemporal=True)
+    rs = np.random.RandomState(0)
+    cols = np.unique(np.concatenate([rs.randint(0, P, 2000), [0, 1, 2, 3, P - 4, P - 3, P - 2, P - 1]]))
+    xs = synth_cols(K, cols, 0)
+    want = ref.wsum_dense(xs, np.float32(wi), scale=r)
+    assert np.array_equal(bits(host(y)[cols]), bits(want))
+    wi2 = [2 * v for v in wi]
+    y2 = kernels.weighted_sum_dense(x, torch.tensor(np.float32(wi2), device=cuda), scale=float(ref.mean_scale(wi2)))
+    assert torch.equal(y.view(torch.int32), y2.view(torch.int32))
+    del x
+    torch.cuda.empty_cache()
