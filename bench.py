@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--nontemporal", type=int, default=-1, help="-1 auto, 0 off, 1 on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time host-resident deltas (H2D + fold + D2H)")
+    ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--all-ranks", action="store_true", help="all_reduce instead of reduce to rank 0")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,10 +115,13 @@ def main():
     if args.gpus != world:
         if world == 1 and args.gpus > 1:
             raise SystemExit("launch N>1 with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(args.backend, rank=rank, world_size=world)
 
     import fedjax_amd  # noqa: F401
     from fedjax_amd import distributed as fd, kernels, tree_util as tu
@@ -152,7 +157,7 @@ def main():
         if world == 1:
             fold(x, wd, out, events)
         else:
-            fd.sharded_weighted_mean(x, wd, W, buckets=args.buckets, out=out,
+            fd.sharded_weighted_mean(x, wd, W, buckets=args.buckets, out=out, all_ranks=args.all_ranks,
                                      partial_fn=lambda xs, wdd, sc, o: fold(xs, wdd, o, events))
 
     for _ in range(args.warmup):
@@ -211,7 +216,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic: counter-hash client deltas 0.01*u[-1,1), integer weights in [1,500]",
             "config": {"workload": desc, "clients": K, "params": P, "clients_per_gpu": Kl,
-                       "parallelism": f"client-sharded x{world}" + (" + RCCL reduce" if world > 1 else ""),
+                       "parallelism": f"client-sharded x{world}" + (
+                           f" + {'RCCL' if args.backend == 'nccl' else args.backend} "
+                           f"{'all_reduce' if args.all_ranks else 'reduce'}" if world > 1 else ""),
                        "buckets": args.buckets if world > 1 else 1, "nontemporal": nt,
                        "variant": args.variant},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",

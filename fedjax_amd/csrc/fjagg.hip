@@ -530,8 +530,17 @@ void launch_dense_t(const DenseArgs& a, dim3 grid, hipStream_t s) {
 struct VariantShape {
   int E, U;
 };
-constexpr VariantShape kVariants[] = {{2, 8}, {1, 8}, {1, 16}, {2, 16}, {4, 4}, {4, 8}, {1, 32}};
+// Index 0 is "auto" (resolved by pick_variant); 1.. are explicit shapes for tuning.
+constexpr VariantShape kVariants[] = {{0, 0}, {2, 8}, {1, 8}, {1, 16}, {2, 16}, {4, 4}, {4, 8}, {1, 32}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+// E=2 x U=8 (32 B per lane per client, 8 clients in flight) measured fastest on
+// the 1024 x 4M slab (profiles/r01_probe.txt); when the parameter axis gives
+// fewer than ~4 workgroups per CU at E=2, halve E to double the workgroups.
+int pick_variant(int64_t nunits) {
+  const int64_t nblk_e2 = (nunits + kThreads * 2 - 1) / (kThreads * 2);
+  return nblk_e2 >= 1024 ? 1 : 2;
+}
 
 template <int IN, class ACC, int OUT, int V, bool NT>
 int launch_dense_v(int variant, const DenseArgs& a, int64_t nblk_units, int64_t gy,
@@ -539,13 +548,13 @@ int launch_dense_v(int variant, const DenseArgs& a, int64_t nblk_units, int64_t 
   const int E = kVariants[variant].E;
   dim3 grid((unsigned)(nblk_units + (a.tail_n > 0 ? 1 : 0)), (unsigned)gy);
   switch (variant) {
-    case 0: launch_dense_t<IN, ACC, OUT, V, 2, 8, NT>(a, grid, s); break;
-    case 1: launch_dense_t<IN, ACC, OUT, V, 1, 8, NT>(a, grid, s); break;
-    case 2: launch_dense_t<IN, ACC, OUT, V, 1, 16, NT>(a, grid, s); break;
-    case 3: launch_dense_t<IN, ACC, OUT, V, 2, 16, NT>(a, grid, s); break;
-    case 4: launch_dense_t<IN, ACC, OUT, V, 4, 4, NT>(a, grid, s); break;
-    case 5: launch_dense_t<IN, ACC, OUT, V, 4, 8, NT>(a, grid, s); break;
-    case 6: launch_dense_t<IN, ACC, OUT, V, 1, 32, NT>(a, grid, s); break;
+    case 1: launch_dense_t<IN, ACC, OUT, V, 2, 8, NT>(a, grid, s); break;
+    case 2: launch_dense_t<IN, ACC, OUT, V, 1, 8, NT>(a, grid, s); break;
+    case 3: launch_dense_t<IN, ACC, OUT, V, 1, 16, NT>(a, grid, s); break;
+    case 4: launch_dense_t<IN, ACC, OUT, V, 2, 16, NT>(a, grid, s); break;
+    case 5: launch_dense_t<IN, ACC, OUT, V, 4, 4, NT>(a, grid, s); break;
+    case 6: launch_dense_t<IN, ACC, OUT, V, 4, 8, NT>(a, grid, s); break;
+    case 7: launch_dense_t<IN, ACC, OUT, V, 1, 32, NT>(a, grid, s); break;
     default: return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
   }
   (void)E;
@@ -611,10 +620,11 @@ int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, in
   const int ib = elem_bytes(in), ob = elem_bytes(out), vw = vwidth(in);
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) % 16 == 0) &&
                    (ld_bytes % 16 == 0) && (y_ystride % 16 == 0) && P >= vw;
-  const int variant = (flags >> 8) & 0xff;
-  if (variant >= kNumVariants) return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
-  const int E = kVariants[variant].E;
   const int V = vec ? vw : 1;
+  int variant = (flags >> 8) & 0xff;
+  if (variant >= kNumVariants) return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
+  if (variant == 0) variant = pick_variant(P / V);
+  const int E = kVariants[variant].E;
   DenseArgs a;
   a.x = x;
   a.ld_bytes = ld_bytes;

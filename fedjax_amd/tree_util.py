@@ -66,6 +66,8 @@ def _find_device(leaves: Iterable[Any]) -> torch.device:
 def _to_tensor(x) -> torch.Tensor:
     if isinstance(x, torch.Tensor):
         return x
+    if hasattr(x, "__dlpack__") and not isinstance(x, (np.ndarray, np.generic)):
+        return torch.from_dlpack(x)  # e.g. a jax.Array on the ROCm device: zero-copy
     if isinstance(x, (bool, np.bool_)):
         raise TypeError("boolean leaves are not supported")
     if isinstance(x, numbers.Integral) and not isinstance(x, np.generic):

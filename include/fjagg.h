@@ -64,7 +64,8 @@ enum fjagg_flags {
   FJAGG_NONTEMPORAL = 1 << 2, /* non-temporal (streaming) loads of the client deltas */
   FJAGG_UNALIGNED = 1 << 3,   /* ptrs path: some pointer is not 16-byte aligned */
 };
-/* bits 8..15 of flags select a kernel variant (0 = default); used by tuning only */
+/* bits 8..15 of flags select a kernel shape of the dense path: 0 = automatic,
+ * 1..7 = fixed (units per lane, clients in flight) for tuning; see fjagg.hip */
 #define FJAGG_VARIANT(v) (((v)&0xff) << 8)
 
 enum fjagg_mode {

@@ -27,7 +27,7 @@ def parity():
         w = torch.tensor(wi.astype(np.float32), device=dev)
         r = ref.mean_scale([int(v) for v in wi])
         want = ref.wsum_dense(xh, wi.astype(np.float32), scale=r)
-        for v in range(7):
+        for v in range(8):
             for nt in (False, True):
                 y = kernels.weighted_sum_dense(x, w, scale=float(r), variant=v, nontemporal=nt)
                 g = y.cpu().numpy()
@@ -51,7 +51,7 @@ def bench(K=1024, P=4 * 1024 * 1024, reps=10):
     nbytes = K * P * 4
     res = {}
     for rnd in range(3):
-        for v in range(7):
+        for v in range(8):
             for nt in (False, True):
                 kernels.weighted_sum_dense(x, w, scale=0.001, out=out, variant=v, nontemporal=nt)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
