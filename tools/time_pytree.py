@@ -1,0 +1,73 @@
+"""Config 2 (128 clients x EMNIST-CNN, 8 leaves) through the pytree path:
+tree_mean wall time (host planning + H2D + launch) and kernel time (HIP events),
+plus the same deltas as a dense slab. Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+import fedjax_amd
+from fedjax_amd import kernels, tree_util as tu
+
+SHAPES = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "conv2_d_1": {"b": (64,), "w": (3, 3, 32, 64)},
+          "linear": {"b": (128,), "w": (9216, 128)}, "linear_1": {"b": (62,), "w": (128, 62)}}
+
+
+def tmap(f, t):
+    return {k: tmap(f, v) for k, v in t.items()} if isinstance(t, dict) else f(t)
+
+
+def main(K=128, reps=20):
+    dev = torch.device("cuda:0")
+    template = tmap(lambda s: np.zeros(s, np.float32), SHAPES)
+    slab = fedjax_amd.ClientDeltaSlab(template, K, device=dev).fill_synthetic(seed=0)
+    P = slab.num_params
+    # separate allocations per (client, leaf), as a reference caller holds them
+    clients = [tmap(lambda v: v.clone(), slab.client(k)) for k in range(K)]
+    weights = np.random.RandomState(1).randint(1, 501, size=K).tolist()
+    pairs = list(zip(clients, weights))
+    for _ in range(3):
+        tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    # kernel-only time: events around the launch inside tree_mean
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ks = []
+    for _ in range(reps):
+        s.record()
+        tu.tree_mean(pairs)
+        e.record()
+        e.synchronize()
+        ks.append(s.elapsed_time(e))
+    wd = slab.weight_vector(weights)
+    r = float(np.float32(1.0 / sum(weights)))
+    out = torch.empty(P, device=dev)
+    dense = {}
+    for nt in (False, True):
+        for v in (0, 1, 2, 3):
+            kernels.weighted_sum_dense(slab.rows, wd, scale=r, out=out, nontemporal=nt, variant=v)
+            s.record()
+            for _ in range(reps):
+                kernels.weighted_sum_dense(slab.rows, wd, scale=r, out=out, nontemporal=nt, variant=v)
+            e.record()
+            e.synchronize()
+            dense[f"v{v}_nt{int(nt)}"] = round(K * P * 4 / (s.elapsed_time(e) / reps / 1e3) / 1e9, 1)
+    nbytes = K * P * 4
+    print(json.dumps({"workload": "configs[1] 128 x EMNIST-CNN (1,206,590 params, 8 leaves)",
+                      "tree_mean_wall_ms": round(wall * 1e3, 4),
+                      "tree_mean_wall_GBs": round(nbytes / wall / 1e9, 1),
+                      "tree_mean_gpu_ms_median": round(float(np.median(ks)), 4),
+                      "tree_mean_gpu_GBs": round(nbytes / (np.median(ks) / 1e3) / 1e9, 1),
+                      "dense_slab_GBs": dense}))
+
+
+if __name__ == "__main__":
+    main()
