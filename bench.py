@@ -37,9 +37,15 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "device-resident aggregated client-delta GB/s, K clients × P fp32 params"
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-WORKLOADS = {
-    "c3": (1024, 4 * 1024 * 1024, "configs[2]: mean aggregator, 1024 clients x 4 M-param (4,194,304) fp32 deltas"),
-    "c2": (128, 1206590, "configs[1]: mean aggregator, 128 clients x 1,206,590-param EMNIST-CNN fp32 deltas"),
+WORKLOADS = {  # name: (clients, params, dtype, description)
+    "c3": (1024, 4 * 1024 * 1024, torch.float32,
+           "configs[2]: mean aggregator, 1024 clients x 4 M-param (4,194,304) fp32 deltas"),
+    "c2": (128, 1206590, torch.float32,
+           "configs[1]: mean aggregator, 128 clients x 1,206,590-param EMNIST-CNN fp32 deltas"),
+    "c5": (8192, 125_000_000, torch.bfloat16,
+           "configs[4]: 8192 clients x 125 M-param bf16 deltas, client-sharded (needs >= 8 GPUs)"),
+    "c5s": (1024, 125_000_000, torch.bfloat16,
+            "configs[4] per-GPU shard: 1024 clients x 125 M-param bf16 deltas on one GPU"),
 }
 
 
@@ -126,18 +132,26 @@ def main():
     import fedjax_amd  # noqa: F401
     from fedjax_amd import distributed as fd, kernels, tree_util as tu
 
-    K, P, desc = WORKLOADS[args.workload]
+    K, P, dtype, desc = WORKLOADS[args.workload]
+    esize = torch.empty((), dtype=dtype).element_size()
     weights = fedavg_weights(K)
     W = 0.0
     for w in weights:
         W += w  # tree_util.py:95
     k0, k1 = fd.shard_range(K, rank, world)
     Kl = k1 - k0
-    x = torch.empty(Kl, P, dtype=torch.float32, device=dev)
+    if Kl > 1024 and dtype == torch.bfloat16:
+        raise SystemExit(f"{args.workload}: {Kl} clients x {P} params per GPU exceed 288 GB; use more GPUs")
+    # ClientDeltaSlab layout: rows padded to 16 bytes (vector path)
+    vw = 16 // esize
+    ld = (P + vw - 1) // vw * vw
+    x = torch.empty(Kl, ld, dtype=dtype, device=dev)[:, :P]
     kernels.fill_synth(x, seed=0, k0=k0)  # the same global client k on every N
     w_local = [weights[k] for k in range(k0, k1)]
-    out = torch.empty(P, dtype=torch.float32, device=dev)
-    nbytes_local = Kl * P * 4
+    out = torch.empty(P, dtype=dtype if world == 1 else torch.float32, device=dev)
+    final = torch.empty(P, dtype=dtype, device=dev) if (world > 1 and dtype != torch.float32) else None
+    ones = torch.ones(1, dtype=torch.float32, device=dev)
+    nbytes_local = Kl * P * esize
     nt = (nbytes_local >= tu.NONTEMPORAL_MIN_BYTES) if args.nontemporal < 0 else bool(args.nontemporal)
     scale = float(np.float32(tu._inverse(W)))
     stream = torch.cuda.current_stream(dev)
@@ -150,7 +164,7 @@ def main():
         kernels.weighted_sum_dense(xs, wd, scale=scale, out=o, nontemporal=nt, variant=args.variant)
         if events is not None:
             e1.record(stream)
-            events.append((e0, e1, xs.shape[0] * xs.shape[1] * 4))
+            events.append((e0, e1, xs.shape[0] * xs.shape[1] * esize))
 
     def step(events=None):
         wd = torch.from_numpy(np.float32(w_local)).pin_memory().to(dev, non_blocking=True)
@@ -159,6 +173,8 @@ def main():
         else:
             fd.sharded_weighted_mean(x, wd, W, buckets=args.buckets, out=out, all_ranks=args.all_ranks,
                                      partial_fn=lambda xs, wdd, sc, o: fold(xs, wdd, o, events))
+            if final is not None and (rank == 0 or args.all_ranks):  # f32 mean -> leaf dtype
+                kernels.weighted_sum_dense(out.view(1, P), ones, out=final)
 
     for _ in range(args.warmup):
         step()
@@ -186,9 +202,9 @@ def main():
 
     e2e = None
     if args.e2e and world == 1:
-        xh = torch.empty(K, P, dtype=torch.float32).pin_memory()
+        xh = torch.empty(K, P, dtype=dtype).pin_memory()
         xh.copy_(x.cpu())
-        yh = torch.empty(P, dtype=torch.float32).pin_memory()
+        yh = torch.empty(P, dtype=out.dtype).pin_memory()
         wd = torch.from_numpy(np.float32(w_local)).to(dev)
         torch.cuda.synchronize()
         ts = time.perf_counter()
@@ -197,11 +213,11 @@ def main():
             kernels.weighted_sum_dense(x, wd, scale=scale, out=out, nontemporal=nt)
             yh.copy_(out, non_blocking=True)
         torch.cuda.synchronize()
-        e2e = K * P * 4 * 3 / (time.perf_counter() - ts) / 1e9
+        e2e = K * P * esize * 3 / (time.perf_counter() - ts) / 1e9
         del xh
 
     if rank == 0:
-        value = K * P * 4 * args.steps / elapsed / 1e9
+        value = K * P * esize * args.steps / elapsed / 1e9
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -213,7 +229,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
             "data": "synthetic: counter-hash client deltas 0.01*u[-1,1), integer weights in [1,500]",
             "config": {"workload": desc, "clients": K, "params": P, "clients_per_gpu": Kl,
                        "parallelism": f"client-sharded x{world}" + (
@@ -228,7 +244,7 @@ def main():
         }
         if e2e is not None:
             res["e2e_host_resident_GBs"] = round(e2e, 2)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and dtype == torch.float32:
             res["cpu_baseline"] = cpu_baseline(K)
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -27,19 +27,31 @@ _REGISTRY: Dict[type, Tuple[Callable, Callable]] = {}
 def register_pytree_node(cls: type, flatten_fn: Callable, unflatten_fn: Callable) -> None:
     """flatten_fn(x) -> (children, aux); unflatten_fn(aux, children) -> x."""
     _REGISTRY[cls] = (flatten_fn, unflatten_fn)
+    _LEAF_TYPES.discard(cls)
+
+
+def register_leaf_type(cls: type) -> None:
+    """Declare ``cls`` a leaf type (skips the container checks in flatten_as)."""
+    if cls not in _REGISTRY:
+        _LEAF_TYPES.add(cls)
 
 
 class TreeDef:
     """Hashable structure of a pytree (node kind, aux data, children)."""
 
-    __slots__ = ("kind", "aux", "children", "num_leaves", "_hash")
+    __slots__ = ("kind", "aux", "children", "leafy", "_hash")
 
     def __init__(self, kind, aux, children):
         self.kind = kind
         self.aux = aux
         self.children = children
-        self.num_leaves = 1 if kind == "leaf" else sum(c.num_leaves for c in children)
+        # every child is a leaf: flatten_as can take the values without recursing
+        self.leafy = bool(children) and all(c.kind == "leaf" for c in children)
         self._hash = None
+
+    @property
+    def num_leaves(self):
+        return 1 if self.kind == "leaf" else sum(c.num_leaves for c in self.children)
 
     def _key(self):
         return (self.kind, self.aux, self.children)
@@ -59,6 +71,7 @@ class TreeDef:
 
 
 _LEAF = TreeDef("leaf", None, ())
+_LEAF_TYPES = set()  # types known to be leaves (fast path); filled by register_leaf_type
 _NONE = TreeDef("none", None, ())
 
 
@@ -100,7 +113,7 @@ def flatten(tree) -> Tuple[List[Any], TreeDef]:
             return _LEAF
         if kind == "none":
             return _NONE
-        return TreeDef(kind, aux, tuple(rec(c) for c in children))
+        return TreeDef(kind, aux, tuple([rec(c) for c in children]))
 
     td = rec(tree)
     return leaves, td
@@ -110,12 +123,60 @@ def leaves_of(tree) -> List[Any]:
     return flatten(tree)[0]
 
 
+def _is_leaf(x) -> bool:
+    return type(x) in _LEAF_TYPES or _node(x)[0] == "leaf"
+
+
 def flatten_as(treedef: TreeDef, tree) -> List[Any]:
-    """Leaves of ``tree``, which must have structure ``treedef`` (ValueError if not)."""
-    leaves, td = flatten(tree)
-    if td != treedef:
-        raise ValueError(f"pytree structure mismatch: expected {treedef!r}, got {td!r}")
-    return leaves
+    """Leaves of ``tree``, which must have structure ``treedef`` (ValueError if not).
+
+    Walks ``treedef`` and checks ``tree`` against it node by node, without
+    building a second TreeDef (this is the per-client hot loop of tree_mean)."""
+    out: List[Any] = []
+    try:
+        _collect(treedef, tree, out)
+    except (KeyError, IndexError, TypeError, _Mismatch):
+        raise ValueError(f"pytree structure mismatch: expected {treedef!r}, got "
+                         f"{flatten(tree)[1]!r}") from None
+    return out
+
+
+class _Mismatch(Exception):
+    pass
+
+
+def _collect(td: TreeDef, x, out: List[Any]) -> None:
+    k = td.kind
+    if k == "leaf":
+        if not _is_leaf(x):
+            raise _Mismatch
+        out.append(x)
+        return
+    if k == "none":
+        if x is not None:
+            raise _Mismatch
+        return
+    t = type(x)
+    if k == "dict":
+        if t is not dict or len(x) != len(td.aux):
+            raise _Mismatch
+        vals = [x[key] for key in td.aux]
+    elif k in ("list", "tuple"):
+        if t is not (list if k == "list" else tuple) or len(x) != td.aux:
+            raise _Mismatch
+        vals = x
+    else:
+        kind, aux, vals = _node(x)
+        if kind != k or aux != td.aux or len(vals) != len(td.children):
+            raise _Mismatch
+    if td.leafy:
+        for v in vals:
+            if not _is_leaf(v):
+                raise _Mismatch
+        out.extend(vals)
+        return
+    for c, v in zip(td.children, vals):
+        _collect(c, v, out)
 
 
 def unflatten(treedef: TreeDef, leaves) -> Any:

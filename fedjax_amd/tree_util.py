@@ -40,8 +40,9 @@ __all__ = [
 ]
 
 # Non-temporal loads pay off once the deltas cannot stay in the 256 MiB Infinity
-# Cache between rounds (profiles/r01_probe.txt: +10 % at 17 GB, -7 % at 0.6 GB).
-NONTEMPORAL_MIN_BYTES = 1 << 30
+# Cache (interleaved A/B, profiles/r01_probe2.jsonl + r01_pytree_c2b.json: +10 % at
+# 17 GB, +13 % at 618 MB on the 16-byte vector path).
+NONTEMPORAL_MIN_BYTES = 256 << 20
 
 _CANONICAL = {
     torch.float32: torch.float32, torch.bfloat16: torch.bfloat16, torch.int32: torch.int32,
@@ -80,8 +81,15 @@ def _to_tensor(x) -> torch.Tensor:
     return torch.from_numpy(a)
 
 
+_NATIVE = (torch.float32, torch.bfloat16, torch.int32)
+pytree.register_leaf_type(torch.Tensor)
+pytree.register_leaf_type(np.ndarray)
+
+
 def _device_leaf(x, device: torch.device) -> torch.Tensor:
     """Leaf as a contiguous device tensor of a canonical dtype (jnp.asarray rules)."""
+    if type(x) is torch.Tensor and x.dtype in _NATIVE and x.device == device and x.is_contiguous():
+        return x  # the common case: a delta already on the GPU
     t = _to_tensor(x)
     dt = _CANONICAL.get(t.dtype)
     if dt is None:
@@ -160,17 +168,17 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
     device = rows[0][0].device if L else None
     outs: List[Optional[torch.Tensor]] = [None] * L
     groups = {}
+    sig0 = [(x.shape, x.dtype) for x in rows[0]]
+    for k in range(1, K):  # rows are on `device` already (_client_rows)
+        if [(x.shape, x.dtype) for x in rows[k]] != sig0:
+            for l, x in enumerate(rows[k]):
+                if x.shape != sig0[l][0]:
+                    raise ValueError(f"leaf {l}: client {k} has shape {tuple(x.shape)}, "
+                                     f"client 0 has {tuple(sig0[l][0])}")
+                if x.dtype != sig0[l][1]:
+                    raise TypeError(f"leaf {l}: client {k} has dtype {x.dtype}, client 0 has {sig0[l][1]}")
     for l in range(L):
         x0 = rows[0][l]
-        for k in range(1, K):
-            xk = rows[k][l]
-            if xk.shape != x0.shape:
-                raise ValueError(f"leaf {l}: client {k} has shape {tuple(xk.shape)}, "
-                                 f"client 0 has {tuple(x0.shape)}")
-            if xk.dtype != x0.dtype:
-                raise TypeError(f"leaf {l}: client {k} has dtype {xk.dtype}, client 0 has {x0.dtype}")
-            if xk.device != device:
-                raise ValueError(f"leaf {l}: client {k} is on {xk.device}, expected {device}")
         in_c, acc_c, out_dt = _leaf_rule(x0.dtype, kinds, scaled_kind)
         if out is not None:
             o = out[l]
@@ -186,7 +194,10 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
         leaf_n = np.array([rows[0][l].numel() for l in ls], dtype=np.int64)
         if not leaf_n.any():
             continue
-        in_ptrs = np.array([[rows[k][l].data_ptr() for l in ls] for k in range(K)], dtype=np.int64)
+        if len(ls) == L:
+            in_ptrs = np.array([[x.data_ptr() for x in row] for row in rows], dtype=np.int64)
+        else:
+            in_ptrs = np.array([[rows[k][l].data_ptr() for l in ls] for k in range(K)], dtype=np.int64)
         out_ptrs = np.array([outs[l].data_ptr() for l in ls], dtype=np.int64)
         unaligned = bool((in_ptrs % 16).any() or (out_ptrs % 16).any())
         blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)

@@ -312,3 +312,29 @@ def test_full_size_configs(K, P, cuda):
     assert torch.equal(y.view(torch.int32), y2.view(torch.int32))
     del x
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------ streaming running sum
+@pytest.mark.parametrize("buffer_clients", [1, 5, 8])
+def test_running_mean_equals_library_fedavg_loop(buffer_clients, cuda, coracle):
+    """fedjax/algorithms/fed_avg.py:132-146 restated: s = 0; s = s + x_k*n_k; s * f32(1/W)."""
+    K, P = 37, 3001
+    xh = coracle.synth_f32(K, P, seed=21)
+    wi = [int(v) for v in ref.fedavg_weights(K, seed=22)]
+    cut = 1000
+    template = {"a": np.zeros(cut, np.float32), "b": np.zeros(P - cut, np.float32)}
+    rm = fedjax_amd.aggregators.RunningMean(template, buffer_clients=buffer_clients, device=cuda)
+    for k in range(K):
+        xk = torch.from_numpy(xh[k]).to(cuda)
+        rm.add({"a": xk[:cut], "b": xk[cut:]}, wi[k])
+    m = rm.result()
+    got = np.concatenate([host(m["a"]), host(m["b"])])
+    s = np.zeros(P, np.float32)
+    for k in range(K):
+        s = s + xh[k] * np.float32(wi[k])
+    W = 0.0
+    for w in wi:
+        W += w
+    want = s * np.float32(1.0 / W)
+    assert np.array_equal(bits(got), bits(want))
+    assert rm.num_clients == K and rm.total_weight == W
