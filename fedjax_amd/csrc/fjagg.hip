@@ -23,7 +23,9 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <mutex>
 #include <type_traits>
+#include <unordered_map>
 
 #include "fjagg.h"
 
@@ -89,8 +91,30 @@ template <int IN, int V> struct Unit {
   using Raw = typename std::conditional<(BYTES == 16), u32x4, unsigned>::type;
 };
 
+// Buffer resource over one client row: base in SGPRs, range-checked to `bytes`
+// (out-of-range lanes read zeros). gfx950 word-3 flags as in the HIP guide (T8).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint8_t* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+// One unit of a client row via buffer_load with a 32-bit lane offset: no per-load
+// address VGPRs (aux 2 = nt).
 template <int IN, int V, bool NT>
-__device__ __forceinline__ typename Unit<IN, V>::Raw load_unit(const uint8_t* p) {
+__device__ __forceinline__ typename Unit<IN, V>::Raw load_unit(__amdgpu_buffer_rsrc_t r,
+                                                               uint32_t off) {
+  constexpr int aux = NT ? 2 : 0;
+  if constexpr (Unit<IN, V>::BYTES == 16) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, aux);
+  } else if constexpr (Elem<IN>::B == 4) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, aux);
+  } else {
+    return (unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, aux);
+  }
+}
+
+template <int IN, int V, bool NT>
+__device__ __forceinline__ typename Unit<IN, V>::Raw load_unit_ptr(const uint8_t* p) {
   if constexpr (Unit<IN, V>::BYTES == 16) {
     if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     else return *reinterpret_cast<const u32x4*>(p);
@@ -199,19 +223,24 @@ __device__ __forceinline__ void load_out_unit(const uint8_t* p, unsigned (&b)[V]
 // Each lane folds E units; unit j of this lane sits at byte offset off[j] of every
 // client row (a 32-bit lane constant) and is written to outp[j]. row(k) returns the
 // wave-uniform base address of client k. Clients are folded in order 0..K-1.
+// The output of the unit at input byte offset off is at obase + off / sizeof(IN) *
+// sizeof(OUT) (same element index); valid[j] == false skips unit j's store.
 template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, class RowFn>
-__device__ __forceinline__ void fold(RowFn row, int64_t K, const uint32_t (&off)[E],
-                                     uint8_t* const (&outp)[E], const bool (&valid)[E],
+__device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
+                                     const uint32_t (&off)[E],
+                                     uint8_t* __restrict__ obase, const bool (&valid)[E],
                                      const typename ACC::T* __restrict__ w, bool do_scale,
                                      float scale, bool accumulate) {
+  constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
+  auto outp = [&](int j) { return obase + (size_t)(off[j] / IB) * OB; };
   using T = typename ACC::T;
   using Raw = typename Unit<IN, V>::Raw;
   T acc[E][V];
   {  // client 0: s_0 = t_0 (tree_util.py:89-91) or out + t_0 (running sum)
-    const uint8_t* r = row(0);
+    const auto r = row_rsrc(row(0), row_bytes);
     Raw v[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) v[j] = load_unit<IN, V, NT>(r + off[j]);
+    for (int j = 0; j < E; ++j) v[j] = load_unit<IN, V, NT>(r, off[j]);
     const T w0 = w[0];
 #pragma unroll
     for (int j = 0; j < E; ++j) {
@@ -224,7 +253,7 @@ __device__ __forceinline__ void fold(RowFn row, int64_t K, const uint32_t (&off)
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         unsigned b[V];
-        load_out_unit<OUT, V>(outp[j], b);
+        load_out_unit<OUT, V>(outp(j), b);
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(init_from<OUT, ACC>(b[i]), acc[j][i]);
       }
@@ -235,9 +264,9 @@ __device__ __forceinline__ void fold(RowFn row, int64_t K, const uint32_t (&off)
     Raw v[U][E];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint8_t* r = row(k + u);
+      const auto r = row_rsrc(row(k + u), row_bytes);
 #pragma unroll
-      for (int j = 0; j < E; ++j) v[u][j] = load_unit<IN, V, NT>(r + off[j]);
+      for (int j = 0; j < E; ++j) v[u][j] = load_unit<IN, V, NT>(r, off[j]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -252,12 +281,12 @@ __device__ __forceinline__ void fold(RowFn row, int64_t K, const uint32_t (&off)
     }
   }
   for (; k < K; ++k) {
-    const uint8_t* r = row(k);
+    const auto r = row_rsrc(row(k), row_bytes);
     const T wk = w[k];
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       T t[V];
-      decode<IN, ACC, V>(load_unit<IN, V, NT>(r + off[j]), t);
+      decode<IN, ACC, V>(load_unit<IN, V, NT>(r, off[j]), t);
 #pragma unroll
       for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(acc[j][i], ACC::mul(t[i], wk));
     }
@@ -268,19 +297,25 @@ __device__ __forceinline__ void fold(RowFn row, int64_t K, const uint32_t (&off)
     unsigned b[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) b[i] = finish<OUT, ACC>(acc[j][i], do_scale, scale);
-    store_unit<OUT, V>(outp[j], b);
+    store_unit<OUT, V>(outp(j), b);
   }
 }
 
 // Dense slab: client k at x + k*ld_bytes; P = nunits*V + tail_n elements.
-// Block 0 folds the tail (if any) with 1-element units; the rest cover the units.
+// Block 0 folds the tail (if any) with 1-element units. Every other block owns the
+// contiguous unit range [b*S, min((b+1)*S, nunits)) and walks it in groups of
+// kThreads*E units (lane tid takes units g + j*kThreads + tid), folding all clients
+// of a group before moving on. The host sizes S so that the grid is one resident
+// wave of workgroups with equal byte shares ("balanced"), or S = kThreads*E for the
+// classic one-tile-per-block launch.
 // blockIdx.y selects a client range [y*kchunk, min(K, (y+1)*kchunk)) and writes to
 // out + y*out_ystride_bytes (FJAGG_MODE_SPLIT); exact mode has gridDim.y == 1.
-template <int IN, class ACC, int OUT, int V, int E, int U, bool NT>
-__global__ __launch_bounds__(kThreads) void k_dense(
+// MINW > 0 asks for MINW waves per SIMD (caps VGPRs: 8 -> 64 registers).
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW>
+__global__ __launch_bounds__(kThreads, MINW) void k_dense(
     const uint8_t* __restrict__ x, int64_t ld_bytes, int64_t K, int64_t nunits, int tail_n,
     const typename ACC::T* __restrict__ w, float scale, int do_scale, int accumulate,
-    uint8_t* __restrict__ out, int64_t kchunk, int64_t out_ystride_bytes) {
+    uint8_t* __restrict__ out, int64_t kchunk, int64_t out_ystride_bytes, int64_t S) {
   constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
   const int tid = threadIdx.x;
   const int64_t k0 = (int64_t)blockIdx.y * kchunk;
@@ -289,34 +324,36 @@ __global__ __launch_bounds__(kThreads) void k_dense(
   const typename ACC::T* wb = w + k0;
   uint8_t* ob = out + (int64_t)blockIdx.y * out_ystride_bytes;
   auto row = [=](int64_t k) { return xb + k * ld_bytes; };
+  const uint32_t row_bytes = (uint32_t)((nunits * V + tail_n) * IB);
   int64_t b = blockIdx.x;
   if (tail_n > 0) {
     if (b == 0) {
       if (tid < tail_n) {
         const int64_t e = nunits * V + tid;
         const uint32_t off[1] = {(uint32_t)(e * IB)};
-        uint8_t* const op[1] = {ob + e * OB};
         const bool valid[1] = {true};
-        fold<IN, ACC, OUT, 1, 1, U, NT>(row, kn, off, op, valid, wb, do_scale != 0, scale,
-                                        accumulate != 0);
+        fold<IN, ACC, OUT, 1, 1, U, NT>(row, row_bytes, kn, off, ob, valid, wb, do_scale != 0,
+                                        scale, accumulate != 0);
       }
       return;
     }
     b -= 1;
   }
-  uint32_t off[E];
-  uint8_t* op[E];
-  bool valid[E];
+  const int64_t u_begin = b * S;
+  const int64_t u_end = (u_begin + S < nunits) ? u_begin + S : nunits;
+  for (int64_t g = u_begin; g < u_end; g += (int64_t)kThreads * E) {
+    uint32_t off[E];
+    bool valid[E];
 #pragma unroll
-  for (int j = 0; j < E; ++j) {
-    int64_t u = b * (kThreads * E) + j * kThreads + tid;
-    valid[j] = u < nunits;
-    if (!valid[j]) u = nunits - 1;  // keep the load in bounds; the store is skipped
-    off[j] = (uint32_t)(u * (V * IB));
-    op[j] = ob + u * (V * OB);
+    for (int j = 0; j < E; ++j) {
+      int64_t u = g + j * kThreads + tid;
+      valid[j] = u < u_end;
+      if (!valid[j]) u = u_end - 1;  // keep the load in bounds; the store is skipped
+      off[j] = (uint32_t)(u * (V * IB));
+    }
+    fold<IN, ACC, OUT, V, E, U, NT>(row, row_bytes, kn, off, ob, valid, wb, do_scale != 0,
+                                    scale, accumulate != 0);
   }
-  fold<IN, ACC, OUT, V, E, U, NT>(row, kn, off, op, valid, wb, do_scale != 0, scale,
-                                  accumulate != 0);
 }
 
 // Pytree path. image = in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[nblk].
@@ -340,19 +377,18 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   const int64_t nunits = n / V;
   uint8_t* ob = reinterpret_cast<uint8_t*>(out_ptrs[leaf]);
   auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]); };
+  const uint32_t row_bytes = (uint32_t)(n * IB);
   if (tail) {
     if (tid < n - nunits * V) {
       const int64_t e = nunits * V + tid;
       const uint32_t off[1] = {(uint32_t)(e * IB)};
-      uint8_t* const op[1] = {ob + e * OB};
       const bool valid[1] = {true};
-      fold<IN, ACC, OUT, 1, 1, U, NT>(row, K, off, op, valid, w, do_scale != 0, scale,
-                                      accumulate != 0);
+      fold<IN, ACC, OUT, 1, 1, U, NT>(row, row_bytes, K, off, ob, valid, w, do_scale != 0,
+                                      scale, accumulate != 0);
     }
     return;
   }
   uint32_t off[E];
-  uint8_t* op[E];
   bool valid[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
@@ -360,10 +396,9 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
     valid[j] = u < nunits;
     if (!valid[j]) u = nunits - 1;
     off[j] = (uint32_t)(u * (V * IB));
-    op[j] = ob + u * (V * OB);
   }
-  fold<IN, ACC, OUT, V, E, U, NT>(row, K, off, op, valid, w, do_scale != 0, scale,
-                                  accumulate != 0);
+  fold<IN, ACC, OUT, V, E, U, NT>(row, row_bytes, K, off, ob, valid, w, do_scale != 0,
+                                  scale, accumulate != 0);
 }
 
 // Per-client sum of squares: grid (nb, K); ws[k*nb + b] = block partial (f32),
@@ -385,19 +420,19 @@ __global__ __launch_bounds__(kThreads) void k_l2sq_partial(const uint8_t* __rest
     const int64_t nfull = (e1 - e0) / VW;
     for (int64_t u = threadIdx.x; u < nfull; u += kThreads) {
       float t[VW];
-      decode<IN, AccF, VW>(load_unit<IN, VW, true>(r + (e0 + u * VW) * IB), t);
+      decode<IN, AccF, VW>(load_unit_ptr<IN, VW, true>(r + (e0 + u * VW) * IB), t);
 #pragma unroll
       for (int i = 0; i < VW; ++i) s = __fadd_rn(s, __fmul_rn(t[i], t[i]));
     }
     for (int64_t e = e0 + nfull * VW + threadIdx.x; e < e1; e += kThreads) {
       float t[1];
-      decode<IN, AccF, 1>(load_unit<IN, 1, false>(r + e * IB), t);
+      decode<IN, AccF, 1>(load_unit_ptr<IN, 1, false>(r + e * IB), t);
       s = __fadd_rn(s, __fmul_rn(t[0], t[0]));
     }
   } else {
     for (int64_t e = e0 + threadIdx.x; e < e1; e += kThreads) {
       float t[1];
-      decode<IN, AccF, 1>(load_unit<IN, 1, false>(r + e * IB), t);
+      decode<IN, AccF, 1>(load_unit_ptr<IN, 1, false>(r + e * IB), t);
       s = __fadd_rn(s, __fmul_rn(t[0], t[0]));
     }
   }
@@ -438,7 +473,7 @@ __global__ __launch_bounds__(kThreads) void k_l2sq_rows(const int64_t* __restric
   float s = 0.f;
   for (int64_t e = e0 + threadIdx.x; e < e1; e += kThreads) {
     float t[1];
-    decode<IN, AccF, 1>(load_unit<IN, 1, false>(x + e * IB), t);
+    decode<IN, AccF, 1>(load_unit_ptr<IN, 1, false>(x + e * IB), t);
     s = __fadd_rn(s, __fmul_rn(t[0], t[0]));
   }
 #pragma unroll
@@ -517,67 +552,125 @@ struct DenseArgs {
   int do_scale, accumulate;
   uint8_t* out;
   int64_t kchunk, out_ystride;
+  bool balanced;
 };
 
-template <int IN, class ACC, int OUT, int V, int E, int U, bool NT>
-void launch_dense_t(const DenseArgs& a, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((k_dense<IN, ACC, OUT, V, E, U, NT>), grid, dim3(kThreads), 0, s, a.x,
-                     a.ld_bytes, a.K, a.nunits, a.tail_n,
+// (CUs, workgroups of `kern` per CU at once), cached per kernel and device. Used
+// only to size balanced grids: never needed for correctness.
+struct Residency {
+  int cus, per_cu;
+};
+Residency residency(const void* kern) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, Residency> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const void* key = reinterpret_cast<const void*>(reinterpret_cast<uintptr_t>(kern) ^ ((uintptr_t)dev << 56));
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  (void)hipGetLastError();
+  const Residency r{cus, per_cu};
+  std::lock_guard<std::mutex> g(mu);
+  cache[key] = r;
+  return r;
+}
+
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW>
+void launch_dense_t(const DenseArgs& a, int64_t gy, hipStream_t s) {
+  auto kern = k_dense<IN, ACC, OUT, V, E, U, NT, MINW>;
+  const int64_t tile = (int64_t)kThreads * E;
+  const int64_t ntiles = (a.nunits + tile - 1) / tile;
+  int64_t nblk = ntiles, S = tile;
+  if (a.balanced && ntiles > 0) {
+    // The same number of workgroups on every CU (c <= what fits at once), each
+    // with an equal, wave-aligned share of the parameter axis: every CU streams
+    // the same bytes and no workgroup waits for a slot (profiles/r01_sweep3.jsonl).
+    const Residency r = residency(reinterpret_cast<const void*>(kern));
+    const int64_t cus = (r.cus + gy - 1) / gy;  // CUs per client range (split mode)
+    int64_t c = (ntiles + cus - 1) / cus;
+    if (c > r.per_cu) c = r.per_cu;
+    if (c < 1) c = 1;
+    S = ((a.nunits + cus * c - 1) / (cus * c) + 63) / 64 * 64;
+    nblk = (a.nunits + S - 1) / S;
+  }
+  dim3 grid((unsigned)(nblk + (a.tail_n > 0 ? 1 : 0)), (unsigned)gy);
+  hipLaunchKernelGGL(kern, grid, dim3(kThreads), 0, s, a.x, a.ld_bytes, a.K, a.nunits, a.tail_n,
                      reinterpret_cast<const typename ACC::T*>(a.w), a.scale, a.do_scale,
-                     a.accumulate, a.out, a.kchunk, a.out_ystride);
+                     a.accumulate, a.out, a.kchunk, a.out_ystride, S);
 }
 
 struct VariantShape {
-  int E, U;
+  int E, U, minw;
 };
 // Index 0 is "auto" (resolved by pick_variant); 1.. are explicit shapes for tuning.
-constexpr VariantShape kVariants[] = {{0, 0}, {2, 8}, {1, 8}, {1, 16}, {2, 16}, {4, 4}, {4, 8}, {1, 32}};
+constexpr VariantShape kVariants[] = {{0, 0, 0},  {2, 8, 0},  {1, 8, 0},  {1, 16, 0},
+                                      {2, 16, 0}, {4, 4, 0},  {4, 8, 0},  {1, 32, 0},
+                                      {2, 8, 8},  {2, 4, 8},  {1, 16, 8}, {4, 4, 4},
+                                      {8, 4, 0},  {8, 8, 0},  {4, 16, 0}, {4, 12, 0}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-// E=2 x U=8 (32 B per lane per client, 8 clients in flight) measured fastest on
-// the 1024 x 4M slab (profiles/r01_probe.txt); when the parameter axis gives
-// fewer than ~4 workgroups per CU at E=2, halve E to double the workgroups.
-int pick_variant(int64_t nunits) {
-  const int64_t nblk_e2 = (nunits + kThreads * 2 - 1) / (kThreads * 2);
-  return nblk_e2 >= 1024 ? 1 : 2;
+// Default shape: E=8 x U=4 (8 units = 128 B per lane per client, 4 clients = 32
+// loads in flight per lane, 3 workgroups per CU) on the balanced grid: fastest or
+// within 2 % of the fastest on every swept shape with K >= 32 and >= 512 Ki f32
+// params; E=1 x U=8 below that (profiles/r01_sweep3.jsonl, r01_sweep4.jsonl).
+int pick_variant(int64_t nunits, int64_t K) {
+  // few clients (short folds) or a narrow parameter axis: many light workgroups
+  if (K < 32 || nunits < 131072) return 2;  // E=1 x U=8
+  return 12;                                // E=8 x U=4
 }
 
 template <int IN, class ACC, int OUT, int V, bool NT>
-int launch_dense_v(int variant, const DenseArgs& a, int64_t nblk_units, int64_t gy,
-                   hipStream_t s) {
-  const int E = kVariants[variant].E;
-  dim3 grid((unsigned)(nblk_units + (a.tail_n > 0 ? 1 : 0)), (unsigned)gy);
-  switch (variant) {
-    case 1: launch_dense_t<IN, ACC, OUT, V, 2, 8, NT>(a, grid, s); break;
-    case 2: launch_dense_t<IN, ACC, OUT, V, 1, 8, NT>(a, grid, s); break;
-    case 3: launch_dense_t<IN, ACC, OUT, V, 1, 16, NT>(a, grid, s); break;
-    case 4: launch_dense_t<IN, ACC, OUT, V, 2, 16, NT>(a, grid, s); break;
-    case 5: launch_dense_t<IN, ACC, OUT, V, 4, 4, NT>(a, grid, s); break;
-    case 6: launch_dense_t<IN, ACC, OUT, V, 4, 8, NT>(a, grid, s); break;
-    case 7: launch_dense_t<IN, ACC, OUT, V, 1, 32, NT>(a, grid, s); break;
-    default: return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
+int launch_dense_v(int variant, const DenseArgs& a, int64_t gy, hipStream_t s) {
+  if constexpr (V == 1) {  // element-granular path (tails, unaligned rows): one shape
+    launch_dense_t<IN, ACC, OUT, 1, 1, 8, NT, 0>(a, gy, s);
+    return check_launch("k_dense");
+  } else {
+    switch (variant) {
+      case 1: launch_dense_t<IN, ACC, OUT, V, 2, 8, NT, 0>(a, gy, s); break;
+      case 2: launch_dense_t<IN, ACC, OUT, V, 1, 8, NT, 0>(a, gy, s); break;
+      case 3: launch_dense_t<IN, ACC, OUT, V, 1, 16, NT, 0>(a, gy, s); break;
+      case 4: launch_dense_t<IN, ACC, OUT, V, 2, 16, NT, 0>(a, gy, s); break;
+      case 5: launch_dense_t<IN, ACC, OUT, V, 4, 4, NT, 0>(a, gy, s); break;
+      case 6: launch_dense_t<IN, ACC, OUT, V, 4, 8, NT, 0>(a, gy, s); break;
+      case 7: launch_dense_t<IN, ACC, OUT, V, 1, 32, NT, 0>(a, gy, s); break;
+      case 8: launch_dense_t<IN, ACC, OUT, V, 2, 8, NT, 8>(a, gy, s); break;
+      case 9: launch_dense_t<IN, ACC, OUT, V, 2, 4, NT, 8>(a, gy, s); break;
+      case 10: launch_dense_t<IN, ACC, OUT, V, 1, 16, NT, 8>(a, gy, s); break;
+      case 11: launch_dense_t<IN, ACC, OUT, V, 4, 4, NT, 4>(a, gy, s); break;
+      case 12: launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0>(a, gy, s); break;
+      case 13: launch_dense_t<IN, ACC, OUT, V, 8, 8, NT, 0>(a, gy, s); break;
+      case 14: launch_dense_t<IN, ACC, OUT, V, 4, 16, NT, 0>(a, gy, s); break;
+      case 15: launch_dense_t<IN, ACC, OUT, V, 4, 12, NT, 0>(a, gy, s); break;
+      default: return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
+    }
+    return check_launch("k_dense");
   }
-  (void)E;
-  return check_launch("k_dense");
 }
 
 template <int IN, class ACC, int OUT>
-int launch_dense_io(bool vec, bool nt, int variant, const DenseArgs& a, int64_t nblk_units,
-                    int64_t gy, hipStream_t s) {
+int launch_dense_io(bool vec, bool nt, int variant, const DenseArgs& a, int64_t gy, hipStream_t s) {
   constexpr int VW = vec_width<IN>();
   if (vec) {
-    return nt ? launch_dense_v<IN, ACC, OUT, VW, true>(variant, a, nblk_units, gy, s)
-              : launch_dense_v<IN, ACC, OUT, VW, false>(variant, a, nblk_units, gy, s);
+    return nt ? launch_dense_v<IN, ACC, OUT, VW, true>(variant, a, gy, s)
+              : launch_dense_v<IN, ACC, OUT, VW, false>(variant, a, gy, s);
   }
-  return nt ? launch_dense_v<IN, ACC, OUT, 1, true>(variant, a, nblk_units, gy, s)
-            : launch_dense_v<IN, ACC, OUT, 1, false>(variant, a, nblk_units, gy, s);
+  return nt ? launch_dense_v<IN, ACC, OUT, 1, true>(variant, a, gy, s)
+            : launch_dense_v<IN, ACC, OUT, 1, false>(variant, a, gy, s);
 }
 
 int launch_dense_dispatch(int in, int acc, int out, bool vec, bool nt, int variant,
-                          const DenseArgs& a, int64_t nblk_units, int64_t gy, hipStream_t s) {
+                          const DenseArgs& a, int64_t gy, hipStream_t s) {
 #define FJ_CASE(I, A, O, ACCT)                                                          \
   if (in == I && acc == A && out == O)                                                  \
-    return launch_dense_io<I, ACCT, O>(vec, nt, variant, a, nblk_units, gy, s);
+    return launch_dense_io<I, ACCT, O>(vec, nt, variant, a, gy, s);
   FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_F32, AccF)
   FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_BF16, AccF)
   FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_BF16, AccF)
@@ -623,8 +716,7 @@ int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, in
   const int V = vec ? vw : 1;
   int variant = (flags >> 8) & 0xff;
   if (variant >= kNumVariants) return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
-  if (variant == 0) variant = pick_variant(P / V);
-  const int E = kVariants[variant].E;
+  if (variant == 0) variant = pick_variant(P / V, K);
   DenseArgs a;
   a.x = x;
   a.ld_bytes = ld_bytes;
@@ -638,11 +730,11 @@ int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, in
   a.out = y;
   a.kchunk = kchunk;
   a.out_ystride = y_ystride;
-  const int64_t nblk = (a.nunits + (int64_t)kThreads * E - 1) / ((int64_t)kThreads * E);
+  a.balanced = !(flags & FJAGG_UNBALANCED);
   (void)ob;
   (void)ib;
   return launch_dense_dispatch(in, acc, out, vec, (flags & FJAGG_NONTEMPORAL) != 0, variant, a,
-                               nblk, gy, s);
+                               gy, s);
 }
 
 // Row bytes are addressed with 32-bit lane offsets: launch column chunks of <= 1 GiB.

@@ -46,7 +46,7 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
                        out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None,
                        accumulate: bool = False, mode: str = "exact",
                        workspace: Optional[torch.Tensor] = None, nontemporal: bool = False,
-                       variant: int = 0) -> torch.Tensor:
+                       variant: int = 0, balanced: bool = True) -> torch.Tensor:
     """Fold a client-major slab ``x[K, P]`` (row stride ``x.stride(0)``, unit column
     stride) with per-client weights ``w[K]`` into ``out[P]``.
 
@@ -74,6 +74,7 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
     dev = _require_device(x, w, out)
     flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
     flags |= (_lib.NONTEMPORAL if nontemporal else 0) | ((variant & 0xFF) << 8)
+    flags |= 0 if balanced else _lib.UNBALANCED
     m = {"exact": _lib.MODE_EXACT, "split": _lib.MODE_SPLIT}[mode]
     ws_ptr, ws_bytes = None, 0
     if m == _lib.MODE_SPLIT:

@@ -63,9 +63,11 @@ enum fjagg_flags {
   FJAGG_ACCUMULATE = 1 << 1,  /* fold starts from the current contents of the output */
   FJAGG_NONTEMPORAL = 1 << 2, /* non-temporal (streaming) loads of the client deltas */
   FJAGG_UNALIGNED = 1 << 3,   /* ptrs path: some pointer is not 16-byte aligned */
+  FJAGG_UNBALANCED = 1 << 4,  /* dense path: one tile per workgroup instead of a balanced
+                                 resident grid (tuning / A-B only) */
 };
 /* bits 8..15 of flags select a kernel shape of the dense path: 0 = automatic,
- * 1..7 = fixed (units per lane, clients in flight) for tuning; see fjagg.hip */
+ * 1..11 = fixed (units per lane, clients in flight, waves/SIMD) for tuning; see fjagg.hip */
 #define FJAGG_VARIANT(v) (((v)&0xff) << 8)
 
 enum fjagg_mode {

@@ -164,10 +164,10 @@ def test_dense_all_variants_bitwise(K, P, cuda, coracle):
     r = ref.mean_scale(wi)
     want = coracle.wsum_f32(xh, np.float32(wi), scale=r)
     w = torch.tensor(np.float32(wi), device=cuda)
-    for variant in range(8):
-        for nt in (False, True):
-            y = kernels.weighted_sum_dense(x, w, scale=float(r), variant=variant, nontemporal=nt)
-            assert np.array_equal(bits(host(y)), bits(want)), (variant, nt)
+    for variant in range(16):
+        for nt, bal in ((False, True), (True, True), (True, False)):
+            y = kernels.weighted_sum_dense(x, w, scale=float(r), variant=variant, nontemporal=nt, balanced=bal)
+            assert np.array_equal(bits(host(y)), bits(want)), (variant, nt, bal)
 
 
 def test_dense_accumulate_and_strided_rows(cuda, coracle):

@@ -1,0 +1,12 @@
+#!/bin/bash
+set -u
+OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+run() { local name=$1 lim=$2 a1=$3; shift 3; timeout -k 10 "$lim" "$@"; local rc=$?; echo "[$name] rc=$rc"; if [ $rc -eq 0 ] || { [ $a1 = 1 ] && [ $rc -eq 1 ]; }; then return 0; fi; exit $rc; }
+run gpu-tests 900 1 bash -c "python -m pytest tests -q -m gpu -rf > $OUT/r01_gpu_tests_s4.log 2>&1"
+tail -3 $OUT/r01_gpu_tests_s4.log
+run sweep 900 0 bash -c "python tools/sweep.py 1024 16777216 bf16 > $OUT/r01_sweep.jsonl && python tools/sweep.py 128 1206590 f32 3 10 >> $OUT/r01_sweep.jsonl && python tools/sweep.py 1024 4194304 f32 3 5 >> $OUT/r01_sweep.jsonl && python tools/sweep.py 128 4194304 f32 3 10 >> $OUT/r01_sweep.jsonl"
+cat $OUT/r01_sweep.jsonl
+run bench-c2 300 0 bash -c "python bench.py --workload c2 --no-cpu-baseline > $OUT/r01_bench_c2b.json 2>&1"
+cat $OUT/r01_bench_c2b.json
+run bench-c5s 600 0 bash -c "python bench.py --workload c5s --steps 5 --warmup 2 > $OUT/r01_bench_c5s.json 2>&1"
+cat $OUT/r01_bench_c5s.json

@@ -1,0 +1,8 @@
+#!/bin/bash
+set -u
+OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+run() { local name=$1 lim=$2 a1=$3; shift 3; timeout -k 10 "$lim" "$@"; local rc=$?; echo "[$name] rc=$rc"; if [ $rc -eq 0 ] || { [ $a1 = 1 ] && [ $rc -eq 1 ]; }; then return 0; fi; exit $rc; }
+run gpu-tests 900 1 bash -c "python -m pytest tests -q -m gpu -rf -k 'dense_all_variants or golden or split' > $OUT/r01_gpu_tests_s6.log 2>&1"
+tail -3 $OUT/r01_gpu_tests_s6.log
+run sweep 1500 0 bash -c "python tools/sweep.py 1024 4194304 f32 3 5 > $OUT/r01_sweep3.jsonl && python tools/sweep.py 128 4194304 f32 3 10 >> $OUT/r01_sweep3.jsonl && python tools/sweep.py 128 2097152 f32 3 10 >> $OUT/r01_sweep3.jsonl && python tools/sweep.py 128 1048576 f32 3 10 >> $OUT/r01_sweep3.jsonl && python tools/sweep.py 1024 16777216 bf16 2 3 >> $OUT/r01_sweep3.jsonl && python tools/sweep.py 128 1206590 f32 3 10 >> $OUT/r01_sweep3.jsonl"
+cat $OUT/r01_sweep3.jsonl
