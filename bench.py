@@ -113,6 +113,8 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also time host-resident deltas (H2D + fold + D2H)")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--all-ranks", action="store_true", help="all_reduce instead of reduce to rank 0")
+    ap.add_argument("--with-norms", action="store_true",
+                    help="fuse every client's delta l2 norm into the fold (examples/fed_avg.py:79-81)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -155,13 +157,20 @@ def main():
     nt = (nbytes_local >= tu.NONTEMPORAL_MIN_BYTES) if args.nontemporal < 0 else bool(args.nontemporal)
     scale = float(np.float32(tu._inverse(W)))
     stream = torch.cuda.current_stream(dev)
+    l2sq = torch.empty(Kl, dtype=torch.float32, device=dev) if args.with_norms else None
+    l2ws = torch.empty(max(4, int(kernels._lib.load().fjagg_wsum_l2_workspace_bytes(Kl, P))),
+                       dtype=torch.uint8, device=dev) if args.with_norms else None
     kernel_ms = []
 
     def fold(xs, wd, o, events):
         if events is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        kernels.weighted_sum_dense(xs, wd, scale=scale, out=o, nontemporal=nt, variant=args.variant)
+        if args.with_norms:
+            kernels.weighted_sum_l2_dense(xs, wd, scale=scale, out=o, l2sq=l2sq, nontemporal=nt,
+                                          workspace=l2ws)
+        else:
+            kernels.weighted_sum_dense(xs, wd, scale=scale, out=o, nontemporal=nt, variant=args.variant)
         if events is not None:
             e1.record(stream)
             events.append((e0, e1, xs.shape[0] * xs.shape[1] * esize))
@@ -236,10 +245,11 @@ def main():
                            f" + {'RCCL' if args.backend == 'nccl' else args.backend} "
                            f"{'all_reduce' if args.all_ranks else 'reduce'}" if world > 1 else ""),
                        "buckets": args.buckets if world > 1 else 1, "nontemporal": nt,
-                       "variant": args.variant},
+                       "variant": args.variant, "fused_l2_norms": bool(args.with_norms)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": load_traffic(args.workload),
-                         "kernel": "k_dense<f32> weighted fold", "bytes_per_launch": bytes_per_launch,
+                         "kernel": ("k_dense_l2 fold + per-client l2" if args.with_norms else "k_dense weighted fold"),
+                         "bytes_per_launch": bytes_per_launch,
                          "mean_launch_ms": round(mean_kernel_s * 1e3, 4)},
         }
         if e2e is not None:

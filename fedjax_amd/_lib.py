@@ -39,6 +39,8 @@ _SIGNATURES = {
     "fjagg_split_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_ptrs_plan": (_i64, [_i32, _i32, _vp, _i32, _vp, _i64]),
     "fjagg_wsum_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _i32, _vp]),
+    "fjagg_wsum_l2_workspace_bytes": (_i64, [_i64, _i64]),
+    "fjagg_wsum_l2_dense": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "fjagg_l2sq_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_l2sq_dense": (_i32, [_i32, _vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp]),
     "fjagg_l2sq_rows_workspace_bytes": (_i64, [_i64, _i64]),

@@ -219,18 +219,47 @@ __device__ __forceinline__ void load_out_unit(const uint8_t* p, unsigned (&b)[V]
   }
 }
 
+// ------------------------------------------------------------- fused l2 hooks
+// Per-client sum of squares accumulated during the fold (fjagg_wsum_l2_dense):
+// each lane sums the squares of its units of client k, the wave reduces that with
+// a fixed xor butterfly and lane 0 adds it to its wave's LDS slot [wave][k].
+struct NoNorm {
+  template <class T, int V>
+  __device__ __forceinline__ void add(const T (&)[V], bool) {}
+  __device__ __forceinline__ void end_client(int64_t) {}
+};
+struct LdsNorm {
+  float* slot;  // this wave's K floats in LDS
+  float q;
+  template <class T, int V>
+  __device__ __forceinline__ void add(const T (&t)[V], bool valid) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) s = __fadd_rn(s, __fmul_rn((float)t[i], (float)t[i]));
+    q = __fadd_rn(q, valid ? s : 0.f);
+  }
+  __device__ __forceinline__ void end_client(int64_t k) {
+    float v = q;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o, 64));
+    if ((threadIdx.x & 63) == 0) slot[k] = __fadd_rn(slot[k], v);
+    q = 0.f;
+  }
+};
+
 // ------------------------------------------------------------------ fold body
 // Each lane folds E units; unit j of this lane sits at byte offset off[j] of every
 // client row (a 32-bit lane constant) and is written to outp[j]. row(k) returns the
 // wave-uniform base address of client k. Clients are folded in order 0..K-1.
 // The output of the unit at input byte offset off is at obase + off / sizeof(IN) *
 // sizeof(OUT) (same element index); valid[j] == false skips unit j's store.
-template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, class RowFn>
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, class RowFn,
+          class NORM = NoNorm>
 __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
                                      const uint32_t (&off)[E],
                                      uint8_t* __restrict__ obase, const bool (&valid)[E],
                                      const typename ACC::T* __restrict__ w, bool do_scale,
-                                     float scale, bool accumulate) {
+                                     float scale, bool accumulate, NORM nrm = NORM()) {
   constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
   auto outp = [&](int j) { return obase + (size_t)(off[j] / IB) * OB; };
   using T = typename ACC::T;
@@ -246,9 +275,11 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
     for (int j = 0; j < E; ++j) {
       T t[V];
       decode<IN, ACC, V>(v[j], t);
+      nrm.add(t, valid[j]);
 #pragma unroll
       for (int i = 0; i < V; ++i) acc[j][i] = ACC::mul(t[i], w0);
     }
+    nrm.end_client(0);
     if (accumulate) {
 #pragma unroll
       for (int j = 0; j < E; ++j) {
@@ -275,9 +306,11 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
       for (int j = 0; j < E; ++j) {
         T t[V];
         decode<IN, ACC, V>(v[u][j], t);
+        nrm.add(t, valid[j]);
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(acc[j][i], ACC::mul(t[i], wk));
       }
+      nrm.end_client(k + u);
     }
   }
   for (; k < K; ++k) {
@@ -287,9 +320,11 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
     for (int j = 0; j < E; ++j) {
       T t[V];
       decode<IN, ACC, V>(load_unit<IN, V, NT>(r, off[j]), t);
+      nrm.add(t, valid[j]);
 #pragma unroll
       for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(acc[j][i], ACC::mul(t[i], wk));
     }
+    nrm.end_client(k);
   }
 #pragma unroll
   for (int j = 0; j < E; ++j) {
@@ -353,6 +388,92 @@ __global__ __launch_bounds__(kThreads, MINW) void k_dense(
     }
     fold<IN, ACC, OUT, V, E, U, NT>(row, row_bytes, kn, off, ob, valid, wb, do_scale != 0,
                                     scale, accumulate != 0);
+  }
+}
+
+// k_dense + per-client squared norms (exact mode, float fold). Dynamic LDS holds
+// (kThreads/64) x K floats; block b writes its per-client partials to ws[b*K + k]
+// and k_l2_combine adds the gridDim.x partials of each client in block order.
+template <int IN, int OUT, int V, int E, int U, bool NT>
+__global__ __launch_bounds__(kThreads) void k_dense_l2(
+    const uint8_t* __restrict__ x, int64_t ld_bytes, int64_t K, int64_t nunits, int tail_n,
+    const float* __restrict__ w, float scale, int do_scale, int accumulate,
+    uint8_t* __restrict__ out, int64_t S, float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) float l2lds[];
+  constexpr int IB = Elem<IN>::B;
+  const int tid = threadIdx.x;
+  for (int64_t i = tid; i < (kThreads / 64) * K; i += kThreads) l2lds[i] = 0.f;
+  __syncthreads();
+  LdsNorm nrm{l2lds + (tid >> 6) * K, 0.f};
+  auto row = [=](int64_t k) { return x + k * ld_bytes; };
+  const uint32_t row_bytes = (uint32_t)((nunits * V + tail_n) * IB);
+  int64_t b = blockIdx.x;
+  bool is_tail = false;
+  if (tail_n > 0) {
+    if (b == 0) {
+      is_tail = true;
+      const bool active = tid < tail_n;  // every lane joins the wave reductions
+      const int64_t e = nunits * V + (active ? tid : 0);
+      const uint32_t off[1] = {(uint32_t)(e * IB)};
+      const bool valid[1] = {active};
+      fold<IN, AccF, OUT, 1, 1, U, NT>(row, row_bytes, K, off, out, valid, w, do_scale != 0,
+                                       scale, accumulate != 0, nrm);
+    }
+    b -= 1;
+  }
+  if (!is_tail) {
+    const int64_t u_begin = b * S;
+    const int64_t u_end = (u_begin + S < nunits) ? u_begin + S : nunits;
+    for (int64_t g = u_begin; g < u_end; g += (int64_t)kThreads * E) {
+      uint32_t off[E];
+      bool valid[E];
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        int64_t u = g + j * kThreads + tid;
+        valid[j] = u < u_end;
+        if (!valid[j]) u = u_end - 1;
+        off[j] = (uint32_t)(u * (V * IB));
+      }
+      fold<IN, AccF, OUT, V, E, U, NT>(row, row_bytes, K, off, out, valid, w, do_scale != 0,
+                                       scale, accumulate != 0, nrm);
+    }
+  }
+  __syncthreads();
+  for (int64_t k = tid; k < K; k += kThreads) {
+    float t = l2lds[k];
+#pragma unroll
+    for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, l2lds[i * K + k]);
+    ws[(int64_t)blockIdx.x * K + k] = t;
+  }
+}
+
+// out[k] = sum over b of ws[b*K + k]. Workgroup = 64 clients x 16 waves: wave w sums
+// partials b = w, w+16, ... (coalesced 256-B rows, 4 loads in flight), then the 16
+// wave sums are added in wave order: deterministic, latency cost ~nb/64 loads.
+constexpr int kCombineWaves = 16;
+__global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* __restrict__ ws,
+                                                                   int64_t nb, int64_t K,
+                                                                   float* __restrict__ out) {
+  __shared__ float part[kCombineWaves][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t k = (int64_t)blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (k < K) {
+    int64_t b = wv;
+    for (; b + 3 * kCombineWaves < nb; b += 4 * kCombineWaves) {
+      const float a0 = ws[b * K + k], a1 = ws[(b + kCombineWaves) * K + k];
+      const float a2 = ws[(b + 2 * kCombineWaves) * K + k], a3 = ws[(b + 3 * kCombineWaves) * K + k];
+      s = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(s, a0), a1), a2), a3);
+    }
+    for (; b < nb; b += kCombineWaves) s = __fadd_rn(s, ws[b * K + k]);
+  }
+  part[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && k < K) {
+    float t = part[0][lane];
+#pragma unroll
+    for (int i = 1; i < kCombineWaves; ++i) t = __fadd_rn(t, part[i][lane]);
+    out[k] = t;
   }
 }
 
@@ -560,19 +681,20 @@ struct DenseArgs {
 struct Residency {
   int cus, per_cu;
 };
-Residency residency(const void* kern) {
+Residency residency(const void* kern, size_t smem = 0) {
   static std::mutex mu;
   static std::unordered_map<const void*, Residency> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  const void* key = reinterpret_cast<const void*>(reinterpret_cast<uintptr_t>(kern) ^ ((uintptr_t)dev << 56));
+  const void* key = reinterpret_cast<const void*>(reinterpret_cast<uintptr_t>(kern) ^
+                                                  ((uintptr_t)dev << 56) ^ ((uintptr_t)smem << 40));
   {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
   }
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0) != hipSuccess || per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, smem) != hipSuccess || per_cu < 1)
     per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
@@ -581,6 +703,20 @@ Residency residency(const void* kern) {
   std::lock_guard<std::mutex> g(mu);
   cache[key] = r;
   return r;
+}
+
+// Balanced grid (see launch_dense_t): units per workgroup S and workgroup count.
+void balanced_grid(const Residency& r, int64_t nunits, int64_t tile, int64_t gy, int64_t* S_out,
+                   int64_t* nblk_out) {
+  const int64_t ntiles = (nunits + tile - 1) / tile;
+  const int64_t cus = (r.cus + gy - 1) / gy;
+  int64_t c = (ntiles + cus - 1) / cus;
+  if (c > r.per_cu) c = r.per_cu;
+  if (c < 1) c = 1;
+  int64_t S = ((nunits + cus * c - 1) / (cus * c) + 63) / 64 * 64;
+  if (S < 64) S = 64;
+  *S_out = S;
+  *nblk_out = (nunits + S - 1) / S;
 }
 
 template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW>
@@ -593,13 +729,7 @@ void launch_dense_t(const DenseArgs& a, int64_t gy, hipStream_t s) {
     // The same number of workgroups on every CU (c <= what fits at once), each
     // with an equal, wave-aligned share of the parameter axis: every CU streams
     // the same bytes and no workgroup waits for a slot (profiles/r01_sweep3.jsonl).
-    const Residency r = residency(reinterpret_cast<const void*>(kern));
-    const int64_t cus = (r.cus + gy - 1) / gy;  // CUs per client range (split mode)
-    int64_t c = (ntiles + cus - 1) / cus;
-    if (c > r.per_cu) c = r.per_cu;
-    if (c < 1) c = 1;
-    S = ((a.nunits + cus * c - 1) / (cus * c) + 63) / 64 * 64;
-    nblk = (a.nunits + S - 1) / S;
+    balanced_grid(residency(reinterpret_cast<const void*>(kern)), a.nunits, tile, gy, &S, &nblk);
   }
   dim3 grid((unsigned)(nblk + (a.tail_n > 0 ? 1 : 0)), (unsigned)gy);
   hipLaunchKernelGGL(kern, grid, dim3(kThreads), 0, s, a.x, a.ld_bytes, a.K, a.nunits, a.tail_n,
@@ -776,6 +906,44 @@ int launch_ptrs_io(bool vec, bool nt, const int64_t* img, int L, int64_t K, int6
   return launch_ptrs_t<IN, ACC, OUT, 1>(nt, img, L, K, nblk, w, scale, do_scale, accumulate, s);
 }
 
+template <int IN, int OUT, int V, int E, int U, bool NT>
+int launch_dense_l2_t(const DenseArgs& a, float* ws, int64_t ws_floats, float* l2, hipStream_t s) {
+  auto kern = k_dense_l2<IN, OUT, V, E, U, NT>;
+  const size_t smem = (size_t)(kThreads / 64) * a.K * sizeof(float);
+  int64_t S = (int64_t)kThreads * E, nblk = 0;
+  balanced_grid(residency(reinterpret_cast<const void*>(kern), smem), a.nunits, (int64_t)kThreads * E,
+                1, &S, &nblk);
+  if (a.nunits == 0) nblk = 0;
+  const int64_t grid = nblk + (a.tail_n > 0 ? 1 : 0);
+  if (grid * a.K > ws_floats)
+    return fail(FJAGG_EINVAL, "l2 workspace too small (%lld workgroups x %lld clients)",
+                (long long)grid, (long long)a.K);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), smem, s, a.x, a.ld_bytes, a.K,
+                     a.nunits, a.tail_n, reinterpret_cast<const float*>(a.w), a.scale, a.do_scale,
+                     a.accumulate, a.out, S, ws);
+  int rc = check_launch("k_dense_l2");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((a.K + 63) / 64)), dim3(64 * kCombineWaves), 0, s,
+                     ws, grid, a.K, l2);
+  return check_launch("k_l2_combine");
+}
+
+template <int IN, int OUT>
+int launch_dense_l2_io(bool vec, bool nt, int variant, const DenseArgs& a, float* ws,
+                       int64_t ws_floats, float* l2, hipStream_t s) {
+  constexpr int VW = vec_width<IN>();
+  if (!vec)
+    return nt ? launch_dense_l2_t<IN, OUT, 1, 1, 8, true>(a, ws, ws_floats, l2, s)
+              : launch_dense_l2_t<IN, OUT, 1, 1, 8, false>(a, ws, ws_floats, l2, s);
+  if (variant == 12)
+    return nt ? launch_dense_l2_t<IN, OUT, VW, 8, 4, true>(a, ws, ws_floats, l2, s)
+              : launch_dense_l2_t<IN, OUT, VW, 8, 4, false>(a, ws, ws_floats, l2, s);
+  return nt ? launch_dense_l2_t<IN, OUT, VW, 1, 8, true>(a, ws, ws_floats, l2, s)
+            : launch_dense_l2_t<IN, OUT, VW, 1, 8, false>(a, ws, ws_floats, l2, s);
+}
+
+constexpr int64_t kL2MaxClients = 4096;  // (kThreads/64) x K floats of LDS <= 64 KiB
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -887,6 +1055,66 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
   FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
 #undef FJ_CASE
   return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination");
+}
+
+int64_t fjagg_wsum_l2_workspace_bytes(int64_t K, int64_t P) {
+  if (K < 1 || P < 1) return 0;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  (void)hipGetLastError();
+  const int64_t max_blocks = (int64_t)cus * (2048 / kThreads) + 1;  // resident cap + tail block
+  return max_blocks * K * 4;
+}
+
+int fjagg_wsum_l2_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_dev, int64_t ld,
+                        int64_t K, int64_t P, const void* w_dev, float scale, void* out_dev,
+                        float* l2sq_dev, int flags, void* ws_dev, int64_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  int rc = validate_common(in_dtype, acc_dtype, out_dtype, K, flags, scale);
+  if (rc) return rc;
+  if (acc_dtype != FJAGG_F32 || in_dtype == FJAGG_I32 || out_dtype == FJAGG_I32)
+    return fail(FJAGG_EUNSUPPORTED, "fused l2 norms need float inputs and a float fold");
+  if (K > kL2MaxClients)
+    return fail(FJAGG_EUNSUPPORTED, "fused l2 norms support K <= %lld", (long long)kL2MaxClients);
+  if (P < 1 || ld < P) return fail(FJAGG_EINVAL, "need 1 <= P <= ld");
+  if (P * elem_bytes(in_dtype) > kMaxRowBytes)
+    return fail(FJAGG_EUNSUPPORTED, "fused l2 norms need rows <= 1 GiB");
+  if (!x_dev || !w_dev || !out_dev || !l2sq_dev || !ws_dev)
+    return fail(FJAGG_EINVAL, "null pointer argument");
+  const int ib = elem_bytes(in_dtype), vw = vwidth(in_dtype);
+  const uint8_t* x = reinterpret_cast<const uint8_t*>(x_dev);
+  uint8_t* y = reinterpret_cast<uint8_t*>(out_dev);
+  const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) % 16 == 0) &&
+                   ((ld * ib) % 16 == 0) && P >= vw;
+  const int V = vec ? vw : 1;
+  DenseArgs a;
+  a.x = x;
+  a.ld_bytes = ld * ib;
+  a.K = K;
+  a.nunits = P / V;
+  a.tail_n = (int)(P - a.nunits * V);
+  a.w = w_dev;
+  a.scale = scale;
+  a.do_scale = (flags & FJAGG_SCALE) ? 1 : 0;
+  a.accumulate = (flags & FJAGG_ACCUMULATE) ? 1 : 0;
+  a.out = y;
+  a.kchunk = K;
+  a.out_ystride = 0;
+  a.balanced = true;
+  const int variant = pick_variant(a.nunits, K);
+  const bool nt = (flags & FJAGG_NONTEMPORAL) != 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* ws = reinterpret_cast<float*>(ws_dev);
+  const int64_t wsf = ws_bytes / 4;
+  if (in_dtype == FJAGG_F32 && out_dtype == FJAGG_F32)
+    return launch_dense_l2_io<FJAGG_F32, FJAGG_F32>(vec, nt, variant, a, ws, wsf, l2sq_dev, s);
+  if (in_dtype == FJAGG_BF16 && out_dtype == FJAGG_BF16)
+    return launch_dense_l2_io<FJAGG_BF16, FJAGG_BF16>(vec, nt, variant, a, ws, wsf, l2sq_dev, s);
+  if (in_dtype == FJAGG_BF16 && out_dtype == FJAGG_F32)
+    return launch_dense_l2_io<FJAGG_BF16, FJAGG_F32>(vec, nt, variant, a, ws, wsf, l2sq_dev, s);
+  return fail(FJAGG_EUNSUPPORTED, "fused l2 norms: unsupported dtype combination");
 }
 
 int64_t fjagg_l2sq_workspace_bytes(int64_t K, int64_t P) {

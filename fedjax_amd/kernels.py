@@ -90,6 +90,35 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
     return out
 
 
+def weighted_sum_l2_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[float] = None,
+                          out: Optional[torch.Tensor] = None, l2sq: Optional[torch.Tensor] = None,
+                          accumulate: bool = False, nontemporal: bool = False,
+                          workspace: Optional[torch.Tensor] = None):
+    """``weighted_sum_dense`` (exact mode, float fold) plus every client's squared
+    L2 norm from the same pass: returns ``(out[P], l2sq[K])``."""
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("x must be a [K, P] tensor with unit column stride")
+    K, P = x.shape
+    if w.shape != (K,) or w.dtype != torch.float32 or not w.is_contiguous():
+        raise TypeError(f"w must be a contiguous float32 tensor of shape ({K},)")
+    if out is None:
+        out = torch.empty(P, dtype=x.dtype, device=x.device)
+    if l2sq is None:
+        l2sq = torch.empty(K, dtype=torch.float32, device=x.device)
+    dev = _require_device(x, w, out, l2sq)
+    need = int(_lib.load().fjagg_wsum_l2_workspace_bytes(K, P))
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty(max(need, 4), dtype=torch.uint8, device=dev)
+    flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
+    flags |= _lib.NONTEMPORAL if nontemporal else 0
+    ld = x.stride(0) if K > 1 else P
+    _lib.call("fjagg_wsum_l2_dense", dtype_code(x.dtype), _lib.F32, dtype_code(out.dtype), x.data_ptr(),
+              ld, K, P, w.data_ptr(), float(scale if scale is not None else 1.0), out.data_ptr(),
+              l2sq.data_ptr(), flags, workspace.data_ptr(), workspace.numel() * workspace.element_size(),
+              _stream_handle(dev))
+    return out, l2sq
+
+
 def split_workspace_bytes(K: int, P: int) -> int:
     return int(_lib.load().fjagg_split_workspace_bytes(K, P))
 

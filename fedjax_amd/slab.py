@@ -91,14 +91,27 @@ class ClientDeltaSlab:
             self.rows, w_dev, scale=None if scale is None else float(np.float32(scale)), out=out,
             accumulate=accumulate, mode=mode, nontemporal=nt, variant=variant)
 
-    def mean(self, weights: Sequence, *, out: Optional[torch.Tensor] = None, mode: str = "exact") -> PyTree:
+    def mean(self, weights: Sequence, *, out: Optional[torch.Tensor] = None, mode: str = "exact",
+             with_norms: bool = False):
         """Weighted mean of the K rows — ``tree_mean(zip(clients, weights))`` with the
-        reference's W and f32(1/W) (tree_util.py:86-96), one dense launch."""
+        reference's W and f32(1/W) (tree_util.py:86-96), one dense launch.
+
+        ``with_norms=True`` also returns every client's delta l2 norm (float32[K],
+        the ``delta_l2_norm`` diagnostic of examples/fed_avg.py:79-81) computed in
+        the same pass over the slab: ``(mean, norms)``."""
         W = 0.0
         for x in weights:
             W += tree_util._host_weight(x)
-        flat = self.weighted_sum_flat(self.weight_vector(weights), scale=tree_util._inverse(W),
-                                      out=out, mode=mode)
+        scale = tree_util._inverse(W)
+        if with_norms:
+            if mode != "exact":
+                raise ValueError("fused norms run in exact mode")
+            nbytes = self.rows.numel() * self.rows.element_size()
+            flat, l2sq = kernels.weighted_sum_l2_dense(
+                self.rows, self.weight_vector(weights), scale=float(np.float32(scale)), out=out,
+                nontemporal=nbytes >= tree_util.NONTEMPORAL_MIN_BYTES)
+            return self.unflatten(flat), torch.sqrt(l2sq)
+        flat = self.weighted_sum_flat(self.weight_vector(weights), scale=scale, out=out, mode=mode)
         return self.unflatten(flat)
 
     def l2_norms(self) -> torch.Tensor:

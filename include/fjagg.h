@@ -126,6 +126,21 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
                     int flags, void* stream);
 
 /*
+ * fjagg_wsum_dense (exact mode) fused with the per-client squared L2 norms of the
+ * same deltas, in ONE pass over the K x P slab: out as fjagg_wsum_dense (bitwise
+ * the same), l2sq_dev[k] = sum_p x_k[p]^2 in f32 with a fixed reduction order
+ * (lane partials -> wave xor-butterfly -> LDS per wave -> workgroups in order).
+ * Replaces the per-client tree_l2_norm pass of examples/fed_avg.py:79-81 and
+ * fedjax/algorithms/fed_avg.py:142-144 (tree_util.py:105-114) for the whole round.
+ * Float inputs (f32, bf16), float fold, K <= 4096, rows <= 1 GiB.
+ */
+int64_t fjagg_wsum_l2_workspace_bytes(int64_t K, int64_t P);
+int fjagg_wsum_l2_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_dev,
+                        int64_t ld, int64_t K, int64_t P, const void* w_dev, float scale,
+                        void* out_dev, float* l2sq_dev, int flags, void* ws_dev,
+                        int64_t ws_bytes, void* stream);
+
+/*
  * Squared L2 norm of each of K client deltas (the per-client diagnostic of
  * examples/fed_avg.py:79-81 -> tree_util.py:105-108), accumulated in f32 per
  * workgroup and combined in a fixed order: deterministic, not bitwise equal to

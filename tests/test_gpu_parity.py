@@ -338,3 +338,45 @@ def test_running_mean_equals_library_fedavg_loop(buffer_clients, cuda, coracle):
     want = s * np.float32(1.0 / W)
     assert np.array_equal(bits(got), bits(want))
     assert rm.num_clients == K and rm.total_weight == W
+
+
+# ------------------------------------------------------------ fused fold + l2 norms
+@pytest.mark.parametrize("K,P,dt", [(1, 7, "f32"), (37, 10007, "f32"), (128, 1206590, "f32"),
+                                    (300, 65536 + 5, "f32"), (64, 20000, "bf16"), (5, 3, "f32")])
+def test_fused_l2_matches_fold_and_norms(K, P, dt, cuda, coracle):
+    tdt = torch.float32 if dt == "f32" else torch.bfloat16
+    vw = 4 if dt == "f32" else 8
+    x = torch.empty(K, (P + vw - 1) // vw * vw, dtype=tdt, device=cuda)[:, :P]
+    kernels.fill_synth(x, seed=31)
+    wi = [int(v) for v in ref.fedavg_weights(K, seed=32)]
+    r = float(ref.mean_scale(wi))
+    w = torch.tensor(np.float32(wi), device=cuda)
+    y0 = kernels.weighted_sum_dense(x, w, scale=r)
+    for nt in (False, True):
+        y1, l2 = kernels.weighted_sum_l2_dense(x, w, scale=r, nontemporal=nt)
+        assert np.array_equal(bits(host(y1)), bits(host(y0)))
+        xf = x.float().cpu().numpy().astype(np.float64)
+        want = (xf ** 2).sum(1)
+        npt.assert_allclose(host(l2), want, rtol=2e-6)
+    y2, l2b = kernels.weighted_sum_l2_dense(x, w, scale=r)
+    assert torch.equal(l2, l2b)  # deterministic
+
+
+def test_fused_l2_unaligned_and_slab(cuda, coracle):
+    K, P = 9, 1001
+    base = torch.empty(K, P + 1, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(base, seed=33)
+    x = base[:, 1:]
+    w = torch.arange(1, K + 1, dtype=torch.float32, device=cuda)
+    y, l2 = kernels.weighted_sum_l2_dense(x, w)
+    xh = coracle.synth_f32(K, P + 1, seed=33)[:, 1:]
+    assert np.array_equal(bits(host(y)), bits(coracle.wsum_f32(xh, np.arange(1, K + 1, dtype=np.float32))))
+    npt.assert_allclose(host(l2), (xh.astype(np.float64) ** 2).sum(1), rtol=2e-6)
+    template = {"a": np.zeros(100, np.float32), "b": np.zeros((7, 11), np.float32)}
+    slab = fedjax_amd.ClientDeltaSlab(template, 12, device=cuda).fill_synthetic(seed=34)
+    wi = list(range(1, 13))
+    m0 = slab.mean(wi)
+    m1, norms = slab.mean(wi, with_norms=True)
+    for a, b in zip(fedjax_amd.pytree.leaves_of(m0), fedjax_amd.pytree.leaves_of(m1)):
+        assert torch.equal(a, b)
+    npt.assert_allclose(host(norms), host(slab.l2_norms()), rtol=2e-6)
