@@ -50,7 +50,6 @@ int check_launch(const char* what) {
 }
 
 constexpr int kThreads = 256;   // 4 waves of 64
-constexpr int kPtrsE = 2;       // units per lane of the pytree kernel (fixed by the plan)
 constexpr int kSplitMax = 64;   // max client ranges in FJAGG_MODE_SPLIT
 constexpr int64_t kSplitHeader = 256;  // bytes of ones at the head of the split workspace
 
@@ -477,49 +476,67 @@ __global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* 
   }
 }
 
-// Pytree path. image = in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[nblk].
-// block word: bits 0..39 first unit, 40..61 leaf, 62 tail flag.
-template <int IN, class ACC, int OUT, int V, int U, bool NT>
+// Pytree path. image = in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk].
+// Block b: word 0 = first unit (bits 0..39) | leaf (40..61) | tail flag (62);
+// word 1 = end unit (exclusive). A workgroup walks its unit range of one leaf in
+// groups of kThreads*8 units (E=8, U=4: the dense default; lanes past the range
+// are masked) when the range gives a lane more than one unit, else in groups of
+// kThreads units (E=1, U=8).
+template <int IN, class ACC, int OUT, int V, bool NT>
 __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ img, int L,
                                                    int64_t K,
                                                    const typename ACC::T* __restrict__ w,
                                                    float scale, int do_scale, int accumulate) {
-  constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
-  constexpr int E = kPtrsE;
+  constexpr int IB = Elem<IN>::B;
   const int tid = threadIdx.x;
   const int64_t* in_ptrs = img;
   const int64_t* out_ptrs = img + K * L;
   const int64_t* leaf_n = out_ptrs + L;
-  const int64_t be = leaf_n[L + blockIdx.x];
+  const int64_t* blk = leaf_n + L + 2 * (int64_t)blockIdx.x;
+  const int64_t be = blk[0];
   const int leaf = (int)((be >> 40) & 0x3fffff);
   const bool tail = (be >> 62) & 1;
   const int64_t u0 = be & ((1ll << 40) - 1);
+  const int64_t u1 = blk[1];
   const int64_t n = leaf_n[leaf];
   const int64_t nunits = n / V;
   uint8_t* ob = reinterpret_cast<uint8_t*>(out_ptrs[leaf]);
   auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]); };
   const uint32_t row_bytes = (uint32_t)(n * IB);
+  const bool dsc = do_scale != 0, acm = accumulate != 0;
   if (tail) {
     if (tid < n - nunits * V) {
       const int64_t e = nunits * V + tid;
       const uint32_t off[1] = {(uint32_t)(e * IB)};
       const bool valid[1] = {true};
-      fold<IN, ACC, OUT, 1, 1, U, NT>(row, row_bytes, K, off, ob, valid, w, do_scale != 0,
-                                      scale, accumulate != 0);
+      fold<IN, ACC, OUT, 1, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm);
     }
     return;
   }
-  uint32_t off[E];
-  bool valid[E];
+  if constexpr (V > 1) {
+    if (u1 - u0 > (int64_t)kThreads) {  // more than one unit per lane: E=8 groups, masked
+      for (int64_t g = u0; g < u1; g += (int64_t)kThreads * 8) {
+        uint32_t off[8];
+        bool valid[8];
 #pragma unroll
-  for (int j = 0; j < E; ++j) {
-    int64_t u = u0 + j * kThreads + tid;
-    valid[j] = u < nunits;
-    if (!valid[j]) u = nunits - 1;
-    off[j] = (uint32_t)(u * (V * IB));
+        for (int j = 0; j < 8; ++j) {
+          int64_t u = g + j * kThreads + tid;
+          valid[j] = u < u1;
+          if (!valid[j]) u = u1 - 1;
+          off[j] = (uint32_t)(u * (V * IB));
+        }
+        fold<IN, ACC, OUT, V, 8, 4, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm);
+      }
+      return;
+    }
   }
-  fold<IN, ACC, OUT, V, E, U, NT>(row, row_bytes, K, off, ob, valid, w, do_scale != 0,
-                                  scale, accumulate != 0);
+  for (int64_t g = u0; g < u1; g += kThreads) {
+    int64_t u = g + tid;
+    const bool valid[1] = {u < u1};
+    if (!valid[0]) u = u1 - 1;
+    const uint32_t off[1] = {(uint32_t)(u * (V * IB))};
+    fold<IN, ACC, OUT, V, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm);
+  }
 }
 
 // Per-client sum of squares: grid (nb, K); ws[k*nb + b] = block partial (f32),
@@ -889,11 +906,11 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
                   float scale, int do_scale, int accumulate, hipStream_t s) {
   const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
   if (nt)
-    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, 8, true>), dim3((unsigned)nblk), dim3(kThreads), 0,
-                       s, img, L, K, wt, scale, do_scale, accumulate);
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
+                       img, L, K, wt, scale, do_scale, accumulate);
   else
-    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, 8, false>), dim3((unsigned)nblk), dim3(kThreads),
-                       0, s, img, L, K, wt, scale, do_scale, accumulate);
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
+                       img, L, K, wt, scale, do_scale, accumulate);
   return check_launch("k_ptrs");
 }
 
@@ -1010,23 +1027,41 @@ int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, i
     return fail(FJAGG_EINVAL, "bad dtype %d", in_dtype);
   if (L < 0 || L >= (1 << 22)) return fail(FJAGG_EINVAL, "bad leaf count %d", L);
   const int64_t V = (flags & FJAGG_UNALIGNED) ? 1 : vwidth(in_dtype);
-  const int64_t per = (int64_t)kThreads * kPtrsE;
-  int64_t nblk = 0;
-  for (int l = 0; l < L; ++l) {  // tails first: they are latency-bound, start them early
+  int64_t total = 0;
+  for (int l = 0; l < L; ++l) {
     const int64_t n = leaf_n[l];
     if (n < 0 || n * elem_bytes(in_dtype) > kMaxRowBytes)
       return fail(FJAGG_EINVAL, "leaf %d: %lld elements unsupported", l, (long long)n);
-    if (n % V) {
-      if (nblk < blocks_cap) blocks[nblk] = ((int64_t)l << 40) | (1ll << 62);
-      ++nblk;
-    }
+    total += n / V;
   }
+  // balanced unit share per workgroup, as for the dense path (balanced_grid): the
+  // same number of E=8 workgroups on every CU, at most kPlanPerCU of them per CU
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  (void)hipGetLastError();
+  constexpr int64_t kPlanPerCU = 3;  // E=8 x U=4 fold: 3 workgroups per CU (VGPR-limited)
+  const int64_t tile = (int64_t)kThreads * 8;
+  const int64_t ntiles = (total + tile - 1) / tile;
+  int64_t c = (ntiles + cus - 1) / cus;
+  if (c > kPlanPerCU) c = kPlanPerCU;
+  if (c < 1) c = 1;
+  int64_t S = ((total + cus * c - 1) / (cus * c) + 63) / 64 * 64;
+  if (S < 64) S = 64;
+  int64_t nblk = 0;
+  auto put = [&](int64_t w0, int64_t w1) {
+    if (nblk < blocks_cap) {
+      blocks[2 * nblk] = w0;
+      blocks[2 * nblk + 1] = w1;
+    }
+    ++nblk;
+  };
+  for (int l = 0; l < L; ++l)  // tails first: latency-bound, start them early
+    if (leaf_n[l] % V) put(((int64_t)l << 40) | (1ll << 62), 0);
   for (int l = 0; l < L; ++l) {
     const int64_t nunits = leaf_n[l] / V;
-    for (int64_t u = 0; u < nunits; u += per) {
-      if (nblk < blocks_cap) blocks[nblk] = ((int64_t)l << 40) | u;
-      ++nblk;
-    }
+    for (int64_t u = 0; u < nunits; u += S) put(((int64_t)l << 40) | u, (u + S < nunits) ? u + S : nunits);
   }
   return nblk;
 }

@@ -124,16 +124,16 @@ def split_workspace_bytes(K: int, P: int) -> int:
 
 
 def ptrs_plan(in_code: int, leaf_n: Sequence[int], unaligned: bool) -> np.ndarray:
-    """Block table of the pytree kernel (host int64 array)."""
+    """Workgroup table of the pytree kernel (host int64 array, 2 words per workgroup)."""
     lib = _lib.load()
     n = np.ascontiguousarray(leaf_n, dtype=np.int64)
     flags = _lib.UNALIGNED if unaligned else 0
     need = lib.fjagg_ptrs_plan(in_code, flags, n.ctypes.data, len(n), None, 0)
     _lib.check(0 if need >= 0 else int(need), "fjagg_ptrs_plan")
-    blocks = np.empty(max(need, 1), dtype=np.int64)
+    blocks = np.empty(2 * max(need, 1), dtype=np.int64)
     got = lib.fjagg_ptrs_plan(in_code, flags, n.ctypes.data, len(n), blocks.ctypes.data, need)
     _lib.check(0 if got >= 0 else int(got), "fjagg_ptrs_plan")
-    return blocks[:need]
+    return blocks[:2 * need]
 
 
 def weighted_sum_ptrs(in_code: int, acc_code: int, out_code: int, image_dev: torch.Tensor,

@@ -215,7 +215,7 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
         flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
         flags |= (_lib.UNALIGNED if unaligned else 0) | (_lib.NONTEMPORAL if nt else 0)
         _lib.call("fjagg_wsum_ptrs", in_c, acc_c, out_c, image_dev.data_ptr(), len(ls), K,
-                  len(blocks), w_dev_ptr, float(np.float32(scale) if scale is not None else 1.0),
+                  len(blocks) // 2, w_dev_ptr, float(np.float32(scale) if scale is not None else 1.0),
                   flags, torch.cuda.current_stream(device).cuda_stream)
     return outs
 

@@ -108,16 +108,17 @@ int64_t fjagg_split_workspace_bytes(int64_t K, int64_t P);
  * Pytree path: K clients x L leaves, each leaf a separate allocation.
  * Launches ONE kernel over every leaf. The plan image is an int64 array in
  * device memory laid out as
- *     in_ptrs [K*L]   client k, leaf l at k*L + l (device addresses)
+ *     in_ptrs [K*L]    client k, leaf l at k*L + l (device addresses)
  *     out_ptrs[L]
- *     leaf_n  [L]     elements per leaf
- *     blocks  [nblk]  from fjagg_ptrs_plan()
+ *     leaf_n  [L]      elements per leaf
+ *     blocks  [2*nblk] from fjagg_ptrs_plan(): per workgroup (first unit | leaf | tail
+ *                      flag, end unit), unit ranges balanced across the CUs
  * Replaces: jax.tree.map over leaves inside tree_weight/tree_add,
  * fedjax/core/tree_util.py:32,50, for the whole tree_mean loop :85-96.
  */
-/* Fills blocks[] (up to blocks_cap entries) for leaves of leaf_n[l] elements and
- * returns the number of blocks the plan needs (negative FJAGG_E* on error); call
- * with blocks_cap = 0 to size the array. flags: FJAGG_UNALIGNED if any client or
+/* Fills blocks[] (2 int64 per workgroup, up to blocks_cap workgroups) for leaves of
+ * leaf_n[l] elements and returns the number of workgroups the plan needs (negative
+ * FJAGG_E* on error); call with blocks_cap = 0 to size the array. flags: FJAGG_UNALIGNED if any client or
  * output pointer is not 16-byte aligned (the same flag must go to the launch). */
 int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, int64_t* blocks,
                         int64_t blocks_cap);

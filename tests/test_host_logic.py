@@ -54,36 +54,45 @@ def test_leaf_canonicalisation_rules():
 
 
 def _decode(blocks):
-    return [((b >> 40) & 0x3FFFFF, bool((b >> 62) & 1), b & ((1 << 40) - 1)) for b in blocks.tolist()]
+    b = blocks.reshape(-1, 2).tolist()
+    return [((w0 >> 40) & 0x3FFFFF, bool((w0 >> 62) & 1), w0 & ((1 << 40) - 1), w1) for w0, w1 in b]
 
 
 @pytest.mark.parametrize("unaligned", [False, True])
 def test_ptrs_plan_covers_every_unit_once(unaligned):
     leaf_n = [32, 288, 64, 18432, 128, 1179648, 62, 7936, 0, 3, 1]
     V = 1 if unaligned else 4
-    per = 256 * 2
     blocks = kernels.ptrs_plan(_lib.F32, leaf_n, unaligned)
-    seen = {l: [] for l in range(len(leaf_n))}
-    tails = set()
     dec = _decode(blocks)
     # tails come first (latency-bound blocks start early)
     first_main = next((i for i, d in enumerate(dec) if not d[1]), len(dec))
     assert all(d[1] for d in dec[:first_main]) and not any(d[1] for d in dec[first_main:])
-    for leaf, tail, u0 in dec:
-        if tail:
-            tails.add(leaf)
-        else:
-            seen[leaf].append(u0)
+    tails = {d[0] for d in dec if d[1]}
+    ranges = {l: [] for l in range(len(leaf_n))}
+    for leaf, tail, u0, u1 in dec:
+        if not tail:
+            assert u0 < u1
+            ranges[leaf].append((u0, u1))
+    sizes = [u1 - u0 for r in ranges.values() for u0, u1 in r]
     for l, n in enumerate(leaf_n):
+        r = sorted(ranges[l])
+        covered = [u for u0, u1 in r for u in (u0, u1)]
         nunits = n // V
-        assert sorted(seen[l]) == list(range(0, nunits, per))
+        if nunits:
+            assert r[0][0] == 0 and r[-1][1] == nunits
+            assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        else:
+            assert not r
         assert (l in tails) == (n % V != 0)
+    # balanced: every range is at most the common share S (a multiple of 64 units)
+    S = max(sizes)
+    assert S % 64 == 0 and all(sz <= S for sz in sizes)
 
 
 def test_ptrs_plan_bf16_units():
     blocks = kernels.ptrs_plan(_lib.BF16, [17], False)
     dec = _decode(blocks)
-    assert dec == [(0, True, 0), (0, False, 0)]  # 2 units of 8 + a 1-element tail
+    assert dec == [(0, True, 0, 0), (0, False, 0, 2)]  # 2 units of 8 + a 1-element tail
 
 
 def test_shard_range_partitions_clients():

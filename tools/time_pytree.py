@@ -69,5 +69,26 @@ def main(K=128, reps=20):
                       "dense_slab_GBs": dense}))
 
 
+def main_c3(K=1024, P=4 * 1024 * 1024, reps=5):
+    """configs[2] through tree_mean with every client delta its own allocation."""
+    dev = torch.device("cuda:0")
+    base = torch.empty(K, P, device=dev)
+    kernels.fill_synth(base, seed=0)
+    clients = [{"w": base[k]} for k in range(K)]  # separate rows = separate device pointers
+    weights = np.random.RandomState(1).randint(1, 501, size=K).tolist()
+    pairs = list(zip(clients, weights))
+    tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    print(json.dumps({"workload": "configs[2] via tree_mean, 1024 client tensors x 4 Mi f32",
+                      "tree_mean_wall_ms": round(wall * 1e3, 3),
+                      "tree_mean_wall_GBs": round(K * P * 4 / wall / 1e9, 1)}))
+
+
 if __name__ == "__main__":
     main()
+    main_c3()
