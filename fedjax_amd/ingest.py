@@ -23,6 +23,7 @@ The device-resident fold is ~120× faster, so the ingestion rate is the E2E rate
 from __future__ import annotations
 
 import enum
+import warnings
 from typing import Any, List, Optional, Union
 
 import msgpack
@@ -287,7 +288,12 @@ class DeltaIngestor:
                 raise ValueError(f"client {k}: leaf of {a.size} bytes, slab expects "
                                  f"{size * self.slab.storage.element_size()}")
             if a.size:  # torch's host copy is multithreaded for large buffers
-                src = torch.frombuffer(a, dtype=torch.uint8) if not a.flags.writeable else torch.from_numpy(a)
+                if a.flags.writeable:
+                    src = torch.from_numpy(a)
+                else:  # a read-only view into the payload: only ever read here
+                    with warnings.catch_warnings():
+                        warnings.simplefilter("ignore", UserWarning)
+                        src = torch.frombuffer(a, dtype=torch.uint8)
                 row[off:off + a.size].copy_(src)
             off += a.size
         dst = self.slab.storage[k].view(torch.uint8)[: self.row_bytes]

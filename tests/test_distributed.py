@@ -76,3 +76,40 @@ def test_sharded_mean_world2_gloo(all_ranks, coracle):
         y = res[rank][0]
         assert np.all(np.abs(y.astype(np.float64) - want) <= bound), rank
         assert res[rank][1] == float(sum(weights))
+
+
+def _worker_ragged(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fedjax_amd import distributed as fd
+        Kr = 7
+        weights = [0.5 + k for k in range(Kr)]
+        k0, k1 = fd.shard_range(Kr, rank, world)
+        x = torch.from_numpy(ref.synth(k1 - k0, 999, seed=4, k0=k0))
+        wl = torch.tensor(np.float32(weights[k0:k1]))
+        W = fd.total_weight(weights[k0:k1])
+        out = fd.sharded_weighted_mean(x, wl, W, buckets=2, partial_fn=_oracle_partial)
+        q.put((rank, k1 - k0, out.numpy().copy(), W))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ragged_shards_world3_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_ragged, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = {r: (n, y, W) for r, n, y, W in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [res[r][0] for r in range(3)] == [3, 2, 2]
+    weights = [0.5 + k for k in range(7)]
+    assert all(res[r][2] == sum(weights) for r in range(3))
+    x = ref.synth(7, 999, seed=4)
+    want = ref.wsum_dense(x, np.float32(weights), scale=ref.mean_scale(weights))
+    np.testing.assert_allclose(res[0][1], want, rtol=2e-6, atol=1e-9)

@@ -380,3 +380,80 @@ def test_fused_l2_unaligned_and_slab(cuda, coracle):
     for a, b in zip(fedjax_amd.pytree.leaves_of(m0), fedjax_amd.pytree.leaves_of(m1)):
         assert torch.equal(a, b)
     npt.assert_allclose(host(norms), host(slab.l2_norms()), rtol=2e-6)
+
+
+# ----------------------------------------------------------------- more edge cases
+def test_bf16_pytree_tree_mean_vs_f64(cuda, coracle):
+    K, P = 12, 5003
+    xb = coracle.synth_bf16(K, P, seed=51)
+    xt = torch.from_numpy(xb.view(np.int16)).view(torch.bfloat16).to(cuda)
+    cut = 2001
+    trees = [{"a": xt[k, :cut], "b": xt[k, cut:].reshape(-1)} for k in range(K)]
+    wi = [int(v) for v in ref.fedavg_weights(K, seed=52)]
+    m = tu.tree_mean(zip(trees, wi))
+    assert m["a"].dtype == torch.bfloat16
+    got = bf16_to_f32(np.concatenate([host(m["a"]), host(m["b"])])).astype(np.float64)
+    r = 1.0 / sum(wi)
+    y64 = coracle.wsum_bf16_f64(xb, np.float64(wi), r)
+    tsum = np.abs(bf16_to_f32(xb).astype(np.float64) * np.float32(wi)[:, None]).sum(0)
+    assert np.all(np.abs(got - y64) <= 2.0 ** -8 * np.abs(y64) + (K + 3) * U * r * tsum)
+
+
+def test_split_mode_bf16_and_accumulate(cuda, coracle):
+    K, P = 640, 3000
+    x = torch.empty(K, P + 8 - P % 8, dtype=torch.bfloat16, device=cuda)[:, :P]
+    kernels.fill_synth(x, seed=53)
+    xb = coracle.synth_bf16(K, P, seed=53)
+    w = np.float32(ref.fedavg_weights(K, seed=54))
+    wd = torch.from_numpy(w).to(cuda)
+    y = host(kernels.weighted_sum_dense(x, wd, out_dtype=torch.float32, mode="split"))
+    y64 = coracle.wsum_bf16_f64(xb, np.float64(w), 1.0)
+    tsum = np.abs(bf16_to_f32(xb).astype(np.float64) * w[:, None]).sum(0)
+    assert np.all(np.abs(y - y64) <= (K + 66) * U * tsum + U * np.abs(y64))
+    init = np.linspace(-1, 1, P).astype(np.float32)
+    out = torch.from_numpy(init.copy()).to(cuda)
+    kernels.weighted_sum_dense(x, wd, out=out, accumulate=True, mode="split")
+    y2 = host(out).astype(np.float64)
+    assert np.all(np.abs(y2 - (y64 + init)) <= (K + 67) * U * (tsum + np.abs(init)) + U * np.abs(y64 + init))
+
+
+def test_rows_over_one_gib_are_chunked(cuda):
+    K, P = 2, 300_000_000  # 1.2 GB rows: two column launches of <= 1 GiB each
+    x = torch.empty(K, P, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(x, seed=55)
+    wi = [3, 5]
+    y = kernels.weighted_sum_dense(x, torch.tensor(np.float32(wi), device=cuda), scale=float(ref.mean_scale(wi)))
+    cols = np.array([0, 1, 268435455, 268435456, 268435457, P - 1])
+    xs = synth_cols(K, cols, 55)
+    want = ref.wsum_dense(xs, np.float32(wi), scale=ref.mean_scale(wi))
+    assert np.array_equal(bits(host(y)[cols]), bits(want))
+    del x, y
+    torch.cuda.empty_cache()
+
+
+def test_int_dense_fold_with_scale_and_float_weights(cuda):
+    xi = (np.arange(40, dtype=np.int32).reshape(4, 10) - 20) * 1000
+    x = torch.from_numpy(xi).to(cuda)
+    wi = np.array([3, 1, 4, 1], np.int32)
+    y = kernels.weighted_sum_dense(x, torch.from_numpy(wi).to(cuda), scale=0.125)
+    s = (xi * wi[:, None]).sum(0).astype(np.int32)
+    assert y.dtype == torch.float32 and np.array_equal(host(y), s.astype(np.float32) * np.float32(0.125))
+    wf = np.float32([0.5, 1.5, 2.0, 0.25])
+    yf = kernels.weighted_sum_dense(x, torch.from_numpy(wf).to(cuda))
+    want = ref.wsum_dense(xi.astype(np.float32), wf)
+    assert np.array_equal(bits(host(yf)), bits(want))
+
+
+def test_empty_and_scalar_leaves(cuda):
+    trees = [({"e": torch.zeros(0, device=cuda), "s": torch.tensor(float(k), device=cuda),
+               "v": torch.full((3,), float(k), device=cuda)}, k + 1) for k in range(3)]
+    m = tu.tree_mean(trees)
+    assert m["e"].shape == (0,) and m["s"].shape == ()
+    want = (0 * 1 + 1 * 2 + 2 * 3) / 6
+    npt.assert_allclose(host(m["s"]), want, rtol=1e-7)
+    npt.assert_allclose(host(m["v"]), [want] * 3, rtol=1e-7)
+
+
+def test_oversize_leaf_is_rejected():
+    with pytest.raises(_lib.FjaggError):
+        kernels.ptrs_plan(_lib.F32, [300_000_000], False)
