@@ -247,7 +247,8 @@ def main():
                        "buckets": args.buckets if world > 1 else 1, "nontemporal": nt,
                        "variant": args.variant, "fused_l2_norms": bool(args.with_norms)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": load_traffic(args.workload),
+                         "frac": round(achieved / PEAK_HBM_GBS, 4),
+                         "traffic": load_traffic(args.workload) if (world == 1 and not args.with_norms) else None,
                          "kernel": ("k_dense_l2 fold + per-client l2" if args.with_norms else "k_dense weighted fold"),
                          "bytes_per_launch": bytes_per_launch,
                          "mean_launch_ms": round(mean_kernel_s * 1e3, 4)},
