@@ -23,6 +23,7 @@ the oracle's C restatement of the reference op sequence (oracle/fold_ref.c,
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -113,6 +114,8 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also time host-resident deltas (H2D + fold + D2H)")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--all-ranks", action="store_true", help="all_reduce instead of reduce to rank 0")
+    ap.add_argument("--server", choices=["none", "sgd", "adam"], default="none",
+                    help="fuse the server optimizer step into the fold (N=1; examples/fed_avg.py:97-101)")
     ap.add_argument("--with-norms", action="store_true",
                     help="fuse every client's delta l2 norm into the fold (examples/fed_avg.py:79-81)")
     args = ap.parse_args()
@@ -157,6 +160,7 @@ def main():
     nt = (nbytes_local >= tu.NONTEMPORAL_MIN_BYTES) if args.nontemporal < 0 else bool(args.nontemporal)
     scale = float(np.float32(tu._inverse(W)))
     stream = torch.cuda.current_stream(dev)
+    nonlocal_state = [None]
     l2sq = torch.empty(Kl, dtype=torch.float32, device=dev) if args.with_norms else None
     l2ws = torch.empty(max(4, int(kernels._lib.load().fjagg_wsum_l2_workspace_bytes(Kl, P))),
                        dtype=torch.uint8, device=dev) if args.with_norms else None
@@ -175,9 +179,30 @@ def main():
             e1.record(stream)
             events.append((e0, e1, xs.shape[0] * xs.shape[1] * esize))
 
+    if args.server != "none":
+        if world > 1 or dtype != torch.float32:
+            raise SystemExit("--server runs at N=1 on f32 slabs")
+        from fedjax_amd import _lib as flib, server as fsrv
+        sopt = fsrv.sgd(10 ** -1.5) if args.server == "sgd" else fsrv.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)
+        sparams = torch.zeros(P, dtype=torch.float32, device=dev)
+        sstate = sopt.init(sparams)
+
     def step(events=None):
         wd = torch.from_numpy(np.float32(w_local)).pin_memory().to(dev, non_blocking=True)
-        if world == 1:
+        if args.server != "none":
+            nonlocal_state[0] = sopt.descriptor(1)
+            if events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            flib.call("fjagg_server_update_dense", flib.F32, x.data_ptr(), x.stride(0), Kl, P, wd.data_ptr(),
+                      scale, ctypes.byref(nonlocal_state[0]), sparams.data_ptr(),
+                      sstate.get("m").data_ptr() if "m" in sstate else None,
+                      sstate.get("v").data_ptr() if "v" in sstate else None, None,
+                      flib.NONTEMPORAL if nt else 0, stream.cuda_stream)
+            if events is not None:
+                e1.record(stream)
+                events.append((e0, e1, Kl * P * esize))
+        elif world == 1:
             fold(x, wd, out, events)
         else:
             fd.sharded_weighted_mean(x, wd, W, buckets=args.buckets, out=out, all_ranks=args.all_ranks,
@@ -245,11 +270,14 @@ def main():
                            f" + {'RCCL' if args.backend == 'nccl' else args.backend} "
                            f"{'all_reduce' if args.all_ranks else 'reduce'}" if world > 1 else ""),
                        "buckets": args.buckets if world > 1 else 1, "nontemporal": nt,
-                       "variant": args.variant, "fused_l2_norms": bool(args.with_norms)},
+                       "variant": args.variant, "fused_l2_norms": bool(args.with_norms),
+                       "fused_server_step": args.server},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4),
-                         "traffic": load_traffic(args.workload) if (world == 1 and not args.with_norms) else None,
-                         "kernel": ("k_dense_l2 fold + per-client l2" if args.with_norms else "k_dense weighted fold"),
+                         "traffic": load_traffic(args.workload) if (world == 1 and not args.with_norms
+                                                                    and args.server == "none") else None,
+                         "kernel": ("k_dense_opt fold + server " + args.server if args.server != "none" else
+                                    "k_dense_l2 fold + per-client l2" if args.with_norms else "k_dense weighted fold"),
                          "bytes_per_launch": bytes_per_launch,
                          "mean_launch_ms": round(mean_kernel_s * 1e3, 4)},
         }

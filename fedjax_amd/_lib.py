@@ -39,6 +39,7 @@ _SIGNATURES = {
     "fjagg_split_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_ptrs_plan": (_i64, [_i32, _i32, _vp, _i32, _vp, _i64]),
     "fjagg_wsum_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _i32, _vp]),
+    "fjagg_server_update_dense": (_i32, [_i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "fjagg_wsum_l2_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_wsum_l2_dense": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "fjagg_l2sq_workspace_bytes": (_i64, [_i64, _i64]),
@@ -48,6 +49,17 @@ _SIGNATURES = {
     "fjagg_fill_synth": (_i32, [_i32, _vp, _i64, _i64, _i64, _i64, _u64, _f32, _vp]),
 }
 SYMBOLS = tuple(_SIGNATURES)
+
+
+class ServerOpt(ctypes.Structure):
+    """struct fjagg_server_opt (include/fjagg.h)."""
+    _fields_ = [("kind", ctypes.c_int), ("nesterov", ctypes.c_int), ("neg_lr", ctypes.c_float),
+                ("decay", ctypes.c_float), ("one_minus_b1", ctypes.c_float), ("b1", ctypes.c_float),
+                ("one_minus_b2", ctypes.c_float), ("b2", ctypes.c_float), ("bc1", ctypes.c_float),
+                ("bc2", ctypes.c_float), ("eps", ctypes.c_float), ("eps_root", ctypes.c_float)]
+
+
+OPT_SGD, OPT_MOMENTUM, OPT_ADAM = 1, 2, 3
 
 
 class FjaggError(RuntimeError):

@@ -246,6 +246,44 @@ struct LdsNorm {
   }
 };
 
+// ----------------------------------------------------------------- epilogues
+// PlainEpi: the fold's result goes to the output (tree_mean). OptEpi: the mean
+// y = fl(s * scale) feeds the server optimizer step of the round in registers
+// (optax sgd / trace / adam op sequence, fedjax/core/optimizers.py:57-66,148-178,
+// 227-250) and only the updated params and optimizer state are written.
+__device__ __forceinline__ float div_rn(float a, float b) { return (float)((double)a / (double)b); }
+__device__ __forceinline__ float sqrt_rn(float a) { return (float)__dsqrt_rn((double)a); }
+
+struct PlainEpi {};
+struct OptEpi {
+  fjagg_server_opt o;
+  float* __restrict__ params;
+  float* __restrict__ m;
+  float* __restrict__ v;
+  float* __restrict__ mean;  // optional: also store the mean (diagnostics)
+  __device__ __forceinline__ void apply(int64_t e, float g) const {
+    if (mean) mean[e] = g;
+    float p = params[e], u;
+    if (o.kind == FJAGG_OPT_SGD) {
+      u = g;
+    } else if (o.kind == FJAGG_OPT_MOMENTUM) {  // optax.trace: g + decay * t
+      const float t = __fadd_rn(g, __fmul_rn(o.decay, m[e]));
+      m[e] = t;
+      u = o.nesterov ? __fadd_rn(g, __fmul_rn(o.decay, t)) : t;
+    } else {  // optax.scale_by_adam
+      const float mu = __fadd_rn(__fmul_rn(o.one_minus_b1, g), __fmul_rn(o.b1, m[e]));
+      const float nu = __fadd_rn(__fmul_rn(o.one_minus_b2, __fmul_rn(g, g)), __fmul_rn(o.b2, v[e]));
+      m[e] = mu;
+      v[e] = nu;
+      // f32 div / sqrt evaluated in f64 and rounded once: correctly rounded (53 >=
+      // 2*24 + 2, double rounding is innocuous), as IEEE binary32 div/sqrt must be.
+      const float mh = div_rn(mu, o.bc1), nh = div_rn(nu, o.bc2);
+      u = div_rn(mh, __fadd_rn(sqrt_rn(__fadd_rn(nh, o.eps_root)), o.eps));
+    }
+    params[e] = __fadd_rn(p, __fmul_rn(o.neg_lr, u));  // scale_by_learning_rate, apply_updates
+  }
+};
+
 // ------------------------------------------------------------------ fold body
 // Each lane folds E units; unit j of this lane sits at byte offset off[j] of every
 // client row (a 32-bit lane constant) and is written to outp[j]. row(k) returns the
@@ -253,12 +291,13 @@ struct LdsNorm {
 // The output of the unit at input byte offset off is at obase + off / sizeof(IN) *
 // sizeof(OUT) (same element index); valid[j] == false skips unit j's store.
 template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, class RowFn,
-          class NORM = NoNorm>
+          class NORM = NoNorm, class EPI = PlainEpi>
 __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
                                      const uint32_t (&off)[E],
                                      uint8_t* __restrict__ obase, const bool (&valid)[E],
                                      const typename ACC::T* __restrict__ w, bool do_scale,
-                                     float scale, bool accumulate, NORM nrm = NORM()) {
+                                     float scale, bool accumulate, NORM nrm = NORM(),
+                                     const EPI& epi = EPI()) {
   constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
   auto outp = [&](int j) { return obase + (size_t)(off[j] / IB) * OB; };
   using T = typename ACC::T;
@@ -328,10 +367,16 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     if (!valid[j]) continue;
-    unsigned b[V];
+    if constexpr (std::is_same<EPI, OptEpi>::value) {
+      const int64_t e0 = off[j] / IB;
 #pragma unroll
-    for (int i = 0; i < V; ++i) b[i] = finish<OUT, ACC>(acc[j][i], do_scale, scale);
-    store_unit<OUT, V>(outp(j), b);
+      for (int i = 0; i < V; ++i) epi.apply(e0 + i, __uint_as_float(finish<FJAGG_F32, ACC>(acc[j][i], do_scale, scale)));
+    } else {
+      unsigned b[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) b[i] = finish<OUT, ACC>(acc[j][i], do_scale, scale);
+      store_unit<OUT, V>(outp(j), b);
+    }
   }
 }
 
@@ -473,6 +518,46 @@ __global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* 
 #pragma unroll
     for (int i = 1; i < kCombineWaves; ++i) t = __fadd_rn(t, part[i][lane]);
     out[k] = t;
+  }
+}
+
+// Exact fold of the slab + the server optimizer step in the epilogue (no mean
+// round trip through HBM). Same grid/unit layout as k_dense.
+template <int IN, int V, int E, int U, bool NT>
+__global__ __launch_bounds__(kThreads) void k_dense_opt(
+    const uint8_t* __restrict__ x, int64_t ld_bytes, int64_t K, int64_t nunits, int tail_n,
+    const float* __restrict__ w, float scale, int64_t S, OptEpi epi) {
+  constexpr int IB = Elem<IN>::B;
+  const int tid = threadIdx.x;
+  auto row = [=](int64_t k) { return x + k * ld_bytes; };
+  const uint32_t row_bytes = (uint32_t)((nunits * V + tail_n) * IB);
+  int64_t b = blockIdx.x;
+  if (tail_n > 0) {
+    if (b == 0) {
+      if (tid < tail_n) {
+        const uint32_t off[1] = {(uint32_t)((nunits * V + tid) * IB)};
+        const bool valid[1] = {true};
+        fold<IN, AccF, FJAGG_F32, 1, 1, U, NT>(row, row_bytes, K, off, nullptr, valid, w, true,
+                                               scale, false, NoNorm(), epi);
+      }
+      return;
+    }
+    b -= 1;
+  }
+  const int64_t u_begin = b * S;
+  const int64_t u_end = (u_begin + S < nunits) ? u_begin + S : nunits;
+  for (int64_t g = u_begin; g < u_end; g += (int64_t)kThreads * E) {
+    uint32_t off[E];
+    bool valid[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      int64_t u = g + j * kThreads + tid;
+      valid[j] = u < u_end;
+      if (!valid[j]) u = u_end - 1;
+      off[j] = (uint32_t)(u * (V * IB));
+    }
+    fold<IN, AccF, FJAGG_F32, V, E, U, NT>(row, row_bytes, K, off, nullptr, valid, w, true, scale,
+                                           false, NoNorm(), epi);
   }
 }
 
@@ -959,6 +1044,33 @@ int launch_dense_l2_io(bool vec, bool nt, int variant, const DenseArgs& a, float
             : launch_dense_l2_t<IN, OUT, VW, 1, 8, false>(a, ws, ws_floats, l2, s);
 }
 
+template <int IN, int V, int E, int U, bool NT>
+int launch_dense_opt_t(const DenseArgs& a, const OptEpi& epi, hipStream_t s) {
+  auto kern = k_dense_opt<IN, V, E, U, NT>;
+  int64_t S = (int64_t)kThreads * E, nblk = 0;
+  balanced_grid(residency(reinterpret_cast<const void*>(kern)), a.nunits, (int64_t)kThreads * E, 1,
+                &S, &nblk);
+  if (a.nunits == 0) nblk = 0;
+  const int64_t grid = nblk + (a.tail_n > 0 ? 1 : 0);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), 0, s, a.x, a.ld_bytes, a.K,
+                     a.nunits, a.tail_n, reinterpret_cast<const float*>(a.w), a.scale, S, epi);
+  return check_launch("k_dense_opt");
+}
+
+template <int IN>
+int launch_dense_opt_io(bool vec, bool nt, int variant, const DenseArgs& a, const OptEpi& epi,
+                        hipStream_t s) {
+  constexpr int VW = vec_width<IN>();
+  if (!vec)
+    return nt ? launch_dense_opt_t<IN, 1, 1, 8, true>(a, epi, s)
+              : launch_dense_opt_t<IN, 1, 1, 8, false>(a, epi, s);
+  if (variant == 12)
+    return nt ? launch_dense_opt_t<IN, VW, 8, 4, true>(a, epi, s)
+              : launch_dense_opt_t<IN, VW, 8, 4, false>(a, epi, s);
+  return nt ? launch_dense_opt_t<IN, VW, 1, 8, true>(a, epi, s)
+            : launch_dense_opt_t<IN, VW, 1, 8, false>(a, epi, s);
+}
+
 constexpr int64_t kL2MaxClients = 4096;  // (kThreads/64) x K floats of LDS <= 64 KiB
 
 }  // namespace
@@ -1090,6 +1202,46 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
   FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
 #undef FJ_CASE
   return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination");
+}
+
+int fjagg_server_update_dense(int in_dtype, const void* x_dev, int64_t ld, int64_t K, int64_t P,
+                              const float* w_dev, float scale, const fjagg_server_opt* opt,
+                              float* params_dev, float* m_dev, float* v_dev, float* mean_dev,
+                              int flags, void* stream) {
+  g_err[0] = 0;
+  if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16)
+    return fail(FJAGG_EUNSUPPORTED, "server update: f32 or bf16 deltas");
+  if (!opt || opt->kind < FJAGG_OPT_SGD || opt->kind > FJAGG_OPT_ADAM)
+    return fail(FJAGG_EINVAL, "server update: bad optimizer descriptor");
+  if (K < 1 || P < 1 || ld < P) return fail(FJAGG_EINVAL, "bad shape (K=%lld, P=%lld)", (long long)K, (long long)P);
+  if (P * elem_bytes(in_dtype) > kMaxRowBytes) return fail(FJAGG_EUNSUPPORTED, "rows > 1 GiB");
+  if (!x_dev || !w_dev || !params_dev) return fail(FJAGG_EINVAL, "null pointer argument");
+  if (opt->kind != FJAGG_OPT_SGD && !m_dev) return fail(FJAGG_EINVAL, "optimizer state m is null");
+  if (opt->kind == FJAGG_OPT_ADAM && !v_dev) return fail(FJAGG_EINVAL, "optimizer state v is null");
+  const int ib = elem_bytes(in_dtype), vw = vwidth(in_dtype);
+  const uint8_t* x = reinterpret_cast<const uint8_t*>(x_dev);
+  const bool vec = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && ((ld * ib) % 16 == 0) && P >= vw;
+  const int V = vec ? vw : 1;
+  DenseArgs a;
+  a.x = x;
+  a.ld_bytes = ld * ib;
+  a.K = K;
+  a.nunits = P / V;
+  a.tail_n = (int)(P - a.nunits * V);
+  a.w = w_dev;
+  a.scale = scale;
+  a.do_scale = 1;
+  a.accumulate = 0;
+  a.out = nullptr;
+  a.kchunk = K;
+  a.out_ystride = 0;
+  a.balanced = true;
+  const OptEpi epi{*opt, params_dev, m_dev, v_dev, mean_dev};
+  const int variant = pick_variant(a.nunits, K);
+  const bool nt = (flags & FJAGG_NONTEMPORAL) != 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (in_dtype == FJAGG_F32) return launch_dense_opt_io<FJAGG_F32>(vec, nt, variant, a, epi, s);
+  return launch_dense_opt_io<FJAGG_BF16>(vec, nt, variant, a, epi, s);
 }
 
 int64_t fjagg_wsum_l2_workspace_bytes(int64_t K, int64_t P) {

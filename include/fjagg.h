@@ -142,6 +142,37 @@ int fjagg_wsum_l2_dense(int in_dtype, int acc_dtype, int out_dtype, const void* 
                         int64_t ws_bytes, void* stream);
 
 /*
+ * Server optimizer step fused into the fold's epilogue. The round's mean
+ * g = fl(fold * scale) (bitwise the fjagg_wsum_dense value) is consumed in
+ * registers by the server optimizer of examples/fed_avg.py:97-101 /
+ * fedjax/algorithms/fed_avg.py:150-154, restating optax's op sequence
+ * (fedjax/core/optimizers.py:57-66 apply = update + apply_updates):
+ *   SGD       p += neg_lr * g
+ *   MOMENTUM  t = g + decay*t; u = nesterov ? g + decay*t : t; p += neg_lr * u
+ *   ADAM      mu = (1-b1) g + b1 mu; nu = (1-b2) g*g + b2 nu;
+ *             u = (mu/bc1) / (sqrt(nu/bc2 + eps_root) + eps); p += neg_lr * u
+ * with every constant pre-rounded to f32 on the host as JAX's weak typing does
+ * (bc1 = f32(1 - b1^t), bc2 = f32(1 - b2^t) for the step count t after the
+ * increment). params, m (mu / trace) and v (nu) are float32[P], updated in place;
+ * mean_dev (optional) also receives g. Only the params/state are written: the
+ * mean never round-trips through HBM.
+ */
+enum fjagg_opt_kind { FJAGG_OPT_SGD = 1, FJAGG_OPT_MOMENTUM = 2, FJAGG_OPT_ADAM = 3 };
+typedef struct fjagg_server_opt {
+  int kind;
+  int nesterov;
+  float neg_lr;
+  float decay;
+  float one_minus_b1, b1, one_minus_b2, b2;
+  float bc1, bc2;
+  float eps, eps_root;
+} fjagg_server_opt;
+int fjagg_server_update_dense(int in_dtype, const void* x_dev, int64_t ld, int64_t K, int64_t P,
+                              const float* w_dev, float scale, const fjagg_server_opt* opt,
+                              float* params_dev, float* m_dev, float* v_dev, float* mean_dev,
+                              int flags, void* stream);
+
+/*
  * Squared L2 norm of each of K client deltas (the per-client diagnostic of
  * examples/fed_avg.py:79-81 -> tree_util.py:105-108), accumulated in f32 per
  * workgroup and combined in a fixed order: deterministic, not bitwise equal to

@@ -457,3 +457,65 @@ def test_empty_and_scalar_leaves(cuda):
 def test_oversize_leaf_is_rejected():
     with pytest.raises(_lib.FjaggError):
         kernels.ptrs_plan(_lib.F32, [300_000_000], False)
+
+
+# ------------------------------------------------------- fused server optimizer step
+def _np_server_step(opt, d, g, p, m, v):
+    """numpy restatement of optax's op order (sgd / trace / scale_by_adam, then
+    scale_by_learning_rate and apply_updates) with the descriptor's f32 constants."""
+    f = np.float32
+    if opt.kind == 1:
+        u = g
+    elif opt.kind == 2:
+        m = g + f(d.decay) * m
+        u = g + f(d.decay) * m if opt.nesterov else m
+    else:
+        m = f(d.one_minus_b1) * g + f(d.b1) * m
+        v = f(d.one_minus_b2) * (g * g) + f(d.b2) * v
+        u = (m / f(d.bc1)) / (np.sqrt(v / f(d.bc2) + f(d.eps_root)) + f(d.eps))
+    return p + f(d.neg_lr) * u, m, v
+
+
+@pytest.mark.parametrize("make", [lambda s: s.sgd(0.5), lambda s: s.sgd(0.1, momentum=0.9),
+                                  lambda s: s.sgd(0.1, momentum=0.9, nesterov=True),
+                                  lambda s: s.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)])
+def test_fused_server_update_matches_restated_optax(make, cuda, coracle):
+    from fedjax_amd import server
+    opt = make(server)
+    K, P = 33, 10007
+    template = {"a": np.zeros(7, np.float32), "b": np.zeros(P - 7, np.float32)}
+    slab = fedjax_amd.ClientDeltaSlab(template, K, device=cuda)
+    params = torch.from_numpy(coracle.synth_f32(1, P, seed=61)[0].copy()).to(cuda)
+    state = opt.init(params)
+    p_np = host(params).copy()
+    m_np = np.zeros(P, np.float32)
+    v_np = np.zeros(P, np.float32)
+    for rnd in range(3):
+        slab.fill_synthetic(seed=62 + rnd)
+        xh = coracle.synth_f32(K, P, seed=62 + rnd)
+        wi = [int(x) for x in ref.fedavg_weights(K, seed=70 + rnd)]
+        mean_out = torch.empty(P, device=cuda)
+        state = server.fused_mean_update(slab, wi, opt, params, state, mean_out=mean_out)
+        g = coracle.wsum_f32(xh, np.float32(wi), scale=ref.mean_scale(wi))
+        assert np.array_equal(bits(host(mean_out)), bits(g))
+        d = opt.descriptor(state["count"])
+        p_np, m_np, v_np = _np_server_step(opt, d, g, p_np, m_np, v_np)
+        assert np.array_equal(bits(host(params)), bits(p_np)), rnd
+        if "m" in state:
+            assert np.array_equal(bits(host(state["m"])), bits(m_np))
+        if "v" in state:
+            assert np.array_equal(bits(host(state["v"])), bits(v_np))
+    assert state["count"] == 3
+
+
+def test_fused_server_update_reproduces_fedavg_example_kat(cuda):
+    # examples/fed_avg_test.py:52-56: server sgd(lr=1.0) after tree_mean of two clients
+    from fedjax_amd import server
+    deltas = [fr.client_update(fr.SERVER_PARAMS, x, 2, 2, 0)["w"] for _, x in fr.CLIENTS]
+    slab = fedjax_amd.ClientDeltaSlab({"w": np.zeros(3, np.float32)}, 2, device=cuda)
+    for k, d in enumerate(deltas):
+        slab.set_client(k, {"w": torch.from_numpy(d)})
+    params = torch.from_numpy(fr.SERVER_PARAMS["w"].copy()).to(cuda)
+    opt = server.sgd(1.0)
+    server.fused_mean_update(slab, [len(x) for _, x in fr.CLIENTS], opt, params, opt.init(params))
+    npt.assert_allclose(host(params), [0., 1.4425802, 2.8851604])
