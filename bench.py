@@ -160,7 +160,6 @@ def main():
     nt = (nbytes_local >= tu.NONTEMPORAL_MIN_BYTES) if args.nontemporal < 0 else bool(args.nontemporal)
     scale = float(np.float32(tu._inverse(W)))
     stream = torch.cuda.current_stream(dev)
-    nonlocal_state = [None]
     l2sq = torch.empty(Kl, dtype=torch.float32, device=dev) if args.with_norms else None
     l2ws = torch.empty(max(4, int(kernels._lib.load().fjagg_wsum_l2_workspace_bytes(Kl, P))),
                        dtype=torch.uint8, device=dev) if args.with_norms else None
@@ -190,12 +189,12 @@ def main():
     def step(events=None):
         wd = torch.from_numpy(np.float32(w_local)).pin_memory().to(dev, non_blocking=True)
         if args.server != "none":
-            nonlocal_state[0] = sopt.descriptor(1)
+            desc = sopt.descriptor(1)  # copied by value into the kernel arguments at launch
             if events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
             flib.call("fjagg_server_update_dense", flib.F32, x.data_ptr(), x.stride(0), Kl, P, wd.data_ptr(),
-                      scale, ctypes.byref(nonlocal_state[0]), sparams.data_ptr(),
+                      scale, ctypes.byref(desc), sparams.data_ptr(),
                       sstate.get("m").data_ptr() if "m" in sstate else None,
                       sstate.get("v").data_ptr() if "v" in sstate else None, None,
                       flib.NONTEMPORAL if nt else 0, stream.cuda_stream)
