@@ -8,13 +8,19 @@
 //   * one lane owns E "units" of 16 bytes (4 f32 / 8 bf16) of the parameter axis and
 //     walks all K clients in order, so the fold is the reference's exact sequence
 //     (no cross-lane reduction, no FMA: compiled with -ffp-contract=off);
-//   * the row base of client k is wave-uniform (an SGPR), the lane offset is a
-//     32-bit VGPR constant, so each load is one global_load_dwordx4 with saddr;
-//   * U clients are loaded before they are folded, giving U*E*16 B in flight per
-//     lane (latency hiding through MLP, not through LDS: there is no reuse);
+//   * each client row is read through a buffer descriptor built on the scalar unit
+//     (SGPRs) with a loop-invariant 32-bit lane offset: no address VGPRs per load,
+//     range-checked rows;
+//   * U clients are loaded before they are folded, giving E*U 16-byte loads in
+//     flight per lane (latency hiding through MLP, not through LDS: no reuse);
+//   * the grid is "balanced": the same number of workgroups on every CU, each with
+//     an equal contiguous share of the parameter axis (no tail of late workgroups);
 //   * element tails and unaligned leaves use the same body with 1-element units;
-//   * the pytree path walks a device-resident (client, leaf) pointer table with
-//     a block table, so ONE launch covers every leaf of every client;
+//   * the pytree path walks a device-resident (client, leaf) pointer table with a
+//     workgroup table of unit ranges, so ONE launch covers every leaf of every client;
+//   * epilogue variants: per-client l2 norms accumulated during the same pass
+//     (k_dense_l2), and the server optimizer step consuming the mean in registers
+//     (k_dense_opt);
 //   * FJAGG_MODE_SPLIT splits the client axis over blockIdx.y for shapes whose
 //     parameter axis cannot fill 256 CUs, and combines the range sums in order.
 #include <hip/hip_runtime.h>
