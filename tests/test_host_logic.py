@@ -112,3 +112,17 @@ def test_bucket_edges_are_aligned_and_cover():
             assert e[0][0] == 0 and e[-1][1] == P
             assert all(a[1] == b[0] for a, b in zip(e, e[1:]))
             assert all(p0 % distributed.BUCKET_ALIGN == 0 for p0, _ in e)
+
+
+def test_server_descriptor_constants_follow_jax_weak_typing():
+    from fedjax_amd import server
+    opt = server.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)
+    d = opt.descriptor(3)
+    f = np.float32
+    assert d.kind == _lib.OPT_ADAM
+    assert d.neg_lr == f(-(10 ** -2.5))
+    assert d.one_minus_b1 == f(1 - 0.9) and d.b1 == f(0.9)  # Python-float 1-b1, then f32
+    assert d.bc1 == f(1) - np.power(f(0.9), f(3)) and d.bc2 == f(1) - np.power(f(0.999), f(3))
+    s = server.sgd(0.1, momentum=0.9, nesterov=True)
+    assert s.kind == _lib.OPT_MOMENTUM and s.descriptor(1).nesterov == 1
+    assert server.sgd(1.0).kind == _lib.OPT_SGD
