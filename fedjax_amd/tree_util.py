@@ -86,10 +86,19 @@ pytree.register_leaf_type(torch.Tensor)
 pytree.register_leaf_type(np.ndarray)
 
 
-def _device_leaf(x, device: torch.device) -> torch.Tensor:
+def _device_index(device: torch.device) -> int:
+    """x.get_device() value of tensors on ``device`` (-1 for the host)."""
+    if device.type != "cuda":
+        return -1
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+def _device_leaf(x, device: torch.device, index: Optional[int] = None) -> torch.Tensor:
     """Leaf as a contiguous device tensor of a canonical dtype (jnp.asarray rules)."""
-    if type(x) is torch.Tensor and x.dtype in _NATIVE and x.device == device and x.is_contiguous():
-        return x  # the common case: a delta already on the GPU
+    if index is None:
+        index = _device_index(device)
+    if type(x) is torch.Tensor and x.dtype in _NATIVE and x.get_device() == index and x.is_contiguous():
+        return x  # the common case: a delta already on the GPU (cheapest accessors first)
     t = _to_tensor(x)
     dt = _CANONICAL.get(t.dtype)
     if dt is None:
@@ -168,11 +177,12 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
     device = rows[0][0].device if L else None
     outs: List[Optional[torch.Tensor]] = [None] * L
     groups = {}
-    sig0 = [(x.shape, x.dtype) for x in rows[0]]
+    # x.size() is ~8x cheaper than x.shape; this loop runs once per (client, leaf)
+    sig0 = [(x.size(), x.dtype) for x in rows[0]]
     for k in range(1, K):  # rows are on `device` already (_client_rows)
-        if [(x.shape, x.dtype) for x in rows[k]] != sig0:
+        if [(x.size(), x.dtype) for x in rows[k]] != sig0:
             for l, x in enumerate(rows[k]):
-                if x.shape != sig0[l][0]:
+                if x.size() != sig0[l][0]:
                     raise ValueError(f"leaf {l}: client {k} has shape {tuple(x.shape)}, "
                                      f"client 0 has {tuple(sig0[l][0])}")
                 if x.dtype != sig0[l][1]:
@@ -182,11 +192,11 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
         in_c, acc_c, out_dt = _leaf_rule(x0.dtype, kinds, scaled_kind)
         if out is not None:
             o = out[l]
-            if o.dtype != out_dt or o.shape != x0.shape or not o.is_contiguous() or o.device != device:
+            if o.dtype != out_dt or o.size() != x0.size() or not o.is_contiguous() or o.device != device:
                 raise ValueError(f"leaf {l}: destination must be a contiguous {out_dt} tensor "
                                  f"of shape {tuple(x0.shape)} on {device}")
         else:
-            o = torch.empty(x0.shape, dtype=out_dt, device=device)
+            o = torch.empty(x0.size(), dtype=out_dt, device=device)
         outs[l] = o
         groups.setdefault((in_c, acc_c, kernels.dtype_code(out_dt)), []).append(l)
 
@@ -223,9 +233,11 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
 def _client_rows(trees: Sequence[PyTree]) -> Tuple[pytree.TreeDef, List[List[torch.Tensor]]]:
     leaves0, td = pytree.flatten(trees[0])
     device = _find_device(leaves0)
-    rows = [[_device_leaf(x, device) for x in leaves0]]
+    idx = _device_index(device)
+    dl = _device_leaf
+    rows = [[dl(x, device, idx) for x in leaves0]]
     for t in trees[1:]:
-        rows.append([_device_leaf(x, device) for x in pytree.flatten_as(td, t)])
+        rows.append([dl(x, device, idx) for x in pytree.flatten_as(td, t)])
     return td, rows
 
 

@@ -519,3 +519,14 @@ def test_fused_server_update_reproduces_fedavg_example_kat(cuda):
     opt = server.sgd(1.0)
     server.fused_mean_update(slab, [len(x) for _, x in fr.CLIENTS], opt, params, opt.init(params))
     npt.assert_allclose(host(params), [0., 1.4425802, 2.8851604])
+
+
+def test_emnist_fed_avg_rounds_example(cuda):
+    import importlib.util, os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples",
+                        "emnist_fed_avg_rounds.py")
+    spec = importlib.util.spec_from_file_location("emnist_rounds", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    hist = mod.run(rounds=3, verbose=False)
+    assert all(h["same_mean"] and h["same_params"] and h["norm_rel_diff"] < 2e-6 for h in hist), hist
