@@ -8,6 +8,7 @@ HIP kernels of ``libfjagg.so`` (C ABI: include/fjagg.h).
 """
 
 from fedjax_amd import aggregators
+from fedjax_amd import random
 from fedjax_amd import server
 from fedjax_amd import tree_util
 from fedjax_amd.dataclasses import dataclass

@@ -1,0 +1,389 @@
+"""Launch engine of the compression-aggregator kernels (include/fjcomp.h).
+
+Builds the (client, leaf) tables the kernels walk, uploads them in one pinned H2D
+copy per launch group, and strings the launches together for the three round
+shapes of ``fedjax/aggregators/compression.py``:
+
+* ``quantized_mean``   stats -> quantize + fold          (uniform, binary, terngrad)
+* ``rotated_quantized_mean``  shared rotation per leaf: signs -> WHT -> stats ->
+                       quantize + fold in the rotated domain -> ONE inverse WHT of
+                       the mean (the rotation is linear and identical for every
+                       client, compression.py:241-251, so the per-client inverses of
+                       the reference commute with the weighted mean)
+* ``drive_mean``       per-client rotation: signs -> WHT -> sums -> DRIVE + inverse
+                       WHT -> dense fold (compression.py:298-308)
+
+Everything is asynchronous on torch's current stream; only the arithmetic-coding
+bit count (``hist=True``) reads results back. Device work is batched over clients
+to a workspace budget so HBM holds K rotated deltas only when it fits.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from fedjax_amd import _lib
+
+ROW = np.dtype([("ptr", "<u8"), ("n", "<i8")])
+SIGN_JOB = np.dtype([("k0", "<u4"), ("k1", "<u4"), ("d", "<i8"), ("words", "<u8")])
+WHT_JOB = np.dtype([("src", "<u8"), ("mid", "<u8"), ("dst", "<u8"), ("signs", "<u8"), ("stats", "<u8"),
+                    ("n_in", "<i8"), ("n_out", "<i8"), ("log2d", "<i4"), ("kind", "<i4"),
+                    ("sqrt_d", "<f4"), ("reserved", "<f4")])
+QPARAMS = np.dtype([("vmin", "<f4"), ("vmax", "<f4"), ("range", "<f4"), ("thr", "<f4"), ("rcp_range", "<f8")])
+STATS = np.dtype([("min", "<f8"), ("max", "<f8"), ("absmax", "<f8"), ("sum", "<f8"), ("sumsq", "<f8"),
+                  ("sumabs", "<f8")])
+assert ROW.itemsize == 16 and SIGN_JOB.itemsize == 24 and WHT_JOB.itemsize == 72
+assert QPARAMS.itemsize == 24 and STATS.itemsize == 48
+
+WHT_BITS = 13       # butterfly bits of pass 0
+WHT_HIGH_BITS = 8   # butterfly bits of each later pass
+WHT_MAX_LOG2 = 34
+QBLOCK = 256  # k_quant_fold threads (element pairs) per workgroup
+SIGN_BLOCK = 256
+DEFAULT_WORKSPACE_BYTES = 4 << 30
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class Upload:
+    """Host tables packed 16-byte aligned into one pinned buffer, copied once."""
+
+    def __init__(self):
+        self._parts: List[Tuple[int, np.ndarray]] = []
+        self._size = 0
+        self.dev: Optional[torch.Tensor] = None
+
+    def add(self, arr: np.ndarray) -> int:
+        off = (self._size + 15) & ~15
+        b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        self._parts.append((off, b))
+        self._size = off + b.size
+        return off
+
+    def commit(self, device: torch.device) -> int:
+        host = np.zeros(max(self._size, 16), dtype=np.uint8)
+        for off, b in self._parts:
+            host[off:off + b.size] = b
+        self.dev = torch.from_numpy(host).pin_memory().to(device, non_blocking=True)
+        return self.dev.data_ptr()
+
+
+# ----------------------------------------------------------------------------- tiling
+def log2_exact(d: int) -> int:
+    m = int(d).bit_length() - 1
+    if d < 1 or (1 << m) != d:
+        raise ValueError(f"Walsh-Hadamard length must be a power of two, got {d}")
+    return m
+
+
+def padded_size(n: int) -> int:
+    """walsh_hadamard.py:142: ``2 ** ceil(log2(n))``."""
+    if n < 1:
+        raise ValueError("cannot rotate an empty leaf (the reference fails on log2(0))")
+    return 1 << (int(n) - 1).bit_length()
+
+
+def wht_passes(m: int) -> int:
+    return 1 if m <= WHT_BITS else 1 + -(-(m - WHT_BITS) // WHT_HIGH_BITS)
+
+
+def wht_pass_bits(m: int, p: int) -> Tuple[int, int]:
+    """(lo, nb): pass p does butterfly bits [lo, lo + nb)."""
+    lo = 0 if p == 0 else WHT_BITS + WHT_HIGH_BITS * (p - 1)
+    return lo, max(0, min(WHT_BITS if p == 0 else WHT_HIGH_BITS, m - lo))
+
+
+def wht_tiles(m: int, p: int) -> int:
+    """Tiles of pass p of a 2^m job (mirror of wht_tiling in fjcomp.hip)."""
+    if p >= wht_passes(m):
+        return 0
+    lo, nb = wht_pass_bits(m, p)
+    c = min(1 << lo, (1 << WHT_BITS) >> nb)
+    return (1 << m) // (c << nb)
+
+
+def sqrt_f32(d: int) -> float:
+    """``jnp.sqrt(d)`` for a Python int d: f32(sqrt(f32(d))), correctly rounded."""
+    return float(np.sqrt(np.float32(d)))
+
+
+# ----------------------------------------------------------------------------- launches
+def row_stats(rows: Sequence[Tuple[int, int]], method: int, device: torch.device,
+              want_qparams: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Stats (and quantizer parameters) of rows given as (device pointer, n)."""
+    R = len(rows)
+    tab = np.empty(R, dtype=ROW)
+    tab["ptr"] = [p for p, _ in rows]
+    tab["n"] = [n for _, n in rows]
+    if (tab["n"] < 1).any():
+        raise ValueError("quantizing an empty leaf: the reference fails on amin/amax of an empty array")
+    chunks = np.maximum(1, (tab["n"] + _lib.STATS_CHUNK - 1) // _lib.STATS_CHUNK)
+    prefix = np.concatenate([[0], np.cumsum(chunks)]).astype(np.int64)
+    nchunks = int(prefix[-1])
+    up = Upload()
+    o_rows, o_pre = up.add(tab), up.add(prefix)
+    base = up.commit(device)
+    stats = torch.empty(R * STATS.itemsize, dtype=torch.uint8, device=device)
+    qp = torch.empty(R * QPARAMS.itemsize, dtype=torch.uint8, device=device) if want_qparams else None
+    ws_bytes = int(_lib.load().fjcomp_row_stats_workspace_bytes(nchunks))
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device)
+    _lib.call("fjcomp_row_stats", base + o_rows, base + o_pre, R, nchunks, method, stats.data_ptr(),
+              None if qp is None else qp.data_ptr(), ws.data_ptr(), ws_bytes, _stream(device))
+    return stats, qp
+
+
+def qparams_host(vmin: float, vmax: float) -> np.ndarray:
+    """Quantizer parameters for explicitly given v_min / v_max (compression.py:58-61)."""
+    q = np.zeros(1, dtype=QPARAMS)
+    lo, hi = np.float32(vmin), np.float32(vmax)
+    rng = np.float32(hi - lo)
+    q["vmin"], q["vmax"], q["range"] = lo, hi, rng
+    with np.errstate(divide="ignore"):
+        q["rcp_range"] = np.float64(1.0) / np.float64(rng)
+    return q
+
+
+def quant_fold(method: int, in_ptrs: np.ndarray, keys: np.ndarray, qparams_ptr: int, w: np.ndarray,
+               leaf_n: np.ndarray, out_ptrs: np.ndarray, device: torch.device, *, num_levels: int = 2,
+               scale: Optional[float] = None, accumulate: bool = False,
+               hist: Optional[torch.Tensor] = None) -> None:
+    """k_quant_fold over in_ptrs [K, L] with keys [K, L, 2] and weights w [K]."""
+    K, L = in_ptrs.shape
+    leaf_n = np.ascontiguousarray(leaf_n, dtype=np.int64)
+    blocks = ((leaf_n + 1) // 2 + QBLOCK - 1) // QBLOCK
+    prefix = np.concatenate([[0], np.cumsum(blocks)]).astype(np.int64)
+    up = Upload()
+    o_in = up.add(np.ascontiguousarray(in_ptrs, dtype=np.uint64))
+    o_keys = up.add(np.ascontiguousarray(keys, dtype=np.uint32))
+    o_w = up.add(np.ascontiguousarray(w, dtype=np.float32))
+    o_n = up.add(leaf_n)
+    o_pre = up.add(prefix)
+    o_out = up.add(np.ascontiguousarray(out_ptrs, dtype=np.uint64))
+    base = up.commit(device)
+    flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
+    _lib.call("fjcomp_quant_fold", method, base + o_in, base + o_keys, qparams_ptr, base + o_w, K, L, base + o_n,
+              base + o_pre, int(prefix[-1]), int(num_levels), float(np.float32(scale if scale is not None else 1.0)),
+              flags, base + o_out, None if hist is None else hist.data_ptr(), _stream(device))
+    return up
+
+
+def rademacher_words(keys: np.ndarray, ds: Sequence[int], device: torch.device) -> Tuple[torch.Tensor, np.ndarray]:
+    """Sign bits for jobs (keys [J, 2], lengths ds): one word buffer, per-job word offsets."""
+    J = len(ds)
+    ds = np.asarray(ds, dtype=np.int64)
+    nwords = (ds + 31) // 32
+    woff = np.concatenate([[0], np.cumsum(nwords)]).astype(np.int64)
+    words = torch.empty(max(int(woff[-1]), 1), dtype=torch.int32, device=device)
+    jobs = np.empty(J, dtype=SIGN_JOB)
+    keys = np.asarray(keys, dtype=np.uint32).reshape(J, 2)
+    jobs["k0"], jobs["k1"], jobs["d"] = keys[:, 0], keys[:, 1], ds
+    jobs["words"] = words.data_ptr() + 4 * woff[:-1]
+    blocks = ((ds + 1) // 2 + SIGN_BLOCK - 1) // SIGN_BLOCK
+    prefix = np.concatenate([[0], np.cumsum(blocks)]).astype(np.int64)
+    up = Upload()
+    o_jobs, o_pre = up.add(jobs), up.add(prefix)
+    base = up.commit(device)
+    _lib.call("fjcomp_rademacher", base + o_jobs, base + o_pre, J, int(prefix[-1]), _stream(device))
+    return words, woff
+
+
+def run_wht(jobs: np.ndarray, device: torch.device) -> Upload:
+    """Launch every pass of the WHT jobs (structured WHT_JOB array)."""
+    J = len(jobs)
+    if J == 0:
+        return Upload()
+    ms = jobs["log2d"].astype(np.int64)
+    if (ms < 0).any() or (ms > WHT_MAX_LOG2).any():
+        raise ValueError("Walsh-Hadamard length out of range")
+    npass = max(wht_passes(int(m)) for m in ms)
+    pre = np.zeros((npass, J + 1), dtype=np.int64)
+    for p in range(npass):
+        pre[p, 1:] = np.cumsum([wht_tiles(int(m), p) for m in ms])
+    totals = np.ascontiguousarray(pre[:, -1])
+    up = Upload()
+    o_jobs, o_pre = up.add(jobs), up.add(pre)
+    base = up.commit(device)
+    _lib.call("fjcomp_wht", base + o_jobs, base + o_pre, J, npass, totals.ctypes.data, _stream(device))
+    return up
+
+
+def wht_job(src: int, mid: int, dst: int, d: int, *, kind: int, n_in: Optional[int] = None,
+            n_out: Optional[int] = None, signs: int = 0, stats: int = 0) -> np.ndarray:
+    j = np.zeros(1, dtype=WHT_JOB)
+    j["src"], j["mid"], j["dst"], j["signs"], j["stats"] = src, mid, dst, signs, stats
+    j["n_in"] = d if n_in is None else n_in
+    j["n_out"] = d if n_out is None else n_out
+    j["log2d"], j["kind"], j["sqrt_d"] = log2_exact(d), kind, sqrt_f32(d)
+    return j
+
+
+# ----------------------------------------------------------------------------- rounds
+def _leaf_layout(leaf_n: Sequence[int]):
+    ds = [padded_size(n) for n in leaf_n]
+    offs = np.concatenate([[0], np.cumsum(ds)]).astype(np.int64)
+    return ds, offs
+
+
+def _batch_size(K: int, per_client_bytes: int, budget: int) -> int:
+    return max(1, min(K, budget // max(per_client_bytes, 1)))
+
+
+def quantized_mean(method: int, rows: List[List[torch.Tensor]], keys: np.ndarray, w: np.ndarray,
+                   scale: Optional[float], outs: List[torch.Tensor], *, num_levels: int = 2,
+                   hist: bool = False, qparams: Optional[torch.Tensor] = None):
+    """outs[l] = [scale *] sum_k fl(Q(rows[k][l]) * w_k) (tree_mean over quantized
+    deltas). Returns (hist tensor or None, qparams tensor)."""
+    device = outs[0].device
+    K, L = len(rows), len(rows[0])
+    if qparams is None:
+        _, qparams = row_stats([(x.data_ptr(), x.numel()) for r in rows for x in r], method, device)
+    leaf_n = np.array([x.numel() for x in rows[0]], dtype=np.int64)
+    h = None
+    if hist:
+        if K * L * (num_levels + 1) > (1 << 28):
+            raise ValueError("arithmetic-coding histogram too large (K * leaves * (num_levels + 1) > 2^28)")
+        h = torch.zeros(K * L * (num_levels + 1), dtype=torch.int32, device=device)
+    in_ptrs = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.uint64)
+    out_ptrs = np.array([o.data_ptr() for o in outs], dtype=np.uint64)
+    quant_fold(method, in_ptrs, keys, qparams.data_ptr(), w, leaf_n, out_ptrs, device, num_levels=num_levels,
+               scale=scale, hist=h)
+    return h, qparams
+
+
+def rotated_quantized_mean(rows: List[List[torch.Tensor]], rot_keys: np.ndarray, client_keys: np.ndarray,
+                           w: np.ndarray, scale: Optional[float], outs: List[torch.Tensor], *, num_levels: int,
+                           workspace_bytes: int = DEFAULT_WORKSPACE_BYTES) -> None:
+    """rotated_uniform_stochastic_quantizer's round (compression.py:238-256), inverse
+    rotation applied once to the mean."""
+    device = outs[0].device
+    K, L = len(rows), len(rows[0])
+    leaf_n = [x.numel() for x in rows[0]]
+    ds, offs = _leaf_layout(leaf_n)
+    D = int(offs[-1])
+    signs, woff = rademacher_words(rot_keys, ds, device)
+    sptr = [signs.data_ptr() + 4 * int(o) for o in woff[:-1]]
+    acc = torch.empty(D, dtype=torch.float32, device=device)
+    B = _batch_size(K, 4 * D, workspace_bytes)
+    Y = torch.empty((B, D), dtype=torch.float32, device=device)
+    leaf_d = np.array(ds, dtype=np.int64)
+    keep = []
+    for k0 in range(0, K, B):
+        kb = min(B, K - k0)
+        jobs = np.concatenate([
+            wht_job(rows[k0 + b][l].data_ptr(), Y[b].data_ptr() + 4 * int(offs[l]),
+                    Y[b].data_ptr() + 4 * int(offs[l]), ds[l], kind=_lib.WHT_ROTATE, n_in=leaf_n[l], signs=sptr[l])
+            for b in range(kb) for l in range(L)])
+        keep.append(run_wht(jobs, device))
+        yrows = [(Y[b].data_ptr() + 4 * int(offs[l]), ds[l]) for b in range(kb) for l in range(L)]
+        _, qp = row_stats(yrows, _lib.COMP_UNIFORM, device)
+        in_ptrs = np.array([[p for p, _ in yrows[b * L:(b + 1) * L]] for b in range(kb)], dtype=np.uint64)
+        out_ptrs = np.array([acc.data_ptr() + 4 * int(offs[l]) for l in range(L)], dtype=np.uint64)
+        last = k0 + kb == K
+        keep.append(quant_fold(_lib.COMP_UNIFORM, in_ptrs, client_keys[k0:k0 + kb], qp.data_ptr(), w[k0:k0 + kb],
+                               leaf_d, out_ptrs, device, num_levels=num_levels,
+                               scale=scale if last else None, accumulate=k0 > 0))
+        keep.append(qp)
+    jobs = np.concatenate([
+        wht_job(acc.data_ptr() + 4 * int(offs[l]), acc.data_ptr() + 4 * int(offs[l]), outs[l].data_ptr(), ds[l],
+                kind=_lib.WHT_UNROTATE, n_out=leaf_n[l], signs=sptr[l]) for l in range(L)])
+    keep.append(run_wht(jobs, device))
+    # keep the tables alive until the stream has consumed them (the caching allocator
+    # reuses freed blocks only in stream order, so dropping them afterwards is safe)
+    del keep
+
+
+def drive_mean(rows: List[List[torch.Tensor]], client_keys: np.ndarray, w: np.ndarray, scale: Optional[float],
+               out_flat: torch.Tensor, *, workspace_bytes: int = DEFAULT_WORKSPACE_BYTES) -> None:
+    """structured_drive_quantizer's round (compression.py:292-308) into out_flat [P]
+    (leaves concatenated in flatten order)."""
+    from fedjax_amd import kernels  # local: kernels imports nothing from here
+
+    device = out_flat.device
+    K, L = len(rows), len(rows[0])
+    leaf_n = [x.numel() for x in rows[0]]
+    ds, offs = _leaf_layout(leaf_n)
+    D = int(offs[-1])
+    P = int(sum(leaf_n))
+    loff = np.concatenate([[0], np.cumsum(leaf_n)]).astype(np.int64)
+    Pp = (P + 3) // 4 * 4
+    B = _batch_size(K, 4 * (D + Pp), workspace_bytes)
+    Y = torch.empty((B, D), dtype=torch.float32, device=device)
+    Z = torch.empty((B, Pp), dtype=torch.float32, device=device)
+    w_dev = torch.from_numpy(np.ascontiguousarray(w, dtype=np.float32)).to(device)
+    for k0 in range(0, K, B):
+        kb = min(B, K - k0)
+        signs, woff = rademacher_words(client_keys[k0:k0 + kb].reshape(-1, 2), ds * kb, device)
+        sptr = lambda b, l: signs.data_ptr() + 4 * int(woff[b * L + l])
+        ydst = lambda b, l: Y[b].data_ptr() + 4 * int(offs[l])
+        fwd = np.concatenate([
+            wht_job(rows[k0 + b][l].data_ptr(), ydst(b, l), ydst(b, l), ds[l], kind=_lib.WHT_ROTATE,
+                    n_in=leaf_n[l], signs=sptr(b, l)) for b in range(kb) for l in range(L)])
+        t1 = run_wht(fwd, device)
+        stats, _ = row_stats([(ydst(b, l), ds[l]) for b in range(kb) for l in range(L)], 0, device,
+                             want_qparams=False)
+        inv = np.concatenate([
+            wht_job(ydst(b, l), ydst(b, l), Z[b].data_ptr() + 4 * int(loff[l]), ds[l],
+                    kind=_lib.WHT_UNROTATE_DRIVE, n_out=leaf_n[l], signs=sptr(b, l),
+                    stats=stats.data_ptr() + STATS.itemsize * (b * L + l)) for b in range(kb) for l in range(L)])
+        t2 = run_wht(inv, device)
+        last = k0 + kb == K
+        kernels.weighted_sum_dense(Z[:kb, :P], w_dev[k0:k0 + kb], scale=scale if last else None, out=out_flat,
+                                   accumulate=k0 > 0)
+        del t1, t2, signs, stats
+
+
+# ----------------------------------------------------------------------------- bits
+def _log2_f32(x: np.ndarray) -> np.ndarray:
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return (np.log(x.astype(np.float32)) / np.log(np.float32(2))).astype(np.float32)
+
+
+def arithmetic_bits_from_counts(counts: np.ndarray, d: int) -> np.float32:
+    """compression.py:125-149 given the histogram of the d values' distinct values."""
+    f32 = np.float32
+    hist = np.asarray(counts, dtype=np.int64)
+    k = hist.size
+    p = (hist.astype(f32) / f32(hist.sum())).astype(f32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ent = f32(-np.sum((p * _log2_f32(p)).astype(f32), dtype=f32))
+        e = f32(np.exp(f32(1)))
+        hist_bits = f32(f32(k) * _log2_f32(np.array([f32(f32(e * f32(d + k)) / f32(k))]))[0])
+    return f32(f32(f32(hist_bits + f32(f32(d) * ent)) + f32(64)) + f32(2))
+
+
+def arithmetic_bits(hist: torch.Tensor, qparams: torch.Tensor, K: int, leaf_n: Sequence[int],
+                    num_levels: int) -> List[np.float32]:
+    """Per-client bit counts (sum over leaves) from the level histograms: the level
+    values are recomputed with the kernel's f32 op sequence and equal values merged,
+    which is jnp.unique + jnp.histogram of the quantized leaf (compression.py:143-149)."""
+    f32 = np.float32
+    L = len(leaf_n)
+    nb = num_levels + 1
+    H = hist.cpu().numpy().reshape(K, L, nb)
+    Q = np.frombuffer(qparams.cpu().numpy().tobytes(), dtype=QPARAMS).reshape(K, L)
+    lm1 = f32(num_levels - 1)
+    with np.errstate(all="ignore"):
+        qv = (np.arange(num_levels, dtype=f32) / lm1).astype(f32)
+    out = []
+    for k in range(K):
+        bits = 0
+        for l in range(L):
+            q = Q[k, l]
+            with np.errstate(all="ignore"):
+                vals = (q["vmin"] + (qv * q["range"]).astype(f32)).astype(f32)
+            vals = np.concatenate([vals, [f32(np.nan)]])
+            vals = np.nan_to_num(vals, nan=0.0, posinf=np.finfo(f32).max, neginf=-np.finfo(f32).max).astype(f32)
+            cnt = H[k, l]
+            nz = cnt > 0
+            uniq, inv = np.unique(vals[nz], return_inverse=True)
+            merged = np.zeros(uniq.size, dtype=np.int64)
+            np.add.at(merged, inv, cnt[nz])
+            bits = bits + arithmetic_bits_from_counts(merged, int(leaf_n[l]))
+        out.append(f32(bits))
+    return out

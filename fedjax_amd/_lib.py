@@ -1,4 +1,5 @@
-"""ctypes binding of ``libfjagg.so`` — the C ABI declared in ``include/fjagg.h``.
+"""ctypes binding of ``libfjagg.so`` — the C ABI declared in ``include/fjagg.h``
+(aggregation) and ``include/fjcomp.h`` (compression aggregators).
 
 The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950) into
 ``fedjax_amd/_build/libfjagg.so``. It links against the HIP runtime by soname
@@ -29,9 +30,15 @@ SCALE, ACCUMULATE, NONTEMPORAL, UNALIGNED, UNBALANCED = 1, 2, 4, 8, 16
 # enum fjagg_mode
 MODE_EXACT, MODE_SPLIT = 0, 1
 ABI_VERSION = 1
+COMP_ABI_VERSION = 1
+# include/fjcomp.h
+COMP_UNIFORM, COMP_TERNGRAD, COMP_BINARY = 1, 2, 3
+WHT_PLAIN, WHT_ROTATE, WHT_UNROTATE, WHT_UNROTATE_DRIVE = 0, 1, 2, 3
+STATS_CHUNK = 16384
 
 # every symbol include/fjagg.h declares: (name, restype, argtypes)
 _i64, _i32, _f32, _vp, _u64 = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint64
+_u32 = ctypes.c_uint32
 _SIGNATURES = {
     "fjagg_last_error": (ctypes.c_char_p, []),
     "fjagg_abi_version": (_i32, []),
@@ -47,6 +54,20 @@ _SIGNATURES = {
     "fjagg_l2sq_rows_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_l2sq_rows": (_i32, [_i32, _vp, _i64, _i64, _i64, _i32, _vp, _vp, _i64, _vp]),
     "fjagg_fill_synth": (_i32, [_i32, _vp, _i64, _i64, _i64, _i64, _u64, _f32, _vp]),
+    # include/fjcomp.h
+    "fjcomp_abi_version": (_i32, []),
+    "fjcomp_threefry2x32": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
+    "fjcomp_random_split": (_i32, [_vp, _i64, _i64, _vp]),
+    "fjcomp_prng_sequence": (_i32, [_vp, _i64, _vp]),
+    "fjcomp_random_bits": (_i32, [_u32, _u32, _i64, _vp, _vp]),
+    "fjcomp_uniform": (_i32, [_u32, _u32, _i64, _vp, _vp]),
+    "fjcomp_rademacher": (_i32, [_vp, _vp, _i64, _i64, _vp]),
+    "fjcomp_row_stats_workspace_bytes": (_i64, [_i64]),
+    "fjcomp_row_stats": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _vp]),
+    "fjcomp_quant_fold": (_i32, [_i32, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i64, _i32, _f32, _i32, _vp,
+                                 _vp, _vp]),
+    "fjcomp_wht_tiles": (_i64, [_i32, _i32]),
+    "fjcomp_wht": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
 }
 SYMBOLS = tuple(_SIGNATURES)
 
@@ -101,8 +122,9 @@ def load() -> ctypes.CDLL:
             if fn is None:
                 raise FjaggError(f"{LIB_PATH} does not export {name}")
             fn.restype, fn.argtypes = res, args
-        if lib.fjagg_abi_version() != ABI_VERSION:
-            raise FjaggError(f"ABI mismatch: library {lib.fjagg_abi_version()} != {ABI_VERSION}")
+        if lib.fjagg_abi_version() != ABI_VERSION or lib.fjcomp_abi_version() != COMP_ABI_VERSION:
+            raise FjaggError(f"ABI mismatch: library {lib.fjagg_abi_version()}/{lib.fjcomp_abi_version()} "
+                             f"!= {ABI_VERSION}/{COMP_ABI_VERSION}")
         runtimes = hip_runtimes_mapped()
         if len(runtimes) > 1:
             raise FjaggError(f"two HIP runtimes mapped into one process: {runtimes}")

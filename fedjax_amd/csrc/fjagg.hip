@@ -35,11 +35,14 @@
 
 #include "fjagg.h"
 
+// Shared with fjcomp.hip (same library): the thread-local message behind fjagg_last_error().
+__attribute__((visibility("hidden"))) thread_local char fjagg_g_err[512] = "";
+
 namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-thread_local char g_err[512] = "";
+#define g_err fjagg_g_err
 
 int fail(int code, const char* fmt, ...) {
   va_list ap;

@@ -1,0 +1,674 @@
+// fjcomp.hip — MI355X (gfx950) kernels for FedJAX's compression aggregators
+// (fedjax/aggregators/compression.py, walsh_hadamard.py). C ABI: include/fjcomp.h.
+//
+// A compression round in the reference is, per client and per leaf, a chain of jitted
+// XLA calls: amin/amax (or std), a jax.random.uniform draw, the elementwise quantizer,
+// and for the rotated variants a Walsh-Hadamard transform on each side; tree_mean then
+// folds the quantized deltas. Here the round is a few launches over (client, leaf) tables:
+//
+//   k_row_stats / k_stats_combine  one HBM pass per row: min/max/|max| and f64 sums,
+//                                  combined per row in a fixed order (deterministic),
+//                                  then turned into the quantizer's per-row constants;
+//   k_quant_fold                   threefry draw + quantizer + tree_mean fold in one
+//                                  pass: a lane owns the element PAIR (i, i + h) that one
+//                                  threefry2x32 call produces (JAX's counter layout), walks
+//                                  the clients in order and keeps the running sum in a
+//                                  register. Threefry costs ~40 VALU ops per element, so
+//                                  this kernel is VALU-bound, not HBM-bound;
+//   k_rademacher                   the rotation signs, one bit per element, packed with
+//                                  wave ballots; computed once per key and read by both the
+//                                  forward and the inverse rotation;
+//   k_wht                          Walsh-Hadamard in passes over LDS tiles of 8192 f32: pass 0
+//                                  does the 13 low butterfly bits on contiguous tiles, later
+//                                  passes 8 bits each on 256 strided rows x 32 contiguous
+//                                  floats (128-byte segments: coalesced); butterflies run
+//                                  radix-16 in registers (4 stages per LDS round trip); the
+//                                  rotation prologue (zero pad, sign) and epilogue (sign,
+//                                  / sqrt(d), truncate) are fused into the first/last pass.
+//
+// Arithmetic follows the reference's float32 op sequence. Division: a quotient by a
+// per-row constant b is RN_f32(a * RN_f64(1/b)); the f64 error (< 2^-52 relative) is
+// below the distance from a/b to any f32 rounding midpoint (>= 2^-49 relative for
+// f32 a, b), so the result equals the correctly rounded f32 quotient. Per-element
+// quotients use f64 division rounded once (double rounding is innocuous for p = 53 >=
+// 2*24 + 2). Compiled with -ffp-contract=off: no multiply-add contraction anywhere.
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "fjcomp.h"
+
+extern thread_local char fjagg_g_err[512];
+
+static_assert(sizeof(fjcomp_stats) == 48, "fjcomp_stats layout");
+static_assert(sizeof(fjcomp_qparams) == 24, "fjcomp_qparams layout");
+static_assert(sizeof(fjcomp_row) == 16, "fjcomp_row layout");
+static_assert(sizeof(fjcomp_sign_job) == 24, "fjcomp_sign_job layout");
+static_assert(sizeof(fjcomp_wht_job) == 72, "fjcomp_wht_job layout");
+
+namespace {
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(fjagg_g_err, sizeof(fjagg_g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(FJAGG_EHIP, "%s: %s", what, hipGetErrorString(e));
+  return FJAGG_OK;
+}
+
+// ------------------------------------------------------------------ threefry2x32-20
+__host__ __device__ inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+#define FJ_TF_ROUND(r) \
+  x0 += x1;            \
+  x1 = rotl32(x1, r);  \
+  x1 ^= x0;
+#define FJ_TF_ROT0 FJ_TF_ROUND(13) FJ_TF_ROUND(15) FJ_TF_ROUND(26) FJ_TF_ROUND(6)
+#define FJ_TF_ROT1 FJ_TF_ROUND(17) FJ_TF_ROUND(29) FJ_TF_ROUND(16) FJ_TF_ROUND(24)
+
+// Threefry-2x32 with 20 rounds and JAX's key schedule (jax/_src/prng.py).
+__host__ __device__ inline void threefry(uint32_t k0, uint32_t k1, uint32_t& x0, uint32_t& x1) {
+  const uint32_t k2 = k0 ^ k1 ^ 0x1BD11BDAu;
+  x0 += k0;
+  x1 += k1;
+  FJ_TF_ROT0 x0 += k1; x1 += k2 + 1u;
+  FJ_TF_ROT1 x0 += k2; x1 += k0 + 2u;
+  FJ_TF_ROT0 x0 += k0; x1 += k1 + 3u;
+  FJ_TF_ROT1 x0 += k1; x1 += k2 + 4u;
+  FJ_TF_ROT0 x0 += k2; x1 += k0 + 5u;
+}
+
+// jax.random.uniform's bits -> [0, 1): bitcast((b >> 9) | 1.0f) - 1
+__device__ inline float bits_to_unit(uint32_t b) { return __uint_as_float((b >> 9) | 0x3f800000u) - 1.0f; }
+
+// ------------------------------------------------------------------ f32 helpers
+__device__ inline float nan_to_num(float x) {
+  if (x != x) return 0.0f;
+  if (x == INFINITY) return FLT_MAX;
+  if (x == -INFINITY) return -FLT_MAX;
+  return x;
+}
+// numpy's maximum(0, a) / minimum(a, 1) for non-NaN a (first argument wins ties)
+__device__ inline float clamp01(float a) {
+  a = (a <= 1.0f) ? a : 1.0f;
+  return (0.0f >= a) ? 0.0f : a;
+}
+__device__ inline float xla_sign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x); }
+// correctly rounded a / b given r = RN_f64(1 / b) (see the header comment)
+__device__ inline float div_by(float a, double r) { return (float)((double)a * r); }
+__device__ inline float div_rn(float a, float b) { return (float)((double)a / (double)b); }
+__device__ inline double nan_min(double a, double b) { return (a != a) ? a : ((b != b) ? b : (b < a ? b : a)); }
+__device__ inline double nan_max(double a, double b) { return (a != a) ? a : ((b != b) ? b : (b > a ? b : a)); }
+
+// segment of block b in a running-sum table prefix[nseg + 1] (skips empty segments)
+__device__ inline int64_t find_segment(const int64_t* __restrict__ prefix, int64_t nseg, int64_t b) {
+  int64_t lo = 0, hi = nseg;  // prefix[lo] <= b < prefix[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (prefix[mid] <= b) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// ------------------------------------------------------------------ random bits
+__global__ __launch_bounds__(256) void k_random_bits(uint32_t k0, uint32_t k1, int64_t n, uint32_t* __restrict__ out,
+                                                      float* __restrict__ outf) {
+  const int64_t h = (n + 1) >> 1;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= h) return;
+  uint32_t x0 = (uint32_t)i, x1 = (uint32_t)(i + h < n ? i + h : 0);
+  threefry(k0, k1, x0, x1);
+  if (out) {
+    out[i] = x0;
+    if (i + h < n) out[i + h] = x1;
+  } else {
+    outf[i] = fmaxf(0.0f, bits_to_unit(x0));
+    if (i + h < n) outf[i + h] = fmaxf(0.0f, bits_to_unit(x1));
+  }
+}
+
+// ------------------------------------------------------------------ rademacher signs
+// Sign of element g is bit 31 of its uniform draw's bits (uniform < 0.5 <=> +1).
+__global__ __launch_bounds__(256) void k_rademacher(const fjcomp_sign_job* __restrict__ jobs,
+                                                     const int64_t* __restrict__ prefix, int64_t J) {
+  const int64_t b = blockIdx.x;
+  const int64_t j = find_segment(prefix, J, b);
+  const fjcomp_sign_job jb = jobs[j];
+  const int64_t d = jb.d, h = (d + 1) >> 1;
+  const int64_t i = (b - prefix[j]) * 256 + threadIdx.x;
+  uint32_t x0 = (uint32_t)i, x1 = (uint32_t)(i + h < d ? i + h : 0);
+  const bool valid = i < h, second = i + h < d;
+  if (valid) threefry(jb.key[0], jb.key[1], x0, x1);
+  const uint64_t m0 = __ballot(valid && (x0 >> 31));
+  const uint64_t m1 = __ballot(valid && second && (x1 >> 31));
+  const int lane = threadIdx.x & 63;
+  if (d < 64) {  // one word, written by the first lane of the job's first wave
+    if (b == prefix[j] && threadIdx.x == 0) {
+      const uint64_t lo = m0 & ((1ull << h) - 1), hi = m1 & ((1ull << (d - h)) - 1);
+      jb.words[0] = (uint32_t)(lo | (hi << h));
+    }
+    return;
+  }
+  const int64_t i0 = i - lane;  // wave's first pair; h and i0 are multiples of 32
+  if (i0 >= h) return;
+  if (lane == 0) jb.words[i0 >> 5] = (uint32_t)m0;
+  if (lane == 1 && i0 + 32 < h) jb.words[(i0 >> 5) + 1] = (uint32_t)(m0 >> 32);
+  if (lane == 2) jb.words[(i0 + h) >> 5] = (uint32_t)m1;
+  if (lane == 3 && i0 + 32 < h) jb.words[((i0 + h) >> 5) + 1] = (uint32_t)(m1 >> 32);
+}
+
+// ------------------------------------------------------------------ row statistics
+constexpr int kStatsThreads = 256;
+constexpr int kStatsChunk = FJCOMP_STATS_CHUNK;
+
+struct Partial {
+  double mn, mx, amx, s1, s2, sa;
+};
+static_assert(sizeof(Partial) == 48, "Partial");
+
+__device__ inline void merge(Partial& a, const Partial& b) {
+  a.mn = nan_min(a.mn, b.mn);
+  a.mx = nan_max(a.mx, b.mx);
+  a.amx = nan_max(a.amx, b.amx);
+  a.s1 += b.s1;
+  a.s2 += b.s2;
+  a.sa += b.sa;
+}
+
+__device__ inline Partial shfl_xor(const Partial& p, int m) {
+  Partial q;
+  q.mn = __shfl_xor(p.mn, m);
+  q.mx = __shfl_xor(p.mx, m);
+  q.amx = __shfl_xor(p.amx, m);
+  q.s1 = __shfl_xor(p.s1, m);
+  q.s2 = __shfl_xor(p.s2, m);
+  q.sa = __shfl_xor(p.sa, m);
+  return q;
+}
+
+__global__ __launch_bounds__(kStatsThreads) void k_row_stats(const fjcomp_row* __restrict__ rows,
+                                                              const int64_t* __restrict__ prefix, int64_t R,
+                                                              Partial* __restrict__ part) {
+  const int64_t b = blockIdx.x;
+  const int64_t r = find_segment(prefix, R, b);
+  const fjcomp_row row = rows[r];
+  const int64_t c0 = (b - prefix[r]) * kStatsChunk;
+  const int64_t c1 = min(row.n, c0 + kStatsChunk);
+  Partial p = {INFINITY, -INFINITY, -INFINITY, 0.0, 0.0, 0.0};
+  for (int64_t e = c0 + threadIdx.x; e < c1; e += kStatsThreads) {
+    const float x = row.ptr[e];
+    const double v = (double)x;
+    p.mn = nan_min(p.mn, v);
+    p.mx = nan_max(p.mx, v);
+    p.amx = nan_max(p.amx, fabs(v));
+    p.s1 += v;
+    p.s2 += v * v;
+    p.sa += fabs(v);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) merge(p, shfl_xor(p, m));
+  __shared__ Partial sp[kStatsThreads / 64];
+  if ((threadIdx.x & 63) == 0) sp[threadIdx.x >> 6] = p;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Partial t = sp[0];
+    for (int w = 1; w < kStatsThreads / 64; ++w) merge(t, sp[w]);
+    part[b] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_stats_combine(const fjcomp_row* __restrict__ rows,
+                                                        const int64_t* __restrict__ prefix, int64_t R,
+                                                        const Partial* __restrict__ part, int method,
+                                                        fjcomp_stats* __restrict__ stats,
+                                                        fjcomp_qparams* __restrict__ qp) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= R) return;
+  Partial t = part[prefix[r]];
+  for (int64_t c = prefix[r] + 1; c < prefix[r + 1]; ++c) merge(t, part[c]);
+  stats[r] = fjcomp_stats{t.mn, t.mx, t.amx, t.s1, t.s2, t.sa};
+  if (!qp) return;
+  fjcomp_qparams q;
+  if (method == FJCOMP_TERNGRAD) {
+    // jnp.std (ddof 0) in f64, rounded once; thr = f32(2.5) * sigma (compression.py:331-332)
+    const double n = (double)rows[r].n;
+    const double mean = t.s1 / n;
+    double var = t.s2 / n - mean * mean;
+    var = var > 0.0 ? var : (var == var ? 0.0 : var);
+    const float sigma = (float)sqrt(var);
+    const float thr = 2.5f * sigma;
+    const float amx = (float)t.amx;
+    // amax(|clip(v)|): clipped entries become exactly thr (compression.py:333-335)
+    const float vmax = (amx > thr) ? thr : amx;
+    q.vmin = 0.0f;
+    q.vmax = vmax;
+    q.range = vmax - 0.0f;
+    q.thr = thr;
+  } else {
+    q.vmin = (float)t.mn;
+    q.vmax = (float)t.mx;
+    q.range = q.vmax - q.vmin;
+    q.thr = 0.0f;
+  }
+  q.rcp_range = 1.0 / (double)q.range;
+  qp[r] = q;
+}
+
+// ------------------------------------------------------------------ quantize + fold
+constexpr int kQThreads = 256;
+constexpr int kHistLdsBins = 4096;
+
+struct UniformQ {
+  float lm1;
+  double rcp_lm1;
+  // uniform_stochastic_quantize (compression.py:84-97); *level = chosen level index
+  __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float* level) const {
+    float a = nan_to_num(div_by(v - p.vmin, p.rcp_range));
+    a = clamp01(a);
+    const float fl = floorf(a * lm1), ce = ceilf(a * lm1);
+    const float v_ceil = div_by(ce, rcp_lm1);
+    const float v_floor = div_by(fl, rcp_lm1);
+    const float thr = nan_to_num(div_rn(a - v_floor, v_ceil - v_floor));
+    const bool down = u > thr;
+    *level = down ? fl : ce;
+    const float q = down ? v_floor : v_ceil;
+    return p.vmin + q * p.range;
+  }
+};
+
+struct BinaryQ {
+  // binary_stochastic_quantize (compression.py:58-63)
+  __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float*) const {
+    const float a = clamp01(nan_to_num(div_by(v - p.vmin, p.rcp_range)));
+    return (u > a) ? p.vmin : p.vmax;
+  }
+};
+
+struct TernQ {
+  // terngrad_quantize (compression.py:323-336) with binary_stochastic_quantize(|v|, 0, vmax)
+  __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float*) const {
+    const float vc = (fabsf(v) > p.thr) ? p.thr * xla_sign(v) : v;
+    const float av = fabsf(vc);
+    const float a = clamp01(nan_to_num(div_by(av - 0.0f, p.rcp_range)));
+    const float r = (u > a) ? 0.0f : p.vmax;
+    return r * xla_sign(vc);
+  }
+};
+
+template <class Q, bool HIST>
+__global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* const* __restrict__ in_ptrs,
+                                                           const uint32_t* __restrict__ keys,
+                                                           const fjcomp_qparams* __restrict__ qps,
+                                                           const float* __restrict__ w, int64_t K, int64_t L,
+                                                           const int64_t* __restrict__ leaf_n,
+                                                           const int64_t* __restrict__ prefix, float scale,
+                                                           int flags, float* const* __restrict__ out_ptrs,
+                                                           int32_t* __restrict__ hist, int nbins) {
+  const int64_t b = blockIdx.x;
+  const int64_t l = find_segment(prefix, L, b);
+  const int64_t n = leaf_n[l], h = (n + 1) >> 1;
+  const int64_t i = (b - prefix[l]) * kQThreads + threadIdx.x;
+  const bool valid = i < h, second = i + h < n;
+  float* __restrict__ out = out_ptrs[l];
+  const bool accumulate = flags & FJAGG_ACCUMULATE;
+  float s0 = 0.0f, s1 = 0.0f;
+  if (valid && accumulate) {
+    s0 = out[i];
+    if (second) s1 = out[i + h];
+  }
+  __shared__ int32_t sh[HIST ? kHistLdsBins : 1];
+  const bool lds_hist = HIST && nbins <= kHistLdsBins;
+  for (int64_t k = 0; k < K; ++k) {
+    const int64_t row = k * L + l;
+    const float* __restrict__ x = in_ptrs[row];
+    const uint32_t k0 = keys[2 * row], k1 = keys[2 * row + 1];
+    const fjcomp_qparams p = qps[row];
+    const float wk = w[k];
+    float lv0 = -1.0f, lv1 = -1.0f;
+    if (valid) {
+      const float v0 = x[i];
+      const float v1 = second ? x[i + h] : 0.0f;
+      uint32_t c0 = (uint32_t)i, c1 = (uint32_t)(second ? i + h : 0);
+      threefry(k0, k1, c0, c1);
+      const float q0 = quant(v0, bits_to_unit(c0), p, &lv0);
+      const float t0 = q0 * wk;
+      s0 = (k == 0 && !accumulate) ? t0 : s0 + t0;
+      if (second) {
+        const float q1 = quant(v1, bits_to_unit(c1), p, &lv1);
+        const float t1 = q1 * wk;
+        s1 = (k == 0 && !accumulate) ? t1 : s1 + t1;
+      }
+    }
+    if constexpr (HIST) {
+      int32_t* __restrict__ hrow = hist + row * nbins;
+      const int top = nbins - 1;
+      auto bin = [&](float lv) { return (lv >= 0.0f && lv < (float)top) ? (int)lv : top; };
+      if (lds_hist) {
+        for (int e = threadIdx.x; e < nbins; e += kQThreads) sh[e] = 0;
+        __syncthreads();
+        if (valid) {
+          atomicAdd(&sh[bin(lv0)], 1);
+          if (second) atomicAdd(&sh[bin(lv1)], 1);
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < nbins; e += kQThreads)
+          if (sh[e]) atomicAdd(&hrow[e], sh[e]);
+        __syncthreads();
+      } else if (valid) {
+        atomicAdd(&hrow[bin(lv0)], 1);
+        if (second) atomicAdd(&hrow[bin(lv1)], 1);
+      }
+    }
+  }
+  if (!valid) return;
+  if (flags & FJAGG_SCALE) {
+    s0 = s0 * scale;
+    s1 = s1 * scale;
+  }
+  out[i] = s0;
+  if (second) out[i + h] = s1;
+}
+
+// ------------------------------------------------------------------ Walsh-Hadamard
+constexpr int kWhtBits = 13;    // butterfly bits of pass 0 (contiguous tiles of 8192)
+constexpr int kWhtHighBits = 8; // later passes: 2^8 strided rows x >= 32 contiguous floats (128 B)
+constexpr int kWhtTile = 1 << kWhtBits;
+constexpr int kWhtThreads = 512;
+
+__host__ __device__ inline int wht_passes(int m) {
+  return m <= kWhtBits ? 1 : 1 + (m - kWhtBits + kWhtHighBits - 1) / kWhtHighBits;
+}
+
+// Tiling of pass p of a 2^m job: the pass does butterfly bits [lo, lo + nb); a tile holds
+// all 2^nb values of those bits for c consecutive values of the lower bits.
+struct WhtTiling {
+  int lo, nb, lc;
+  int64_t c, tile, tiles;
+};
+__host__ __device__ inline WhtTiling wht_tiling(int m, int pass) {
+  WhtTiling t;
+  t.lo = pass == 0 ? 0 : kWhtBits + kWhtHighBits * (pass - 1);
+  const int cap = pass == 0 ? kWhtBits : kWhtHighBits;
+  t.nb = m - t.lo < cap ? m - t.lo : cap;
+  if (t.nb < 0) t.nb = 0;
+  const int64_t span = (int64_t)1 << t.lo;
+  const int64_t cmax = (int64_t)kWhtTile >> t.nb;
+  t.c = span < cmax ? span : cmax;
+  t.lc = 0;
+  while (((int64_t)1 << t.lc) < t.c) ++t.lc;
+  t.tile = t.c << t.nb;
+  t.tiles = ((int64_t)1 << m) / t.tile;
+  return t;
+}
+
+__device__ inline int lds_pad(int e) { return e + (e >> 5); }
+
+template <int G>
+__device__ inline void wht_group(float* sm, int64_t tile, int p) {
+  const int nq = (int)(tile >> G);
+  for (int q = threadIdx.x; q < nq; q += kWhtThreads) {
+    const int base = ((q >> p) << (p + G)) | (q & ((1 << p) - 1));
+    float v[1 << G];
+#pragma unroll
+    for (int r = 0; r < (1 << G); ++r) v[r] = sm[lds_pad(base + (r << p))];
+#pragma unroll
+    for (int s = 0; s < G; ++s)
+#pragma unroll
+      for (int r = 0; r < (1 << G); ++r)
+        if (!(r & (1 << s))) {
+          const float a = v[r], c = v[r | (1 << s)];
+          v[r] = a + c;
+          v[r | (1 << s)] = a - c;
+        }
+#pragma unroll
+    for (int r = 0; r < (1 << G); ++r) sm[lds_pad(base + (r << p))] = v[r];
+  }
+}
+
+__device__ inline float sign_of(const uint32_t* __restrict__ s, int64_t g) {
+  return ((s[g >> 5] >> (g & 31)) & 1u) ? -1.0f : 1.0f;
+}
+
+__global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __restrict__ jobs,
+                                                      const int64_t* __restrict__ prefix, int64_t J, int pass) {
+  __shared__ float sm[kWhtTile + kWhtTile / 32];
+  const int64_t b = blockIdx.x;
+  const int64_t j = find_segment(prefix, J, b);
+  const fjcomp_wht_job jb = jobs[j];
+  const int m = jb.log2d;
+  const WhtTiling t = wht_tiling(m, pass);
+  const int64_t tix = b - prefix[j];
+  const int64_t cph = ((int64_t)1 << t.lo) / t.c;
+  const int64_t base = ((tix / cph) << (t.lo + t.nb)) + (tix % cph) * t.c;
+  const bool first = pass == 0, last = pass == wht_passes(m) - 1;
+  const int kind = jb.kind;
+  const double rcp_sqrt_d = 1.0 / (double)jb.sqrt_d;
+  double rcp_b = 0.0;
+  float A = 0.0f;
+  if (first && kind == FJCOMP_WHT_UNROTATE_DRIVE) {
+    A = (float)jb.stats->sumsq;
+    rcp_b = 1.0 / (double)(float)jb.stats->sumabs;
+  }
+  const float* __restrict__ src = first ? jb.src : jb.mid;
+  for (int e = threadIdx.x; e < t.tile; e += kWhtThreads) {
+    const int64_t g = base + ((int64_t)(e >> t.lc) << t.lo) + (e & (t.c - 1));
+    float v;
+    if (first && kind == FJCOMP_WHT_ROTATE) {
+      v = g < jb.n_in ? src[g] : 0.0f;
+      v = v * sign_of(jb.signs, g);
+    } else if (first && kind == FJCOMP_WHT_UNROTATE_DRIVE) {
+      v = div_by(A * xla_sign(src[g]), rcp_b);  // drive_pytree: (sum(y^2) * sign(y)) / sum(|y|)
+    } else {
+      v = src[g];
+    }
+    sm[lds_pad(e)] = v;
+  }
+  __syncthreads();
+  for (int s0 = 0; s0 < t.nb; s0 += 4) {
+    const int p = t.lc + s0;
+    switch (t.nb - s0 < 4 ? t.nb - s0 : 4) {
+      case 1: wht_group<1>(sm, t.tile, p); break;
+      case 2: wht_group<2>(sm, t.tile, p); break;
+      case 3: wht_group<3>(sm, t.tile, p); break;
+      default: wht_group<4>(sm, t.tile, p); break;
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < t.tile; e += kWhtThreads) {
+    const int64_t g = base + ((int64_t)(e >> t.lc) << t.lo) + (e & (t.c - 1));
+    float v = sm[lds_pad(e)];
+    if (!last) {
+      jb.mid[g] = v;
+      continue;
+    }
+    if (g >= jb.n_out) continue;
+    if (kind == FJCOMP_WHT_ROTATE) {
+      v = div_by(v, rcp_sqrt_d);
+    } else if (kind != FJCOMP_WHT_PLAIN) {
+      v = div_by(v * sign_of(jb.signs, g), rcp_sqrt_d);
+    }
+    jb.dst[g] = v;
+  }
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+void host_split(const uint32_t key[2], int64_t num, uint32_t* out) {
+  // threefry_2x32(key, iota(2*num)).reshape(num, 2): flat = [y0 | y1]
+  std::vector<uint32_t> flat(2 * num);
+  for (int64_t i = 0; i < num; ++i) {
+    uint32_t x0 = (uint32_t)i, x1 = (uint32_t)(num + i);
+    threefry(key[0], key[1], x0, x1);
+    flat[i] = x0;
+    flat[num + i] = x1;
+  }
+  memcpy(out, flat.data(), sizeof(uint32_t) * 2 * num);
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+int fjcomp_abi_version(void) { return FJCOMP_ABI_VERSION; }
+
+int fjcomp_threefry2x32(const uint32_t key[2], const uint32_t* x0, const uint32_t* x1, int64_t n, uint32_t* y0,
+                        uint32_t* y1) {
+  fjagg_g_err[0] = 0;
+  if (!key || n < 0 || (n && (!x0 || !x1 || !y0 || !y1))) return fail(FJAGG_EINVAL, "threefry2x32: bad arguments");
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t a = x0[i], b = x1[i];
+    threefry(key[0], key[1], a, b);
+    y0[i] = a;
+    y1[i] = b;
+  }
+  return FJAGG_OK;
+}
+
+int fjcomp_random_split(const uint32_t* keys, int64_t nkeys, int64_t num, uint32_t* out) {
+  fjagg_g_err[0] = 0;
+  if (nkeys < 0 || num < 0 || ((nkeys && num) && (!keys || !out)) || num > (int64_t)1 << 31)
+    return fail(FJAGG_EINVAL, "random_split: bad arguments (nkeys=%lld num=%lld)", (long long)nkeys, (long long)num);
+  for (int64_t k = 0; k < nkeys; ++k) host_split(keys + 2 * k, num, out + 2 * num * k);
+  return FJAGG_OK;
+}
+
+int fjcomp_prng_sequence(uint32_t key[2], int64_t n, uint32_t* subkeys) {
+  fjagg_g_err[0] = 0;
+  if (!key || n < 0 || (n && !subkeys)) return fail(FJAGG_EINVAL, "prng_sequence: bad arguments");
+  uint32_t two[4];
+  for (int64_t i = 0; i < n; ++i) {  // haiku: reserve(1) = split(key, 2); key <- [0]; yield [1]
+    host_split(key, 2, two);
+    key[0] = two[0];
+    key[1] = two[1];
+    subkeys[2 * i] = two[2];
+    subkeys[2 * i + 1] = two[3];
+  }
+  return FJAGG_OK;
+}
+
+static int random_common(uint32_t k0, uint32_t k1, int64_t n, uint32_t* out, float* outf, void* stream) {
+  fjagg_g_err[0] = 0;
+  if (n < 0 || n > (int64_t)UINT32_MAX) return fail(FJAGG_EINVAL, "random: n=%lld outside [0, 2^32)", (long long)n);
+  if (n == 0) return FJAGG_OK;
+  if (!out && !outf) return fail(FJAGG_EINVAL, "random: null output");
+  const int64_t h = (n + 1) >> 1;
+  hipLaunchKernelGGL(k_random_bits, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, as_stream(stream), k0, k1, n,
+                     out, outf);
+  return check_launch("k_random_bits");
+}
+
+int fjcomp_random_bits(uint32_t k0, uint32_t k1, int64_t n, uint32_t* out, void* stream) {
+  return random_common(k0, k1, n, out, nullptr, stream);
+}
+
+int fjcomp_uniform(uint32_t k0, uint32_t k1, int64_t n, float* out, void* stream) {
+  return random_common(k0, k1, n, nullptr, out, stream);
+}
+
+int fjcomp_rademacher(const fjcomp_sign_job* jobs, const int64_t* block_prefix, int64_t J, int64_t nblocks,
+                      void* stream) {
+  fjagg_g_err[0] = 0;
+  if (J < 0 || nblocks < 0 || (J && (!jobs || !block_prefix)) || nblocks > INT32_MAX)
+    return fail(FJAGG_EINVAL, "rademacher: bad arguments");
+  if (!J || !nblocks) return FJAGG_OK;
+  hipLaunchKernelGGL(k_rademacher, dim3((unsigned)nblocks), dim3(256), 0, as_stream(stream), jobs, block_prefix, J);
+  return check_launch("k_rademacher");
+}
+
+int64_t fjcomp_row_stats_workspace_bytes(int64_t nchunks) { return nchunks < 1 ? 0 : nchunks * (int64_t)sizeof(Partial); }
+
+int fjcomp_row_stats(const fjcomp_row* rows, const int64_t* chunk_prefix, int64_t R, int64_t nchunks, int method,
+                     fjcomp_stats* stats, fjcomp_qparams* qparams, void* ws, int64_t ws_bytes, void* stream) {
+  fjagg_g_err[0] = 0;
+  if (R < 0 || nchunks < R || (R && (!rows || !chunk_prefix || !stats)) || nchunks > INT32_MAX)
+    return fail(FJAGG_EINVAL, "row_stats: bad arguments (R=%lld nchunks=%lld)", (long long)R, (long long)nchunks);
+  if (qparams && method != FJCOMP_UNIFORM && method != FJCOMP_TERNGRAD && method != FJCOMP_BINARY)
+    return fail(FJAGG_EINVAL, "row_stats: qparams need method UNIFORM, BINARY or TERNGRAD, got %d", method);
+  if (!R) return FJAGG_OK;
+  if (!ws || ws_bytes < fjcomp_row_stats_workspace_bytes(nchunks))
+    return fail(FJAGG_EINVAL, "row_stats: workspace %lld B < %lld B", (long long)ws_bytes,
+                (long long)fjcomp_row_stats_workspace_bytes(nchunks));
+  hipStream_t s = as_stream(stream);
+  Partial* part = static_cast<Partial*>(ws);
+  hipLaunchKernelGGL(k_row_stats, dim3((unsigned)nchunks), dim3(kStatsThreads), 0, s, rows, chunk_prefix, R, part);
+  if (int rc = check_launch("k_row_stats")) return rc;
+  hipLaunchKernelGGL(k_stats_combine, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, rows, chunk_prefix, R, part,
+                     method, stats, qparams);
+  return check_launch("k_stats_combine");
+}
+
+int fjcomp_quant_fold(int method, const float* const* in_ptrs, const uint32_t* keys, const fjcomp_qparams* qparams,
+                      const float* w, int64_t K, int64_t L, const int64_t* leaf_n, const int64_t* block_prefix,
+                      int64_t nblocks, int num_levels, float scale, int flags, float* const* out_ptrs, int32_t* hist,
+                      void* stream) {
+  fjagg_g_err[0] = 0;
+  if (K < 1 || L < 0 || nblocks < 0 || nblocks > INT32_MAX)
+    return fail(FJAGG_EINVAL, "quant_fold: bad sizes (K=%lld L=%lld nblocks=%lld)", (long long)K, (long long)L,
+                (long long)nblocks);
+  if (L && (!in_ptrs || !keys || !qparams || !w || !leaf_n || !block_prefix || !out_ptrs))
+    return fail(FJAGG_EINVAL, "quant_fold: null table");
+  if (flags & ~(FJAGG_SCALE | FJAGG_ACCUMULATE)) return fail(FJAGG_EINVAL, "quant_fold: unsupported flags %#x", flags);
+  if (!L || !nblocks) return FJAGG_OK;
+  hipStream_t s = as_stream(stream);
+  if (method == FJCOMP_UNIFORM) {
+    if (num_levels < 1) return fail(FJAGG_EINVAL, "quant_fold: num_levels=%d", num_levels);
+    UniformQ q;
+    q.lm1 = (float)(num_levels - 1);
+    q.rcp_lm1 = 1.0 / (double)q.lm1;
+    if (hist) {
+      hipLaunchKernelGGL((k_quant_fold<UniformQ, true>), dim3((unsigned)nblocks), dim3(kQThreads), 0, s, q, in_ptrs,
+                         keys, qparams, w, K, L, leaf_n, block_prefix, scale, flags, out_ptrs, hist, num_levels + 1);
+    } else {
+      hipLaunchKernelGGL((k_quant_fold<UniformQ, false>), dim3((unsigned)nblocks), dim3(kQThreads), 0, s, q, in_ptrs,
+                         keys, qparams, w, K, L, leaf_n, block_prefix, scale, flags, out_ptrs, hist, 0);
+    }
+  } else if (method == FJCOMP_BINARY) {
+    if (hist) return fail(FJAGG_EINVAL, "quant_fold: histogram only for UNIFORM");
+    hipLaunchKernelGGL((k_quant_fold<BinaryQ, false>), dim3((unsigned)nblocks), dim3(kQThreads), 0, s, BinaryQ{},
+                       in_ptrs, keys, qparams, w, K, L, leaf_n, block_prefix, scale, flags, out_ptrs, hist, 0);
+  } else if (method == FJCOMP_TERNGRAD) {
+    if (hist) return fail(FJAGG_EINVAL, "quant_fold: histogram only for UNIFORM");
+    hipLaunchKernelGGL((k_quant_fold<TernQ, false>), dim3((unsigned)nblocks), dim3(kQThreads), 0, s, TernQ{}, in_ptrs,
+                       keys, qparams, w, K, L, leaf_n, block_prefix, scale, flags, out_ptrs, hist, 0);
+  } else {
+    return fail(FJAGG_EINVAL, "quant_fold: unknown method %d", method);
+  }
+  return check_launch("k_quant_fold");
+}
+
+int64_t fjcomp_wht_tiles(int log2d, int pass) {
+  if (log2d < 0 || log2d > FJCOMP_WHT_MAX_LOG2 || pass < 0 || pass >= wht_passes(log2d)) return 0;
+  return wht_tiling(log2d, pass).tiles;
+}
+
+int fjcomp_wht(const fjcomp_wht_job* jobs, const int64_t* pass_prefix, int64_t J, int npass, const int64_t* pass_tiles,
+               void* stream) {
+  fjagg_g_err[0] = 0;
+  if (J < 0 || npass < 0 || npass > wht_passes(FJCOMP_WHT_MAX_LOG2) || (J && (!jobs || !pass_prefix || !pass_tiles)))
+    return fail(FJAGG_EINVAL, "wht: bad arguments (J=%lld npass=%d)", (long long)J, npass);
+  hipStream_t s = as_stream(stream);
+  for (int p = 0; p < npass && J; ++p) {
+    if (pass_tiles[p] < 0 || pass_tiles[p] > INT32_MAX) return fail(FJAGG_EINVAL, "wht: pass %d tiles", p);
+    if (!pass_tiles[p]) continue;
+    hipLaunchKernelGGL(k_wht, dim3((unsigned)pass_tiles[p]), dim3(kWhtThreads), 0, s, jobs, pass_prefix + p * (J + 1),
+                       J, p);
+    if (int rc = check_launch("k_wht")) return rc;
+  }
+  return FJAGG_OK;
+}
+
+}  // extern "C"

@@ -13,13 +13,15 @@ import torch
 from fedjax_amd import _lib, kernels
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "fjagg.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("fjagg.h", "fjcomp.h")]
 
 
 def header_symbols():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return set(re.findall(r"\b(fjagg_\w+)\s*\(", src))
+    syms = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        syms |= set(re.findall(r"\b(fj(?:agg|comp)_\w+)\s*\(", src))
+    return syms
 
 
 def test_header_and_binding_agree():
@@ -29,7 +31,7 @@ def test_header_and_binding_agree():
 def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
-    exported = set(re.findall(r"\bT (fjagg_\w+)", out))
+    exported = set(re.findall(r"\bT (fj(?:agg|comp)_\w+)", out))
     assert header_symbols() <= exported, header_symbols() - exported
 
 
