@@ -347,3 +347,10 @@ def test_bf16_leaves_rejected(cuda):
     q = comp.uniform_stochastic_quantizer(3, random.PRNGKey(0))
     with pytest.raises(TypeError):
         q.apply([("a", {"w": torch.ones(4, dtype=torch.bfloat16, device=cuda)}, 1.)], q.init())
+
+
+def test_mismatched_client_shapes_rejected(cuda):
+    q = comp.terngrad_quantizer(random.PRNGKey(0))
+    bad = [("a", {"w": torch.ones(4, device=cuda)}, 1.), ("b", {"w": torch.ones(3, device=cuda)}, 1.)]
+    with pytest.raises(ValueError):
+        q.apply(bad, q.init())
