@@ -36,6 +36,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+BUCKET_CANDIDATES = (1, 2, 4, 8)  # N>1 auto-tune: 1 = no overlap; more = shorter exposed reduce tail
 METRIC = "device-resident aggregated client-delta GB/s, K clients × P fp32 params"
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 WORKLOADS = {  # name: (clients, params, dtype, description)
@@ -107,7 +108,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
-    ap.add_argument("--buckets", type=int, default=4)
+    ap.add_argument("--buckets", type=int, default=0,
+                    help="N>1: parameter buckets of the fold/reduce pipeline; 0 = pick the fastest of "
+                         "BUCKET_CANDIDATES during warmup (max over ranks)")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=-1, help="-1 auto, 0 off, 1 on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -204,11 +207,37 @@ def main():
         elif world == 1:
             fold(x, wd, out, events)
         else:
-            fd.sharded_weighted_mean(x, wd, W, buckets=args.buckets, out=out, all_ranks=args.all_ranks,
+            fd.sharded_weighted_mean(x, wd, W, buckets=buckets, out=out, all_ranks=args.all_ranks,
                                      partial_fn=lambda xs, wdd, sc, o: fold(xs, wdd, o, events))
             if final is not None and (rank == 0 or args.all_ranks):  # f32 mean -> leaf dtype
                 kernels.weighted_sum_dense(out.view(1, P), ones, out=final)
 
+    def wall(nsteps):
+        """Max-over-ranks wall time of nsteps steps, bracketed like the timed region."""
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(nsteps):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    buckets = args.buckets or 4
+    tune = {}
+    if world > 1 and args.buckets == 0:
+        # every rank measures every candidate and sees the same max-over-ranks times,
+        # so all ranks pick the same bucket count without another exchange
+        for b in BUCKET_CANDIDATES:
+            if P // b < fd.BUCKET_ALIGN:
+                continue
+            buckets = b
+            wall(2)
+            tune[b] = wall(5) / 5 * 1e3
+        buckets = min(tune, key=tune.get)
+        log(f"bucket auto-tune (ms/step, max over ranks): {tune} -> {buckets}")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -268,7 +297,9 @@ def main():
                        "parallelism": f"client-sharded x{world}" + (
                            f" + {'RCCL' if args.backend == 'nccl' else args.backend} "
                            f"{'all_reduce' if args.all_ranks else 'reduce'}" if world > 1 else ""),
-                       "buckets": args.buckets if world > 1 else 1, "nontemporal": nt,
+                       "buckets": buckets if world > 1 else 1,
+                       "bucket_autotune_ms": {str(b): round(t, 4) for b, t in tune.items()} or None,
+                       "nontemporal": nt,
                        "variant": args.variant, "fused_l2_norms": bool(args.with_norms),
                        "fused_server_step": args.server},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -117,14 +117,22 @@ def sqrt_f32(d: int) -> float:
 def row_stats(rows: Sequence[Tuple[int, int]], method: int, device: torch.device,
               want_qparams: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Stats (and quantizer parameters) of rows given as (device pointer, n)."""
-    R = len(rows)
+    return row_stats_table([p for p, _ in rows], [n for _, n in rows], method, device, want_qparams)
+
+
+def row_stats_table(ptrs, ns, method: int, device: torch.device,
+                    want_qparams: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """:func:`row_stats` with the row pointers and lengths as arrays."""
+    ns = np.asarray(ns, dtype=np.int64).reshape(-1)
+    R = ns.size
     tab = np.empty(R, dtype=ROW)
-    tab["ptr"] = [p for p, _ in rows]
-    tab["n"] = [n for _, n in rows]
-    if (tab["n"] < 1).any():
+    tab["ptr"] = np.asarray(ptrs, dtype=np.uint64).reshape(-1)
+    tab["n"] = ns
+    if (ns < 1).any():
         raise ValueError("quantizing an empty leaf: the reference fails on amin/amax of an empty array")
-    chunks = np.maximum(1, (tab["n"] + _lib.STATS_CHUNK - 1) // _lib.STATS_CHUNK)
-    prefix = np.concatenate([[0], np.cumsum(chunks)]).astype(np.int64)
+    chunks = np.maximum(1, (ns + _lib.STATS_CHUNK - 1) // _lib.STATS_CHUNK)
+    prefix = np.zeros(R + 1, dtype=np.int64)
+    np.cumsum(chunks, out=prefix[1:])
     nchunks = int(prefix[-1])
     up = Upload()
     o_rows, o_pre = up.add(tab), up.add(prefix)
@@ -193,6 +201,14 @@ def rademacher_words(keys: np.ndarray, ds: Sequence[int], device: torch.device) 
     return words, woff
 
 
+def _tiles_by_pass(ms: np.ndarray) -> np.ndarray:
+    """[npass, J] tile counts of every pass of 2^m jobs (evaluated once per distinct m)."""
+    uniq, inv = np.unique(ms, return_inverse=True)
+    npass = max(wht_passes(int(m)) for m in uniq)
+    per_m = np.array([[wht_tiles(int(m), p) for m in uniq] for p in range(npass)], dtype=np.int64)
+    return per_m[:, inv.reshape(-1)]
+
+
 def run_wht(jobs: np.ndarray, device: torch.device) -> Upload:
     """Launch every pass of the WHT jobs (structured WHT_JOB array)."""
     J = len(jobs)
@@ -201,10 +217,10 @@ def run_wht(jobs: np.ndarray, device: torch.device) -> Upload:
     ms = jobs["log2d"].astype(np.int64)
     if (ms < 0).any() or (ms > WHT_MAX_LOG2).any():
         raise ValueError("Walsh-Hadamard length out of range")
-    npass = max(wht_passes(int(m)) for m in ms)
+    tiles = _tiles_by_pass(ms)
+    npass = tiles.shape[0]
     pre = np.zeros((npass, J + 1), dtype=np.int64)
-    for p in range(npass):
-        pre[p, 1:] = np.cumsum([wht_tiles(int(m), p) for m in ms])
+    np.cumsum(tiles, axis=1, out=pre[:, 1:])
     totals = np.ascontiguousarray(pre[:, -1])
     up = Upload()
     o_jobs, o_pre = up.add(jobs), up.add(pre)
@@ -213,14 +229,28 @@ def run_wht(jobs: np.ndarray, device: torch.device) -> Upload:
     return up
 
 
+def wht_jobs(src, mid, dst, d, *, kind: int, n_in=None, n_out=None, signs=0, stats=0) -> np.ndarray:
+    """WHT_JOB table; every argument is a scalar or an array broadcast to the job count.
+    d are the (power-of-two) transform lengths; n_in / n_out default to d."""
+    cols = np.broadcast_arrays(*(np.asarray(a, dtype=np.uint64 if i < 3 or i > 5 else np.int64)
+                                 for i, a in enumerate((src, mid, dst, d,
+                                                        d if n_in is None else n_in,
+                                                        d if n_out is None else n_out,
+                                                        signs, stats))))
+    src, mid, dst, d, n_in, n_out, signs, stats = (c.reshape(-1) for c in cols)
+    ud, inv = np.unique(d, return_inverse=True)
+    log2 = np.array([log2_exact(int(x)) for x in ud], dtype=np.int32)[inv.reshape(-1)]
+    j = np.zeros(d.size, dtype=WHT_JOB)
+    j["src"], j["mid"], j["dst"], j["signs"], j["stats"] = src, mid, dst, signs, stats
+    j["n_in"], j["n_out"] = n_in, n_out
+    j["log2d"], j["kind"] = log2, kind
+    j["sqrt_d"] = np.sqrt(d.astype(np.float32))  # jnp.sqrt(d): correctly rounded f32
+    return j
+
+
 def wht_job(src: int, mid: int, dst: int, d: int, *, kind: int, n_in: Optional[int] = None,
             n_out: Optional[int] = None, signs: int = 0, stats: int = 0) -> np.ndarray:
-    j = np.zeros(1, dtype=WHT_JOB)
-    j["src"], j["mid"], j["dst"], j["signs"], j["stats"] = src, mid, dst, signs, stats
-    j["n_in"] = d if n_in is None else n_in
-    j["n_out"] = d if n_out is None else n_out
-    j["log2d"], j["kind"], j["sqrt_d"] = log2_exact(d), kind, sqrt_f32(d)
-    return j
+    return wht_jobs(src, mid, dst, d, kind=kind, n_in=n_in, n_out=n_out, signs=signs, stats=stats)
 
 
 # ----------------------------------------------------------------------------- rounds
@@ -241,15 +271,15 @@ def quantized_mean(method: int, rows: List[List[torch.Tensor]], keys: np.ndarray
     deltas). Returns (hist tensor or None, qparams tensor)."""
     device = outs[0].device
     K, L = len(rows), len(rows[0])
-    if qparams is None:
-        _, qparams = row_stats([(x.data_ptr(), x.numel()) for r in rows for x in r], method, device)
+    in_ptrs = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.uint64)
     leaf_n = np.array([x.numel() for x in rows[0]], dtype=np.int64)
+    if qparams is None:
+        _, qparams = row_stats_table(in_ptrs.reshape(-1), np.tile(leaf_n, K), method, device)
     h = None
     if hist:
         if K * L * (num_levels + 1) > (1 << 28):
             raise ValueError("arithmetic-coding histogram too large (K * leaves * (num_levels + 1) > 2^28)")
         h = torch.zeros(K * L * (num_levels + 1), dtype=torch.int32, device=device)
-    in_ptrs = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.uint64)
     out_ptrs = np.array([o.data_ptr() for o in outs], dtype=np.uint64)
     quant_fold(method, in_ptrs, keys, qparams.data_ptr(), w, leaf_n, out_ptrs, device, num_levels=num_levels,
                scale=scale, hist=h)
@@ -272,27 +302,28 @@ def rotated_quantized_mean(rows: List[List[torch.Tensor]], rot_keys: np.ndarray,
     B = _batch_size(K, 4 * D, workspace_bytes)
     Y = torch.empty((B, D), dtype=torch.float32, device=device)
     leaf_d = np.array(ds, dtype=np.int64)
+    leaf_n = np.asarray(leaf_n, dtype=np.int64)
+    loff = 4 * offs[:-1].astype(np.uint64)
+    sptr = np.asarray(sptr, dtype=np.uint64)
+    src_all = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.uint64)
     keep = []
     for k0 in range(0, K, B):
         kb = min(B, K - k0)
-        jobs = np.concatenate([
-            wht_job(rows[k0 + b][l].data_ptr(), Y[b].data_ptr() + 4 * int(offs[l]),
-                    Y[b].data_ptr() + 4 * int(offs[l]), ds[l], kind=_lib.WHT_ROTATE, n_in=leaf_n[l], signs=sptr[l])
-            for b in range(kb) for l in range(L)])
-        keep.append(run_wht(jobs, device))
-        yrows = [(Y[b].data_ptr() + 4 * int(offs[l]), ds[l]) for b in range(kb) for l in range(L)]
-        _, qp = row_stats(yrows, _lib.COMP_UNIFORM, device)
-        in_ptrs = np.array([[p for p, _ in yrows[b * L:(b + 1) * L]] for b in range(kb)], dtype=np.uint64)
-        out_ptrs = np.array([acc.data_ptr() + 4 * int(offs[l]) for l in range(L)], dtype=np.uint64)
+        ybase = np.uint64(Y.data_ptr()) + np.uint64(4 * D) * np.arange(kb, dtype=np.uint64)[:, None]
+        ydst = ybase + loff[None, :]  # [kb, L]
+        keep.append(run_wht(wht_jobs(src_all[k0:k0 + kb], ydst, ydst, leaf_d[None, :], kind=_lib.WHT_ROTATE,
+                                     n_in=leaf_n[None, :], signs=sptr[None, :]), device))
+        _, qp = row_stats_table(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1),
+                                _lib.COMP_UNIFORM, device)
+        out_ptrs = np.uint64(acc.data_ptr()) + loff
         last = k0 + kb == K
-        keep.append(quant_fold(_lib.COMP_UNIFORM, in_ptrs, client_keys[k0:k0 + kb], qp.data_ptr(), w[k0:k0 + kb],
+        keep.append(quant_fold(_lib.COMP_UNIFORM, ydst, client_keys[k0:k0 + kb], qp.data_ptr(), w[k0:k0 + kb],
                                leaf_d, out_ptrs, device, num_levels=num_levels,
                                scale=scale if last else None, accumulate=k0 > 0))
         keep.append(qp)
-    jobs = np.concatenate([
-        wht_job(acc.data_ptr() + 4 * int(offs[l]), acc.data_ptr() + 4 * int(offs[l]), outs[l].data_ptr(), ds[l],
-                kind=_lib.WHT_UNROTATE, n_out=leaf_n[l], signs=sptr[l]) for l in range(L)])
-    keep.append(run_wht(jobs, device))
+    accp = np.uint64(acc.data_ptr()) + loff
+    keep.append(run_wht(wht_jobs(accp, accp, [o.data_ptr() for o in outs], leaf_d, kind=_lib.WHT_UNROTATE,
+                                 n_out=leaf_n, signs=sptr), device))
     # keep the tables alive until the stream has consumed them (the caching allocator
     # reuses freed blocks only in stream order, so dropping them afterwards is safe)
     del keep
@@ -316,22 +347,25 @@ def drive_mean(rows: List[List[torch.Tensor]], client_keys: np.ndarray, w: np.nd
     Y = torch.empty((B, D), dtype=torch.float32, device=device)
     Z = torch.empty((B, Pp), dtype=torch.float32, device=device)
     w_dev = torch.from_numpy(np.ascontiguousarray(w, dtype=np.float32)).to(device)
+    leaf_n = np.asarray(leaf_n, dtype=np.int64)
+    leaf_d = np.asarray(ds, dtype=np.int64)
+    yoff = 4 * offs[:-1].astype(np.uint64)
+    zoff = 4 * loff[:-1].astype(np.uint64)
+    src_all = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.uint64)
     for k0 in range(0, K, B):
         kb = min(B, K - k0)
         signs, woff = rademacher_words(client_keys[k0:k0 + kb].reshape(-1, 2), ds * kb, device)
-        sptr = lambda b, l: signs.data_ptr() + 4 * int(woff[b * L + l])
-        ydst = lambda b, l: Y[b].data_ptr() + 4 * int(offs[l])
-        fwd = np.concatenate([
-            wht_job(rows[k0 + b][l].data_ptr(), ydst(b, l), ydst(b, l), ds[l], kind=_lib.WHT_ROTATE,
-                    n_in=leaf_n[l], signs=sptr(b, l)) for b in range(kb) for l in range(L)])
-        t1 = run_wht(fwd, device)
-        stats, _ = row_stats([(ydst(b, l), ds[l]) for b in range(kb) for l in range(L)], 0, device,
-                             want_qparams=False)
-        inv = np.concatenate([
-            wht_job(ydst(b, l), ydst(b, l), Z[b].data_ptr() + 4 * int(loff[l]), ds[l],
-                    kind=_lib.WHT_UNROTATE_DRIVE, n_out=leaf_n[l], signs=sptr(b, l),
-                    stats=stats.data_ptr() + STATS.itemsize * (b * L + l)) for b in range(kb) for l in range(L)])
-        t2 = run_wht(inv, device)
+        sptr = (np.uint64(signs.data_ptr()) + 4 * woff[:-1].astype(np.uint64)).reshape(kb, L)
+        bidx = np.arange(kb, dtype=np.uint64)[:, None]
+        ydst = np.uint64(Y.data_ptr()) + np.uint64(4 * D) * bidx + yoff[None, :]
+        zdst = np.uint64(Z.data_ptr()) + np.uint64(4 * Pp) * bidx + zoff[None, :]
+        t1 = run_wht(wht_jobs(src_all[k0:k0 + kb], ydst, ydst, leaf_d[None, :], kind=_lib.WHT_ROTATE,
+                              n_in=leaf_n[None, :], signs=sptr), device)
+        stats, _ = row_stats_table(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1), 0, device,
+                                   want_qparams=False)
+        sts = np.uint64(stats.data_ptr()) + np.uint64(STATS.itemsize) * np.arange(kb * L, dtype=np.uint64)
+        t2 = run_wht(wht_jobs(ydst, ydst, zdst, leaf_d[None, :], kind=_lib.WHT_UNROTATE_DRIVE,
+                              n_out=leaf_n[None, :], signs=sptr, stats=sts.reshape(kb, L)), device)
         last = k0 + kb == K
         kernels.weighted_sum_dense(Z[:kb, :P], w_dev[k0:k0 + kb], scale=scale if last else None, out=out_flat,
                                    accumulate=k0 > 0)
@@ -361,29 +395,57 @@ def arithmetic_bits(hist: torch.Tensor, qparams: torch.Tensor, K: int, leaf_n: S
                     num_levels: int) -> List[np.float32]:
     """Per-client bit counts (sum over leaves) from the level histograms: the level
     values are recomputed with the kernel's f32 op sequence and equal values merged,
-    which is jnp.unique + jnp.histogram of the quantized leaf (compression.py:143-149)."""
-    f32 = np.float32
+    which is jnp.unique + jnp.histogram of the quantized leaf (compression.py:143-149).
+    Vectorised over the K x L (client, leaf) rows; rows with the same number of
+    distinct values share one array pass (numpy's row reductions are the 1-D ones)."""
     L = len(leaf_n)
     nb = num_levels + 1
-    H = hist.cpu().numpy().reshape(K, L, nb)
-    Q = np.frombuffer(qparams.cpu().numpy().tobytes(), dtype=QPARAMS).reshape(K, L)
+    H = hist.cpu().numpy().reshape(K * L, nb).astype(np.int64)
+    Q = np.frombuffer(qparams.cpu().numpy().tobytes(), dtype=QPARAMS).reshape(K * L)
+    return arithmetic_bits_host(H, Q, K, leaf_n, num_levels)
+
+
+def arithmetic_bits_host(H: np.ndarray, Q: np.ndarray, K: int, leaf_n: Sequence[int],
+                         num_levels: int) -> List[np.float32]:
+    """:func:`arithmetic_bits` on host arrays H [K*L, num_levels + 1], Q [K*L]."""
+    f32 = np.float32
+    L = len(leaf_n)
+    R = K * L
+    nb = num_levels + 1
     lm1 = f32(num_levels - 1)
+    fmax = np.finfo(f32).max
     with np.errstate(all="ignore"):
         qv = (np.arange(num_levels, dtype=f32) / lm1).astype(f32)
-    out = []
-    for k in range(K):
-        bits = 0
-        for l in range(L):
-            q = Q[k, l]
-            with np.errstate(all="ignore"):
-                vals = (q["vmin"] + (qv * q["range"]).astype(f32)).astype(f32)
-            vals = np.concatenate([vals, [f32(np.nan)]])
-            vals = np.nan_to_num(vals, nan=0.0, posinf=np.finfo(f32).max, neginf=-np.finfo(f32).max).astype(f32)
-            cnt = H[k, l]
-            nz = cnt > 0
-            uniq, inv = np.unique(vals[nz], return_inverse=True)
-            merged = np.zeros(uniq.size, dtype=np.int64)
-            np.add.at(merged, inv, cnt[nz])
-            bits = bits + arithmetic_bits_from_counts(merged, int(leaf_n[l]))
-        out.append(f32(bits))
-    return out
+        vals = (Q["vmin"][:, None] + (qv[None, :] * Q["range"][:, None]).astype(f32)).astype(f32)
+    vals = np.concatenate([vals, np.zeros((R, 1), f32)], axis=1)  # the NaN bin: nan_to_num(NaN) = 0
+    vals = np.nan_to_num(vals, nan=0.0, posinf=fmax, neginf=-fmax).astype(f32)
+    # distinct values of the occupied bins, ascending (np.unique order), counts merged
+    big = np.where(H > 0, vals, np.inf)
+    order = np.argsort(big, axis=1, kind="stable")
+    sv = np.take_along_axis(big, order, axis=1)
+    sc = np.take_along_axis(H, order, axis=1)
+    occupied = sc > 0
+    new = occupied.copy()
+    new[:, 1:] &= sv[:, 1:] != sv[:, :-1]
+    grp = np.cumsum(new, axis=1) - 1  # group index of each occupied sorted bin
+    u = new.sum(axis=1)  # distinct values per row
+    flat = (np.arange(R)[:, None] * nb + grp)[occupied]
+    merged = np.bincount(flat, weights=sc[occupied], minlength=R * nb).astype(np.int64).reshape(R, nb)
+    d = np.asarray(leaf_n, dtype=np.int64)[np.arange(R) % L]
+    e = f32(np.exp(f32(1)))
+    per_row = np.zeros(R, dtype=f32)
+    for k in np.unique(u):
+        sel = np.nonzero(u == k)[0]
+        hist = np.ascontiguousarray(merged[sel, :k])
+        with np.errstate(divide="ignore", invalid="ignore"):
+            p = (hist.astype(f32) / hist.sum(axis=1).astype(f32)[:, None]).astype(f32)
+            ent = (-np.sum((p * _log2_f32(p)).astype(f32), axis=1, dtype=f32)).astype(f32)
+            dk = d[sel]
+            hist_bits = (f32(k) * _log2_f32(((e * (dk + k).astype(f32)).astype(f32) / f32(k)).astype(f32))).astype(f32)
+            per_row[sel] = (((hist_bits + (dk.astype(f32) * ent).astype(f32)).astype(f32) + f32(64)).astype(f32)
+                            + f32(2)).astype(f32)
+    per_row = per_row.reshape(K, L)
+    bits = per_row[:, 0].copy()
+    for l in range(1, L):
+        bits = (bits + per_row[:, l]).astype(f32)
+    return [f32(b) for b in bits]

@@ -199,6 +199,33 @@ __device__ inline Partial shfl_xor(const Partial& p, int m) {
   return q;
 }
 
+// Per-lane accumulator: min / max / |max| in f32 (exact; NaN tracked by a flag, as the
+// f64 nan_min / nan_max fold it into), sums in f64. v*v of an f32 v is exact in f64, so
+// fma(v, v, s) is the rounding of s + v*v.
+struct LaneStats {
+  float mn = INFINITY, mx = -INFINITY, amx = -INFINITY;
+  double s1 = 0.0, s2 = 0.0, sa = 0.0;
+  bool nan = false;
+  __device__ inline void add(float x) {
+    nan |= x != x;
+    mn = fminf(mn, x);
+    mx = fmaxf(mx, x);
+    const float a = fabsf(x);
+    amx = fmaxf(amx, a);
+    const double v = (double)x;
+    s1 += v;
+    s2 = __fma_rn(v, v, s2);
+    sa += (double)a;
+  }
+  __device__ inline Partial partial() const {
+    const double qn = __longlong_as_double(0x7ff8000000000000ll);
+    return Partial{nan ? qn : (double)mn, nan ? qn : (double)mx, nan ? qn : (double)amx, s1, s2, sa};
+  }
+};
+
+// One workgroup per 16 Ki-element chunk of a row: a scalar head up to the first 16-byte
+// boundary, float4 loads four deep per lane, a scalar tail; then the fixed-order wave
+// butterfly and a per-workgroup combine in wave order (deterministic).
 __global__ __launch_bounds__(kStatsThreads) void k_row_stats(const fjcomp_row* __restrict__ rows,
                                                               const int64_t* __restrict__ prefix, int64_t R,
                                                               Partial* __restrict__ part) {
@@ -207,17 +234,36 @@ __global__ __launch_bounds__(kStatsThreads) void k_row_stats(const fjcomp_row* _
   const fjcomp_row row = rows[r];
   const int64_t c0 = (b - prefix[r]) * kStatsChunk;
   const int64_t c1 = min(row.n, c0 + kStatsChunk);
-  Partial p = {INFINITY, -INFINITY, -INFINITY, 0.0, 0.0, 0.0};
-  for (int64_t e = c0 + threadIdx.x; e < c1; e += kStatsThreads) {
-    const float x = row.ptr[e];
-    const double v = (double)x;
-    p.mn = nan_min(p.mn, v);
-    p.mx = nan_max(p.mx, v);
-    p.amx = nan_max(p.amx, fabs(v));
-    p.s1 += v;
-    p.s2 += v * v;
-    p.sa += fabs(v);
+  const float* __restrict__ x = row.ptr + c0;
+  const int n = (int)(c1 - c0);
+  const bool vec = ((uintptr_t)x & 3) == 0;  // else everything goes through the scalar tail
+  const int head = vec ? min(n, (int)(((16 - ((uintptr_t)x & 15)) & 15) >> 2)) : 0;
+  const int nv = vec ? (n - head) >> 2 : 0;
+  LaneStats st;
+  if ((int)threadIdx.x < head) st.add(x[threadIdx.x]);
+  const float4* __restrict__ xv = reinterpret_cast<const float4*>(x + head);
+  int i = threadIdx.x;
+  for (; i + 3 * kStatsThreads < nv; i += 4 * kStatsThreads) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = xv[i + u * kStatsThreads];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      st.add(v[u].x);
+      st.add(v[u].y);
+      st.add(v[u].z);
+      st.add(v[u].w);
+    }
   }
+  for (; i < nv; i += kStatsThreads) {
+    const float4 v = xv[i];
+    st.add(v.x);
+    st.add(v.y);
+    st.add(v.z);
+    st.add(v.w);
+  }
+  for (int e = head + 4 * nv + threadIdx.x; e < n; e += kStatsThreads) st.add(x[e]);
+  Partial p = st.partial();
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) merge(p, shfl_xor(p, m));
   __shared__ Partial sp[kStatsThreads / 64];
@@ -230,15 +276,20 @@ __global__ __launch_bounds__(kStatsThreads) void k_row_stats(const fjcomp_row* _
   }
 }
 
+// One wave per row: lane j merges chunks j, j + 64, ... in order, then a fixed butterfly.
 __global__ __launch_bounds__(256) void k_stats_combine(const fjcomp_row* __restrict__ rows,
                                                         const int64_t* __restrict__ prefix, int64_t R,
                                                         const Partial* __restrict__ part, int method,
                                                         fjcomp_stats* __restrict__ stats,
                                                         fjcomp_qparams* __restrict__ qp) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
-  Partial t = part[prefix[r]];
-  for (int64_t c = prefix[r] + 1; c < prefix[r + 1]; ++c) merge(t, part[c]);
+  const int lane = threadIdx.x & 63;
+  Partial t = {INFINITY, -INFINITY, -INFINITY, 0.0, 0.0, 0.0};
+  for (int64_t c = prefix[r] + lane; c < prefix[r + 1]; c += 64) merge(t, part[c]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) merge(t, shfl_xor(t, m));
+  if (lane != 0) return;
   stats[r] = fjcomp_stats{t.mn, t.mx, t.amx, t.s1, t.s2, t.sa};
   if (!qp) return;
   fjcomp_qparams q;
@@ -606,7 +657,7 @@ int fjcomp_row_stats(const fjcomp_row* rows, const int64_t* chunk_prefix, int64_
   Partial* part = static_cast<Partial*>(ws);
   hipLaunchKernelGGL(k_row_stats, dim3((unsigned)nchunks), dim3(kStatsThreads), 0, s, rows, chunk_prefix, R, part);
   if (int rc = check_launch("k_row_stats")) return rc;
-  hipLaunchKernelGGL(k_stats_combine, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, rows, chunk_prefix, R, part,
+  hipLaunchKernelGGL(k_stats_combine, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, s, rows, chunk_prefix, R, part,
                      method, stats, qparams);
   return check_launch("k_stats_combine");
 }

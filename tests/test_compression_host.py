@@ -122,3 +122,58 @@ def test_host_argument_validation():
     assert lib.fjcomp_random_bits(0, 0, 1 << 33, None, None) == -1
     tiles = (ctypes.c_int64 * 1)(0)
     assert lib.fjcomp_wht(None, None, 1, 1, tiles, None) == -1
+
+
+def _arith_bits_rowwise(H, Q, K, leaf_n, num_levels):
+    """Per-(client, leaf) restatement: level values -> np.unique merge -> oracle bit count."""
+    f32 = np.float32
+    L = len(leaf_n)
+    qv = (np.arange(num_levels, dtype=f32) / f32(num_levels - 1)).astype(f32)
+    out = []
+    for k in range(K):
+        bits = 0
+        for l in range(L):
+            q = Q[k * L + l]
+            with np.errstate(all="ignore"):
+                vals = (q["vmin"] + (qv * q["range"]).astype(f32)).astype(f32)
+            vals = cref.nan_to_num(np.concatenate([vals, [f32(np.nan)]]).astype(f32))
+            cnt = H[k * L + l]
+            nz = cnt > 0
+            uniq, inv = np.unique(vals[nz], return_inverse=True)
+            merged = np.zeros(uniq.size, dtype=np.int64)
+            np.add.at(merged, inv.reshape(-1), cnt[nz])
+            bits = bits + cref.arithmetic_bits_from_counts(merged, int(leaf_n[l]))
+        out.append(f32(bits))
+    return out
+
+
+@pytest.mark.parametrize("num_levels", [2, 3, 16])
+def test_arithmetic_bits_vectorised_matches_rowwise(num_levels):
+    rs = np.random.RandomState(num_levels)
+    K, leaf_n = 37, [32, 288, 64, 18432, 128, 1179648, 62, 7936]
+    L = len(leaf_n)
+    R = K * L
+    Q = np.zeros(R, dtype=C.QPARAMS)
+    Q["vmin"] = rs.standard_normal(R).astype(np.float32)
+    Q["range"] = np.abs(rs.standard_normal(R)).astype(np.float32)
+    Q["range"][::7] = 0.0  # constant rows: every level collapses onto vmin
+    Q["vmin"][::11] = np.inf  # NaN level values after the range product
+    Q["vmin"][::13] = 0.0  # a level equal to the NaN bin's 0
+    H = rs.randint(0, 50, size=(R, num_levels + 1)).astype(np.int64)
+    H[rs.rand(R, num_levels + 1) < 0.3] = 0
+    H[::5, :] = 0
+    H[::5, 0] = 9  # single occupied bin
+    got = C.arithmetic_bits_host(H, Q, K, leaf_n, num_levels)
+    want = _arith_bits_rowwise(H, Q, K, leaf_n, num_levels)
+    assert np.array_equal(np.array(got, np.float32).view(np.uint32), np.array(want, np.float32).view(np.uint32))
+
+
+def test_wht_jobs_vectorised_matches_single():
+    d = np.array([32, 512, 2 ** 21], dtype=np.int64)
+    j = C.wht_jobs(np.array([[1, 2, 3]], np.uint64) * 16, 64, [5 * 16, 6 * 16, 7 * 16], d[None, :],
+                   kind=2, n_in=[30, 300, 2 ** 20 + 1], signs=np.array([[8, 9, 10]], np.uint64) * 16)
+    for i in range(3):
+        one = C.wht_job(16 * (i + 1), 64, 16 * (5 + i), int(d[i]), kind=2, n_in=[30, 300, 2 ** 20 + 1][i],
+                        signs=16 * (8 + i))
+        assert j[i].tobytes() == one[0].tobytes()
+    assert list(j["log2d"]) == [5, 9, 21] and j["sqrt_d"][2] == np.float32(np.sqrt(np.float32(2 ** 21)))
