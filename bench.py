@@ -117,8 +117,15 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also time host-resident deltas (H2D + fold + D2H)")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--all-ranks", action="store_true", help="all_reduce instead of reduce to rank 0")
+    ap.add_argument("--engine", choices=["auto", "native", "torch"], default="auto",
+                    help="N>1 exchange: native RCCL pipeline (include/fjcomm.h), torch.distributed, or the "
+                         "faster of the two measured during warmup")
     ap.add_argument("--server", choices=["none", "sgd", "adam"], default="none",
                     help="fuse the server optimizer step into the fold (N=1; examples/fed_avg.py:97-101)")
+    ap.add_argument("--rehearse-shard", type=int, default=0, metavar="N",
+                    help="one GPU, world 1: run rank 0's share of an N-way shard through the full sharded "
+                         "step (RCCL communicator of one rank). Timing rehearsal only: no cross-GPU traffic")
+    ap.add_argument("--clients", type=int, default=0, help="override the workload's client count (experiments)")
     ap.add_argument("--with-norms", action="store_true",
                     help="fuse every client's delta l2 norm into the fold (examples/fed_avg.py:79-81)")
     args = ap.parse_args()
@@ -131,7 +138,15 @@ def main():
             raise SystemExit("launch N>1 with torch.distributed.run (one rank per GPU)")
     dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
-    if world > 1:
+    nshard = world
+    if args.rehearse_shard > 1:
+        if world != 1:
+            raise SystemExit("--rehearse-shard runs as a single process")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        nshard = args.rehearse_shard
+    sharded = nshard > 1
+    if sharded:
         if args.backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
@@ -141,12 +156,14 @@ def main():
     from fedjax_amd import distributed as fd, kernels, tree_util as tu
 
     K, P, dtype, desc = WORKLOADS[args.workload]
+    if args.clients:
+        K, desc = args.clients, desc + f" [clients overridden: {args.clients}]"
     esize = torch.empty((), dtype=dtype).element_size()
     weights = fedavg_weights(K)
     W = 0.0
     for w in weights:
         W += w  # tree_util.py:95
-    k0, k1 = fd.shard_range(K, rank, world)
+    k0, k1 = fd.shard_range(K, rank, nshard)
     Kl = k1 - k0
     if Kl > 1024 and dtype == torch.bfloat16:
         raise SystemExit(f"{args.workload}: {Kl} clients x {P} params per GPU exceed 288 GB; use more GPUs")
@@ -156,8 +173,8 @@ def main():
     x = torch.empty(Kl, ld, dtype=dtype, device=dev)[:, :P]
     kernels.fill_synth(x, seed=0, k0=k0)  # the same global client k on every N
     w_local = [weights[k] for k in range(k0, k1)]
-    out = torch.empty(P, dtype=dtype if world == 1 else torch.float32, device=dev)
-    final = torch.empty(P, dtype=dtype, device=dev) if (world > 1 and dtype != torch.float32) else None
+    out = torch.empty(P, dtype=dtype if not sharded else torch.float32, device=dev)
+    final = torch.empty(P, dtype=dtype, device=dev) if (sharded and dtype != torch.float32) else None
     ones = torch.ones(1, dtype=torch.float32, device=dev)
     nbytes_local = Kl * P * esize
     nt = (nbytes_local >= tu.NONTEMPORAL_MIN_BYTES) if args.nontemporal < 0 else bool(args.nontemporal)
@@ -170,7 +187,7 @@ def main():
 
     def fold(xs, wd, o, events):
         if events is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, e1 = kernels.Event(), kernels.Event()
             e0.record(stream)
         if args.with_norms:
             kernels.weighted_sum_l2_dense(xs, wd, scale=scale, out=o, l2sq=l2sq, nontemporal=nt,
@@ -182,19 +199,34 @@ def main():
             events.append((e0, e1, xs.shape[0] * xs.shape[1] * esize))
 
     if args.server != "none":
-        if world > 1 or dtype != torch.float32:
+        if sharded or dtype != torch.float32:
             raise SystemExit("--server runs at N=1 on f32 slabs")
         from fedjax_amd import _lib as flib, server as fsrv
         sopt = fsrv.sgd(10 ** -1.5) if args.server == "sgd" else fsrv.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)
         sparams = torch.zeros(P, dtype=torch.float32, device=dev)
         sstate = sopt.init(sparams)
 
+    # N>1 exchange engines: "native" = one fjcomm_sharded_wsum_dense call per step (own RCCL
+    # communicator, device-scope events between fold and reduce buckets); "torch" = per-bucket
+    # HIP fold + torch.distributed collective (ProcessGroupNCCL)
+    comm = None
+    if sharded and args.backend == "nccl" and args.engine in ("auto", "native") and not args.with_norms:
+        try:
+            comm = fd.RcclCommunicator(device=dev)
+        except Exception as e:  # noqa: BLE001 - the torch engine still runs
+            if args.engine == "native":
+                raise
+            log(f"native RCCL communicator unavailable ({e}); using torch.distributed")
+    engine = "native" if comm is not None else "torch"
+    buckets = args.buckets or 1
+    root = 0
+
     def step(events=None):
         wd = torch.from_numpy(np.float32(w_local)).pin_memory().to(dev, non_blocking=True)
         if args.server != "none":
             desc = sopt.descriptor(1)  # copied by value into the kernel arguments at launch
             if events is not None:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0, e1 = kernels.Event(), kernels.Event()
                 e0.record(stream)
             flib.call("fjagg_server_update_dense", flib.F32, x.data_ptr(), x.stride(0), Kl, P, wd.data_ptr(),
                       scale, ctypes.byref(desc), sparams.data_ptr(),
@@ -204,13 +236,22 @@ def main():
             if events is not None:
                 e1.record(stream)
                 events.append((e0, e1, Kl * P * esize))
-        elif world == 1:
+        elif not sharded:
             fold(x, wd, out, events)
+        elif engine == "native":
+            evs = None
+            if events is not None:
+                evs = [kernels.Event() for _ in range(2 * buckets)]
+            fd.sharded_weighted_mean(x, wd, W, buckets=buckets, out=out, all_ranks=args.all_ranks, comm=comm,
+                                     nontemporal=nt, fold_events=evs)
+            if evs is not None:
+                for (p0, p1), i in zip(fd.bucket_edges(P, buckets), range(0, 2 * buckets, 2)):
+                    events.append((evs[i], evs[i + 1], Kl * (p1 - p0) * esize))
         else:
             fd.sharded_weighted_mean(x, wd, W, buckets=buckets, out=out, all_ranks=args.all_ranks,
                                      partial_fn=lambda xs, wdd, sc, o: fold(xs, wdd, o, events))
-            if final is not None and (rank == 0 or args.all_ranks):  # f32 mean -> leaf dtype
-                kernels.weighted_sum_dense(out.view(1, P), ones, out=final)
+        if sharded and final is not None and (rank == root or args.all_ranks):  # f32 mean -> leaf dtype
+            kernels.weighted_sum_dense(out.view(1, P), ones, out=final)
 
     def wall(nsteps):
         """Max-over-ranks wall time of nsteps steps, bracketed like the timed region."""
@@ -225,35 +266,38 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    buckets = args.buckets or 4
     tune = {}
-    if world > 1 and args.buckets == 0:
+    if sharded and args.buckets == 0:
         # every rank measures every candidate and sees the same max-over-ranks times,
-        # so all ranks pick the same bucket count without another exchange
-        for b in BUCKET_CANDIDATES:
-            if P // b < fd.BUCKET_ALIGN:
-                continue
-            buckets = b
-            wall(2)
-            tune[b] = wall(5) / 5 * 1e3
-        buckets = min(tune, key=tune.get)
-        log(f"bucket auto-tune (ms/step, max over ranks): {tune} -> {buckets}")
+        # so all ranks pick the same (engine, buckets) without another exchange
+        engines = ["native", "torch"] if comm is not None and args.engine == "auto" else [engine]
+        for eng in engines:
+            for b in BUCKET_CANDIDATES:
+                if P // b < fd.BUCKET_ALIGN:
+                    continue
+                engine, buckets = eng, b
+                wall(2)
+                tune[f"{eng}/{b}"] = wall(5) / 5 * 1e3
+        best = min(tune, key=tune.get)
+        engine, buckets = best.split("/")[0], int(best.split("/")[1])
+        log(f"exchange auto-tune (ms/step, max over ranks): {tune} -> {best}")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     events = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(events)
+    t_issue = time.perf_counter() - t0  # host time to enqueue the steps (host-bound if ~ elapsed)
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
+    if sharded:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -263,7 +307,7 @@ def main():
     achieved = bytes_per_launch / mean_kernel_s / 1e9
 
     e2e = None
-    if args.e2e and world == 1:
+    if args.e2e and not sharded:
         xh = torch.empty(K, P, dtype=dtype).pin_memory()
         xh.copy_(x.cpu())
         yh = torch.empty(P, dtype=out.dtype).pin_memory()
@@ -279,7 +323,7 @@ def main():
         del xh
 
     if rank == 0:
-        value = K * P * esize * args.steps / elapsed / 1e9
+        value = (K if nshard == world else Kl) * P * esize * args.steps / elapsed / 1e9
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -288,23 +332,26 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
             "data": "synthetic: counter-hash client deltas 0.01*u[-1,1), integer weights in [1,500]",
             "config": {"workload": desc, "clients": K, "params": P, "clients_per_gpu": Kl,
-                       "parallelism": f"client-sharded x{world}" + (
+                       "parallelism": f"client-sharded x{nshard}" + (
                            f" + {'RCCL' if args.backend == 'nccl' else args.backend} "
-                           f"{'all_reduce' if args.all_ranks else 'reduce'}" if world > 1 else ""),
-                       "buckets": buckets if world > 1 else 1,
-                       "bucket_autotune_ms": {str(b): round(t, 4) for b, t in tune.items()} or None,
+                           f"{'all_reduce' if args.all_ranks else 'reduce'}" if sharded else "") + (
+                           " (REHEARSAL: one GPU runs rank 0's share, RCCL world 1)" if nshard != world else ""),
+                       "buckets": buckets if sharded else 1,
+                       "exchange_engine": engine if sharded else None,
+                       "exchange_autotune_ms": {k: round(t, 4) for k, t in tune.items()} or None,
                        "nontemporal": nt,
                        "variant": args.variant, "fused_l2_norms": bool(args.with_norms),
                        "fused_server_step": args.server},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4),
-                         "traffic": load_traffic(args.workload) if (world == 1 and not args.with_norms
+                         "traffic": load_traffic(args.workload) if (not sharded and not args.with_norms
                                                                     and args.server == "none") else None,
                          "kernel": ("k_dense_opt fold + server " + args.server if args.server != "none" else
                                     "k_dense_l2 fold + per-client l2" if args.with_norms else "k_dense weighted fold"),
@@ -313,10 +360,15 @@ def main():
         }
         if e2e is not None:
             res["e2e_host_resident_GBs"] = round(e2e, 2)
-        if world == 1 and not args.no_cpu_baseline and dtype == torch.float32:
+        if nshard != world:
+            res["rehearsal_projected_whole_job_GBs"] = round(value * nshard, 2)
+        if not sharded and not args.no_cpu_baseline and dtype == torch.float32:
             res["cpu_baseline"] = cpu_baseline(K)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
+    if sharded:
         dist.destroy_process_group()
 
 

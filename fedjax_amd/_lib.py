@@ -1,5 +1,6 @@
 """ctypes binding of ``libfjagg.so`` — the C ABI declared in ``include/fjagg.h``
-(aggregation) and ``include/fjcomp.h`` (compression aggregators).
+(aggregation), ``include/fjcomp.h`` (compression aggregators) and
+``include/fjcomm.h`` (client-sharded aggregation over RCCL, timing events).
 
 The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950) into
 ``fedjax_amd/_build/libfjagg.so``. It links against the HIP runtime by soname
@@ -31,6 +32,9 @@ SCALE, ACCUMULATE, NONTEMPORAL, UNALIGNED, UNBALANCED = 1, 2, 4, 8, 16
 MODE_EXACT, MODE_SPLIT = 0, 1
 ABI_VERSION = 1
 COMP_ABI_VERSION = 1
+COMM_ABI_VERSION = 1
+COMM_ID_BYTES = 128
+COMM_MAX_BUCKETS = 64
 # include/fjcomp.h
 COMP_UNIFORM, COMP_TERNGRAD, COMP_BINARY = 1, 2, 3
 WHT_PLAIN, WHT_ROTATE, WHT_UNROTATE, WHT_UNROTATE_DRIVE = 0, 1, 2, 3
@@ -68,6 +72,17 @@ _SIGNATURES = {
                                  _vp, _vp]),
     "fjcomp_wht_tiles": (_i64, [_i32, _i32]),
     "fjcomp_wht": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    # include/fjcomm.h
+    "fjcomm_abi_version": (_i32, []),
+    "fjcomm_unique_id": (_i32, [_vp]),
+    "fjcomm_init": (_i32, [_vp, _vp, _i32, _i32]),
+    "fjcomm_destroy": (_i32, [_vp]),
+    "fjcomm_sharded_wsum_dense": (_i32, [_vp, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _i32, _i32, _i32, _vp,
+                                         _vp]),
+    "fjagg_event_create": (_i32, [_vp]),
+    "fjagg_event_destroy": (_i32, [_vp]),
+    "fjagg_event_record": (_i32, [_vp, _vp]),
+    "fjagg_event_elapsed_ms": (_i32, [_vp, _vp, _vp]),
 }
 SYMBOLS = tuple(_SIGNATURES)
 
@@ -122,9 +137,9 @@ def load() -> ctypes.CDLL:
             if fn is None:
                 raise FjaggError(f"{LIB_PATH} does not export {name}")
             fn.restype, fn.argtypes = res, args
-        if lib.fjagg_abi_version() != ABI_VERSION or lib.fjcomp_abi_version() != COMP_ABI_VERSION:
-            raise FjaggError(f"ABI mismatch: library {lib.fjagg_abi_version()}/{lib.fjcomp_abi_version()} "
-                             f"!= {ABI_VERSION}/{COMP_ABI_VERSION}")
+        got = (lib.fjagg_abi_version(), lib.fjcomp_abi_version(), lib.fjcomm_abi_version())
+        if got != (ABI_VERSION, COMP_ABI_VERSION, COMM_ABI_VERSION):
+            raise FjaggError(f"ABI mismatch: library {got} != {(ABI_VERSION, COMP_ABI_VERSION, COMM_ABI_VERSION)}")
         runtimes = hip_runtimes_mapped()
         if len(runtimes) > 1:
             raise FjaggError(f"two HIP runtimes mapped into one process: {runtimes}")

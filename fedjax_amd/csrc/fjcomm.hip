@@ -1,0 +1,259 @@
+// fjcomm.hip — client-sharded weighted mean over the GPUs of one node: each rank folds
+// its clients with the dense fold of fjagg.hip, RCCL sums the per-rank partials over
+// xGMI. C ABI and the pipeline it issues: include/fjcomm.h.
+//
+// Every bucket but the last is reduced on the communicator's own high-priority stream,
+// waiting only for that bucket's fold (an event with a device-scope release), so those
+// reduces overlap the following folds; the last bucket is reduced on the caller's
+// stream, because a cross-queue hop back costs ~30 us of GPU-side latency on MI355X
+// (profiles/r01g_*) and nothing is left to overlap it with.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "fjagg.h"
+#include "fjcomm.h"
+
+extern thread_local char fjagg_g_err[512];
+
+namespace {
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(fjagg_g_err, sizeof(fjagg_g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(FJAGG_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------------ RCCL, resolved at run time
+// Declared here with the ABI of rccl.h (ncclResult_t / ncclDataType_t / ncclRedOp_t are
+// C enums, ncclComm_t a pointer, ncclUniqueId 128 opaque bytes).
+struct NcclId {
+  char internal[FJCOMM_ID_BYTES];
+};
+typedef void* NcclComm;
+constexpr int kNcclSuccess = 0;
+constexpr int kNcclFloat32 = 7;
+constexpr int kNcclSum = 0;
+
+struct Rccl {
+  int (*get_unique_id)(NcclId*) = nullptr;
+  int (*comm_init_rank)(NcclComm*, int, NcclId, int) = nullptr;
+  int (*comm_destroy)(NcclComm) = nullptr;
+  int (*reduce)(const void*, void*, size_t, int, int, int, NcclComm, hipStream_t) = nullptr;
+  int (*all_reduce)(const void*, void*, size_t, int, int, NcclComm, hipStream_t) = nullptr;
+  const char* (*error_string)(int) = nullptr;
+  bool ok = false;
+};
+
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl t;
+    // the copy torch loaded (libtorch_hip needs librccl.so.1), else the system one
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return t;
+    t.get_unique_id = reinterpret_cast<decltype(t.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+    t.comm_init_rank = reinterpret_cast<decltype(t.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+    t.comm_destroy = reinterpret_cast<decltype(t.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    t.reduce = reinterpret_cast<decltype(t.reduce)>(dlsym(h, "ncclReduce"));
+    t.all_reduce = reinterpret_cast<decltype(t.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    t.error_string = reinterpret_cast<decltype(t.error_string)>(dlsym(h, "ncclGetErrorString"));
+    t.ok = t.get_unique_id && t.comm_init_rank && t.comm_destroy && t.reduce && t.all_reduce && t.error_string;
+    return t;
+  }();
+  return r;
+}
+
+int nccl_fail(int rc, const char* what) {
+  return fail(FJAGG_EHIP, "%s: RCCL error %d (%s)", what, rc, rccl().error_string ? rccl().error_string(rc) : "?");
+}
+
+int need_rccl() {
+  if (!rccl().ok) return fail(FJAGG_EUNSUPPORTED, "librccl.so.1 (ncclGetUniqueId, ncclCommInitRank, ...) not found");
+  return FJAGG_OK;
+}
+
+struct Comm {
+  NcclComm nc = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+  hipStream_t cs = nullptr;
+  hipEvent_t ready[FJCOMM_MAX_BUCKETS] = {};
+  hipEvent_t done = nullptr;
+};
+
+// Cross-stream dependency events: no timing, device-scope release.
+hipError_t make_dep_event(hipEvent_t* e) {
+  hipError_t rc = hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice);
+  if (rc != hipSuccess) {  // runtime without the release flags: plain untimed event
+    (void)hipGetLastError();
+    rc = hipEventCreateWithFlags(e, hipEventDisableTiming);
+  }
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fjcomm_abi_version(void) { return FJCOMM_ABI_VERSION; }
+
+int fjcomm_unique_id(uint8_t* id) {
+  fjagg_g_err[0] = 0;
+  if (int rc = need_rccl()) return rc;
+  if (!id) return fail(FJAGG_EINVAL, "null id");
+  NcclId u;
+  if (int rc = rccl().get_unique_id(&u)) return nccl_fail(rc, "ncclGetUniqueId");
+  memcpy(id, u.internal, FJCOMM_ID_BYTES);
+  return FJAGG_OK;
+}
+
+int fjcomm_init(void** comm, const uint8_t* id, int nranks, int rank) {
+  fjagg_g_err[0] = 0;
+  if (int rc = need_rccl()) return rc;
+  if (!comm || !id) return fail(FJAGG_EINVAL, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(FJAGG_EINVAL, "bad rank %d of %d", rank, nranks);
+  Comm* c = new Comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  hipError_t e = hipGetDevice(&c->device);
+  int lo = 0, hi = 0;
+  if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, hi);
+  for (int b = 0; e == hipSuccess && b < FJCOMM_MAX_BUCKETS; ++b) e = make_dep_event(&c->ready[b]);
+  if (e == hipSuccess) e = make_dep_event(&c->done);
+  if (e != hipSuccess) {
+    int rc = hip_fail(e, "fjcomm_init");
+    fjcomm_destroy(c);
+    return rc;
+  }
+  NcclId u;
+  memcpy(u.internal, id, FJCOMM_ID_BYTES);
+  if (int rc = rccl().comm_init_rank(&c->nc, nranks, u, rank)) {
+    rc = nccl_fail(rc, "ncclCommInitRank");
+    c->nc = nullptr;
+    fjcomm_destroy(c);
+    return rc;
+  }
+  *comm = c;
+  return FJAGG_OK;
+}
+
+int fjcomm_destroy(void* comm) {
+  Comm* c = reinterpret_cast<Comm*>(comm);
+  if (!c) return FJAGG_OK;
+  if (c->cs) (void)hipStreamSynchronize(c->cs);
+  if (c->nc && rccl().ok) rccl().comm_destroy(c->nc);
+  for (hipEvent_t& e : c->ready)
+    if (e) (void)hipEventDestroy(e);
+  if (c->done) (void)hipEventDestroy(c->done);
+  if (c->cs) (void)hipStreamDestroy(c->cs);
+  delete c;
+  return FJAGG_OK;
+}
+
+int fjcomm_sharded_wsum_dense(void* comm, int in_dtype, const void* x_dev, int64_t ld, int64_t K,
+                              int64_t P, const void* w_dev, float scale, float* out_dev,
+                              int nbuckets, int root, int flags, void* stream, void* const* fold_events) {
+  fjagg_g_err[0] = 0;
+  Comm* c = reinterpret_cast<Comm*>(comm);
+  if (!c || !c->nc) return fail(FJAGG_EINVAL, "not an initialised communicator");
+  if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16) return fail(FJAGG_EINVAL, "in_dtype must be F32 or BF16");
+  if (K < 0 || P < 0 || ld < P) return fail(FJAGG_EINVAL, "need K >= 0 and 0 <= P <= ld");
+  if (nbuckets < 1 || nbuckets > FJCOMM_MAX_BUCKETS)
+    return fail(FJAGG_EINVAL, "nbuckets must be in [1, %d]", FJCOMM_MAX_BUCKETS);
+  if (root >= c->nranks) return fail(FJAGG_EINVAL, "root %d >= nranks %d", root, c->nranks);
+  if (P == 0) return FJAGG_OK;
+  if (!out_dev || (K > 0 && (!x_dev || !w_dev))) return fail(FJAGG_EINVAL, "null pointer argument");
+  if (flags & ~(FJAGG_NONTEMPORAL | FJAGG_VARIANT(0xff)))
+    return fail(FJAGG_EINVAL, "flags may hold FJAGG_NONTEMPORAL and FJAGG_VARIANT bits only");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t esz = in_dtype == FJAGG_BF16 ? 2 : 4;
+  // buckets: multiples of 1024 elements, so every bucket keeps the rows' 16-byte alignment
+  int64_t step = (P + nbuckets - 1) / nbuckets;
+  step = (step + 1023) / 1024 * 1024;
+  const int nb = (int)((P + step - 1) / step);
+  for (int b = 0; b < nb; ++b) {
+    const int64_t p0 = b * step;
+    const int64_t n = P - p0 < step ? P - p0 : step;
+    float* seg = out_dev + p0;
+    if (fold_events) {
+      if (hipError_t e = hipEventRecord(reinterpret_cast<hipEvent_t>(fold_events[2 * b]), s))
+        return hip_fail(e, "hipEventRecord");
+    }
+    if (K > 0) {
+      const uint8_t* xb = reinterpret_cast<const uint8_t*>(x_dev) + p0 * esz;
+      if (int rc = fjagg_wsum_dense(in_dtype, FJAGG_F32, FJAGG_F32, xb, ld, K, n, w_dev, scale, seg,
+                                    flags | FJAGG_SCALE, FJAGG_MODE_EXACT, nullptr, 0, stream))
+        return rc;
+    } else if (hipError_t e = hipMemsetAsync(seg, 0, n * sizeof(float), s)) {
+      return hip_fail(e, "hipMemsetAsync");
+    }
+    if (fold_events) {
+      if (hipError_t e = hipEventRecord(reinterpret_cast<hipEvent_t>(fold_events[2 * b + 1]), s))
+        return hip_fail(e, "hipEventRecord");
+    }
+    // Buckets before the last reduce on the communicator's stream, overlapping the next
+    // fold. The last one is reduced on the caller's stream itself: a cross-queue hop costs
+    // ~30 us of GPU-side latency on MI355X (profiles/r01g_*), and nothing is left to overlap.
+    hipStream_t rs = s;
+    if (b + 1 < nb) {
+      if (hipError_t e = hipEventRecord(c->ready[b], s)) return hip_fail(e, "hipEventRecord");
+      if (hipError_t e = hipStreamWaitEvent(c->cs, c->ready[b], 0)) return hip_fail(e, "hipStreamWaitEvent");
+      rs = c->cs;
+    } else if (nb > 1) {  // collectives of one communicator stay in issue order
+      if (hipError_t e = hipEventRecord(c->done, c->cs)) return hip_fail(e, "hipEventRecord");
+      if (hipError_t e = hipStreamWaitEvent(s, c->done, 0)) return hip_fail(e, "hipStreamWaitEvent");
+    }
+    const int rc = root >= 0
+                       ? rccl().reduce(seg, seg, (size_t)n, kNcclFloat32, kNcclSum, root, c->nc, rs)
+                       : rccl().all_reduce(seg, seg, (size_t)n, kNcclFloat32, kNcclSum, c->nc, rs);
+    if (rc != kNcclSuccess) return nccl_fail(rc, root >= 0 ? "ncclReduce" : "ncclAllReduce");
+  }
+  return FJAGG_OK;
+}
+
+int fjagg_event_create(void** ev) {
+  fjagg_g_err[0] = 0;
+  if (!ev) return fail(FJAGG_EINVAL, "null argument");
+  hipEvent_t e = nullptr;
+  hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  if (rc != hipSuccess) {
+    (void)hipGetLastError();
+    rc = hipEventCreateWithFlags(&e, hipEventDefault);
+  }
+  if (rc != hipSuccess) return hip_fail(rc, "hipEventCreateWithFlags");
+  *ev = e;
+  return FJAGG_OK;
+}
+
+int fjagg_event_destroy(void* ev) {
+  if (ev) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev));
+  return FJAGG_OK;
+}
+
+int fjagg_event_record(void* ev, void* stream) {
+  fjagg_g_err[0] = 0;
+  if (hipError_t e = hipEventRecord(reinterpret_cast<hipEvent_t>(ev), reinterpret_cast<hipStream_t>(stream)))
+    return hip_fail(e, "hipEventRecord");
+  return FJAGG_OK;
+}
+
+int fjagg_event_elapsed_ms(float* ms, void* start, void* end) {
+  fjagg_g_err[0] = 0;
+  if (!ms) return fail(FJAGG_EINVAL, "null argument");
+  if (hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(end))) return hip_fail(e, "hipEventSynchronize");
+  if (hipError_t e = hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(start), reinterpret_cast<hipEvent_t>(end)))
+    return hip_fail(e, "hipEventElapsedTime");
+  return FJAGG_OK;
+}
+
+}  // extern "C"

@@ -12,6 +12,15 @@ summed by ``reduce`` (or ``all_reduce``) over xGMI — the only exchange step.
 The parameter axis is cut into buckets so the reduce of bucket b overlaps the
 fold of bucket b+1 (the collective runs on RCCL's own stream).
 
+Two exchange engines share that contract:
+
+* :class:`RcclCommunicator` + :func:`sharded_weighted_mean` with ``comm=`` — the
+  native pipeline of ``include/fjcomm.h``: ONE library call folds the buckets on the
+  caller's stream and reduces each on the communicator's high-priority stream, with
+  device-scope events between them (no per-bucket system-scope cache write-back, no
+  per-bucket Python);
+* ``torch.distributed`` collectives (``comm=None``) — any backend (gloo on CPU tests).
+
 Numerics: the result differs from the single-GPU exact fold only by the G-way
 combine and the per-rank scaling; tests/test_distributed.py and the GPU tests
 check it against the per-element bound in DESIGN.md §4.
@@ -19,13 +28,14 @@ check it against the per-element bound in DESIGN.md §4.
 
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
-from fedjax_amd import kernels, tree_util
+from fedjax_amd import _lib, kernels, tree_util
 
 # bucket edges are multiples of this many elements (keeps 16-byte alignment)
 BUCKET_ALIGN = 1024
@@ -62,10 +72,70 @@ def _default_partial(x: torch.Tensor, w: torch.Tensor, scale: float, out: torch.
                                nontemporal=nbytes >= tree_util.NONTEMPORAL_MIN_BYTES)
 
 
+class RcclCommunicator:
+    """An RCCL communicator over the ranks of ``group`` (one process per GPU), made by
+    ``fjcomm_init`` on the current device; rank 0's ``ncclUniqueId`` is broadcast over
+    ``group`` (a torch.distributed group of any backend). Collective: every rank of the
+    group constructs it. ``close()`` (or garbage collection) destroys it."""
+
+    def __init__(self, group=None, device: Optional[torch.device] = None):
+        lib = _lib.load()
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+            _lib.check(lib.fjcomm_unique_id(buf), "fjcomm_unique_id")
+            uid.copy_(torch.frombuffer(bytearray(buf), dtype=torch.uint8))
+        backend = dist.get_backend(group)
+        t = uid.to(dev) if backend == "nccl" else uid
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        ids = (ctypes.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(t.cpu().numpy().tobytes())
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            _lib.check(lib.fjcomm_init(ctypes.byref(handle), ids, self.world_size, self.rank), "fjcomm_init")
+        self.handle = handle
+        self.device = dev
+
+    def close(self) -> None:
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            _lib.load().fjcomm_destroy(self.handle)
+            self.handle = None
+
+    __del__ = close
+
+
+def _native_sharded(comm: RcclCommunicator, x_local: torch.Tensor, w_local: torch.Tensor, scale: float,
+                    out: torch.Tensor, root: int, buckets: int, nontemporal: Optional[bool],
+                    fold_events=None) -> None:
+    K, P = x_local.shape
+    if x_local.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError("the native sharded fold takes float32 or bfloat16 deltas")
+    if K and x_local.stride(1) != 1:
+        raise ValueError("client rows need unit column stride")
+    if out.dtype != torch.float32 or out.numel() != P or not out.is_contiguous():
+        raise ValueError("out must be a contiguous float32 [P] tensor")
+    if w_local.dtype != torch.float32 or w_local.numel() != K:
+        raise ValueError("w_local must be float32 [K_g]")
+    nbytes = K * P * x_local.element_size()
+    nt = (nbytes >= tree_util.NONTEMPORAL_MIN_BYTES) if nontemporal is None else nontemporal
+    ev = None
+    if fold_events is not None:
+        ev = (ctypes.c_void_p * len(fold_events))(*[e.handle for e in fold_events])
+    _lib.call("fjcomm_sharded_wsum_dense", comm.handle, kernels.dtype_code(x_local.dtype),
+              x_local.data_ptr() if K else None, x_local.stride(0) if K else P, K, P,
+              w_local.data_ptr() if K else None, float(np.float32(scale)), out.data_ptr(), int(buckets), int(root),
+              _lib.NONTEMPORAL if nt else 0, torch.cuda.current_stream(out.device).cuda_stream, ev)
+
+
 def sharded_weighted_mean(x_local: torch.Tensor, w_local: torch.Tensor, W_total, *, group=None,
                           dst: int = 0, all_ranks: bool = False, buckets: int = 4,
                           out: Optional[torch.Tensor] = None,
-                          partial_fn: Optional[Callable] = None) -> torch.Tensor:
+                          partial_fn: Optional[Callable] = None,
+                          comm: Optional[RcclCommunicator] = None,
+                          nontemporal: Optional[bool] = None,
+                          fold_events=None) -> torch.Tensor:
     """Weighted mean over all ranks' client rows.
 
     x_local: this rank's client deltas [K_g, P] (unit column stride, may be K_g = 0
@@ -74,11 +144,20 @@ def sharded_weighted_mean(x_local: torch.Tensor, w_local: torch.Tensor, W_total,
     Returns the float32 mean [P] — valid on ``dst`` (every rank with ``all_ranks``).
     partial_fn(x, w, scale, out) computes ``out = fl(sum_k x_k w_k) * scale`` for one
     bucket; the default is the HIP kernel (tests inject the oracle to run on gloo).
+    comm: an :class:`RcclCommunicator` selects the native pipeline (``fjcomm.h``);
+    fold_events then takes 2*buckets :class:`fedjax_amd.kernels.Event` that bracket
+    each bucket's fold on the current stream.
     """
     P = x_local.shape[1]
     scale = float(np.float32(tree_util._inverse(W_total)))
     if out is None:
         out = torch.empty(P, dtype=torch.float32, device=x_local.device)
+    if comm is not None:
+        if partial_fn is not None:
+            raise ValueError("partial_fn and comm are exclusive (the native pipeline folds in the library)")
+        root = -1 if all_ranks else (dist.get_group_rank(group, dst) if group is not None else dst)
+        _native_sharded(comm, x_local, w_local, scale, out, root, buckets, nontemporal, fold_events)
+        return out
     fn = partial_fn or _default_partial
     works = []
     for p0, p1 in bucket_edges(P, buckets):

@@ -1,0 +1,81 @@
+/*
+ * fjcomm.h — C ABI of the client-sharded aggregation over the GPUs of one node
+ * (part of libfjagg.so; conventions as in fjagg.h).
+ *
+ * The reference has no device-side reduction: ForEachClientPmapBackend spreads
+ * client training over jax.local_devices() and copies every client output back
+ * to devices[0] (fedjax/core/for_each_client.py:266-357, gather at :351-353),
+ * where tree_mean (fedjax/core/tree_util.py:76-96) folds all K clients. Here
+ * every GPU (one process per GPU) folds its own K/N clients and the N float32
+ * partials are summed by RCCL over xGMI. The step is issued by ONE call:
+ *
+ *     stream (compute)     fold b0 | fold b1 | ... | fold bL | wait(done) | reduce bL
+ *                               \ev0      \ev1
+ *     comm stream (RCCL)         reduce b0  reduce b1 ... done
+ *
+ * so the reduce of parameter bucket b overlaps the fold of bucket b+1, and the
+ * last bucket is reduced on the caller's stream (no cross-queue hop back at the
+ * end of the step; with one bucket the step is fold + reduce on one stream). The
+ * cross-stream events are created with a device-scope release (no system-scope
+ * cache write-back: the RCCL kernels run on the same device and read the
+ * partial through its L2).
+ *
+ * RCCL is the library torch already loaded (resolved with dlopen(RTLD_NOLOAD)
+ * of librccl.so.1, then a regular dlopen), so one RCCL runtime serves both
+ * torch.distributed and this communicator.
+ */
+#ifndef FJCOMM_H_
+#define FJCOMM_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FJCOMM_ABI_VERSION 1
+#define FJCOMM_ID_BYTES 128 /* sizeof(ncclUniqueId) */
+#define FJCOMM_MAX_BUCKETS 64
+
+int fjcomm_abi_version(void);
+
+/* ncclGetUniqueId: rank 0 creates the id, every rank passes it to fjcomm_init. */
+int fjcomm_unique_id(uint8_t* id /* FJCOMM_ID_BYTES */);
+
+/* ncclCommInitRank on the current HIP device (collective: every rank calls it), plus
+ * the communicator's stream (high priority) and its events. Allocates; call once. */
+int fjcomm_init(void** comm, const uint8_t* id, int nranks, int rank);
+int fjcomm_destroy(void* comm);
+
+/*
+ * One round of the sharded weighted mean on this rank:
+ *   out_dev[p] = fl(sum_{k<K} fl(x_k[p] * w_k)) * scale        (this rank's partial,
+ *                 bitwise fjagg_wsum_dense with FJAGG_SCALE on the bucket)
+ * then out_dev += the other ranks' partials (ncclReduce to `root`, or ncclAllReduce
+ * when root < 0), bucket by bucket as described above. x_dev is this rank's client-
+ * major slab [K x ld] of in_dtype (F32 or BF16); w_dev float[K]; the partial and the
+ * result are float32 [P]. `stream` waits for the last collective, so work queued on
+ * it afterwards sees the reduced result (valid on root, or everywhere with root < 0).
+ * fold_events: NULL, or 2*nbuckets events made by fjagg_event_create; the fold of
+ * bucket b is bracketed by fold_events[2b], fold_events[2b+1] on `stream`.
+ * K may be 0 (the rank contributes zeros). flags: FJAGG_NONTEMPORAL and the
+ * FJAGG_VARIANT bits of fjagg_wsum_dense.
+ * Replaces: the gather-to-devices[0] + tree_mean of for_each_client.py:351-353 and
+ * tree_util.py:85-96 for one round.
+ */
+int fjcomm_sharded_wsum_dense(void* comm, int in_dtype, const void* x_dev, int64_t ld, int64_t K,
+                              int64_t P, const void* w_dev, float scale, float* out_dev,
+                              int nbuckets, int root, int flags, void* stream, void* const* fold_events);
+
+/* Timing events without the system-scope fence (hipEventDisableSystemFence): recording
+ * one costs no cache write-back, so bracketing every launch does not perturb it. */
+int fjagg_event_create(void** ev);
+int fjagg_event_destroy(void* ev);
+int fjagg_event_record(void* ev, void* stream);
+int fjagg_event_elapsed_ms(float* ms, void* start, void* end); /* synchronises on `end` */
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FJCOMM_H_ */

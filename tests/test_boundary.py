@@ -13,14 +13,14 @@ import torch
 from fedjax_amd import _lib, kernels
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("fjagg.h", "fjcomp.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("fjagg.h", "fjcomp.h", "fjcomm.h")]
 
 
 def header_symbols():
     syms = set()
     for h in HEADERS:
         src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
-        syms |= set(re.findall(r"\b(fj(?:agg|comp)_\w+)\s*\(", src))
+        syms |= set(re.findall(r"\b(fj(?:agg|comp|comm)_\w+)\s*\(", src))
     return syms
 
 
@@ -31,7 +31,7 @@ def test_header_and_binding_agree():
 def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
-    exported = set(re.findall(r"\bT (fj(?:agg|comp)_\w+)", out))
+    exported = set(re.findall(r"\bT (fj(?:agg|comp|comm)_\w+)", out))
     assert header_symbols() <= exported, header_symbols() - exported
 
 
@@ -105,3 +105,13 @@ def test_fails_loudly_without_gpu():
         fedjax_amd.tree_util.tree_mean([({"w": np.ones(3, np.float32)}, 1)])
     with pytest.raises(_lib.FjaggError):
         fedjax_amd.aggregators.mean_aggregator().apply([("a", {"w": np.ones(3, np.float32)}, 2.)], None)
+
+
+def test_comm_host_side_validation_without_gpu():
+    lib = _lib.load()
+    assert lib.fjcomm_abi_version() == _lib.COMM_ABI_VERSION
+    rc = lib.fjcomm_sharded_wsum_dense(None, _lib.F32, 16, 4, 1, 4, 16, 1.0, 16, 1, 0, 0, None, None)
+    assert rc == -1  # FJAGG_EINVAL
+    assert b"communicator" in lib.fjagg_last_error()
+    assert lib.fjcomm_init(None, None, 1, 0) in (-1, -3)  # null handle / RCCL absent
+    assert lib.fjcomm_destroy(None) == 0

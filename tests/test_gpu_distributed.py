@@ -70,3 +70,62 @@ def test_sharded_mean_world2_on_gpu(cuda, coracle):
     for rank in (0, 1):
         for got in res[rank]:
             assert np.all(np.abs(got.astype(np.float64) - want) <= bound)
+
+
+def _native_worker(port, q):
+    """World-1 RCCL communicator: the native fold+reduce pipeline of include/fjcomm.h."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from fedjax_amd import distributed as fd, kernels
+        weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
+        W = 0.0
+        for w in weights:
+            W += w
+        comm = fd.RcclCommunicator(device=dev)
+        x = torch.empty(K, P + 3, dtype=torch.float32, device=dev)[:, :P]  # ld > P
+        kernels.fill_synth(x, seed=9)
+        wl = torch.tensor(np.float32(weights), device=dev)
+        res = {}
+        for buckets, all_ranks in ((1, False), (3, False), (7, True)):
+            evs = [kernels.Event() for _ in range(2 * buckets)]
+            y = fd.sharded_weighted_mean(x, wl, W, buckets=buckets, all_ranks=all_ranks, comm=comm,
+                                         fold_events=evs)
+            torch.cuda.synchronize()
+            ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(0, 2 * buckets, 2)]
+            res[(buckets, all_ranks)] = (y.cpu().numpy(), ms)
+        xb = torch.empty(K, P, dtype=torch.bfloat16, device=dev)
+        kernels.fill_synth(xb, seed=9)
+        yb = fd.sharded_weighted_mean(xb, wl, W, buckets=2, comm=comm)
+        y0 = fd.sharded_weighted_mean(x[:0], wl[:0], W, buckets=2, comm=comm,
+                                      out=torch.full((P,), 7.0, device=dev))
+        torch.cuda.synchronize()
+        q.put((res, yb.cpu().numpy(), y0.cpu().numpy()))
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_rccl_pipeline_world1(cuda, coracle):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_native_worker, args=(_port(), q))
+    p.start()
+    res, yb, y0 = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
+    x = coracle.synth_f32(K, P, seed=9)
+    r = ref.mean_scale(weights)
+    want = coracle.wsum_f32(x, np.float32(weights), scale=r)
+    for key, (y, ms) in res.items():
+        # one rank: the partial is the exact fold (per-element, so bucketing is invisible)
+        assert np.array_equal(y.view(np.uint32), want.astype(np.float32).view(np.uint32)), key
+        assert all(m > 0 for m in ms), key
+    assert np.all(y0 == 0)  # a rank without clients contributes zeros
+    xb = (coracle.synth_bf16(K, P, seed=9).astype(np.uint32) << 16).view(np.float32)  # bf16 -> f32 exactly
+    want_b = coracle.wsum_f32(np.ascontiguousarray(xb), np.float32(weights), scale=r)
+    assert np.array_equal(yb.view(np.uint32), want_b.astype(np.float32).view(np.uint32))
