@@ -197,7 +197,8 @@ def sharded_tree_mean(local_pytrees_and_weights, *, W_total=None, group=None, ds
     views = [flat[o:o + n].view(x.shape) for o, n, x in zip(offs[:-1], sizes, rows[0])]
     if any(x.dtype != torch.float32 for x in rows[0]):
         raise TypeError("sharded_tree_mean needs float32 leaves")
-    tree_util._fold(rows, weights, scale=tree_util._inverse(W_total), out=views, accumulate=False)
+    tree_util._fold(rows, weights, scale=tree_util._inverse(W_total), out=views, accumulate=False,
+                    validated=True)
     if all_ranks:
         dist.all_reduce(flat, group=group)
     else:

@@ -39,7 +39,7 @@ def register_leaf_type(cls: type) -> None:
 class TreeDef:
     """Hashable structure of a pytree (node kind, aux data, children)."""
 
-    __slots__ = ("kind", "aux", "children", "leafy", "_hash")
+    __slots__ = ("kind", "aux", "children", "leafy", "_hash", "_fast")
 
     def __init__(self, kind, aux, children):
         self.kind = kind
@@ -48,6 +48,7 @@ class TreeDef:
         # every child is a leaf: flatten_as can take the values without recursing
         self.leafy = bool(children) and all(c.kind == "leaf" for c in children)
         self._hash = None
+        self._fast = False  # compiled leaf accessor (None: not compilable), see _compile
 
     @property
     def num_leaves(self):
@@ -132,6 +133,16 @@ def flatten_as(treedef: TreeDef, tree) -> List[Any]:
 
     Walks ``treedef`` and checks ``tree`` against it node by node, without
     building a second TreeDef (this is the per-client hot loop of tree_mean)."""
+    fast = treedef._fast
+    if fast is False:  # first use of this TreeDef object: compiled once per structure
+        fast = _FAST.get(treedef, False)
+        if fast is False:
+            fast = _FAST[treedef] = _compile(treedef) if len(_FAST) < 4096 else None
+        treedef._fast = fast
+    if fast is not None:
+        leaves = fast(tree)
+        if leaves is not None:
+            return leaves
     out: List[Any] = []
     try:
         _collect(treedef, tree, out)
@@ -143,6 +154,57 @@ def flatten_as(treedef: TreeDef, tree) -> List[Any]:
 
 class _Mismatch(Exception):
     pass
+
+
+_FAST: Dict[TreeDef, Any] = {}  # structure -> compiled accessor (or None)
+
+
+def _compile(td: TreeDef):
+    """Straight-line accessor for trees of dict / list / tuple / None nodes with leaves of
+    registered leaf types: returns the leaf list, or None whenever anything differs from
+    ``td`` (then flatten_as takes the general walk, which also builds the error). Other
+    node kinds are not compiled (returns None)."""
+    lines, names = [], []
+    counter = [0]
+
+    def var():
+        counter[0] += 1
+        return f"v{counter[0]}"
+
+    def emit(t: TreeDef, ref: str) -> bool:
+        k = t.kind
+        if k == "leaf":
+            lines.append(f"if type({ref}) not in LT: return None")
+            names.append(ref)
+            return True
+        if k == "none":
+            lines.append(f"if {ref} is not None: return None")
+            return True
+        if k == "dict":
+            lines.append(f"if type({ref}) is not dict or len({ref}) != {len(t.aux)}: return None")
+            keys = list(t.aux)
+        elif k in ("list", "tuple"):
+            lines.append(f"if type({ref}) is not {k} or len({ref}) != {t.aux}: return None")
+            keys = list(range(t.aux))
+        else:
+            return False
+        for key, c in zip(keys, t.children):
+            v = var()
+            lines.append(f"{v} = {ref}[{key!r}]")
+            if not emit(c, v):
+                return False
+        return True
+
+    try:
+        if not emit(td, "x"):
+            return None
+        body = "\n    ".join(lines + [f"return [{', '.join(names)}]"])
+        src = f"def fast(x):\n  try:\n    {body}\n  except (KeyError, IndexError, TypeError):\n    return None\n"
+        ns = {"LT": _LEAF_TYPES}
+        exec(compile(src, f"<pytree accessor {len(names)} leaves>", "exec"), ns)  # noqa: S102 - generated
+        return ns["fast"]
+    except (SyntaxError, RecursionError, ValueError):
+        return None
 
 
 def _collect(td: TreeDef, x, out: List[Any]) -> None:

@@ -120,6 +120,8 @@ _WEAK_INT, _WEAK_FLOAT, _STRONG_INT, _STRONG_FLOAT = range(4)
 def _host_weight(w):
     """A weight as the host value the reference would compute with: Python numbers
     stay Python numbers (weakly typed); arrays/tensors become numpy scalars."""
+    if type(w) is int or type(w) is float:
+        return w
     if isinstance(w, torch.Tensor):
         if w.numel() != 1:
             raise ValueError("weights must be scalars")
@@ -133,6 +135,11 @@ def _host_weight(w):
 
 
 def _weight_kind(w) -> int:
+    t = type(w)
+    if t is int:
+        return _WEAK_INT
+    if t is float:
+        return _WEAK_FLOAT
     if isinstance(w, np.generic):
         if isinstance(w, np.bool_):
             return _STRONG_INT
@@ -165,10 +172,11 @@ def _leaf_rule(dt: torch.dtype, kinds: Sequence[int], scaled_kind: Optional[int]
 
 def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
           out: Optional[List[torch.Tensor]] = None, accumulate: bool = False,
-          nontemporal: Optional[bool] = None) -> List[torch.Tensor]:
+          nontemporal: Optional[bool] = None, validated: bool = False) -> List[torch.Tensor]:
     """y_l = [out_l +] sum_k fl(rows[k][l] * w_k) [* scale] for every leaf l, one
     kernel launch per (input, fold, output) dtype group. ``out`` gives the
-    destination tensors (fresh ones otherwise); ``accumulate`` folds into them."""
+    destination tensors (fresh ones otherwise); ``accumulate`` folds into them.
+    ``validated``: rows come from _client_rows (shapes and dtypes already checked)."""
     if accumulate and out is None:
         raise ValueError("accumulate needs out")
     K, L = len(rows), len(rows[0])
@@ -177,16 +185,12 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
     device = rows[0][0].device if L else None
     outs: List[Optional[torch.Tensor]] = [None] * L
     groups = {}
-    # x.size() is ~8x cheaper than x.shape; this loop runs once per (client, leaf)
-    sig0 = [(x.size(), x.dtype) for x in rows[0]]
-    for k in range(1, K):  # rows are on `device` already (_client_rows)
-        if [(x.size(), x.dtype) for x in rows[k]] != sig0:
-            for l, x in enumerate(rows[k]):
-                if x.size() != sig0[l][0]:
-                    raise ValueError(f"leaf {l}: client {k} has shape {tuple(x.shape)}, "
-                                     f"client 0 has {tuple(sig0[l][0])}")
-                if x.dtype != sig0[l][1]:
-                    raise TypeError(f"leaf {l}: client {k} has dtype {x.dtype}, client 0 has {sig0[l][1]}")
+    if not validated:
+        # x.size() is ~8x cheaper than x.shape; this loop runs once per (client, leaf)
+        sig0 = [(x.size(), x.dtype) for x in rows[0]]
+        for k in range(1, K):  # rows are on `device` already (_client_rows)
+            if [(x.size(), x.dtype) for x in rows[k]] != sig0:
+                _check_row(k, rows[k], sig0)
     for l in range(L):
         x0 = rows[0][l]
         in_c, acc_c, out_dt = _leaf_rule(x0.dtype, kinds, scaled_kind)
@@ -230,14 +234,35 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
     return outs
 
 
+def _check_row(k: int, row: List[torch.Tensor], sig0) -> None:
+    for l, x in enumerate(row):
+        if x.size() != sig0[l][0]:
+            raise ValueError(f"leaf {l}: client {k} has shape {tuple(x.shape)}, "
+                             f"client 0 has {tuple(sig0[l][0])}")
+        if x.dtype != sig0[l][1]:
+            raise TypeError(f"leaf {l}: client {k} has dtype {x.dtype}, client 0 has {sig0[l][1]}")
+
+
 def _client_rows(trees: Sequence[PyTree]) -> Tuple[pytree.TreeDef, List[List[torch.Tensor]]]:
+    """Flatten every client's pytree into canonical device leaves, checking that all
+    clients match client 0's structure, leaf shapes and dtypes (what _fold assumes)."""
     leaves0, td = pytree.flatten(trees[0])
     device = _find_device(leaves0)
     idx = _device_index(device)
-    dl = _device_leaf
-    rows = [[dl(x, device, idx) for x in leaves0]]
-    for t in trees[1:]:
-        rows.append([dl(x, device, idx) for x in pytree.flatten_as(td, t)])
+    dl, T, flat = _device_leaf, torch.Tensor, pytree.flatten_as
+    row0 = [dl(x, device, idx) for x in leaves0]
+    rows = [row0]
+    dt0 = [x.dtype for x in row0]
+    sz0 = [x.size() for x in row0]
+    for k in range(1, len(trees)):
+        r = flat(td, trees[k])
+        # the common case in one pass per (client, leaf): already a contiguous device tensor
+        # of client 0's dtype and shape (_device_leaf's fast path + _fold's signature check)
+        if not all([type(x) is T and x.dtype is d and x.get_device() == idx and x.is_contiguous() and x.size() == s
+                    for x, d, s in zip(r, dt0, sz0)]):
+            r = [dl(x, device, idx) for x in r]
+            _check_row(k, r, list(zip(sz0, dt0)))
+        rows.append(r)
     return td, rows
 
 
@@ -247,7 +272,7 @@ def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
     td, rows = _client_rows([pytree_])
     if not rows[0]:
         return pytree.unflatten(td, [])
-    return pytree.unflatten(td, _fold(rows, [_host_weight(weight)]))
+    return pytree.unflatten(td, _fold(rows, [_host_weight(weight)], validated=True))
 
 
 def tree_inverse_weight(pytree_: PyTree, weight: float) -> PyTree:
@@ -275,7 +300,7 @@ def tree_add(left: PyTree, right: PyTree) -> PyTree:
     td, rows = _client_rows([left, right])
     if not rows[0]:
         return pytree.unflatten(td, [])
-    return pytree.unflatten(td, _fold(rows, [1, 1]))
+    return pytree.unflatten(td, _fold(rows, [1, 1], validated=True))
 
 
 def tree_sum(pytrees: Iterable[PyTree]) -> PyTree:
@@ -286,7 +311,7 @@ def tree_sum(pytrees: Iterable[PyTree]) -> PyTree:
     td, rows = _client_rows(trees)
     if not rows[0]:
         return pytree.unflatten(td, [])
-    return pytree.unflatten(td, _fold(rows, [1] * len(trees)))
+    return pytree.unflatten(td, _fold(rows, [1] * len(trees), validated=True))
 
 
 def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
@@ -309,7 +334,7 @@ def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
     if not rows[0]:
         return pytree.unflatten(td, [])
     inv = _inverse(sum_weight)
-    return pytree.unflatten(td, _fold(rows, weights, scale=inv))
+    return pytree.unflatten(td, _fold(rows, weights, scale=inv, validated=True))
 
 
 def tree_size(pytree_: PyTree) -> int:
