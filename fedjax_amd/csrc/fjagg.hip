@@ -576,11 +576,12 @@ __global__ __launch_bounds__(kThreads) void k_dense_opt(
 // groups of kThreads*8 units (E=8, U=4: the dense default; lanes past the range
 // are masked) when the range gives a lane more than one unit, else in groups of
 // kThreads units (E=1, U=8).
-template <int IN, class ACC, int OUT, int V, bool NT>
+template <int IN, class ACC, int OUT, int V, bool NT, bool L2 = false>
 __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ img, int L,
                                                    int64_t K,
                                                    const typename ACC::T* __restrict__ w,
-                                                   float scale, int do_scale, int accumulate) {
+                                                   float scale, int do_scale, int accumulate,
+                                                   float* __restrict__ ws = nullptr) {
   constexpr int IB = Elem<IN>::B;
   const int tid = threadIdx.x;
   const int64_t* in_ptrs = img;
@@ -598,38 +599,60 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]); };
   const uint32_t row_bytes = (uint32_t)(n * IB);
   const bool dsc = do_scale != 0, acm = accumulate != 0;
+  // L2: per-client squared norms of this block's units, (kThreads/64) x K floats in LDS
+  extern __shared__ __attribute__((aligned(16))) float l2lds[];
+  using Norm = typename std::conditional<L2, LdsNorm, NoNorm>::type;
+  Norm nrm{};
+  if constexpr (L2) {
+    for (int64_t i = tid; i < (kThreads / 64) * K; i += kThreads) l2lds[i] = 0.f;
+    __syncthreads();
+    nrm = LdsNorm{l2lds + (tid >> 6) * K, 0.f};
+  }
   if (tail) {
-    if (tid < n - nunits * V) {
-      const int64_t e = nunits * V + tid;
+    const bool active = tid < n - nunits * V;
+    if (L2 || active) {  // with L2 every lane joins the per-client wave reductions
+      const int64_t e = nunits * V + (active ? tid : 0);
       const uint32_t off[1] = {(uint32_t)(e * IB)};
-      const bool valid[1] = {true};
-      fold<IN, ACC, OUT, 1, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm);
+      const bool valid[1] = {active};
+      fold<IN, ACC, OUT, 1, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm);
     }
-    return;
-  }
-  if constexpr (V > 1) {
-    if (u1 - u0 > (int64_t)kThreads) {  // more than one unit per lane: E=8 groups, masked
-      for (int64_t g = u0; g < u1; g += (int64_t)kThreads * 8) {
-        uint32_t off[8];
-        bool valid[8];
+  } else {
+    bool done = false;
+    if constexpr (V > 1) {
+      if (u1 - u0 > (int64_t)kThreads) {  // more than one unit per lane: E=8 groups, masked
+        for (int64_t g = u0; g < u1; g += (int64_t)kThreads * 8) {
+          uint32_t off[8];
+          bool valid[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          int64_t u = g + j * kThreads + tid;
-          valid[j] = u < u1;
-          if (!valid[j]) u = u1 - 1;
-          off[j] = (uint32_t)(u * (V * IB));
+          for (int j = 0; j < 8; ++j) {
+            int64_t u = g + j * kThreads + tid;
+            valid[j] = u < u1;
+            if (!valid[j]) u = u1 - 1;
+            off[j] = (uint32_t)(u * (V * IB));
+          }
+          fold<IN, ACC, OUT, V, 8, 4, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm);
         }
-        fold<IN, ACC, OUT, V, 8, 4, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm);
+        done = true;
       }
-      return;
+    }
+    if (!done) {
+      for (int64_t g = u0; g < u1; g += kThreads) {
+        int64_t u = g + tid;
+        const bool valid[1] = {u < u1};
+        if (!valid[0]) u = u1 - 1;
+        const uint32_t off[1] = {(uint32_t)(u * (V * IB))};
+        fold<IN, ACC, OUT, V, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm);
+      }
     }
   }
-  for (int64_t g = u0; g < u1; g += kThreads) {
-    int64_t u = g + tid;
-    const bool valid[1] = {u < u1};
-    if (!valid[0]) u = u1 - 1;
-    const uint32_t off[1] = {(uint32_t)(u * (V * IB))};
-    fold<IN, ACC, OUT, V, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm);
+  if constexpr (L2) {
+    __syncthreads();
+    for (int64_t k = tid; k < K; k += kThreads) {
+      float t = l2lds[k];
+#pragma unroll
+      for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, l2lds[i * K + k]);
+      ws[(int64_t)blockIdx.x * K + k] = t;
+    }
   }
 }
 
@@ -997,24 +1020,40 @@ int dense_exact_chunked(int in, int acc, int out, const uint8_t* x, int64_t ld_b
 
 template <int IN, class ACC, int OUT, int V>
 int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w,
-                  float scale, int do_scale, int accumulate, hipStream_t s) {
+                  float scale, int do_scale, int accumulate, float* ws, float* l2, hipStream_t s) {
   const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
+  if constexpr (std::is_same<ACC, AccF>::value) {
+    if (ws) {  // fused per-client squared l2 norms: block partials, then ordered combine
+      const size_t smem = (size_t)(kThreads / 64) * K * sizeof(float);
+      if (nt)
+        hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true>), dim3((unsigned)nblk), dim3(kThreads), smem, s,
+                           img, L, K, wt, scale, do_scale, accumulate, ws);
+      else
+        hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true>), dim3((unsigned)nblk), dim3(kThreads), smem,
+                           s, img, L, K, wt, scale, do_scale, accumulate, ws);
+      if (int rc = check_launch("k_ptrs (l2)")) return rc;
+      hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s,
+                         ws, nblk, K, l2);
+      return check_launch("k_l2_combine");
+    }
+  }
   if (nt)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
   else
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
   return check_launch("k_ptrs");
 }
 
 template <int IN, class ACC, int OUT>
 int launch_ptrs_io(bool vec, bool nt, const int64_t* img, int L, int64_t K, int64_t nblk,
-                   const void* w, float scale, int do_scale, int accumulate, hipStream_t s) {
+                   const void* w, float scale, int do_scale, int accumulate, float* ws, float* l2,
+                   hipStream_t s) {
   if (vec)
     return launch_ptrs_t<IN, ACC, OUT, vec_width<IN>()>(nt, img, L, K, nblk, w, scale, do_scale,
-                                                        accumulate, s);
-  return launch_ptrs_t<IN, ACC, OUT, 1>(nt, img, L, K, nblk, w, scale, do_scale, accumulate, s);
+                                                        accumulate, ws, l2, s);
+  return launch_ptrs_t<IN, ACC, OUT, 1>(nt, img, L, K, nblk, w, scale, do_scale, accumulate, ws, l2, s);
 }
 
 template <int IN, int OUT, int V, int E, int U, bool NT>
@@ -1187,6 +1226,28 @@ int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, i
   return nblk;
 }
 
+namespace {
+int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,
+                   int64_t K, int64_t nblk, const void* w_dev, float scale, int flags, float* ws,
+                   float* l2, void* stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool vec = !(flags & FJAGG_UNALIGNED);
+  const bool nt = (flags & FJAGG_NONTEMPORAL) != 0;
+  const int ds = (flags & FJAGG_SCALE) ? 1 : 0, ac = (flags & FJAGG_ACCUMULATE) ? 1 : 0;
+#define FJ_CASE(I, A, O, ACCT)                                                                 \
+  if (in_dtype == I && acc_dtype == A && out_dtype == O)                                       \
+    return launch_ptrs_io<I, ACCT, O>(vec, nt, image_dev, L, K, nblk, w_dev, scale, ds, ac, ws, l2, s);
+  FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_BF16, AccF)
+  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
+  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
+#undef FJ_CASE
+  return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination");
+}
+}  // namespace
+
 int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,
                     int64_t K, int64_t nblk, const void* w_dev, float scale, int flags,
                     void* stream) {
@@ -1196,21 +1257,32 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
   if (nblk == 0) return FJAGG_OK;
   if (nblk < 0 || nblk > 0x7fffffff || !image_dev || !w_dev || L < 1)
     return fail(FJAGG_EINVAL, "bad plan (nblk=%lld, L=%d)", (long long)nblk, L);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool vec = !(flags & FJAGG_UNALIGNED);
-  const bool nt = (flags & FJAGG_NONTEMPORAL) != 0;
-  const int ds = (flags & FJAGG_SCALE) ? 1 : 0, ac = (flags & FJAGG_ACCUMULATE) ? 1 : 0;
-#define FJ_CASE(I, A, O, ACCT)                                                                 \
-  if (in_dtype == I && acc_dtype == A && out_dtype == O)                                       \
-    return launch_ptrs_io<I, ACCT, O>(vec, nt, image_dev, L, K, nblk, w_dev, scale, ds, ac, s);
-  FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_F32, AccF)
-  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_BF16, AccF)
-  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_F32, AccF)
-  FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
-  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
-  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
-#undef FJ_CASE
-  return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination");
+  return wsum_ptrs_impl(in_dtype, acc_dtype, out_dtype, image_dev, L, K, nblk, w_dev, scale, flags,
+                        nullptr, nullptr, stream);
+}
+
+int64_t fjagg_wsum_l2_ptrs_workspace_bytes(int64_t K, int64_t nblk) {
+  return (K < 1 || nblk < 1) ? 0 : K * nblk * 4;
+}
+
+int fjagg_wsum_l2_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,
+                       int64_t K, int64_t nblk, const void* w_dev, float scale, float* l2sq_dev,
+                       int flags, void* ws_dev, int64_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  int rc = validate_common(in_dtype, acc_dtype, out_dtype, K, flags, scale);
+  if (rc) return rc;
+  if (acc_dtype != FJAGG_F32 || in_dtype == FJAGG_I32)
+    return fail(FJAGG_EUNSUPPORTED, "fused l2 norms need float inputs and a float fold");
+  if (K > kL2MaxClients)
+    return fail(FJAGG_EUNSUPPORTED, "fused l2 norms support K <= %lld", (long long)kL2MaxClients);
+  if (nblk < 1 || nblk > 0x7fffffff || !image_dev || !w_dev || L < 1)
+    return fail(FJAGG_EINVAL, "bad plan (nblk=%lld, L=%d)", (long long)nblk, L);
+  if (!l2sq_dev || !ws_dev) return fail(FJAGG_EINVAL, "null pointer argument");
+  if (ws_bytes < fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk))
+    return fail(FJAGG_EINVAL, "l2 workspace too small (need %lld bytes)",
+                (long long)fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk));
+  return wsum_ptrs_impl(in_dtype, acc_dtype, out_dtype, image_dev, L, K, nblk, w_dev, scale, flags,
+                        reinterpret_cast<float*>(ws_dev), l2sq_dev, stream);
 }
 
 int fjagg_server_update_dense(int in_dtype, const void* x_dev, int64_t ld, int64_t K, int64_t P,

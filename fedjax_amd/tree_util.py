@@ -36,7 +36,7 @@ from fedjax_amd.typing import PyTree
 __all__ = [
     "tree_weight", "tree_inverse_weight", "tree_zeros_like", "tree_add", "tree_sum",
     "tree_mean", "tree_size", "tree_l2_squared", "tree_l2_norm", "tree_clip_by_global_norm",
-    "tree_l2_norms",
+    "tree_l2_norms", "tree_mean_with_l2_norms",
 ]
 
 # Non-temporal loads pay off once the deltas cannot stay in the 256 MiB Infinity
@@ -172,11 +172,14 @@ def _leaf_rule(dt: torch.dtype, kinds: Sequence[int], scaled_kind: Optional[int]
 
 def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
           out: Optional[List[torch.Tensor]] = None, accumulate: bool = False,
-          nontemporal: Optional[bool] = None, validated: bool = False) -> List[torch.Tensor]:
+          nontemporal: Optional[bool] = None, validated: bool = False,
+          l2sq: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
     """y_l = [out_l +] sum_k fl(rows[k][l] * w_k) [* scale] for every leaf l, one
     kernel launch per (input, fold, output) dtype group. ``out`` gives the
     destination tensors (fresh ones otherwise); ``accumulate`` folds into them.
-    ``validated``: rows come from _client_rows (shapes and dtypes already checked)."""
+    ``validated``: rows come from _client_rows (shapes and dtypes already checked).
+    ``l2sq`` (float32 [K]): also write every client's squared l2 norm over all leaves,
+    from the same pass (fjagg_wsum_l2_ptrs; float leaves of one dtype)."""
     if accumulate and out is None:
         raise ValueError("accumulate needs out")
     K, L = len(rows), len(rows[0])
@@ -204,9 +207,16 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
         outs[l] = o
         groups.setdefault((in_c, acc_c, kernels.dtype_code(out_dt)), []).append(l)
 
+    if l2sq is not None:
+        if len(groups) != 1 or next(iter(groups))[1] != _lib.F32 or next(iter(groups))[0] == _lib.I32:
+            raise TypeError("fused l2 norms need float leaves of one dtype and a float fold")
+        if l2sq.dtype != torch.float32 or l2sq.numel() != K or l2sq.device != device:
+            raise ValueError(f"l2sq must be a float32 [{K}] tensor on {device}")
     for (in_c, acc_c, out_c), ls in groups.items():
         leaf_n = np.array([rows[0][l].numel() for l in ls], dtype=np.int64)
         if not leaf_n.any():
+            if l2sq is not None:
+                l2sq.zero_()
             continue
         if len(ls) == L:
             in_ptrs = np.array([[x.data_ptr() for x in row] for row in rows], dtype=np.int64)
@@ -228,9 +238,17 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
         nt = (total_bytes >= NONTEMPORAL_MIN_BYTES) if nontemporal is None else nontemporal
         flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
         flags |= (_lib.UNALIGNED if unaligned else 0) | (_lib.NONTEMPORAL if nt else 0)
-        _lib.call("fjagg_wsum_ptrs", in_c, acc_c, out_c, image_dev.data_ptr(), len(ls), K,
-                  len(blocks) // 2, w_dev_ptr, float(np.float32(scale) if scale is not None else 1.0),
-                  flags, torch.cuda.current_stream(device).cuda_stream)
+        nblk = len(blocks) // 2
+        sc = float(np.float32(scale) if scale is not None else 1.0)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        if l2sq is None:
+            _lib.call("fjagg_wsum_ptrs", in_c, acc_c, out_c, image_dev.data_ptr(), len(ls), K, nblk,
+                      w_dev_ptr, sc, flags, stream)
+        else:
+            need = int(_lib.load().fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk))
+            ws = torch.empty(max(need, 4), dtype=torch.uint8, device=device)
+            _lib.call("fjagg_wsum_l2_ptrs", in_c, acc_c, out_c, image_dev.data_ptr(), len(ls), K, nblk,
+                      w_dev_ptr, sc, l2sq.data_ptr(), flags, ws.data_ptr(), ws.numel(), stream)
     return outs
 
 
@@ -335,6 +353,31 @@ def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
         return pytree.unflatten(td, [])
     inv = _inverse(sum_weight)
     return pytree.unflatten(td, _fold(rows, weights, scale=inv, validated=True))
+
+
+def tree_mean_with_l2_norms(pytrees_and_weights: Iterable[Tuple[PyTree, float]]):
+    """``(tree_mean(pairs), [tree_l2_norm(tree) for tree, _ in pairs])`` from ONE pass over
+    the client deltas (fjagg_wsum_l2_ptrs): the mean of examples/fed_avg.py:82 and the
+    per-client ``delta_l2_norm`` diagnostic of :79-81 (tree_util.py:105-114).
+
+    The mean is bitwise :func:`tree_mean`'s. The norms (float32 [K] on the device) sum
+    squares in f32 in a fixed order; float leaves of one dtype.
+    Returns ``(None, None)`` for no clients."""
+    trees, weights = [], []
+    sum_weight = 0.0
+    for tree, weight in pytrees_and_weights:
+        w = _host_weight(weight)
+        trees.append(tree)
+        weights.append(w)
+        sum_weight += w  # tree_util.py:95
+    if not trees:
+        return None, None
+    td, rows = _client_rows(trees)
+    if not rows[0]:
+        return pytree.unflatten(td, []), torch.zeros(len(trees), dtype=torch.float32, device=_default_device())
+    l2sq = torch.empty(len(trees), dtype=torch.float32, device=rows[0][0].device)
+    outs = _fold(rows, weights, scale=_inverse(sum_weight), validated=True, l2sq=l2sq)
+    return pytree.unflatten(td, outs), torch.sqrt(l2sq)
 
 
 def tree_size(pytree_: PyTree) -> int:

@@ -127,6 +127,21 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
                     int flags, void* stream);
 
 /*
+ * fjagg_wsum_ptrs fused with every client's squared L2 norm over ALL L leaves, in the
+ * same pass (same plan image and nblk as fjagg_wsum_ptrs; the outputs are bitwise
+ * the fjagg_wsum_ptrs ones). l2sq_dev[k] = sum over leaves and elements of x^2 in f32,
+ * fixed order: lane partial -> wave xor-butterfly -> LDS per wave -> workgroup
+ * partials ws[b*K + k] added in workgroup order. Float inputs, float fold, K <= 4096;
+ * ws_dev of fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk) bytes.
+ * Replaces the per-client tree_l2_norm(delta) of examples/fed_avg.py:79-81
+ * (tree_util.py:105-114) next to the tree_mean of the same deltas (:82).
+ */
+int64_t fjagg_wsum_l2_ptrs_workspace_bytes(int64_t K, int64_t nblk);
+int fjagg_wsum_l2_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev,
+                       int L, int64_t K, int64_t nblk, const void* w_dev, float scale,
+                       float* l2sq_dev, int flags, void* ws_dev, int64_t ws_bytes, void* stream);
+
+/*
  * fjagg_wsum_dense (exact mode) fused with the per-client squared L2 norms of the
  * same deltas, in ONE pass over the K x P slab: out as fjagg_wsum_dense (bitwise
  * the same), l2sq_dev[k] = sum_p x_k[p]^2 in f32 with a fixed reduction order

@@ -530,3 +530,55 @@ def test_emnist_fed_avg_rounds_example(cuda):
     spec.loader.exec_module(mod)
     hist = mod.run(rounds=3, verbose=False)
     assert all(h["same_mean"] and h["same_params"] and h["norm_rel_diff"] < 2e-6 for h in hist), hist
+
+
+# ------------------------------------------------- fused l2 norms on the pytree path
+EMNIST_SHAPES = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "conv2_d_1": {"b": (64,), "w": (3, 3, 32, 64)},
+                 "linear": {"b": (128,), "w": (9216, 128)}, "linear_1": {"b": (62,), "w": (128, 62)}}
+
+
+def _separate_clients(K, shapes, seed, dtype, device, offset=0):
+    """K pytrees of separately allocated leaves (offset > 0: leaves start off 16-byte alignment)."""
+    flat_shapes = [s for _, d in sorted(shapes.items()) for _, s in sorted(d.items())]
+    P = sum(int(np.prod(s)) for s in flat_shapes)
+    base = torch.empty(K, P + offset, dtype=dtype, device=device)
+    kernels.fill_synth(base, seed=seed)
+    clients = []
+    for k in range(K):
+        o, leaves = offset, []
+        for s in flat_shapes:
+            n = int(np.prod(s))
+            leaves.append(base[k, o:o + n].clone().view(s) if offset == 0 else base[k, o:o + n].view(s))
+            o += n
+        it = iter(leaves)
+        clients.append({m: {n: next(it) for n in sorted(d)} for m, d in sorted(shapes.items())})
+    return clients
+
+
+@pytest.mark.parametrize("K,dt,offset", [(10, torch.float32, 0), (128, torch.float32, 0), (33, torch.float32, 1),
+                                         (16, torch.bfloat16, 0), (1, torch.float32, 0)])
+def test_tree_mean_with_l2_norms(K, dt, offset, cuda):
+    clients = _separate_clients(K, EMNIST_SHAPES, 71, dt, cuda, offset)
+    wi = [int(v) for v in ref.fedavg_weights(K, seed=72)]
+    pairs = list(zip(clients, wi))
+    m0 = tu.tree_mean(pairs)
+    m1, norms = tu.tree_mean_with_l2_norms(iter(pairs))  # generators are consumed once
+    for a, b in zip(fedjax_amd.pytree.leaves_of(m0), fedjax_amd.pytree.leaves_of(m1)):
+        assert torch.equal(a, b)  # the fold is bitwise tree_mean's
+    want = np.array([sum(float((x.double() ** 2).sum()) for x in fedjax_amd.pytree.leaves_of(c)) for c in clients])
+    npt.assert_allclose(host(norms), np.sqrt(want), rtol=2e-6)
+    _, norms2 = tu.tree_mean_with_l2_norms(pairs)
+    assert torch.equal(norms, norms2)  # deterministic
+    npt.assert_allclose(host(norms), host(tu.tree_l2_norms(clients)), rtol=2e-6)
+
+
+def test_tree_mean_with_l2_norms_edges(cuda):
+    assert tu.tree_mean_with_l2_norms([]) == (None, None)
+    a = torch.arange(5, dtype=torch.float32, device=cuda)
+    m, n = tu.tree_mean_with_l2_norms([({"x": a}, 1), ({"x": 2 * a}, 3)])
+    npt.assert_allclose(host(n), [np.sqrt(30.0), np.sqrt(120.0)], rtol=1e-6)
+    npt.assert_array_equal(host(m["x"]), host(tu.tree_mean([({"x": a}, 1), ({"x": 2 * a}, 3)])["x"]))
+    with pytest.raises(TypeError):
+        tu.tree_mean_with_l2_norms([({"x": torch.ones(3, dtype=torch.int32, device=cuda)}, 1)])
+    with pytest.raises(TypeError):
+        tu.tree_mean_with_l2_norms([({"x": a, "y": a.bfloat16()}, 1)])

@@ -60,8 +60,18 @@ def main(K=128, reps=20):
             e.record()
             e.synchronize()
             dense[f"v{v}_nt{int(nt)}"] = round(K * P * 4 / (s.elapsed_time(e) / reps / 1e3) / 1e9, 1)
+    # fused per-client l2 norms on the same pytree path (fjagg_wsum_l2_ptrs)
+    for _ in range(3):
+        tu.tree_mean_with_l2_norms(pairs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tu.tree_mean_with_l2_norms(pairs)
+    torch.cuda.synchronize()
+    wall_l2 = (time.perf_counter() - t0) / reps
     nbytes = K * P * 4
     print(json.dumps({"workload": "configs[1] 128 x EMNIST-CNN (1,206,590 params, 8 leaves)",
+                      "tree_mean_with_l2_norms_wall_ms": round(wall_l2 * 1e3, 4),
                       "tree_mean_wall_ms": round(wall * 1e3, 4),
                       "tree_mean_wall_GBs": round(nbytes / wall / 1e9, 1),
                       "tree_mean_gpu_ms_median": round(float(np.median(ks)), 4),
