@@ -113,12 +113,22 @@ __device__ inline float div_rn(float a, float b) { return (float)((double)a / (d
 __device__ inline double nan_min(double a, double b) { return (a != a) ? a : ((b != b) ? b : (b < a ? b : a)); }
 __device__ inline double nan_max(double a, double b) { return (a != a) ? a : ((b != b) ? b : (b > a ? b : a)); }
 
-// segment of block b in a running-sum table prefix[nseg + 1] (skips empty segments)
+// Segment of block b in a running-sum table prefix[nseg + 1] (skips empty segments).
+// Wave-parallel 64-ary search: each round lane i tests pivot lo + i*step with ONE vector
+// load and a ballot, so up to 4096 segments cost two dependent loads instead of log2(nseg)
+// scalar ones (that latency was a large share of the short-lived blocks of k_row_stats,
+// k_wht and k_rademacher). Every lane of the wave must call it with the same b (kernel
+// entry, before any divergence); the result is wave-uniform.
 __device__ inline int64_t find_segment(const int64_t* __restrict__ prefix, int64_t nseg, int64_t b) {
+  const int64_t lane = threadIdx.x & 63;
   int64_t lo = 0, hi = nseg;  // prefix[lo] <= b < prefix[hi]
   while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (prefix[mid] <= b) lo = mid; else hi = mid;
+    const int64_t step = (hi - lo + 63) >> 6;
+    const int64_t idx = lo + lane * step;
+    // lane 0 always passes; prefix[] is nondecreasing, so the passing lanes are a prefix
+    const uint64_t m = __ballot(idx < hi && prefix[idx] <= b);
+    lo += (int64_t)(63 - __builtin_clzll(m)) * step;
+    hi = lo + step < hi ? lo + step : hi;
   }
   return lo;
 }
@@ -210,12 +220,11 @@ struct LaneStats {
     nan |= x != x;
     mn = fminf(mn, x);
     mx = fmaxf(mx, x);
-    const float a = fabsf(x);
-    amx = fmaxf(amx, a);
+    amx = fmaxf(amx, fabsf(x));
     const double v = (double)x;
     s1 += v;
     s2 = __fma_rn(v, v, s2);
-    sa += (double)a;
+    sa += fabs(v);  // |double(x)| == double(|x|): the abs is a free source modifier
   }
   __device__ inline Partial partial() const {
     const double qn = __longlong_as_double(0x7ff8000000000000ll);
@@ -224,7 +233,7 @@ struct LaneStats {
 };
 
 // One workgroup per 16 Ki-element chunk of a row: a scalar head up to the first 16-byte
-// boundary, float4 loads four deep per lane, a scalar tail; then the fixed-order wave
+// boundary, float4 loads eight deep per lane, a scalar tail; then the fixed-order wave
 // butterfly and a per-workgroup combine in wave order (deterministic).
 __global__ __launch_bounds__(kStatsThreads) void k_row_stats(const fjcomp_row* __restrict__ rows,
                                                               const int64_t* __restrict__ prefix, int64_t R,
@@ -243,12 +252,12 @@ __global__ __launch_bounds__(kStatsThreads) void k_row_stats(const fjcomp_row* _
   if ((int)threadIdx.x < head) st.add(x[threadIdx.x]);
   const float4* __restrict__ xv = reinterpret_cast<const float4*>(x + head);
   int i = threadIdx.x;
-  for (; i + 3 * kStatsThreads < nv; i += 4 * kStatsThreads) {
-    float4 v[4];
+  for (; i + 7 * kStatsThreads < nv; i += 8 * kStatsThreads) {
+    float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = xv[i + u * kStatsThreads];
+    for (int u = 0; u < 8; ++u) v[u] = xv[i + u * kStatsThreads];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       st.add(v[u].x);
       st.add(v[u].y);
       st.add(v[u].z);
