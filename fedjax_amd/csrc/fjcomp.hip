@@ -523,18 +523,52 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
     rcp_b = 1.0 / (double)(float)jb.stats->sumabs;
   }
   const float* __restrict__ src = first ? jb.src : jb.mid;
-  for (int e = threadIdx.x; e < t.tile; e += kWhtThreads) {
-    const int64_t g = base + ((int64_t)(e >> t.lc) << t.lo) + (e & (t.c - 1));
-    float v;
-    if (first && kind == FJCOMP_WHT_ROTATE) {
-      v = g < jb.n_in ? src[g] : 0.0f;
-      v = v * sign_of(jb.signs, g);
-    } else if (first && kind == FJCOMP_WHT_UNROTATE_DRIVE) {
-      v = div_by(A * xla_sign(src[g]), rcp_b);  // drive_pytree: (sum(y^2) * sign(y)) / sum(|y|)
-    } else {
-      v = src[g];
+  // Tile element e sits at g(e); runs of consecutive g are the whole tile in pass 0 (c = 1)
+  // and c >= 32 floats later. When runs are multiples of 4, lanes move 16-byte quads (e and
+  // g both multiples of 4, same sign word, lds_pad(e + u) = lds_pad(e) + u); the element
+  // arithmetic is the scalar path's, so results are bitwise the same.
+  const bool quads = ((t.lo == 0 ? t.tile : t.c) & 3) == 0;
+  if (quads && ((uintptr_t)src & 15) == 0) {
+    for (int e = 4 * threadIdx.x; e < t.tile; e += 4 * kWhtThreads) {
+      const int64_t g = base + ((int64_t)(e >> t.lc) << t.lo) + (e & (t.c - 1));
+      float v[4];
+      if (first && kind == FJCOMP_WHT_ROTATE) {
+        if (g + 3 < jb.n_in) {
+          const float4 q = *reinterpret_cast<const float4*>(src + g);
+          v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = g + u < jb.n_in ? src[g + u] : 0.0f;
+        }
+        const uint32_t sw = jb.signs[g >> 5] >> (g & 31);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = v[u] * (((sw >> u) & 1u) ? -1.0f : 1.0f);
+      } else {
+        const float4 q = *reinterpret_cast<const float4*>(src + g);
+        v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+        if (first && kind == FJCOMP_WHT_UNROTATE_DRIVE) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = div_by(A * xla_sign(v[u]), rcp_b);
+        }
+      }
+      const int o = lds_pad(e);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sm[o + u] = v[u];
     }
-    sm[lds_pad(e)] = v;
+  } else {
+    for (int e = threadIdx.x; e < t.tile; e += kWhtThreads) {
+      const int64_t g = base + ((int64_t)(e >> t.lc) << t.lo) + (e & (t.c - 1));
+      float v;
+      if (first && kind == FJCOMP_WHT_ROTATE) {
+        v = g < jb.n_in ? src[g] : 0.0f;
+        v = v * sign_of(jb.signs, g);
+      } else if (first && kind == FJCOMP_WHT_UNROTATE_DRIVE) {
+        v = div_by(A * xla_sign(src[g]), rcp_b);  // drive_pytree: (sum(y^2) * sign(y)) / sum(|y|)
+      } else {
+        v = src[g];
+      }
+      sm[lds_pad(e)] = v;
+    }
   }
   __syncthreads();
   for (int s0 = 0; s0 < t.nb; s0 += 4) {
@@ -546,6 +580,35 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
       default: wht_group<4>(sm, t.tile, p); break;
     }
     __syncthreads();
+  }
+  float* __restrict__ dptr = last ? jb.dst : jb.mid;
+  if (quads && ((uintptr_t)dptr & 15) == 0) {
+    for (int e = 4 * threadIdx.x; e < t.tile; e += 4 * kWhtThreads) {
+      const int64_t g = base + ((int64_t)(e >> t.lc) << t.lo) + (e & (t.c - 1));
+      const int o = lds_pad(e);
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = sm[o + u];
+      if (last) {
+        if (g >= jb.n_out) continue;
+        if (kind == FJCOMP_WHT_ROTATE) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = div_by(v[u], rcp_sqrt_d);
+        } else if (kind != FJCOMP_WHT_PLAIN) {
+          const uint32_t sw = jb.signs[g >> 5] >> (g & 31);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = div_by(v[u] * (((sw >> u) & 1u) ? -1.0f : 1.0f), rcp_sqrt_d);
+        }
+        if (g + 3 >= jb.n_out) {  // truncated to the leaf's n_out elements
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (g + u < jb.n_out) dptr[g + u] = v[u];
+          continue;
+        }
+      }
+      *reinterpret_cast<float4*>(dptr + g) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    return;
   }
   for (int e = threadIdx.x; e < t.tile; e += kWhtThreads) {
     const int64_t g = base + ((int64_t)(e >> t.lc) << t.lo) + (e & (t.c - 1));

@@ -138,6 +138,21 @@ def test_structured_rotation_bitwise(shape, cuda):
     npt.assert_allclose(host(z), x, rtol=1e-4, atol=1e-4)  # walsh_hadamard_test.py:46-55
 
 
+@pytest.mark.parametrize("n,offset", [(100, 1), (18433, 1), (9216 * 128, 2), (9216 * 128 + 3, 0), (64, 3)])
+def test_structured_rotation_unaligned_and_ragged(n, offset, cuda):
+    """16-byte quads vs the scalar path: a source view off 16-byte alignment, lengths that
+    end inside a quad (zero padding) and outputs truncated inside a quad."""
+    x = np.random.RandomState(n).standard_normal(n + offset).astype(F32)
+    key = jr.prng_key(n)
+    t = dev(x, cuda)[offset:]
+    y, s = wh.structured_rotation(t, key)
+    ey, es = cref.structured_rotation(x[offset:], key)
+    same(host(y), ey)
+    z = wh.inverse_structured_rotation(y, key, s)
+    same(host(z), cref.inverse_structured_rotation(ey, key, es))
+    same(host(wh.walsh_hadamard_transform(y)), cref.fwht(ey))
+
+
 def test_structured_rotation_pytree(cuda):  # walsh_hadamard_test.py:57-66
     params = {"a": np.array([[1.0, 0.0, 0.0], [1.0, 2.0, 3.0]], F32), "b": np.array([[1.0, 0.0], [1.0, 2.0]], F32)}
     key = random.PRNGKey(10)
