@@ -95,17 +95,12 @@ __host__ __device__ inline void threefry(uint32_t k0, uint32_t k1, uint32_t& x0,
 __device__ inline float bits_to_unit(uint32_t b) { return __uint_as_float((b >> 9) | 0x3f800000u) - 1.0f; }
 
 // ------------------------------------------------------------------ f32 helpers
-__device__ inline float nan_to_num(float x) {
-  if (x != x) return 0.0f;
-  if (x == INFINITY) return FLT_MAX;
-  if (x == -INFINITY) return -FLT_MAX;
-  return x;
-}
-// numpy's maximum(0, a) / minimum(a, 1) for non-NaN a (first argument wins ties)
-__device__ inline float clamp01(float a) {
-  a = (a <= 1.0f) ? a : 1.0f;
-  return (0.0f >= a) ? 0.0f : a;
-}
+// Branch-free (the branchy forms compiled to exec-mask regions inside the per-element loop).
+// jnp.nan_to_num: NaN -> 0, +-inf -> +-FLT_MAX; med3 of a non-NaN x is exact (keeps -0).
+__device__ inline float nan_to_num(float x) { return x != x ? 0.0f : __builtin_amdgcn_fmed3f(x, -FLT_MAX, FLT_MAX); }
+// numpy's maximum(0, minimum(nan_to_num(a), 1)) (first argument wins ties, so -0 -> +0):
+// NaN and everything <= 0 give +0, +inf gives 1.
+__device__ inline float clamp01_nan(float a) { return a > 0.0f ? fminf(a, 1.0f) : 0.0f; }
 __device__ inline float xla_sign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x); }
 // correctly rounded a / b given r = RN_f64(1 / b) (see the header comment)
 __device__ inline float div_by(float a, double r) { return (float)((double)a * r); }
@@ -334,10 +329,10 @@ constexpr int kHistLdsBins = 4096;
 struct UniformQ {
   float lm1;
   double rcp_lm1;
+  static constexpr bool kTable = false;
   // uniform_stochastic_quantize (compression.py:84-97); *level = chosen level index
   __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float* level) const {
-    float a = nan_to_num(div_by(v - p.vmin, p.rcp_range));
-    a = clamp01(a);
+    const float a = clamp01_nan(div_by(v - p.vmin, p.rcp_range));
     const float fl = floorf(a * lm1), ce = ceilf(a * lm1);
     const float v_ceil = div_by(ce, rcp_lm1);
     const float v_floor = div_by(fl, rcp_lm1);
@@ -349,20 +344,65 @@ struct UniformQ {
   }
 };
 
+// UniformQ with the per-level constants in LDS (num_levels <= kLevelTable): level j's value
+// lev[j] = RN_f32(j / lm1) (the v_floor / v_ceil above) and rd[j] = RN_f64(1 / (lev[j+1] -
+// lev[j])), so the threshold is RN_f32(num * rd[fl]) instead of an f32 division. That is
+// the correctly rounded num / den whenever it is a normal float (the argument of the file
+// header), and every other case gives the same decision u > thr: num is 0 or at least
+// 2^-55 in magnitude unless fl = 0, where num = a >= 0 and any threshold below 2^-23
+// compares like 0 against u (u is 0 or >= 2^-23). When ce == fl both branches pick the
+// same level, so thr (and the unused rd[lm1] = 0) does not matter; no nan_to_num needed.
+constexpr int kLevelTable = 4096;
+struct UniformTQ {
+  float lm1;
+  int num_levels;
+  double rcp_lm1;
+  const float* lev;   // LDS, lm1 + 1 entries (lm1 + 2 with a trailing copy)
+  const double* rd;   // LDS, lm1 + 1 entries
+  static constexpr bool kTable = true;
+  static size_t lds_bytes(int num_levels) { return (size_t)(num_levels + 1) * (sizeof(double) + sizeof(float)) + 16; }
+  __device__ inline void build(void* smem) {
+    double* r = reinterpret_cast<double*>(smem);
+    float* lv = reinterpret_cast<float*>(r + num_levels + 1);
+    const int top = num_levels - 1;  // == lm1
+    for (int j = threadIdx.x; j <= top + 1; j += blockDim.x) lv[j] = div_by((float)(j <= top ? j : top), rcp_lm1);
+    __syncthreads();
+    for (int j = threadIdx.x; j <= top; j += blockDim.x) r[j] = j < top ? 1.0 / (double)(lv[j + 1] - lv[j]) : 0.0;
+    __syncthreads();
+    lev = lv;
+    rd = r;
+  }
+  __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float* level) const {
+    const float a = clamp01_nan(div_by(v - p.vmin, p.rcp_range));
+    const float s = a * lm1;
+    const float fl = floorf(s), ce = ceilf(s);
+    const int j = (int)fl;
+    const float v_floor = lev[j], v_next = lev[j + 1];  // lev has a trailing entry
+    const float v_ceil = ce != fl ? v_next : v_floor;
+    const float thr = (float)((double)(a - v_floor) * rd[j]);
+    const bool down = u > thr;
+    *level = down ? fl : ce;
+    const float q = down ? v_floor : v_ceil;
+    return p.vmin + q * p.range;
+  }
+};
+
 struct BinaryQ {
+  static constexpr bool kTable = false;
   // binary_stochastic_quantize (compression.py:58-63)
   __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float*) const {
-    const float a = clamp01(nan_to_num(div_by(v - p.vmin, p.rcp_range)));
+    const float a = clamp01_nan(div_by(v - p.vmin, p.rcp_range));
     return (u > a) ? p.vmin : p.vmax;
   }
 };
 
 struct TernQ {
+  static constexpr bool kTable = false;
   // terngrad_quantize (compression.py:323-336) with binary_stochastic_quantize(|v|, 0, vmax)
   __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float*) const {
     const float vc = (fabsf(v) > p.thr) ? p.thr * xla_sign(v) : v;
     const float av = fabsf(vc);
-    const float a = clamp01(nan_to_num(div_by(av - 0.0f, p.rcp_range)));
+    const float a = clamp01_nan(div_by(av - 0.0f, p.rcp_range));
     const float r = (u > a) ? 0.0f : p.vmax;
     return r * xla_sign(vc);
   }
@@ -379,6 +419,10 @@ __global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* 
                                                            int32_t* __restrict__ hist, int nbins) {
   const int64_t b = blockIdx.x;
   const int64_t l = find_segment(prefix, L, b);
+  if constexpr (Q::kTable) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char qtab[];
+    quant.build(qtab);
+  }
   const int64_t n = leaf_n[l], h = (n + 1) >> 1;
   const int64_t i = (b - prefix[l]) * kQThreads + threadIdx.x;
   const bool valid = i < h, second = i + h < n;
@@ -749,6 +793,21 @@ int fjcomp_quant_fold(int method, const float* const* in_ptrs, const uint32_t* k
   hipStream_t s = as_stream(stream);
   if (method == FJCOMP_UNIFORM) {
     if (num_levels < 1) return fail(FJAGG_EINVAL, "quant_fold: num_levels=%d", num_levels);
+    if (num_levels <= kLevelTable) {  // level constants in LDS, no per-element division
+      UniformTQ q{};
+      q.lm1 = (float)(num_levels - 1);
+      q.num_levels = num_levels;
+      q.rcp_lm1 = 1.0 / (double)q.lm1;
+      const size_t smem = UniformTQ::lds_bytes(num_levels);
+      if (hist)
+        hipLaunchKernelGGL((k_quant_fold<UniformTQ, true>), dim3((unsigned)nblocks), dim3(kQThreads), smem, s, q,
+                           in_ptrs, keys, qparams, w, K, L, leaf_n, block_prefix, scale, flags, out_ptrs, hist,
+                           num_levels + 1);
+      else
+        hipLaunchKernelGGL((k_quant_fold<UniformTQ, false>), dim3((unsigned)nblocks), dim3(kQThreads), smem, s, q,
+                           in_ptrs, keys, qparams, w, K, L, leaf_n, block_prefix, scale, flags, out_ptrs, hist, 0);
+      return check_launch("k_quant_fold");
+    }
     UniformQ q;
     q.lm1 = (float)(num_levels - 1);
     q.rcp_lm1 = 1.0 / (double)q.lm1;
