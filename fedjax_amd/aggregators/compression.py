@@ -59,19 +59,13 @@ def _f32_leaf(x, device) -> torch.Tensor:
 
 
 def _rows(trees: Sequence[PyTree]):
+    """Client leaves as float32 device tensors; _client_rows has already checked every
+    client against client 0's structure, shapes and dtypes (the kernels size every row
+    from client 0), so only client 0's dtypes need looking at."""
     td, rows = tree_util._client_rows(trees)
-    if rows[0]:
+    if rows and rows[0] and not all(x.dtype == torch.float32 for x in rows[0]):
         device = rows[0][0].device
-        f32 = torch.float32
-        rows = [r if all(x.dtype == f32 for x in r) else [_f32_leaf(x, device) for x in r] for r in rows]
-        sig = [x.size() for x in rows[0]]
-        for k, r in enumerate(rows[1:], 1):  # the kernels size every row from client 0
-            if [x.size() for x in r] == sig:
-                continue
-            for l, x in enumerate(r):
-                if x.shape != sig[l]:
-                    raise ValueError(f"leaf {l}: client {k} has shape {tuple(x.shape)}, client 0 has "
-                                     f"{tuple(sig[l])}")
+        rows = [[_f32_leaf(x, device) for x in r] for r in rows]
     return td, rows
 
 
