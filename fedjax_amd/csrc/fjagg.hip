@@ -888,7 +888,11 @@ constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 int pick_variant(int64_t nunits, int64_t K) {
   // few clients (short folds) or a narrow parameter axis: many light workgroups
   if (K < 32 || nunits < 131072) return 2;  // E=1 x U=8
-  return 12;                                // E=8 x U=4
+  // up to 1 Mi f32 per row the balanced E=8 grid leaves most lanes of its single
+  // workgroup per CU masked (4.6-4.9 TB/s at 512 Ki); E=4 x U=4 streams at 6.6-7.1
+  // (profiles/r01n_sweep.jsonl: the per-bucket shapes of the sharded pipeline)
+  if (nunits <= 262144) return 5;  // E=4 x U=4
+  return 12;                       // E=8 x U=4
 }
 
 template <int IN, class ACC, int OUT, int V, bool NT>

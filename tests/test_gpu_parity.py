@@ -292,7 +292,7 @@ def synth_cols(K, cols, seed, amp=0.01):
     return np.float32(amp) * u
 
 
-@pytest.mark.parametrize("K,P", [(128, 1206590), (1024, 4 * 1024 * 1024)])
+@pytest.mark.parametrize("K,P", [(128, 1206590), (1024, 4 * 1024 * 1024), (40, 700001), (128, 524288)])
 def test_full_size_configs(K, P, cuda):
     """BASELINE configs 2 and 3 at full size: sampled columns bitwise vs the oracle,
     weight-scaling invariance (2w gives the identical bits) over every element."""
