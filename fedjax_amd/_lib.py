@@ -53,6 +53,7 @@ _SIGNATURES = {
     "fjagg_wsum_l2_ptrs_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_wsum_l2_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _vp, _i32, _vp, _i64, _vp]),
     "fjagg_server_update_dense": (_i32, [_i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "fjagg_server_update_ptrs": (_i32, [_i32, _vp, _i32, _i64, _i64, _vp, _f32, _vp, _vp, _i32, _vp]),
     "fjagg_wsum_l2_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_wsum_l2_dense": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "fjagg_l2sq_workspace_bytes": (_i64, [_i64, _i64]),

@@ -656,6 +656,68 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   }
 }
 
+// Pytree path + server optimizer step in the epilogue (fjagg_server_update_ptrs): the
+// plan image of k_ptrs with out_ptrs[L] = the params leaves; state[3L] = m | v | mean leaf
+// pointers (0 where absent). Each workgroup owns one leaf's unit range, so its OptEpi
+// points at that leaf's params / moments and indexes them by the element within the leaf.
+template <int IN, int V, bool NT>
+__global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict__ img, int L, int64_t K,
+                                                       const float* __restrict__ w, float scale,
+                                                       fjagg_server_opt opt, const int64_t* __restrict__ state) {
+  constexpr int IB = Elem<IN>::B;
+  const int tid = threadIdx.x;
+  const int64_t* in_ptrs = img;
+  const int64_t* out_ptrs = img + K * L;
+  const int64_t* leaf_n = out_ptrs + L;
+  const int64_t* blk = leaf_n + L + 2 * (int64_t)blockIdx.x;
+  const int64_t be = blk[0];
+  const int leaf = (int)((be >> 40) & 0x3fffff);
+  const bool tail = (be >> 62) & 1;
+  const int64_t u0 = be & ((1ll << 40) - 1);
+  const int64_t u1 = blk[1];
+  const int64_t n = leaf_n[leaf];
+  const int64_t nunits = n / V;
+  const OptEpi epi{opt, reinterpret_cast<float*>(out_ptrs[leaf]), reinterpret_cast<float*>(state[leaf]),
+                   reinterpret_cast<float*>(state[L + leaf]), reinterpret_cast<float*>(state[2 * L + leaf])};
+  auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]); };
+  const uint32_t row_bytes = (uint32_t)(n * IB);
+  if (tail) {
+    if (tid < n - nunits * V) {
+      const uint32_t off[1] = {(uint32_t)((nunits * V + tid) * IB)};
+      const bool valid[1] = {true};
+      fold<IN, AccF, FJAGG_F32, 1, 1, 8, NT>(row, row_bytes, K, off, nullptr, valid, w, true, scale, false,
+                                             NoNorm(), epi);
+    }
+    return;
+  }
+  if constexpr (V > 1) {
+    if (u1 - u0 > (int64_t)kThreads) {  // E=8 groups, masked (as k_ptrs)
+      for (int64_t g = u0; g < u1; g += (int64_t)kThreads * 8) {
+        uint32_t off[8];
+        bool valid[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          int64_t u = g + j * kThreads + tid;
+          valid[j] = u < u1;
+          if (!valid[j]) u = u1 - 1;
+          off[j] = (uint32_t)(u * (V * IB));
+        }
+        fold<IN, AccF, FJAGG_F32, V, 8, 4, NT>(row, row_bytes, K, off, nullptr, valid, w, true, scale, false,
+                                               NoNorm(), epi);
+      }
+      return;
+    }
+  }
+  for (int64_t g = u0; g < u1; g += kThreads) {
+    int64_t u = g + tid;
+    const bool valid[1] = {u < u1};
+    if (!valid[0]) u = u1 - 1;
+    const uint32_t off[1] = {(uint32_t)(u * (V * IB))};
+    fold<IN, AccF, FJAGG_F32, V, 1, 8, NT>(row, row_bytes, K, off, nullptr, valid, w, true, scale, false,
+                                           NoNorm(), epi);
+  }
+}
+
 // Per-client sum of squares: grid (nb, K); ws[k*nb + b] = block partial (f32),
 // then k_l2sq_combine sums the nb partials of each client in block order.
 template <int IN>
@@ -1263,6 +1325,41 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
     return fail(FJAGG_EINVAL, "bad plan (nblk=%lld, L=%d)", (long long)nblk, L);
   return wsum_ptrs_impl(in_dtype, acc_dtype, out_dtype, image_dev, L, K, nblk, w_dev, scale, flags,
                         nullptr, nullptr, stream);
+}
+
+int fjagg_server_update_ptrs(int in_dtype, const int64_t* image_dev, int L, int64_t K, int64_t nblk,
+                             const float* w_dev, float scale, const fjagg_server_opt* opt,
+                             const int64_t* state_dev, int flags, void* stream) {
+  g_err[0] = 0;
+  if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16)
+    return fail(FJAGG_EUNSUPPORTED, "server update: f32 or bf16 deltas");
+  if (!opt || opt->kind < FJAGG_OPT_SGD || opt->kind > FJAGG_OPT_ADAM)
+    return fail(FJAGG_EINVAL, "server update: bad optimizer descriptor");
+  if (K < 1) return fail(FJAGG_EINVAL, "need K >= 1");
+  if (nblk == 0) return FJAGG_OK;
+  if (nblk < 0 || nblk > 0x7fffffff || !image_dev || !w_dev || !state_dev || L < 1)
+    return fail(FJAGG_EINVAL, "bad plan (nblk=%lld, L=%d)", (long long)nblk, L);
+  if (flags & ~(FJAGG_NONTEMPORAL | FJAGG_UNALIGNED))
+    return fail(FJAGG_EINVAL, "flags may hold FJAGG_NONTEMPORAL and FJAGG_UNALIGNED only");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool vec = !(flags & FJAGG_UNALIGNED), nt = (flags & FJAGG_NONTEMPORAL) != 0;
+  const dim3 grid((unsigned)nblk), block(kThreads);
+#define FJ_OPT_LAUNCH(I, VV)                                                                         \
+  do {                                                                                               \
+    if (nt)                                                                                          \
+      hipLaunchKernelGGL((k_ptrs_opt<I, VV, true>), grid, block, 0, s, image_dev, L, K, w_dev, scale, \
+                         *opt, state_dev);                                                           \
+    else                                                                                             \
+      hipLaunchKernelGGL((k_ptrs_opt<I, VV, false>), grid, block, 0, s, image_dev, L, K, w_dev, scale, \
+                         *opt, state_dev);                                                           \
+  } while (0)
+  if (in_dtype == FJAGG_F32) {
+    if (vec) FJ_OPT_LAUNCH(FJAGG_F32, 4); else FJ_OPT_LAUNCH(FJAGG_F32, 1);
+  } else {
+    if (vec) FJ_OPT_LAUNCH(FJAGG_BF16, 8); else FJ_OPT_LAUNCH(FJAGG_BF16, 1);
+  }
+#undef FJ_OPT_LAUNCH
+  return check_launch("k_ptrs_opt");
 }
 
 int64_t fjagg_wsum_l2_ptrs_workspace_bytes(int64_t K, int64_t nblk) {

@@ -24,7 +24,7 @@ from typing import Optional, Sequence
 import numpy as np
 import torch
 
-from fedjax_amd import _lib, kernels, tree_util
+from fedjax_amd import _lib, kernels, pytree, tree_util
 from fedjax_amd.slab import ClientDeltaSlab
 
 
@@ -40,13 +40,15 @@ class ServerOptimizer:
     eps: float = 1e-8
     eps_root: float = 0.0
 
-    def init(self, params: torch.Tensor) -> dict:
-        """Optimizer state for flat float32 device params (optax init: zeros, count 0)."""
+    def init(self, params) -> dict:
+        """Optimizer state (optax init: zeros, count 0) for flat float32 device params or
+        a pytree of them (then m / v are pytrees of the same structure)."""
+        zeros = torch.zeros_like if isinstance(params, torch.Tensor) else tree_util.tree_zeros_like
         st = {"count": 0}
         if self.kind in (_lib.OPT_MOMENTUM, _lib.OPT_ADAM):
-            st["m"] = torch.zeros_like(params)
+            st["m"] = zeros(params)
         if self.kind == _lib.OPT_ADAM:
-            st["v"] = torch.zeros_like(params)
+            st["v"] = zeros(params)
         return st
 
     def descriptor(self, count: int) -> _lib.ServerOpt:
@@ -113,4 +115,72 @@ def fused_mean_update(slab: ClientDeltaSlab, weights: Sequence, opt: ServerOptim
     return new
 
 
-__all__ = ["ServerOptimizer", "adam", "fused_mean_update", "sgd"]
+def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, state: dict, *,
+                           mean_out=None, nontemporal: Optional[bool] = None) -> dict:
+    """:func:`fused_mean_update` on the pytree path: ``tree_mean`` of the clients' delta
+    pytrees (tree_util.py:76-96) and ``opt``'s update of the ``params`` pytree (float32
+    device leaves, the deltas' structure and shapes, updated in place) in ONE kernel
+    (``fjagg_server_update_ptrs``) — examples/fed_avg.py:82 + :97-101. ``state`` is
+    ``opt.init(params)``; returns the new state. ``mean_out`` (optional pytree of float32
+    leaves) also receives the mean."""
+    pairs = list(pytrees_and_weights)
+    if not pairs:
+        raise ValueError("no clients to aggregate")
+    W = 0.0
+    weights = []
+    for _, w in pairs:
+        w = tree_util._host_weight(w)
+        weights.append(w)
+        W += w  # tree_util.py:95
+    td, rows = tree_util._client_rows([t for t, _ in pairs])
+    K, L = len(rows), len(rows[0])
+    if L == 0:
+        return dict(state, count=state["count"] + 1)
+    dt = rows[0][0].dtype
+    if dt not in (torch.float32, torch.bfloat16) or any(x.dtype != dt for x in rows[0]):
+        raise TypeError("the fused server step takes float32 or bfloat16 deltas of one dtype")
+    device = rows[0][0].device
+
+    def leaves(tree, what):
+        ls = pytree.flatten_as(td, tree)
+        for x, d in zip(ls, rows[0]):
+            if not (isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.is_contiguous()
+                    and x.device == device and x.shape == d.shape):
+                raise ValueError(f"{what} leaves must be contiguous float32 device tensors shaped like the deltas")
+        return ls
+
+    p = leaves(params, "params")
+    m = leaves(state["m"], "state m") if "m" in state else None
+    v = leaves(state["v"], "state v") if "v" in state else None
+    mo = leaves(mean_out, "mean_out") if mean_out is not None else None
+    count = state["count"] + 1  # optax safe_int32_increment
+    desc = opt.descriptor(count)
+    in_c = kernels.dtype_code(dt)
+    leaf_n = np.array([x.numel() for x in rows[0]], dtype=np.int64)
+    in_ptrs = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.int64)
+    out_ptrs = np.array([x.data_ptr() for x in p], dtype=np.int64)
+    st = np.zeros(3 * L, dtype=np.int64)
+    for i, ls in enumerate((m, v, mo)):
+        if ls is not None:
+            st[i * L:(i + 1) * L] = [x.data_ptr() for x in ls]
+    unaligned = bool((in_ptrs % 16).any() or (out_ptrs % 16).any() or (st % 16).any())
+    blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)
+    w_words = np.zeros((K + 1) // 2, dtype=np.int64)
+    w_words.view(np.uint8)[:4 * K] = np.array([np.float32(w) for w in weights], np.float32).view(np.uint8)
+    image = np.concatenate([in_ptrs.ravel(), out_ptrs, leaf_n, blocks, w_words, st])
+    image_dev = torch.from_numpy(image).pin_memory().to(device, non_blocking=True)
+    base = image_dev.data_ptr()
+    w_ptr = base + 8 * (K * L + 2 * L + blocks.size)
+    st_ptr = w_ptr + 8 * w_words.size
+    nbytes = int(leaf_n.sum()) * K * rows[0][0].element_size()
+    nt = nbytes >= tree_util.NONTEMPORAL_MIN_BYTES if nontemporal is None else nontemporal
+    flags = (_lib.NONTEMPORAL if nt else 0) | (_lib.UNALIGNED if unaligned else 0)
+    _lib.call("fjagg_server_update_ptrs", in_c, base, L, K, blocks.size // 2, w_ptr,
+              float(np.float32(tree_util._inverse(W))), ctypes.byref(desc), st_ptr, flags,
+              torch.cuda.current_stream(device).cuda_stream)
+    new = dict(state)
+    new["count"] = count
+    return new
+
+
+__all__ = ["ServerOptimizer", "adam", "fused_mean_update", "fused_tree_mean_update", "sgd"]

@@ -186,6 +186,15 @@ int fjagg_server_update_dense(int in_dtype, const void* x_dev, int64_t ld, int64
                               const float* w_dev, float scale, const fjagg_server_opt* opt,
                               float* params_dev, float* m_dev, float* v_dev, float* mean_dev,
                               int flags, void* stream);
+/* The same step on the pytree path: the plan image of fjagg_wsum_ptrs (same blocks,
+ * nblk; weights f32) with out_ptrs[L] = the float32 params leaves (updated in place)
+ * and state_dev[3*L] (device) = m leaves | v leaves | mean leaves (0 where absent; m
+ * for MOMENTUM/ADAM, v for ADAM; mean optional). flags: FJAGG_NONTEMPORAL,
+ * FJAGG_UNALIGNED. Replaces tree_mean + server_optimizer.apply over the pytrees of
+ * examples/fed_avg.py:82,97-101 in one pass. */
+int fjagg_server_update_ptrs(int in_dtype, const int64_t* image_dev, int L, int64_t K, int64_t nblk,
+                             const float* w_dev, float scale, const fjagg_server_opt* opt,
+                             const int64_t* state_dev, int flags, void* stream);
 
 /*
  * Squared L2 norm of each of K client deltas (the per-client diagnostic of

@@ -582,3 +582,52 @@ def test_tree_mean_with_l2_norms_edges(cuda):
         tu.tree_mean_with_l2_norms([({"x": torch.ones(3, dtype=torch.int32, device=cuda)}, 1)])
     with pytest.raises(TypeError):
         tu.tree_mean_with_l2_norms([({"x": a, "y": a.bfloat16()}, 1)])
+
+
+@pytest.mark.parametrize("make", [lambda s: s.sgd(0.5), lambda s: s.sgd(0.1, momentum=0.9),
+                                  lambda s: s.sgd(0.1, momentum=0.9, nesterov=True),
+                                  lambda s: s.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_fused_tree_server_update_matches_restated_optax(make, offset, cuda, coracle):
+    """Pytree path (fjagg_server_update_ptrs): tree_mean of separate client pytrees + the
+    server step, bitwise against tree_mean followed by the numpy optax restatement."""
+    from fedjax_amd import server
+    opt = make(server)
+    K, sizes = 33, {"a": 8, "b": 10000, "c": (3, 5)}  # offset 0: every leaf 16-byte aligned, c has a tail
+    n = {k: int(np.prod(v)) for k, v in sizes.items()}
+    P = sum(n.values())
+
+    def tree_of(vec):
+        out, o = {}, 0
+        for k in sorted(sizes):
+            out[k] = vec[o:o + n[k]].reshape(sizes[k] if isinstance(sizes[k], tuple) else (n[k],))
+            o += n[k]
+        return out
+
+    base = torch.from_numpy(coracle.synth_f32(1, P + offset, seed=61)[0].copy()).to(cuda)
+    params = tree_of(base[offset:].clone())
+    state = opt.init(params)
+    p_np = {k: host(v).copy() for k, v in params.items()}
+    m_np = {k: np.zeros_like(v) for k, v in p_np.items()}
+    v_np = {k: np.zeros_like(v) for k, v in p_np.items()}
+    for rnd in range(3):
+        ld = (P + offset + 3) // 4 * 4
+        x = torch.zeros(K, ld, device=cuda)
+        x[:, :P + offset] = torch.from_numpy(coracle.synth_f32(K, P + offset, seed=62 + rnd)).to(cuda)
+        clients = [tree_of(x[k, offset:]) for k in range(K)]  # views: offset 1 = unaligned path
+        wi = [int(w) for w in ref.fedavg_weights(K, seed=70 + rnd)]
+        g = tu.tree_mean(list(zip(clients, wi)))
+        mean_out = {k: torch.empty_like(v) for k, v in params.items()}
+        state = server.fused_tree_mean_update(zip(clients, wi), opt, params, state, mean_out=mean_out)
+        d = opt.descriptor(state["count"])
+        for k in sorted(sizes):
+            assert np.array_equal(bits(host(mean_out[k])), bits(host(g[k]))), (rnd, k)
+            p_np[k], m_np[k], v_np[k] = _np_server_step(opt, d, host(g[k]), p_np[k], m_np[k], v_np[k])
+            assert np.array_equal(bits(host(params[k])), bits(p_np[k])), (rnd, k)
+            if "m" in state:
+                assert np.array_equal(bits(host(state["m"][k])), bits(m_np[k]))
+            if "v" in state:
+                assert np.array_equal(bits(host(state["v"][k])), bits(v_np[k]))
+    assert state["count"] == 3
+    with pytest.raises(ValueError):
+        server.fused_tree_mean_update(zip(clients, wi), opt, {"a": params["a"]}, state)
