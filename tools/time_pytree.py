@@ -69,9 +69,23 @@ def main(K=128, reps=20):
         tu.tree_mean_with_l2_norms(pairs)
     torch.cuda.synchronize()
     wall_l2 = (time.perf_counter() - t0) / reps
+    # tree_mean + server Adam step in one kernel on the same pytrees (fjagg_server_update_ptrs)
+    from fedjax_amd import server
+    opt = server.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)
+    params = tmap(lambda v: torch.zeros(v.shape, device=dev), clients[0])
+    st = opt.init(params)
+    for _ in range(3):
+        st = server.fused_tree_mean_update(pairs, opt, params, st)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        st = server.fused_tree_mean_update(pairs, opt, params, st)
+    torch.cuda.synchronize()
+    wall_opt = (time.perf_counter() - t0) / reps
     nbytes = K * P * 4
     print(json.dumps({"workload": "configs[1] 128 x EMNIST-CNN (1,206,590 params, 8 leaves)",
                       "tree_mean_with_l2_norms_wall_ms": round(wall_l2 * 1e3, 4),
+                      "fused_tree_mean_adam_wall_ms": round(wall_opt * 1e3, 4),
                       "tree_mean_wall_ms": round(wall * 1e3, 4),
                       "tree_mean_wall_GBs": round(nbytes / wall / 1e9, 1),
                       "tree_mean_gpu_ms_median": round(float(np.median(ks)), 4),
