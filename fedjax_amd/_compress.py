@@ -26,7 +26,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from fedjax_amd import _lib
+from fedjax_amd import _lib, tree_util
 
 ROW = np.dtype([("ptr", "<u8"), ("n", "<i8")])
 SIGN_JOB = np.dtype([("k0", "<u4"), ("k1", "<u4"), ("d", "<i8"), ("words", "<u8")])
@@ -271,7 +271,7 @@ def quantized_mean(method: int, rows: List[List[torch.Tensor]], keys: np.ndarray
     deltas). Returns (hist tensor or None, qparams tensor)."""
     device = outs[0].device
     K, L = len(rows), len(rows[0])
-    in_ptrs = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.uint64)
+    in_ptrs = tree_util._ptr_table(rows, np.uint64)
     leaf_n = np.array([x.numel() for x in rows[0]], dtype=np.int64)
     if qparams is None:
         _, qparams = row_stats_table(in_ptrs.reshape(-1), np.tile(leaf_n, K), method, device)
@@ -305,7 +305,7 @@ def rotated_quantized_mean(rows: List[List[torch.Tensor]], rot_keys: np.ndarray,
     leaf_n = np.asarray(leaf_n, dtype=np.int64)
     loff = 4 * offs[:-1].astype(np.uint64)
     sptr = np.asarray(sptr, dtype=np.uint64)
-    src_all = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.uint64)
+    src_all = tree_util._ptr_table(rows, np.uint64)
     keep = []
     for k0 in range(0, K, B):
         kb = min(B, K - k0)
@@ -351,7 +351,7 @@ def drive_mean(rows: List[List[torch.Tensor]], client_keys: np.ndarray, w: np.nd
     leaf_d = np.asarray(ds, dtype=np.int64)
     yoff = 4 * offs[:-1].astype(np.uint64)
     zoff = 4 * loff[:-1].astype(np.uint64)
-    src_all = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.uint64)
+    src_all = tree_util._ptr_table(rows, np.uint64)
     for k0 in range(0, K, B):
         kb = min(B, K - k0)
         signs, woff = rademacher_words(client_keys[k0:k0 + kb].reshape(-1, 2), ds * kb, device)

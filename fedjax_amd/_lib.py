@@ -150,6 +150,29 @@ def load() -> ctypes.CDLL:
         return lib
 
 
+HOST_PATH = os.path.join(_HERE, "_build", "_fjhost.so")
+_host = None
+
+
+def host():
+    """The native host helper ``_fjhost`` (fedjax_amd/csrc/fjhost.cpp: pytree walk and
+    pointer table, weight packing; no device work). Raises FjaggError if missing."""
+    global _host
+    if _host is None:
+        import importlib.machinery
+        import importlib.util
+
+        if not os.path.exists(HOST_PATH):
+            raise FjaggError(f"{HOST_PATH} is missing: build it with "
+                             "`python -c 'import __graft_entry__ as g; g.build()'` from the repo root")
+        loader = importlib.machinery.ExtensionFileLoader("_fjhost", HOST_PATH)
+        spec = importlib.util.spec_from_file_location("_fjhost", HOST_PATH, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        _host = mod
+    return _host
+
+
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = load().fjagg_last_error().decode(errors="replace")

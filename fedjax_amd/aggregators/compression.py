@@ -62,8 +62,9 @@ def _rows(trees: Sequence[PyTree]):
     """Client leaves as float32 device tensors; _client_rows has already checked every
     client against client 0's structure, shapes and dtypes (the kernels size every row
     from client 0), so only client 0's dtypes need looking at."""
-    td, rows = tree_util._client_rows(trees)
-    if rows and rows[0] and not all(x.dtype == torch.float32 for x in rows[0]):
+    td, rows = tree_util._client_table(trees)
+    if rows[0] and not all(x.dtype == torch.float32 for x in rows[0]):
+        td, rows = tree_util._client_rows(trees)
         device = rows[0][0].device
         rows = [[_f32_leaf(x, device) for x in r] for r in rows]
     return td, rows

@@ -1,0 +1,226 @@
+// fjhost.cpp — native host side of the pytree aggregation path (CPython extension).
+//
+// tree_mean over separate client pytrees (fedjax/core/tree_util.py:76-96, called from
+// examples/fed_avg.py:82 and aggregator.py:100) spends its host time walking K pytrees
+// and reading, per (client, leaf), the tensor's type / dtype / device / contiguity /
+// shape and device pointer. In Python that is five attribute calls per leaf; here it
+// is a handful of loads from the TensorImpl. The GPU arithmetic stays in libfjagg.so
+// (include/fjagg.h); this module only builds the kernel's pointer table and weight
+// vector, and never touches device memory.
+//
+// Everything here answers "the fast case holds" or "it does not": on any mismatch
+// (structure, leaf type, dtype, shape, device, layout, an unusual weight) the caller
+// falls back to the Python path, which converts what it can and raises the reference's
+// errors (ValueError / TypeError). So this module never decides an error itself.
+//
+// Entry points (all positional):
+//   gather_rows(trees, k0, spec, row0, dev_index, ptrs) -> int
+//       Walk trees[k0:] against `spec` (pytree.native_spec of client 0's TreeDef) and
+//       write the device pointer of client k's leaf l to ptrs[k*L + l] (int64 buffer),
+//       for k = k0 .. len(trees)-1, L = len(row0). Every leaf must be a torch.Tensor on
+//       cuda:dev_index (-1: host tensors, for the CPU tests), strided and contiguous,
+//       with row0[l]'s dtype and shape. Also writes row0's pointers to row 0 when k0 == 1.
+//       Returns 0, or -(k+1) for the first client k that does not match.
+//   fold_weights(weights, f32_out, i32_out_or_None) -> (W, kinds) | None
+//       For weights that are all Python int / float (not bool): f32_out[k] =
+//       float32(w_k) (numpy's np.float32(w) rounding), i32_out[k] = the int32 wrap of an
+//       integer weight (0 for a float one), W = sum(w) accumulated left to right from 0.0
+//       in double, exactly as tree_util.py:86,95 (`sum_weight = 0.; sum_weight +=
+//       weight`), kinds = bit 0: some weight is a float, bit 1: some weight is an int.
+//       None when any weight is something else (numpy scalar, tensor, bool, |w| >=
+//       2**53, ...): the caller then uses the Python path.
+
+#include <Python.h>
+
+#include <torch/csrc/autograd/python_variable.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace {
+
+struct Walk {
+  const std::vector<at::ScalarType>* dtypes;
+  const std::vector<c10::IntArrayRef>* sizes;
+  c10::DeviceIndex dev;
+  int64_t* out;  // row of L pointers
+  size_t leaf;
+};
+
+enum { kLeaf = 0, kNone = 1, kDict = 2, kList = 3, kTuple = 4 };
+
+// 0: matches; 1: mismatch (no Python error set); -1: Python error set.
+int leaf(PyObject* x, Walk& w) {
+  if (Py_TYPE(x) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) return 1;
+  size_t l = w.leaf++;
+  if (l >= w.dtypes->size()) return 1;
+  const at::Tensor& t = THPVariable_Unpack(x);
+  if (t.layout() != c10::kStrided) return 1;
+  if (w.dev >= 0 ? (!t.is_cuda() || t.get_device() != w.dev) : !t.is_cpu()) return 1;
+  if (t.scalar_type() != (*w.dtypes)[l] || t.sizes() != (*w.sizes)[l] || !t.is_contiguous()) return 1;
+  w.out[l] = reinterpret_cast<int64_t>(t.data_ptr());
+  return 0;
+}
+
+int walk(PyObject* spec, PyObject* x, Walk& w) {
+  if (PyLong_CheckExact(spec)) {
+    long k = PyLong_AsLong(spec);
+    if (k == kLeaf) return leaf(x, w);
+    if (k == kNone) return x == Py_None ? 0 : 1;
+    return 1;
+  }
+  if (!PyTuple_CheckExact(spec) || PyTuple_GET_SIZE(spec) != 3) return 1;
+  long kind = PyLong_AsLong(PyTuple_GET_ITEM(spec, 0));
+  PyObject* aux = PyTuple_GET_ITEM(spec, 1);
+  PyObject* children = PyTuple_GET_ITEM(spec, 2);
+  Py_ssize_t n = PyTuple_GET_SIZE(children);
+  if (kind == kDict) {
+    if (!PyDict_CheckExact(x) || PyDict_GET_SIZE(x) != n) return 1;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      PyObject* v = PyDict_GetItemWithError(x, PyTuple_GET_ITEM(aux, i));  // borrowed
+      if (v == nullptr) {
+        if (PyErr_Occurred()) PyErr_Clear();  // e.g. an unhashable comparison: a mismatch
+        return 1;
+      }
+      int rc = walk(PyTuple_GET_ITEM(children, i), v, w);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  if (kind == kList || kind == kTuple) {
+    bool ok = kind == kList ? PyList_CheckExact(x) : PyTuple_CheckExact(x);
+    if (!ok || Py_SIZE(x) != n) return 1;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      PyObject* v = kind == kList ? PyList_GET_ITEM(x, i) : PyTuple_GET_ITEM(x, i);
+      int rc = walk(PyTuple_GET_ITEM(children, i), v, w);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  return 1;
+}
+
+PyObject* gather_rows(PyObject*, PyObject* args) {
+  PyObject *trees, *spec, *row0, *ptrs;
+  Py_ssize_t k0;
+  int dev;
+  if (!PyArg_ParseTuple(args, "O!nOO!iO", &PyList_Type, &trees, &k0, &spec, &PyList_Type, &row0, &dev, &ptrs))
+    return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(trees), L = PyList_GET_SIZE(row0);
+  if (k0 < 0 || k0 > K) {
+    PyErr_SetString(PyExc_ValueError, "gather_rows: k0 out of range");
+    return nullptr;
+  }
+  Py_buffer buf;
+  if (PyObject_GetBuffer(ptrs, &buf, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) != 0) return nullptr;
+  struct Release {
+    Py_buffer* b;
+    ~Release() { PyBuffer_Release(b); }
+  } release{&buf};
+  if (buf.len < static_cast<Py_ssize_t>(sizeof(int64_t)) * K * L) {
+    PyErr_SetString(PyExc_ValueError, "gather_rows: pointer buffer smaller than K*L int64");
+    return nullptr;
+  }
+  auto* out = static_cast<int64_t*>(buf.buf);
+  try {
+    std::vector<at::ScalarType> dtypes;
+    std::vector<c10::IntArrayRef> sizes;
+    dtypes.reserve(L);
+    sizes.reserve(L);
+    for (Py_ssize_t l = 0; l < L; ++l) {
+      PyObject* x = PyList_GET_ITEM(row0, l);
+      if (!THPVariable_Check(x)) {
+        PyErr_SetString(PyExc_TypeError, "gather_rows: row0 must hold tensors");
+        return nullptr;
+      }
+      const at::Tensor& t = THPVariable_Unpack(x);
+      dtypes.push_back(t.scalar_type());
+      sizes.push_back(t.sizes());
+      if (k0 == 1) out[l] = reinterpret_cast<int64_t>(t.data_ptr());
+    }
+    Walk w{&dtypes, &sizes, static_cast<c10::DeviceIndex>(dev), nullptr, 0};
+    for (Py_ssize_t k = k0; k < K; ++k) {
+      w.out = out + k * L;
+      w.leaf = 0;
+      int rc = walk(spec, PyList_GET_ITEM(trees, k), w);
+      if (rc < 0) return nullptr;
+      if (rc > 0 || w.leaf != static_cast<size_t>(L)) return PyLong_FromSsize_t(-(k + 1));
+    }
+    return PyLong_FromLong(0);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
+PyObject* fold_weights(PyObject*, PyObject* args) {
+  PyObject *weights, *f32, *i32;
+  if (!PyArg_ParseTuple(args, "O!OO", &PyList_Type, &weights, &f32, &i32)) return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(weights);
+  Py_buffer bf, bi;
+  if (PyObject_GetBuffer(f32, &bf, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) != 0) return nullptr;
+  bool have_i = i32 != Py_None;
+  if (have_i && PyObject_GetBuffer(i32, &bi, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) != 0) {
+    PyBuffer_Release(&bf);
+    return nullptr;
+  }
+  PyObject* result = nullptr;
+  if (bf.len < 4 * K || (have_i && bi.len < 4 * K)) {
+    PyErr_SetString(PyExc_ValueError, "fold_weights: output buffers smaller than K");
+  } else {
+    auto* fo = static_cast<float*>(bf.buf);
+    auto* io = have_i ? static_cast<int32_t*>(bi.buf) : nullptr;
+    double W = 0.0;
+    long kinds = 0;
+    bool simple = true;
+    for (Py_ssize_t k = 0; k < K && simple; ++k) {
+      PyObject* w = PyList_GET_ITEM(weights, k);
+      double d;
+      if (PyLong_CheckExact(w)) {
+        int overflow = 0;
+        long long v = PyLong_AsLongLongAndOverflow(w, &overflow);
+        // |v| < 2**53: the double is exact, so float(double) is numpy's single rounding
+        if (overflow || v >= (1LL << 53) || v <= -(1LL << 53)) {
+          simple = false;
+          break;
+        }
+        d = static_cast<double>(v);
+        if (io) io[k] = static_cast<int32_t>(static_cast<uint32_t>(static_cast<uint64_t>(v)));
+        kinds |= 2;
+      } else if (PyFloat_CheckExact(w)) {
+        d = PyFloat_AS_DOUBLE(w);
+        if (io) io[k] = 0;  // int32 folds take integer weights only; the caller checks the kinds
+        kinds |= 1;
+      } else {
+        simple = false;
+        break;
+      }
+      fo[k] = static_cast<float>(d);
+      W += d;  // tree_util.py:95, Python float + int / float
+    }
+    if (PyErr_Occurred()) {
+      result = nullptr;
+    } else if (simple) {
+      result = Py_BuildValue("(dl)", W, kinds);
+    } else {
+      Py_INCREF(Py_None);
+      result = Py_None;
+    }
+  }
+  PyBuffer_Release(&bf);
+  if (have_i) PyBuffer_Release(&bi);
+  return result;
+}
+
+PyMethodDef kMethods[] = {
+    {"gather_rows", gather_rows, METH_VARARGS, "pointer table of K client pytrees (see fjhost.cpp)"},
+    {"fold_weights", fold_weights, METH_VARARGS, "f32/i32 weights and W of Python-number weights"},
+    {nullptr, nullptr, 0, nullptr},
+};
+
+PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_fjhost", "native host side of the pytree aggregation path",
+                       -1, kMethods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__fjhost(void) { return PyModule_Create(&kModule); }

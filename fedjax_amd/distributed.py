@@ -190,12 +190,13 @@ def sharded_tree_mean(local_pytrees_and_weights, *, W_total=None, group=None, ds
         W_total = total_weight(weights, group=group, device=dev)
     if not trees:
         raise ValueError("every rank needs at least one client (use shard_range)")
-    td, rows = tree_util._client_rows(trees)
-    sizes = [x.numel() for x in rows[0]]
-    flat = torch.empty(sum(sizes), dtype=torch.float32, device=rows[0][0].device)
+    td, rows = tree_util._client_table(trees)
+    row0 = rows[0]
+    sizes = [x.numel() for x in row0]
+    flat = torch.empty(sum(sizes), dtype=torch.float32, device=row0[0].device)
     offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-    views = [flat[o:o + n].view(x.shape) for o, n, x in zip(offs[:-1], sizes, rows[0])]
-    if any(x.dtype != torch.float32 for x in rows[0]):
+    views = [flat[o:o + n].view(x.shape) for o, n, x in zip(offs[:-1], sizes, row0)]
+    if any(x.dtype != torch.float32 for x in row0):
         raise TypeError("sharded_tree_mean needs float32 leaves")
     tree_util._fold(rows, weights, scale=tree_util._inverse(W_total), out=views, accumulate=False,
                     validated=True)

@@ -207,6 +207,35 @@ def _compile(td: TreeDef):
         return None
 
 
+_SPECS: Dict[TreeDef, Any] = {}  # structure -> native walk spec (or None)
+_SPEC_KIND = {"dict": 2, "list": 3, "tuple": 4}
+
+
+def native_spec(td: TreeDef):
+    """Walk program of ``td`` for fjhost.gather_rows (fedjax_amd/csrc/fjhost.cpp): 0 =
+    leaf, 1 = None, ``(2, keys, children)`` dict (keys in flatten order), ``(3|4, n,
+    children)`` list / tuple. None when ``td`` holds another node kind (namedtuple,
+    OrderedDict, registered classes): those trees take the Python walk."""
+    spec = _SPECS.get(td, False)
+    if spec is False:
+        spec = _SPECS[td] = _spec(td) if len(_SPECS) < 4096 else None
+    return spec
+
+
+def _spec(td: TreeDef):
+    k = td.kind
+    if k == "leaf":
+        return 0
+    if k == "none":
+        return 1
+    if k not in _SPEC_KIND:
+        return None
+    children = tuple(_spec(c) for c in td.children)
+    if any(c is None for c in children):
+        return None
+    return (_SPEC_KIND[k], td.aux if k == "dict" else len(children), children)
+
+
 def _collect(td: TreeDef, x, out: List[Any]) -> None:
     k = td.kind
     if k == "leaf":

@@ -123,27 +123,22 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
     (``fjagg_server_update_ptrs``) — examples/fed_avg.py:82 + :97-101. ``state`` is
     ``opt.init(params)``; returns the new state. ``mean_out`` (optional pytree of float32
     leaves) also receives the mean."""
-    pairs = list(pytrees_and_weights)
-    if not pairs:
+    trees, weights, W = tree_util._collect_pairs(pytrees_and_weights)
+    if not trees:
         raise ValueError("no clients to aggregate")
-    W = 0.0
-    weights = []
-    for _, w in pairs:
-        w = tree_util._host_weight(w)
-        weights.append(w)
-        W += w  # tree_util.py:95
-    td, rows = tree_util._client_rows([t for t, _ in pairs])
-    K, L = len(rows), len(rows[0])
+    td, rows = tree_util._client_table(trees)
+    row0 = rows[0]
+    K, L = len(trees), len(row0)
     if L == 0:
         return dict(state, count=state["count"] + 1)
-    dt = rows[0][0].dtype
-    if dt not in (torch.float32, torch.bfloat16) or any(x.dtype != dt for x in rows[0]):
+    dt = row0[0].dtype
+    if dt not in (torch.float32, torch.bfloat16) or any(x.dtype != dt for x in row0):
         raise TypeError("the fused server step takes float32 or bfloat16 deltas of one dtype")
-    device = rows[0][0].device
+    device = row0[0].device
 
     def leaves(tree, what):
         ls = pytree.flatten_as(td, tree)
-        for x, d in zip(ls, rows[0]):
+        for x, d in zip(ls, row0):
             if not (isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.is_contiguous()
                     and x.device == device and x.shape == d.shape):
                 raise ValueError(f"{what} leaves must be contiguous float32 device tensors shaped like the deltas")
@@ -156,23 +151,25 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
     count = state["count"] + 1  # optax safe_int32_increment
     desc = opt.descriptor(count)
     in_c = kernels.dtype_code(dt)
-    leaf_n = np.array([x.numel() for x in rows[0]], dtype=np.int64)
-    in_ptrs = np.array([[x.data_ptr() for x in r] for r in rows], dtype=np.int64)
+    leaf_n = np.array([x.numel() for x in row0], dtype=np.int64)
+    in_ptrs = tree_util._ptr_table(rows)
     out_ptrs = np.array([x.data_ptr() for x in p], dtype=np.int64)
     st = np.zeros(3 * L, dtype=np.int64)
     for i, ls in enumerate((m, v, mo)):
         if ls is not None:
             st[i * L:(i + 1) * L] = [x.data_ptr() for x in ls]
     unaligned = bool((in_ptrs % 16).any() or (out_ptrs % 16).any() or (st % 16).any())
-    blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)
+    blocks = tree_util._ptrs_plan(in_c, leaf_n, unaligned)
+    w32 = weights.f32 if isinstance(weights, tree_util._Weights) else np.array(
+        [np.float32(w) for w in weights], np.float32)
     w_words = np.zeros((K + 1) // 2, dtype=np.int64)
-    w_words.view(np.uint8)[:4 * K] = np.array([np.float32(w) for w in weights], np.float32).view(np.uint8)
+    w_words.view(np.uint8)[:4 * K] = w32.view(np.uint8)
     image = np.concatenate([in_ptrs.ravel(), out_ptrs, leaf_n, blocks, w_words, st])
     image_dev = torch.from_numpy(image).pin_memory().to(device, non_blocking=True)
     base = image_dev.data_ptr()
     w_ptr = base + 8 * (K * L + 2 * L + blocks.size)
     st_ptr = w_ptr + 8 * w_words.size
-    nbytes = int(leaf_n.sum()) * K * rows[0][0].element_size()
+    nbytes = int(leaf_n.sum()) * K * row0[0].element_size()
     nt = nbytes >= tree_util.NONTEMPORAL_MIN_BYTES if nontemporal is None else nontemporal
     flags = (_lib.NONTEMPORAL if nt else 0) | (_lib.UNALIGNED if unaligned else 0)
     _lib.call("fjagg_server_update_ptrs", in_c, base, L, K, blocks.size // 2, w_ptr,

@@ -170,20 +170,26 @@ def _leaf_rule(dt: torch.dtype, kinds: Sequence[int], scaled_kind: Optional[int]
     return _lib.I32, _lib.F32, torch.float32
 
 
-def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
+def _fold(rows, weights, *, scale=None,
           out: Optional[List[torch.Tensor]] = None, accumulate: bool = False,
           nontemporal: Optional[bool] = None, validated: bool = False,
           l2sq: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
     """y_l = [out_l +] sum_k fl(rows[k][l] * w_k) [* scale] for every leaf l, one
     kernel launch per (input, fold, output) dtype group. ``out`` gives the
     destination tensors (fresh ones otherwise); ``accumulate`` folds into them.
-    ``validated``: rows come from _client_rows (shapes and dtypes already checked).
-    ``l2sq`` (float32 [K]): also write every client's squared l2 norm over all leaves,
-    from the same pass (fjagg_wsum_l2_ptrs; float leaves of one dtype)."""
+    ``rows``: K lists of L leaves, or a :class:`_Table` (client 0's leaves + the K x L
+    pointer table). ``weights``: host weights, or a :class:`_Weights` (already packed).
+    ``validated``: rows come from _client_rows / _client_table (shapes and dtypes
+    already checked). ``l2sq`` (float32 [K]): also write every client's squared l2 norm
+    over all leaves, from the same pass (fjagg_wsum_l2_ptrs; float leaves of one dtype)."""
     if accumulate and out is None:
         raise ValueError("accumulate needs out")
-    K, L = len(rows), len(rows[0])
-    kinds = [_weight_kind(w) for w in weights]
+    table = rows if isinstance(rows, _Table) else None
+    if table is not None:
+        rows, validated = [table.row0], True  # built by _client_table, which checked every client
+    K, L = (len(rows) if table is None else table.ptrs.shape[0]), len(rows[0])
+    packed = weights if isinstance(weights, _Weights) else None
+    kinds = packed.kinds if packed is not None else [_weight_kind(w) for w in weights]
     scaled_kind = None if scale is None else _weight_kind(scale)
     device = rows[0][0].device if L else None
     outs: List[Optional[torch.Tensor]] = [None] * L
@@ -218,14 +224,18 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
             if l2sq is not None:
                 l2sq.zero_()
             continue
-        if len(ls) == L:
+        if table is not None:
+            in_ptrs = table.ptrs if len(ls) == L else table.ptrs[:, ls]
+        elif len(ls) == L:
             in_ptrs = np.array([[x.data_ptr() for x in row] for row in rows], dtype=np.int64)
         else:
             in_ptrs = np.array([[rows[k][l].data_ptr() for l in ls] for k in range(K)], dtype=np.int64)
         out_ptrs = np.array([outs[l].data_ptr() for l in ls], dtype=np.int64)
         unaligned = bool((in_ptrs % 16).any() or (out_ptrs % 16).any())
-        blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)
-        if acc_c == _lib.F32:
+        blocks = _ptrs_plan(in_c, leaf_n, unaligned)
+        if packed is not None:
+            w_host = packed.f32 if acc_c == _lib.F32 else packed.i32
+        elif acc_c == _lib.F32:
             w_host = np.array([np.float32(w) for w in weights], dtype=np.float32)
         else:
             w_host = np.array([np.int64(w) for w in weights], dtype=np.int64).astype(np.int32)
@@ -252,6 +262,84 @@ def _fold(rows: List[List[torch.Tensor]], weights: Sequence[Any], *, scale=None,
     return outs
 
 
+_PLANS = {}  # (in dtype, leaf sizes, unaligned) -> workgroup table (the device is fixed per process)
+
+
+def _ptrs_plan(in_c: int, leaf_n: np.ndarray, unaligned: bool) -> np.ndarray:
+    key = (in_c, leaf_n.tobytes(), unaligned, torch.cuda.current_device())
+    blocks = _PLANS.get(key)
+    if blocks is None:
+        blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)
+        if len(_PLANS) < 1024:
+            _PLANS[key] = blocks
+    return blocks
+
+
+class _Table:
+    """K clients' leaves as client 0's canonical device leaves + an int64 [K, L] table of
+    every client's leaf pointers (built natively by fjhost.gather_rows)."""
+
+    __slots__ = ("row0", "ptrs")
+
+    def __init__(self, row0: List[torch.Tensor], ptrs: np.ndarray):
+        self.row0, self.ptrs = row0, ptrs
+
+    def __len__(self):
+        return self.ptrs.shape[0]
+
+    def __getitem__(self, k):
+        """``rows[0]`` is client 0's leaves in both representations; other clients exist
+        only as pointers (:func:`_ptr_table`)."""
+        if k != 0:
+            raise TypeError("a _Table holds client 0's leaves only; use _ptr_table for the others")
+        return self.row0
+
+
+def _ptr_table(rows, dtype=np.int64) -> np.ndarray:
+    """[K, L] leaf pointers of rows (a _Table or K lists of leaves)."""
+    if isinstance(rows, _Table):
+        return rows.ptrs if dtype == np.int64 else rows.ptrs.astype(dtype)
+    return np.array([[x.data_ptr() for x in r] for r in rows], dtype=dtype)
+
+
+class _Weights:
+    """Weights that were all Python numbers, packed by fjhost.fold_weights: float32 and
+    int32 vectors, their weak-type kinds, and W summed as tree_util.py:86,95 does."""
+
+    __slots__ = ("f32", "i32", "kinds", "total")
+
+    def __init__(self, f32, i32, kinds, total):
+        self.f32, self.i32, self.kinds, self.total = f32, i32, kinds, total
+
+
+def _pack_weights(weights: List[Any]) -> Optional[_Weights]:
+    """_Weights of ``weights`` when they are all Python int / float, else None."""
+    K = len(weights)
+    f32, i32 = np.empty(K, dtype=np.float32), np.empty(K, dtype=np.int32)
+    got = _lib.host().fold_weights(weights, f32, i32)
+    if got is None:
+        return None
+    total, bits = got
+    kinds = ([_WEAK_FLOAT] if bits & 1 else []) + ([_WEAK_INT] if bits & 2 else [])
+    return _Weights(f32, i32, kinds, total)
+
+
+def _client_table(trees: Sequence[PyTree]):
+    """(treedef, rows) like :func:`_client_rows`; rows is a :class:`_Table` when every
+    client's leaves are already contiguous device tensors of client 0's dtypes and
+    shapes on client 0's device (the common case, checked natively), else lists."""
+    leaves0, td = pytree.flatten(trees[0])
+    device = _find_device(leaves0)
+    idx = _device_index(device)
+    row0 = [_device_leaf(x, device, idx) for x in leaves0]
+    spec = pytree.native_spec(td) if row0 else None
+    if spec is not None:
+        ptrs = np.empty((len(trees), len(row0)), dtype=np.int64)
+        if _lib.host().gather_rows(trees if type(trees) is list else list(trees), 1, spec, row0, idx, ptrs) == 0:
+            return td, _Table(row0, ptrs)
+    return _client_rows(trees, (leaves0, td, row0))
+
+
 def _check_row(k: int, row: List[torch.Tensor], sig0) -> None:
     for l, x in enumerate(row):
         if x.size() != sig0[l][0]:
@@ -261,14 +349,19 @@ def _check_row(k: int, row: List[torch.Tensor], sig0) -> None:
             raise TypeError(f"leaf {l}: client {k} has dtype {x.dtype}, client 0 has {sig0[l][1]}")
 
 
-def _client_rows(trees: Sequence[PyTree]) -> Tuple[pytree.TreeDef, List[List[torch.Tensor]]]:
+def _client_rows(trees: Sequence[PyTree], first=None) -> Tuple[pytree.TreeDef, List[List[torch.Tensor]]]:
     """Flatten every client's pytree into canonical device leaves, checking that all
-    clients match client 0's structure, leaf shapes and dtypes (what _fold assumes)."""
-    leaves0, td = pytree.flatten(trees[0])
-    device = _find_device(leaves0)
-    idx = _device_index(device)
+    clients match client 0's structure, leaf shapes and dtypes (what _fold assumes).
+    ``first``: (leaves, treedef, canonical leaves) of client 0 when already computed."""
     dl, T, flat = _device_leaf, torch.Tensor, pytree.flatten_as
-    row0 = [dl(x, device, idx) for x in leaves0]
+    if first is None:
+        leaves0, td = pytree.flatten(trees[0])
+        device = _find_device(leaves0)
+        row0 = [dl(x, device, _device_index(device)) for x in leaves0]
+    else:
+        leaves0, td, row0 = first
+        device = row0[0].device if row0 else _find_device(leaves0)
+    idx = _device_index(device)
     rows = [row0]
     dt0 = [x.dtype for x in row0]
     sz0 = [x.size() for x in row0]
@@ -326,10 +419,28 @@ def tree_sum(pytrees: Iterable[PyTree]) -> PyTree:
     trees = list(pytrees)
     if not trees:
         return None
-    td, rows = _client_rows(trees)
+    td, rows = _client_table(trees)
     if not rows[0]:
         return pytree.unflatten(td, [])
     return pytree.unflatten(td, _fold(rows, [1] * len(trees), validated=True))
+
+
+def _collect_pairs(pairs):
+    """Consume (tree, weight) pairs once: (trees, weights, W) with W summed as
+    tree_util.py:86,95 (a Python float from 0.0; numpy scalars keep their type).
+    ``weights`` is a :class:`_Weights` when every weight is a Python number."""
+    trees, weights = [], []
+    for tree, weight in pairs:
+        trees.append(tree)
+        weights.append(weight)
+    packed = _pack_weights(weights) if trees else None
+    if packed is not None:
+        return trees, packed, packed.total
+    sum_weight = 0.0
+    for i, w in enumerate(weights):
+        w = weights[i] = _host_weight(w)
+        sum_weight += w  # tree_util.py:95
+    return trees, weights, sum_weight
 
 
 def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
@@ -339,16 +450,10 @@ def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
     is bitwise equal to the reference's sequential jit fold for float32 leaves.
     The iterable is consumed once (it may be a generator, compression.py:191).
     """
-    trees, weights = [], []
-    sum_weight = 0.0
-    for tree, weight in pytrees_and_weights:
-        w = _host_weight(weight)
-        trees.append(tree)
-        weights.append(w)
-        sum_weight += w  # tree_util.py:95 (Python float; numpy scalars keep their type)
+    trees, weights, sum_weight = _collect_pairs(pytrees_and_weights)
     if not trees:
         return None  # tree_util.py:96 maps over None
-    td, rows = _client_rows(trees)
+    td, rows = _client_table(trees)
     if not rows[0]:
         return pytree.unflatten(td, [])
     inv = _inverse(sum_weight)
@@ -363,16 +468,10 @@ def tree_mean_with_l2_norms(pytrees_and_weights: Iterable[Tuple[PyTree, float]])
     The mean is bitwise :func:`tree_mean`'s. The norms (float32 [K] on the device) sum
     squares in f32 in a fixed order; float leaves of one dtype.
     Returns ``(None, None)`` for no clients."""
-    trees, weights = [], []
-    sum_weight = 0.0
-    for tree, weight in pytrees_and_weights:
-        w = _host_weight(weight)
-        trees.append(tree)
-        weights.append(w)
-        sum_weight += w  # tree_util.py:95
+    trees, weights, sum_weight = _collect_pairs(pytrees_and_weights)
     if not trees:
         return None, None
-    td, rows = _client_rows(trees)
+    td, rows = _client_table(trees)
     if not rows[0]:
         return pytree.unflatten(td, []), torch.zeros(len(trees), dtype=torch.float32, device=_default_device())
     l2sq = torch.empty(len(trees), dtype=torch.float32, device=rows[0][0].device)

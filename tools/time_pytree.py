@@ -82,11 +82,32 @@ def main(K=128, reps=20):
         st = server.fused_tree_mean_update(pairs, opt, params, st)
     torch.cuda.synchronize()
     wall_opt = (time.perf_counter() - t0) / reps
+    # the reference surface: mean_aggregator().apply over (client_id, delta, weight) triples
+    agg = fedjax_amd.aggregators.mean_aggregator()
+    state = agg.init()
+    triples = [(f"c{k}", c, w) for k, (c, w) in enumerate(pairs)]
+    for _ in range(3):
+        agg.apply(triples, state)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        agg.apply(triples, state)
+    torch.cuda.synchronize()
+    wall_apply = (time.perf_counter() - t0) / reps
+    # host cost per call: time to issue `reps` calls with the GPU idle at the start
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tu.tree_mean(pairs)
+    host = (time.perf_counter() - t0) / reps
+    torch.cuda.synchronize()
     nbytes = K * P * 4
     print(json.dumps({"workload": "configs[1] 128 x EMNIST-CNN (1,206,590 params, 8 leaves)",
                       "tree_mean_with_l2_norms_wall_ms": round(wall_l2 * 1e3, 4),
                       "fused_tree_mean_adam_wall_ms": round(wall_opt * 1e3, 4),
                       "tree_mean_wall_ms": round(wall * 1e3, 4),
+                      "tree_mean_host_issue_ms": round(host * 1e3, 4),
+                      "mean_aggregator_apply_wall_ms": round(wall_apply * 1e3, 4),
                       "tree_mean_wall_GBs": round(nbytes / wall / 1e9, 1),
                       "tree_mean_gpu_ms_median": round(float(np.median(ks)), 4),
                       "tree_mean_gpu_GBs": round(nbytes / (np.median(ks) / 1e3) / 1e9, 1),
