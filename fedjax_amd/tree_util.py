@@ -232,7 +232,7 @@ def _fold(rows, weights, *, scale=None,
             in_ptrs = np.array([[rows[k][l].data_ptr() for l in ls] for k in range(K)], dtype=np.int64)
         out_ptrs = np.array([outs[l].data_ptr() for l in ls], dtype=np.int64)
         unaligned = bool((in_ptrs % 16).any() or (out_ptrs % 16).any())
-        blocks = _ptrs_plan(in_c, leaf_n, unaligned)
+        blocks = _ptrs_plan(in_c, leaf_n, unaligned, device)
         if packed is not None:
             w_host = packed.f32 if acc_c == _lib.F32 else packed.i32
         elif acc_c == _lib.F32:
@@ -265,8 +265,8 @@ def _fold(rows, weights, *, scale=None,
 _PLANS = {}  # (in dtype, leaf sizes, unaligned) -> workgroup table (the device is fixed per process)
 
 
-def _ptrs_plan(in_c: int, leaf_n: np.ndarray, unaligned: bool) -> np.ndarray:
-    key = (in_c, leaf_n.tobytes(), unaligned, torch.cuda.current_device())
+def _ptrs_plan(in_c: int, leaf_n: np.ndarray, unaligned: bool, device: torch.device) -> np.ndarray:
+    key = (in_c, leaf_n.tobytes(), unaligned, device)
     blocks = _PLANS.get(key)
     if blocks is None:
         blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)
