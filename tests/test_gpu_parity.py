@@ -631,3 +631,58 @@ def test_fused_tree_server_update_matches_restated_optax(make, offset, cuda, cor
     assert state["count"] == 3
     with pytest.raises(ValueError):
         server.fused_tree_mean_update(zip(clients, wi), opt, {"a": params["a"]}, state)
+
+
+# ---------------------------------------------------- native host helper (_fjhost)
+def test_native_table_path_is_taken_and_bitwise_equal_to_python_path(cuda, coracle, monkeypatch):
+    """Device-resident clients go through fjhost.gather_rows (a _Table) and give the same
+    bits as the Python per-leaf path (forced by declining the native walk)."""
+    rng = np.random.RandomState(5)
+    shapes = {"conv": {"b": (32,), "w": (3, 3, 1, 32)}, "dense": [(9216, 16), (62,)], "none": None}
+    K = 37
+
+    def make():
+        return {"conv": {k: torch.from_numpy(rng.uniform(-1, 1, s).astype(np.float32)).to(cuda)
+                         for k, s in shapes["conv"].items()},
+                "dense": [torch.from_numpy(rng.uniform(-1, 1, s).astype(np.float32)).to(cuda)
+                          for s in shapes["dense"]], "none": None}
+
+    trees = [make() for _ in range(K)]
+    weights = [int(w) for w in rng.randint(1, 500, K)]
+    _, rows = tu._client_table(trees)
+    assert isinstance(rows, tu._Table)
+    fast = tu.tree_mean(zip(trees, weights))
+    fast_l2, norms = tu.tree_mean_with_l2_norms(zip(trees, weights))
+    monkeypatch.setattr(tu.pytree, "native_spec", lambda td: None)
+    assert isinstance(tu._client_table(trees)[1], list)
+    slow = tu.tree_mean(zip(trees, weights))
+    for a, b, c in zip(tu.pytree.leaves_of(fast), tu.pytree.leaves_of(slow), tu.pytree.leaves_of(fast_l2)):
+        assert np.array_equal(bits(host(a)), bits(host(b))) and np.array_equal(bits(host(a)), bits(host(c)))
+    want = ref.tree_mean([(tu.pytree.leaves_of(jax_free(t)), w) for t, w in zip(trees, weights)])
+    for a, b in zip(tu.pytree.leaves_of(fast), want):
+        assert np.array_equal(bits(host(a)), bits(b))
+
+
+def jax_free(tree):
+    """Host numpy copy of a device pytree (the oracle's input)."""
+    return tu.pytree.unflatten(tu.pytree.flatten(tree)[1], [host(x) for x in tu.pytree.leaves_of(tree)])
+
+
+def test_native_table_declines_mixed_clients(cuda):
+    """A client whose leaf is on the host, of another dtype, or non-contiguous goes through
+    the Python path (copied / canonicalised / rejected exactly as before)."""
+    base = [{"a": torch.full((4, 4), float(k), device=cuda), "b": torch.ones(3, device=cuda)} for k in range(4)]
+    mixed = [dict(t) for t in base]
+    mixed[2]["a"] = mixed[2]["a"].cpu()               # host leaf: copied
+    mixed[3]["a"] = mixed[3]["a"].t().contiguous().t()  # non-contiguous view: made contiguous
+    assert isinstance(tu._client_table(mixed)[1], list)
+    got = tu.tree_mean(zip(mixed, [1, 2, 3, 4]))
+    want = tu.tree_mean(zip(base, [1, 2, 3, 4]))
+    assert torch.equal(got["a"], want["a"]) and torch.equal(got["b"], want["b"])
+    bad = [dict(t) for t in base]
+    bad[1]["b"] = torch.ones(4, device=cuda)
+    with pytest.raises(ValueError):
+        tu.tree_mean(zip(bad, [1, 1, 1, 1]))
+    bad[1]["b"] = torch.ones(3, dtype=torch.bfloat16, device=cuda)
+    with pytest.raises(TypeError):
+        tu.tree_mean(zip(bad, [1, 1, 1, 1]))
