@@ -36,7 +36,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-BUCKET_CANDIDATES = (1, 2, 4, 8)  # N>1 auto-tune: 1 = no overlap; more = shorter exposed reduce tail
+# N>1 auto-tune: 1 = no overlap; more = shorter exposed reduce tail; tapered relative sizes
+# (fd.bucket_edges) hide each reduce behind the next, smaller fold and expose only the last
+BUCKET_CANDIDATES = (1, 2, 4, 8, (3, 1), (7, 1), (4, 2, 1), (8, 4, 2, 1))
 METRIC = "device-resident aggregated client-delta GB/s, K clients × P fp32 params"
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 WORKLOADS = {  # name: (clients, params, dtype, description)
@@ -108,9 +110,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
-    ap.add_argument("--buckets", type=int, default=0,
-                    help="N>1: parameter buckets of the fold/reduce pipeline; 0 = pick the fastest of "
-                         "BUCKET_CANDIDATES during warmup (max over ranks)")
+    ap.add_argument("--buckets", default="0",
+                    help="N>1: parameter buckets of the fold/reduce pipeline, a count or relative sizes "
+                         "like 4:2:1; 0 = pick the fastest of BUCKET_CANDIDATES during warmup (max over ranks)")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=-1, help="-1 auto, 0 off, 1 on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -218,7 +220,8 @@ def main():
                 raise
             log(f"native RCCL communicator unavailable ({e}); using torch.distributed")
     engine = "native" if comm is not None else "torch"
-    buckets = args.buckets or 1
+    buckets = (tuple(float(v) for v in args.buckets.split(":")) if ":" in args.buckets
+               else int(args.buckets)) or 1
     root = 0
 
     def step(events=None):
@@ -239,14 +242,14 @@ def main():
         elif not sharded:
             fold(x, wd, out, events)
         elif engine == "native":
-            evs = None
+            evs, spans = None, fd.bucket_edges(P, buckets)
             if events is not None:
-                evs = [kernels.Event() for _ in range(2 * buckets)]
+                evs = [kernels.Event() for _ in range(2 * len(spans))]
             fd.sharded_weighted_mean(x, wd, W, buckets=buckets, out=out, all_ranks=args.all_ranks, comm=comm,
                                      nontemporal=nt, fold_events=evs)
             if evs is not None:
-                for (p0, p1), i in zip(fd.bucket_edges(P, buckets), range(0, 2 * buckets, 2)):
-                    events.append((evs[i], evs[i + 1], Kl * (p1 - p0) * esize))
+                for i, (p0, p1) in enumerate(spans):
+                    events.append((evs[2 * i], evs[2 * i + 1], Kl * (p1 - p0) * esize))
         else:
             fd.sharded_weighted_mean(x, wd, W, buckets=buckets, out=out, all_ranks=args.all_ranks,
                                      partial_fn=lambda xs, wdd, sc, o: fold(xs, wdd, o, events))
@@ -267,20 +270,20 @@ def main():
         return float(t.item())
 
     tune = {}
-    if sharded and args.buckets == 0:
+    if sharded and args.buckets == "0":
         # every rank measures every candidate and sees the same max-over-ranks times,
         # so all ranks pick the same (engine, buckets) without another exchange
         engines = ["native", "torch"] if comm is not None and args.engine == "auto" else [engine]
         for eng in engines:
             for b in BUCKET_CANDIDATES:
-                if P // b < fd.BUCKET_ALIGN:
-                    continue
+                if len(fd.bucket_edges(P, b)) < (b if isinstance(b, int) else len(b)):
+                    continue  # P too small for that many aligned buckets
                 engine, buckets = eng, b
                 wall(2)
-                tune[f"{eng}/{b}"] = wall(5) / 5 * 1e3
-        best = min(tune, key=tune.get)
-        engine, buckets = best.split("/")[0], int(best.split("/")[1])
-        log(f"exchange auto-tune (ms/step, max over ranks): {tune} -> {best}")
+                tune[(eng, b)] = wall(5) / 5 * 1e3
+        engine, buckets = min(tune, key=tune.get)
+        tune = {f"{e}/{fd.bucket_name(b)}": t for (e, b), t in tune.items()}
+        log(f"exchange auto-tune (ms/step, max over ranks): {tune} -> {engine}/{fd.bucket_name(buckets)}")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -343,7 +346,8 @@ def main():
                            f" + {'RCCL' if args.backend == 'nccl' else args.backend} "
                            f"{'all_reduce' if args.all_ranks else 'reduce'}" if sharded else "") + (
                            " (REHEARSAL: one GPU runs rank 0's share, RCCL world 1)" if nshard != world else ""),
-                       "buckets": buckets if sharded else 1,
+                       "buckets": (buckets if isinstance(buckets, int) else fd.bucket_name(buckets))
+                       if sharded else 1,
                        "exchange_engine": engine if sharded else None,
                        "exchange_autotune_ms": {k: round(t, 4) for k, t in tune.items()} or None,
                        "nontemporal": nt,

@@ -82,6 +82,8 @@ _SIGNATURES = {
     "fjcomm_destroy": (_i32, [_vp]),
     "fjcomm_sharded_wsum_dense": (_i32, [_vp, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _i32, _i32, _i32, _vp,
                                          _vp]),
+    "fjcomm_sharded_wsum_dense_edges": (_i32, [_vp, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i32, _i32,
+                                               _i32, _vp, _vp]),
     "fjagg_event_create": (_i32, [_vp]),
     "fjagg_event_destroy": (_i32, [_vp]),
     "fjagg_event_record": (_i32, [_vp, _vp]),

@@ -299,7 +299,7 @@ struct OptEpi {
 // wave-uniform base address of client k. Clients are folded in order 0..K-1.
 // The output of the unit at input byte offset off is at obase + off / sizeof(IN) *
 // sizeof(OUT) (same element index); valid[j] == false skips unit j's store.
-template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, class RowFn,
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, bool BURST = true, class RowFn,
           class NORM = NoNorm, class EPI = PlainEpi>
 __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
                                      const uint32_t (&off)[E],
@@ -338,14 +338,31 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
     }
   }
   int64_t k = 1;
+  // Row bases of the next group are fetched while this group's loads are in flight:
+  // on the pytree path row(k) is a scalar load from the pointer table, and fetching
+  // it at the top of each group would leave the vector memory pipe idle for that
+  // latency once per group. Clamped to K-1 so the table is never read past its end.
+  const uint8_t* nxt[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) nxt[u] = row(k + u < K ? k + u : K - 1);
   for (; k + U <= K; k += U) {
     Raw v[U][E];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const auto r = row_rsrc(row(k + u), row_bytes);
+      const auto r = row_rsrc(nxt[u], row_bytes);
 #pragma unroll
       for (int j = 0; j < E; ++j) v[u][j] = load_unit<IN, V, NT>(r, off[j]);
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t kn = k + U + u;
+      nxt[u] = row(kn < K ? kn : K - 1);
+    }
+    // BURST (default): every load of the group is issued before the first is consumed
+    // (E*U in flight per lane); otherwise the scheduler interleaves loads and folds. Burst
+    // is faster with one workgroup per CU, interleaved with two or more full tiles per CU
+    // (k_dense picks per launch, launch_dense_v).
+    if constexpr (BURST) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const T wk = w[k + u];
@@ -399,7 +416,7 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
 // blockIdx.y selects a client range [y*kchunk, min(K, (y+1)*kchunk)) and writes to
 // out + y*out_ystride_bytes (FJAGG_MODE_SPLIT); exact mode has gridDim.y == 1.
 // MINW > 0 asks for MINW waves per SIMD (caps VGPRs: 8 -> 64 registers).
-template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW>
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW, bool BURST = false>
 __global__ __launch_bounds__(kThreads, MINW) void k_dense(
     const uint8_t* __restrict__ x, int64_t ld_bytes, int64_t K, int64_t nunits, int tail_n,
     const typename ACC::T* __restrict__ w, float scale, int do_scale, int accumulate,
@@ -439,8 +456,8 @@ __global__ __launch_bounds__(kThreads, MINW) void k_dense(
       if (!valid[j]) u = u_end - 1;  // keep the load in bounds; the store is skipped
       off[j] = (uint32_t)(u * (V * IB));
     }
-    fold<IN, ACC, OUT, V, E, U, NT>(row, row_bytes, kn, off, ob, valid, wb, do_scale != 0,
-                                    scale, accumulate != 0);
+    fold<IN, ACC, OUT, V, E, U, NT, BURST>(row, row_bytes, kn, off, ob, valid, wb, do_scale != 0,
+                                           scale, accumulate != 0);
   }
 }
 
@@ -915,9 +932,9 @@ void balanced_grid(const Residency& r, int64_t nunits, int64_t tile, int64_t gy,
   *nblk_out = (nunits + S - 1) / S;
 }
 
-template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW>
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW, bool BURST = false>
 void launch_dense_t(const DenseArgs& a, int64_t gy, hipStream_t s) {
-  auto kern = k_dense<IN, ACC, OUT, V, E, U, NT, MINW>;
+  auto kern = k_dense<IN, ACC, OUT, V, E, U, NT, MINW, BURST>;
   const int64_t tile = (int64_t)kThreads * E;
   const int64_t ntiles = (a.nunits + tile - 1) / tile;
   int64_t nblk = ntiles, S = tile;
@@ -940,7 +957,8 @@ struct VariantShape {
 constexpr VariantShape kVariants[] = {{0, 0, 0},  {2, 8, 0},  {1, 8, 0},  {1, 16, 0},
                                       {2, 16, 0}, {4, 4, 0},  {4, 8, 0},  {1, 32, 0},
                                       {2, 8, 8},  {2, 4, 8},  {1, 16, 8}, {4, 4, 4},
-                                      {8, 4, 0},  {8, 8, 0},  {4, 16, 0}, {4, 12, 0}};
+                                      {8, 4, 0},  {8, 8, 0},  {4, 16, 0}, {4, 12, 0},
+                                      {8, 4, 0} /* 16: E8U4 burst */, {8, 4, 0} /* 17: E8U4 interleaved */};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 // Default shape: E=8 x U=4 (8 units = 128 B per lane per client, 4 clients = 32
@@ -953,7 +971,7 @@ int pick_variant(int64_t nunits, int64_t K) {
   // up to 1 Mi f32 per row the balanced E=8 grid leaves most lanes of its single
   // workgroup per CU masked (4.6-4.9 TB/s at 512 Ki); E=4 x U=4 streams at 6.6-7.1
   // (profiles/r01n_sweep.jsonl: the per-bucket shapes of the sharded pipeline)
-  if (nunits <= 262144) return 5;  // E=4 x U=4
+  if (nunits < 262144) return 5;  // E=4 x U=4 (at 1 Mi, burst E=8: profiles/r01s_probe_bucket.jsonl)
   return 12;                       // E=8 x U=4
 }
 
@@ -975,7 +993,20 @@ int launch_dense_v(int variant, const DenseArgs& a, int64_t gy, hipStream_t s) {
       case 9: launch_dense_t<IN, ACC, OUT, V, 2, 4, NT, 8>(a, gy, s); break;
       case 10: launch_dense_t<IN, ACC, OUT, V, 1, 16, NT, 8>(a, gy, s); break;
       case 11: launch_dense_t<IN, ACC, OUT, V, 4, 4, NT, 4>(a, gy, s); break;
-      case 12: launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0>(a, gy, s); break;
+      case 12: {
+        // Interleaved schedule when the balanced grid has >= 2 full E=8 tiles per CU
+        // (several workgroups per CU hide latency), burst below that (one workgroup
+        // per CU needs every load of a group in flight): profiles/r01s_probe_bucket.jsonl.
+        const int64_t ntiles = (a.nunits + (int64_t)kThreads * 8 - 1) / ((int64_t)kThreads * 8);
+        const int cus = residency(reinterpret_cast<const void*>(k_dense<IN, ACC, OUT, V, 8, 4, NT, 0>)).cus;
+        if (!a.balanced || ntiles * gy >= 2 * (int64_t)cus)
+          launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0>(a, gy, s);
+        else
+          launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0, true>(a, gy, s);
+        break;
+      }
+      case 16: launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0, true>(a, gy, s); break;
+      case 17: launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0>(a, gy, s); break;
       case 13: launch_dense_t<IN, ACC, OUT, V, 8, 8, NT, 0>(a, gy, s); break;
       case 14: launch_dense_t<IN, ACC, OUT, V, 4, 16, NT, 0>(a, gy, s); break;
       case 15: launch_dense_t<IN, ACC, OUT, V, 4, 12, NT, 0>(a, gy, s); break;

@@ -164,6 +164,27 @@ int fjcomm_sharded_wsum_dense(void* comm, int in_dtype, const void* x_dev, int64
                               int64_t P, const void* w_dev, float scale, float* out_dev,
                               int nbuckets, int root, int flags, void* stream, void* const* fold_events) {
   fjagg_g_err[0] = 0;
+  if (nbuckets < 1 || nbuckets > FJCOMM_MAX_BUCKETS)
+    return fail(FJAGG_EINVAL, "nbuckets must be in [1, %d]", FJCOMM_MAX_BUCKETS);
+  if (P <= 0)  // nothing to cut; the edges variant validates the rest
+    return fjcomm_sharded_wsum_dense_edges(comm, in_dtype, x_dev, ld, K, P, w_dev, scale, out_dev, nullptr, 1,
+                                           root, flags, stream, fold_events);
+  // equal buckets of a multiple of FJCOMM_BUCKET_ALIGN elements (the last one shorter)
+  int64_t step = (P + nbuckets - 1) / nbuckets;
+  step = (step + FJCOMM_BUCKET_ALIGN - 1) / FJCOMM_BUCKET_ALIGN * FJCOMM_BUCKET_ALIGN;
+  const int nb = (int)((P + step - 1) / step);
+  int64_t edges[FJCOMM_MAX_BUCKETS + 1];
+  for (int b = 0; b < nb; ++b) edges[b] = b * step;
+  edges[nb] = P;
+  return fjcomm_sharded_wsum_dense_edges(comm, in_dtype, x_dev, ld, K, P, w_dev, scale, out_dev, edges, nb, root,
+                                         flags, stream, fold_events);
+}
+
+int fjcomm_sharded_wsum_dense_edges(void* comm, int in_dtype, const void* x_dev, int64_t ld, int64_t K,
+                                    int64_t P, const void* w_dev, float scale, float* out_dev,
+                                    const int64_t* edges, int nbuckets, int root, int flags, void* stream,
+                                    void* const* fold_events) {
+  fjagg_g_err[0] = 0;
   Comm* c = reinterpret_cast<Comm*>(comm);
   if (!c || !c->nc) return fail(FJAGG_EINVAL, "not an initialised communicator");
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16) return fail(FJAGG_EINVAL, "in_dtype must be F32 or BF16");
@@ -172,18 +193,24 @@ int fjcomm_sharded_wsum_dense(void* comm, int in_dtype, const void* x_dev, int64
     return fail(FJAGG_EINVAL, "nbuckets must be in [1, %d]", FJCOMM_MAX_BUCKETS);
   if (root >= c->nranks) return fail(FJAGG_EINVAL, "root %d >= nranks %d", root, c->nranks);
   if (P == 0) return FJAGG_OK;
+  if (!edges) return fail(FJAGG_EINVAL, "null edges");
+  if (edges[0] != 0 || edges[nbuckets] != P)
+    return fail(FJAGG_EINVAL, "edges must run from 0 to P = %lld", (long long)P);
+  for (int b = 0; b < nbuckets; ++b) {
+    if (edges[b + 1] <= edges[b]) return fail(FJAGG_EINVAL, "edges must increase strictly (bucket %d)", b);
+    if (edges[b] % FJCOMM_BUCKET_ALIGN)
+      return fail(FJAGG_EINVAL, "edge %lld is not a multiple of %d elements", (long long)edges[b],
+                  FJCOMM_BUCKET_ALIGN);
+  }
   if (!out_dev || (K > 0 && (!x_dev || !w_dev))) return fail(FJAGG_EINVAL, "null pointer argument");
   if (flags & ~(FJAGG_NONTEMPORAL | FJAGG_VARIANT(0xff)))
     return fail(FJAGG_EINVAL, "flags may hold FJAGG_NONTEMPORAL and FJAGG_VARIANT bits only");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t esz = in_dtype == FJAGG_BF16 ? 2 : 4;
-  // buckets: multiples of 1024 elements, so every bucket keeps the rows' 16-byte alignment
-  int64_t step = (P + nbuckets - 1) / nbuckets;
-  step = (step + 1023) / 1024 * 1024;
-  const int nb = (int)((P + step - 1) / step);
+  const int nb = nbuckets;
   for (int b = 0; b < nb; ++b) {
-    const int64_t p0 = b * step;
-    const int64_t n = P - p0 < step ? P - p0 : step;
+    const int64_t p0 = edges[b];
+    const int64_t n = edges[b + 1] - p0;
     float* seg = out_dev + p0;
     if (fold_events) {
       if (hipError_t e = hipEventRecord(reinterpret_cast<hipEvent_t>(fold_events[2 * b]), s))

@@ -324,6 +324,7 @@ __global__ __launch_bounds__(256) void k_stats_combine(const fjcomp_row* __restr
 
 // ------------------------------------------------------------------ quantize + fold
 constexpr int kQThreads = 256;
+constexpr int kQGroup = 4;  // clients whose deltas k_quant_fold loads one group ahead
 constexpr int kHistLdsBins = 4096;
 
 struct UniformQ {
@@ -426,7 +427,16 @@ __global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* 
   const int64_t n = leaf_n[l], h = (n + 1) >> 1;
   const int64_t i = (b - prefix[l]) * kQThreads + threadIdx.x;
   const bool valid = i < h, second = i + h < n;
-  float* __restrict__ out = out_ptrs[l];
+  // Offsets every lane loads unconditionally (masked lanes re-read an element of the
+  // leaf): no branch around the loads, so waiting for one group's deltas never waits
+  // for the next group's as well.
+  const int64_t ia = valid ? i : 0, ib = second ? i + h : ia;
+  // Pointers read from the tables are generic: cast to the global address space, so
+  // that loads are global_load. A FLAT load may also touch LDS, so while one is pending
+  // the compiler waits with vmcnt(0) and that would drain the next group's loads too.
+  typedef __attribute__((address_space(1))) const float GFloat;
+  typedef __attribute__((address_space(1))) float GFloatOut;
+  GFloatOut* out = (GFloatOut*)out_ptrs[l];
   const bool accumulate = flags & FJAGG_ACCUMULATE;
   float s0 = 0.0f, s1 = 0.0f;
   if (valid && accumulate) {
@@ -435,47 +445,76 @@ __global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* 
   }
   __shared__ int32_t sh[HIST ? kHistLdsBins : 1];
   const bool lds_hist = HIST && nbins <= kHistLdsBins;
-  for (int64_t k = 0; k < K; ++k) {
-    const int64_t row = k * L + l;
-    const float* __restrict__ x = in_ptrs[row];
-    const uint32_t k0 = keys[2 * row], k1 = keys[2 * row + 1];
-    const fjcomp_qparams p = qps[row];
-    const float wk = w[k];
-    float lv0 = -1.0f, lv1 = -1.0f;
-    if (valid) {
-      const float v0 = x[i];
-      const float v1 = second ? x[i + h] : 0.0f;
-      uint32_t c0 = (uint32_t)i, c1 = (uint32_t)(second ? i + h : 0);
-      threefry(k0, k1, c0, c1);
-      const float q0 = quant(v0, bits_to_unit(c0), p, &lv0);
-      const float t0 = q0 * wk;
-      s0 = (k == 0 && !accumulate) ? t0 : s0 + t0;
-      if (second) {
-        const float q1 = quant(v1, bits_to_unit(c1), p, &lv1);
-        const float t1 = q1 * wk;
-        s1 = (k == 0 && !accumulate) ? t1 : s1 + t1;
-      }
+  // A lane walks all K clients, so one dependent HBM round trip per client would bound
+  // the kernel. The deltas of the next kQGroup clients are loaded before this group's
+  // threefry draws and quantizers run, which hide their latency. Fold order unchanged.
+  constexpr int G = kQGroup;
+  auto fetch = [&](int64_t kg, float (&a)[G], float (&c)[G]) {
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int64_t k = kg + u < K ? kg + u : K - 1;
+      const GFloat* x = (const GFloat*)in_ptrs[k * L + l];
+      a[u] = x[ia];
+      c[u] = x[ib];
     }
-    if constexpr (HIST) {
-      int32_t* __restrict__ hrow = hist + row * nbins;
-      const int top = nbins - 1;
-      auto bin = [&](float lv) { return (lv >= 0.0f && lv < (float)top) ? (int)lv : top; };
-      if (lds_hist) {
-        for (int e = threadIdx.x; e < nbins; e += kQThreads) sh[e] = 0;
-        __syncthreads();
-        if (valid) {
-          atomicAdd(&sh[bin(lv0)], 1);
-          if (second) atomicAdd(&sh[bin(lv1)], 1);
+  };
+  // fold clients kg .. kg+G-1 (those < K) from their loaded deltas a / c
+  auto fold_group = [&](int64_t kg, const float (&a)[G], const float (&c)[G]) {
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int64_t k = kg + u;
+      if (k >= K) break;  // wave-uniform
+      const int64_t row = k * L + l;
+      const uint32_t k0 = keys[2 * row], k1 = keys[2 * row + 1];
+      const fjcomp_qparams p = qps[row];
+      const float wk = w[k];
+      float lv0 = -1.0f, lv1 = -1.0f;
+      if (valid) {
+        const float v0 = a[u];
+        const float v1 = c[u];  // used only when `second`
+        uint32_t c0 = (uint32_t)i, c1 = (uint32_t)(second ? i + h : 0);
+        threefry(k0, k1, c0, c1);
+        const float q0 = quant(v0, bits_to_unit(c0), p, &lv0);
+        const float t0 = q0 * wk;
+        s0 = (k == 0 && !accumulate) ? t0 : s0 + t0;
+        if (second) {
+          const float q1 = quant(v1, bits_to_unit(c1), p, &lv1);
+          const float t1 = q1 * wk;
+          s1 = (k == 0 && !accumulate) ? t1 : s1 + t1;
         }
-        __syncthreads();
-        for (int e = threadIdx.x; e < nbins; e += kQThreads)
-          if (sh[e]) atomicAdd(&hrow[e], sh[e]);
-        __syncthreads();
-      } else if (valid) {
-        atomicAdd(&hrow[bin(lv0)], 1);
-        if (second) atomicAdd(&hrow[bin(lv1)], 1);
+      }
+      if constexpr (HIST) {
+        int32_t* __restrict__ hrow = hist + row * nbins;
+        const int top = nbins - 1;
+        auto bin = [&](float lv) { return (lv >= 0.0f && lv < (float)top) ? (int)lv : top; };
+        if (lds_hist) {
+          for (int e = threadIdx.x; e < nbins; e += kQThreads) sh[e] = 0;
+          __syncthreads();
+          if (valid) {
+            atomicAdd(&sh[bin(lv0)], 1);
+            if (second) atomicAdd(&sh[bin(lv1)], 1);
+          }
+          __syncthreads();
+          for (int e = threadIdx.x; e < nbins; e += kQThreads)
+            if (sh[e]) atomicAdd(&hrow[e], sh[e]);
+          __syncthreads();
+        } else if (valid) {
+          atomicAdd(&hrow[bin(lv0)], 1);
+          if (second) atomicAdd(&hrow[bin(lv1)], 1);
+        }
       }
     }
+  };
+  // Two register sets in turn (no copies between them, which would wait for the loads):
+  // while one group is folded, the next group's loads are in flight.
+  float xa[G], xb[G], ya[G], yb[G];
+  fetch(0, xa, xb);
+  for (int64_t kg = 0; kg < K; kg += 2 * G) {
+    fetch(kg + G, ya, yb);
+    fold_group(kg, xa, xb);
+    if (kg + G >= K) break;  // wave-uniform
+    fetch(kg + 2 * G, xa, xb);
+    fold_group(kg + G, ya, yb);
   }
   if (!valid) return;
   if (flags & FJAGG_SCALE) {

@@ -29,7 +29,7 @@ check it against the per-element bound in DESIGN.md §4.
 from __future__ import annotations
 
 import ctypes
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -48,11 +48,39 @@ def shard_range(num_clients: int, rank: int, world_size: int) -> Tuple[int, int]
     return k0, k0 + base + (1 if rank < extra else 0)
 
 
-def bucket_edges(P: int, buckets: int) -> List[Tuple[int, int]]:
-    buckets = max(1, int(buckets))
-    step = -(-P // buckets)
-    step = max(BUCKET_ALIGN, -(-step // BUCKET_ALIGN) * BUCKET_ALIGN)
-    return [(p0, min(P, p0 + step)) for p0 in range(0, P, step)]
+def bucket_edges(P: int, buckets: Union[int, Sequence[float]]) -> List[Tuple[int, int]]:
+    """Parameter buckets [p0, p1) covering [0, P); every p0 a multiple of BUCKET_ALIGN.
+
+    ``buckets`` is a count (equal buckets) or a sequence of relative sizes, e.g.
+    ``(4, 2, 1)``: a tapered schedule. Each reduce then overlaps the next, smaller
+    fold, and only the small last bucket's reduce is left exposed at the end of the
+    step. Interior edges are rounded to BUCKET_ALIGN; buckets that round away vanish.
+    """
+    if isinstance(buckets, (int, np.integer)):
+        buckets = max(1, int(buckets))
+        step = -(-P // buckets)
+        step = max(BUCKET_ALIGN, -(-step // BUCKET_ALIGN) * BUCKET_ALIGN)
+        return [(p0, min(P, p0 + step)) for p0 in range(0, P, step)]
+    sizes = [float(s) for s in buckets]
+    if not sizes or any(not s > 0 for s in sizes):
+        raise ValueError(f"bucket sizes must be positive, got {tuple(buckets)}")
+    if P <= 0:
+        return []
+    total, acc, edges = sum(sizes), 0.0, [0]
+    for s in sizes[:-1]:
+        acc += s
+        e = int(round(P * acc / total / BUCKET_ALIGN)) * BUCKET_ALIGN
+        if edges[-1] < e < P:
+            edges.append(e)
+    edges.append(P)
+    return list(zip(edges[:-1], edges[1:]))
+
+
+def bucket_name(buckets) -> str:
+    """``4`` -> "4", ``(4, 2, 1)`` -> "4:2:1" (bench labels)."""
+    if isinstance(buckets, (int, np.integer)):
+        return str(int(buckets))
+    return ":".join(f"{s:g}" for s in buckets)
 
 
 def total_weight(local_weights: Sequence, group=None, device=None):
@@ -107,7 +135,7 @@ class RcclCommunicator:
 
 
 def _native_sharded(comm: RcclCommunicator, x_local: torch.Tensor, w_local: torch.Tensor, scale: float,
-                    out: torch.Tensor, root: int, buckets: int, nontemporal: Optional[bool],
+                    out: torch.Tensor, root: int, buckets, nontemporal: Optional[bool],
                     fold_events=None) -> None:
     K, P = x_local.shape
     if x_local.dtype not in (torch.float32, torch.bfloat16):
@@ -120,17 +148,27 @@ def _native_sharded(comm: RcclCommunicator, x_local: torch.Tensor, w_local: torc
         raise ValueError("w_local must be float32 [K_g]")
     nbytes = K * P * x_local.element_size()
     nt = (nbytes >= tree_util.NONTEMPORAL_MIN_BYTES) if nontemporal is None else nontemporal
+    spans = bucket_edges(P, buckets)
+    if not spans:
+        return
+    if len(spans) > _lib.COMM_MAX_BUCKETS:
+        raise ValueError(f"at most {_lib.COMM_MAX_BUCKETS} buckets")
+    edges = np.array([p0 for p0, _ in spans] + [P], dtype=np.int64)
     ev = None
     if fold_events is not None:
+        if len(fold_events) < 2 * len(spans):
+            raise ValueError(f"fold_events needs 2 events per bucket ({2 * len(spans)})")
         ev = (ctypes.c_void_p * len(fold_events))(*[e.handle for e in fold_events])
-    _lib.call("fjcomm_sharded_wsum_dense", comm.handle, kernels.dtype_code(x_local.dtype),
+    _lib.call("fjcomm_sharded_wsum_dense_edges", comm.handle, kernels.dtype_code(x_local.dtype),
               x_local.data_ptr() if K else None, x_local.stride(0) if K else P, K, P,
-              w_local.data_ptr() if K else None, float(np.float32(scale)), out.data_ptr(), int(buckets), int(root),
-              _lib.NONTEMPORAL if nt else 0, torch.cuda.current_stream(out.device).cuda_stream, ev)
+              w_local.data_ptr() if K else None, float(np.float32(scale)), out.data_ptr(), edges.ctypes.data,
+              len(spans), int(root), _lib.NONTEMPORAL if nt else 0, torch.cuda.current_stream(out.device).cuda_stream,
+              ev)
 
 
 def sharded_weighted_mean(x_local: torch.Tensor, w_local: torch.Tensor, W_total, *, group=None,
-                          dst: int = 0, all_ranks: bool = False, buckets: int = 4,
+                          dst: int = 0, all_ranks: bool = False,
+                          buckets: Union[int, Sequence[float]] = 4,
                           out: Optional[torch.Tensor] = None,
                           partial_fn: Optional[Callable] = None,
                           comm: Optional[RcclCommunicator] = None,
@@ -144,9 +182,10 @@ def sharded_weighted_mean(x_local: torch.Tensor, w_local: torch.Tensor, W_total,
     Returns the float32 mean [P] — valid on ``dst`` (every rank with ``all_ranks``).
     partial_fn(x, w, scale, out) computes ``out = fl(sum_k x_k w_k) * scale`` for one
     bucket; the default is the HIP kernel (tests inject the oracle to run on gloo).
+    buckets: a count of equal buckets or relative sizes (:func:`bucket_edges`).
     comm: an :class:`RcclCommunicator` selects the native pipeline (``fjcomm.h``);
-    fold_events then takes 2*buckets :class:`fedjax_amd.kernels.Event` that bracket
-    each bucket's fold on the current stream.
+    fold_events then takes two :class:`fedjax_amd.kernels.Event` per bucket that
+    bracket each bucket's fold on the current stream.
     """
     P = x_local.shape[1]
     scale = float(np.float32(tree_util._inverse(W_total)))

@@ -67,6 +67,20 @@ int fjcomm_sharded_wsum_dense(void* comm, int in_dtype, const void* x_dev, int64
                               int64_t P, const void* w_dev, float scale, float* out_dev,
                               int nbuckets, int root, int flags, void* stream, void* const* fold_events);
 
+/*
+ * The same step over explicit bucket edges: bucket b is elements [edges[b], edges[b+1]),
+ * edges[0] = 0, edges[nbuckets] = P, strictly increasing, every edge but the last a
+ * multiple of FJCOMM_BUCKET_ALIGN elements (keeps the rows' 16-byte alignment). Unequal
+ * buckets let a tapered schedule (e.g. 4:2:1) hide each reduce behind the next, smaller
+ * fold, so only the small last bucket's reduce is exposed at the end of the step.
+ * fjcomm_sharded_wsum_dense is this call with equal buckets.
+ */
+#define FJCOMM_BUCKET_ALIGN 1024
+int fjcomm_sharded_wsum_dense_edges(void* comm, int in_dtype, const void* x_dev, int64_t ld, int64_t K,
+                                    int64_t P, const void* w_dev, float scale, float* out_dev,
+                                    const int64_t* edges, int nbuckets, int root, int flags, void* stream,
+                                    void* const* fold_events);
+
 /* Timing events without the system-scope fence (hipEventDisableSystemFence): recording
  * one costs no cache write-back, so bracketing every launch does not perturb it. */
 int fjagg_event_create(void** ev);

@@ -32,7 +32,7 @@ def _oracle_partial(x, w, scale, out):
     out.copy_(torch.from_numpy(y))
 
 
-def _worker(rank, world, port, all_ranks, q):
+def _worker(rank, world, port, all_ranks, buckets, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -45,19 +45,20 @@ def _worker(rank, world, port, all_ranks, q):
         k0, k1 = fd.shard_range(K, rank, world)
         x = torch.from_numpy(ref.synth(k1 - k0, P, seed=9, k0=k0))
         wl = torch.tensor(np.float32(weights[k0:k1]))
-        out = fd.sharded_weighted_mean(x, wl, W, buckets=3, all_ranks=all_ranks, partial_fn=_oracle_partial)
+        out = fd.sharded_weighted_mean(x, wl, W, buckets=buckets, all_ranks=all_ranks,
+                                       partial_fn=_oracle_partial)
         W2 = fd.total_weight(weights[k0:k1])
         q.put((rank, out.numpy().copy(), W2))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("all_ranks", [False, True])
-def test_sharded_mean_world2_gloo(all_ranks, coracle):
+@pytest.mark.parametrize("all_ranks,buckets", [(False, 3), (True, 3), (False, (4, 2, 1))])
+def test_sharded_mean_world2_gloo(all_ranks, buckets, coracle):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, all_ranks, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, all_ranks, buckets, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (y, W2)) for r, y, W2 in (q.get(timeout=120) for _ in procs))

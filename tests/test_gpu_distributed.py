@@ -90,12 +90,13 @@ def _native_worker(port, q):
         kernels.fill_synth(x, seed=9)
         wl = torch.tensor(np.float32(weights), device=dev)
         res = {}
-        for buckets, all_ranks in ((1, False), (3, False), (7, True)):
-            evs = [kernels.Event() for _ in range(2 * buckets)]
+        for buckets, all_ranks in ((1, False), (3, False), (7, True), ((3, 1), False), ((4, 2, 1), True)):
+            nb = len(fd.bucket_edges(P, buckets))
+            evs = [kernels.Event() for _ in range(2 * nb)]
             y = fd.sharded_weighted_mean(x, wl, W, buckets=buckets, all_ranks=all_ranks, comm=comm,
                                          fold_events=evs)
             torch.cuda.synchronize()
-            ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(0, 2 * buckets, 2)]
+            ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(0, 2 * nb, 2)]
             res[(buckets, all_ranks)] = (y.cpu().numpy(), ms)
         xb = torch.empty(K, P, dtype=torch.bfloat16, device=dev)
         kernels.fill_synth(xb, seed=9)

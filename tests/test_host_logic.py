@@ -114,6 +114,24 @@ def test_bucket_edges_are_aligned_and_cover():
             assert all(p0 % distributed.BUCKET_ALIGN == 0 for p0, _ in e)
 
 
+def test_tapered_bucket_edges():
+    A = distributed.BUCKET_ALIGN
+    P = 4 * 1024 * 1024
+    assert distributed.bucket_edges(P, (4, 2, 1)) == [(0, 2397184), (2397184, 3595264), (3595264, P)]
+    assert distributed.bucket_edges(P, (3, 1)) == [(0, 3 * P // 4), (3 * P // 4, P)]
+    assert distributed.bucket_edges(P, (1, 1)) == distributed.bucket_edges(P, 2)
+    for P in (1, 1000, 5000, 1206590, 4194304):
+        for spec in ((3, 1), (7, 1), (4, 2, 1), (8, 4, 2, 1), (0.5, 0.25)):
+            e = distributed.bucket_edges(P, spec)
+            assert e[0][0] == 0 and e[-1][1] == P and len(e) <= len(spec)
+            assert all(a[1] == b[0] and a[0] < a[1] for a, b in zip(e, e[1:]))
+            assert all(p0 % A == 0 for p0, _ in e)
+    assert distributed.bucket_edges(0, (3, 1)) == []
+    assert distributed.bucket_name((4, 2, 1)) == "4:2:1" and distributed.bucket_name(2) == "2"
+    with pytest.raises(ValueError):
+        distributed.bucket_edges(100, (1, 0))
+
+
 def test_server_descriptor_constants_follow_jax_weak_typing():
     from fedjax_amd import server
     opt = server.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)
