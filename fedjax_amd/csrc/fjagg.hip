@@ -593,7 +593,7 @@ __global__ __launch_bounds__(kThreads) void k_dense_opt(
 // groups of kThreads*8 units (E=8, U=4: the dense default; lanes past the range
 // are masked) when the range gives a lane more than one unit, else in groups of
 // kThreads units (E=1, U=8).
-template <int IN, class ACC, int OUT, int V, bool NT, bool L2 = false>
+template <int IN, class ACC, int OUT, int V, bool NT, bool L2 = false, bool BURST = true>
 __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ img, int L,
                                                    int64_t K,
                                                    const typename ACC::T* __restrict__ w,
@@ -647,7 +647,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
             if (!valid[j]) u = u1 - 1;
             off[j] = (uint32_t)(u * (V * IB));
           }
-          fold<IN, ACC, OUT, V, 8, 4, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm);
+          fold<IN, ACC, OUT, V, 8, 4, NT, BURST>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm);
         }
         done = true;
       }
@@ -1134,11 +1134,20 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
       return check_launch("k_l2_combine");
     }
   }
-  if (nt)
+  // fold schedule as for the dense path (launch_dense_v): interleaved once the plan has
+  // two or more workgroups per CU, burst below that
+  const bool burst = nblk < 2 * (int64_t)residency(reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true>)).cus;
+  if (nt && burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
                        img, L, K, wt, scale, do_scale, accumulate, nullptr);
-  else
+  else if (nt)
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+  else if (burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+  else
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
                        img, L, K, wt, scale, do_scale, accumulate, nullptr);
   return check_launch("k_ptrs");
 }

@@ -103,8 +103,18 @@ def _native_worker(port, q):
         yb = fd.sharded_weighted_mean(xb, wl, W, buckets=2, comm=comm)
         y0 = fd.sharded_weighted_mean(x[:0], wl[:0], W, buckets=2, comm=comm,
                                       out=torch.full((P,), 7.0, device=dev))
+        # explicit edges are validated: unaligned, non-increasing, not ending at P
+        import ctypes
+        from fedjax_amd import _lib
+        errs = []
+        for edges in ([0, 1000, P], [0, 2048, 2048, P], [0, 1024, P - 1]):
+            e = np.array(edges, dtype=np.int64)
+            rc = _lib.load().fjcomm_sharded_wsum_dense_edges(
+                comm.handle, _lib.F32, x.data_ptr(), x.stride(0), K, P, wl.data_ptr(), 1.0, y0.data_ptr(),
+                e.ctypes.data, len(edges) - 1, 0, 0, torch.cuda.current_stream().cuda_stream, None)
+            errs.append((rc, _lib.load().fjagg_last_error().decode()))
         torch.cuda.synchronize()
-        q.put((res, yb.cpu().numpy(), y0.cpu().numpy()))
+        q.put((res, yb.cpu().numpy(), y0.cpu().numpy(), errs))
         comm.close()
     finally:
         dist.destroy_process_group()
@@ -115,7 +125,7 @@ def test_native_rccl_pipeline_world1(cuda, coracle):
     q = ctx.Queue()
     p = ctx.Process(target=_native_worker, args=(_port(), q))
     p.start()
-    res, yb, y0 = q.get(timeout=300)
+    res, yb, y0, errs = q.get(timeout=300)
     p.join(timeout=60)
     assert p.exitcode == 0
     weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
@@ -127,6 +137,7 @@ def test_native_rccl_pipeline_world1(cuda, coracle):
         assert np.array_equal(y.view(np.uint32), want.astype(np.float32).view(np.uint32)), key
         assert all(m > 0 for m in ms), key
     assert np.all(y0 == 0)  # a rank without clients contributes zeros
+    assert all(rc != 0 and msg for rc, msg in errs), errs  # bad bucket edges are refused before any launch
     xb = (coracle.synth_bf16(K, P, seed=9).astype(np.uint32) << 16).view(np.float32)  # bf16 -> f32 exactly
     want_b = coracle.wsum_f32(np.ascontiguousarray(xb), np.float32(weights), scale=r)
     assert np.array_equal(yb.view(np.uint32), want_b.astype(np.float32).view(np.uint32))
