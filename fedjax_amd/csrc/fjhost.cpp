@@ -29,12 +29,24 @@
 //       weight`), kinds = bit 0: some weight is a float, bit 1: some weight is an int.
 //       None when any weight is something else (numpy scalar, tensor, bool, |w| >=
 //       2**53, ...): the caller then uses the Python path.
+//   fold_table(row0, ptrs, w_f32, scale, has_scale, nt_min_bytes, dev_index, stream,
+//              plan_fn, wsum_fn) -> (rc, outputs) | None
+//       The rest of tree_mean's host work for a gathered table (ptrs from gather_rows,
+//       weights from fold_weights) when every leaf is float32 and every pointer is
+//       16-byte aligned: fresh output leaves shaped like row0, the plan image of
+//       include/fjagg.h in pinned memory (workgroup table from fjagg_ptrs_plan), its
+//       stream-ordered upload, and the fjagg_wsum_ptrs launch on `stream` (FJAGG_SCALE if
+//       has_scale, FJAGG_NONTEMPORAL if the clients' bytes reach nt_min_bytes). rc is the
+//       library's status. None (nothing launched) outside that case: the caller's Python
+//       path then handles it.
 
 #include <Python.h>
 
+#include <ATen/ATen.h>
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
+#include <cstring>
 #include <vector>
 
 namespace {
@@ -212,9 +224,93 @@ PyObject* fold_weights(PyObject*, PyObject* args) {
   return result;
 }
 
+// fjagg_ptrs_plan / fjagg_wsum_ptrs of libfjagg.so (include/fjagg.h), passed in by address
+typedef int64_t (*PlanFn)(int, int, const int64_t*, int, int64_t*, int64_t);
+typedef int (*WsumFn)(int, int, int, const int64_t*, int, int64_t, int64_t, const void*, float, int, void*);
+constexpr int kF32 = 0, kScale = 1, kNontemporal = 4;  // fjagg.h enums
+
+PyObject* fold_table(PyObject*, PyObject* args) {
+  PyObject *row0, *ptrs, *wf;
+  double scale, nt_min_bytes;
+  int has_scale, dev;
+  unsigned long long stream, plan_addr, wsum_addr;
+  if (!PyArg_ParseTuple(args, "O!OOdidiKKK", &PyList_Type, &row0, &ptrs, &wf, &scale, &has_scale, &nt_min_bytes,
+                        &dev, &stream, &plan_addr, &wsum_addr))
+    return nullptr;
+  const Py_ssize_t L = PyList_GET_SIZE(row0);
+  Py_buffer bp, bw;
+  if (PyObject_GetBuffer(ptrs, &bp, PyBUF_C_CONTIGUOUS) != 0) return nullptr;
+  if (PyObject_GetBuffer(wf, &bw, PyBUF_C_CONTIGUOUS) != 0) {
+    PyBuffer_Release(&bp);
+    return nullptr;
+  }
+  struct Release {
+    Py_buffer *a, *b;
+    ~Release() {
+      PyBuffer_Release(a);
+      PyBuffer_Release(b);
+    }
+  } release{&bp, &bw};
+  if (L < 1 || bp.len % (8 * L) != 0) Py_RETURN_NONE;
+  const int64_t K = bp.len / (8 * L);
+  if (K < 1 || bw.len < 4 * K) Py_RETURN_NONE;
+  const auto* in = static_cast<const int64_t*>(bp.buf);
+  try {
+    // fast case only: float32 leaves (fold type and output type are then float32 for any
+    // weights), every pointer 16-byte aligned (the vector plan)
+    std::vector<int64_t> leaf_n(L);
+    int64_t orbits = 0, total = 0;
+    for (Py_ssize_t l = 0; l < L; ++l) {
+      const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(row0, l));
+      if (t.scalar_type() != at::kFloat) Py_RETURN_NONE;
+      leaf_n[l] = t.numel();
+      total += leaf_n[l];
+    }
+    for (int64_t i = 0; i < K * L; ++i) orbits |= in[i];
+    std::vector<at::Tensor> outs;
+    outs.reserve(L);
+    for (Py_ssize_t l = 0; l < L; ++l) {
+      const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(row0, l));
+      outs.push_back(at::empty(t.sizes(), t.options()));
+      orbits |= reinterpret_cast<int64_t>(outs.back().data_ptr());
+    }
+    if (orbits & 15) Py_RETURN_NONE;
+    auto plan = reinterpret_cast<PlanFn>(plan_addr);
+    const int64_t nblk = plan(kF32, 0, leaf_n.data(), static_cast<int>(L), nullptr, 0);
+    if (nblk < 0) Py_RETURN_NONE;
+    // plan image (fjagg.h): in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk] | f32 weights
+    const int64_t nw = (K + 1) / 2, n = K * L + 2 * L + 2 * nblk + nw;
+    at::Tensor img = at::empty({n}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+    int64_t* p = img.data_ptr<int64_t>();
+    std::memcpy(p, in, sizeof(int64_t) * K * L);
+    for (Py_ssize_t l = 0; l < L; ++l) {
+      p[K * L + l] = reinterpret_cast<int64_t>(outs[l].data_ptr());
+      p[K * L + L + l] = leaf_n[l];
+    }
+    if (plan(kF32, 0, leaf_n.data(), static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) Py_RETURN_NONE;
+    p[n - 1] = 0;
+    std::memcpy(p + n - nw, bw.buf, 4 * K);
+    at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);
+    const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
+    const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0);
+    const int64_t* dp = dimg.data_ptr<int64_t>();
+    const int rc = reinterpret_cast<WsumFn>(wsum_addr)(kF32, kF32, kF32, dp, static_cast<int>(L), K, nblk,
+                                                       dp + (n - nw), static_cast<float>(scale), flags,
+                                                       reinterpret_cast<void*>(stream));
+    PyObject* list = PyList_New(L);
+    if (!list) return nullptr;
+    for (Py_ssize_t l = 0; l < L; ++l) PyList_SET_ITEM(list, l, THPVariable_Wrap(std::move(outs[l])));
+    return Py_BuildValue("(iN)", rc, list);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 PyMethodDef kMethods[] = {
     {"gather_rows", gather_rows, METH_VARARGS, "pointer table of K client pytrees (see fjhost.cpp)"},
     {"fold_weights", fold_weights, METH_VARARGS, "f32/i32 weights and W of Python-number weights"},
+    {"fold_table", fold_table, METH_VARARGS, "plan image + output leaves + fjagg_wsum_ptrs launch (see fjhost.cpp)"},
     {nullptr, nullptr, 0, nullptr},
 };
 

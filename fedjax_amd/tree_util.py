@@ -24,6 +24,7 @@ Semantics follow the reference under JAX's defaults (x64 disabled):
 
 from __future__ import annotations
 
+import ctypes
 import numbers
 from typing import Any, Iterable, List, Optional, Sequence, Tuple
 
@@ -185,6 +186,11 @@ def _fold(rows, weights, *, scale=None,
     if accumulate and out is None:
         raise ValueError("accumulate needs out")
     table = rows if isinstance(rows, _Table) else None
+    if (table is not None and out is None and not accumulate and l2sq is None and nontemporal is None
+            and isinstance(weights, _Weights) and table.row0):
+        outs = _native_fold(table, weights, scale)
+        if outs is not None:
+            return outs
     if table is not None:
         rows, validated = [table.row0], True  # built by _client_table, which checked every client
     K, L = (len(rows) if table is None else table.ptrs.shape[0]), len(rows[0])
@@ -200,9 +206,13 @@ def _fold(rows, weights, *, scale=None,
         for k in range(1, K):  # rows are on `device` already (_client_rows)
             if [(x.size(), x.dtype) for x in rows[k]] != sig0:
                 _check_row(k, rows[k], sig0)
+    rules = {}  # leaf dtype -> (in, acc, out dtype): the rule depends on the weights only
     for l in range(L):
         x0 = rows[0][l]
-        in_c, acc_c, out_dt = _leaf_rule(x0.dtype, kinds, scaled_kind)
+        rule = rules.get(x0.dtype)
+        if rule is None:
+            rule = rules[x0.dtype] = _leaf_rule(x0.dtype, kinds, scaled_kind)
+        in_c, acc_c, out_dt = rule
         if out is not None:
             o = out[l]
             if o.dtype != out_dt or o.size() != x0.size() or not o.is_contiguous() or o.device != device:
@@ -231,7 +241,7 @@ def _fold(rows, weights, *, scale=None,
         else:
             in_ptrs = np.array([[rows[k][l].data_ptr() for l in ls] for k in range(K)], dtype=np.int64)
         out_ptrs = np.array([outs[l].data_ptr() for l in ls], dtype=np.int64)
-        unaligned = bool((in_ptrs % 16).any() or (out_ptrs % 16).any())
+        unaligned = bool((int(np.bitwise_or.reduce(in_ptrs, axis=None)) | int(np.bitwise_or.reduce(out_ptrs))) & 15)
         blocks = _ptrs_plan(in_c, leaf_n, unaligned, device)
         if packed is not None:
             w_host = packed.f32 if acc_c == _lib.F32 else packed.i32
@@ -259,6 +269,33 @@ def _fold(rows, weights, *, scale=None,
             ws = torch.empty(max(need, 4), dtype=torch.uint8, device=device)
             _lib.call("fjagg_wsum_l2_ptrs", in_c, acc_c, out_c, image_dev.data_ptr(), len(ls), K, nblk,
                       w_dev_ptr, sc, l2sq.data_ptr(), flags, ws.data_ptr(), ws.numel(), stream)
+    return outs
+
+
+_ENTRY_ADDRS = None  # (fjagg_ptrs_plan, fjagg_wsum_ptrs) addresses for fjhost.fold_table
+
+
+def _native_fold(table: "_Table", packed: "_Weights", scale) -> Optional[List[torch.Tensor]]:
+    """The common case of :func:`_fold` in one native call (fjhost.fold_table): float32
+    leaves, aligned pointers, Python-number weights, fresh outputs. It builds the same plan
+    image and launches the same kernel as the Python path below; None when the case does
+    not hold (nothing launched)."""
+    global _ENTRY_ADDRS
+    if _ENTRY_ADDRS is None:
+        lib = _lib.load()
+        _ENTRY_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
+                             for f in ("fjagg_ptrs_plan", "fjagg_wsum_ptrs"))
+    dev = table.row0[0].device
+    if dev.type != "cuda":
+        return None
+    sc = float(np.float32(scale)) if scale is not None else 1.0
+    got = _lib.host().fold_table(table.row0, table.ptrs, packed.f32, sc, scale is not None,
+                                 float(NONTEMPORAL_MIN_BYTES), dev.index, torch.cuda.current_stream(dev).cuda_stream,
+                                 *_ENTRY_ADDRS)
+    if got is None:
+        return None
+    rc, outs = got
+    _lib.check(rc, "fjagg_wsum_ptrs")
     return outs
 
 
@@ -429,10 +466,10 @@ def _collect_pairs(pairs):
     """Consume (tree, weight) pairs once: (trees, weights, W) with W summed as
     tree_util.py:86,95 (a Python float from 0.0; numpy scalars keep their type).
     ``weights`` is a :class:`_Weights` when every weight is a Python number."""
-    trees, weights = [], []
-    for tree, weight in pairs:
-        trees.append(tree)
-        weights.append(weight)
+    if type(pairs) is not list:
+        pairs = list(pairs)
+    trees = [tree for tree, _ in pairs]  # unpacks each pair as `for pytree, weight in ...` does
+    weights = [weight for _, weight in pairs]
     packed = _pack_weights(weights) if trees else None
     if packed is not None:
         return trees, packed, packed.total

@@ -686,3 +686,30 @@ def test_native_table_declines_mixed_clients(cuda):
     bad[1]["b"] = torch.ones(3, dtype=torch.bfloat16, device=cuda)
     with pytest.raises(TypeError):
         tu.tree_mean(zip(bad, [1, 1, 1, 1]))
+
+
+def test_native_fold_table_is_used_and_declines(cuda):
+    """fjhost.fold_table (the native rest of tree_mean) launches for float32, aligned
+    tables and gives the Python path's bits; bf16 leaves and unaligned views decline it."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    trees = [{"a": torch.randn(1000, generator=g).to(cuda), "b": torch.randn(7, generator=g).to(cuda)}
+             for _ in range(5)]
+    w = [1, 2, 3, 4, 5]
+    _, rows = tu._client_table(trees)
+    assert isinstance(rows, tu._Table)
+    packed = tu._pack_weights(w)
+    fast = tu._native_fold(rows, packed, tu._inverse(15.0))
+    assert fast is not None
+    slow = tu._fold([[t["a"], t["b"]] for t in trees], w, scale=tu._inverse(15.0), validated=True)
+    for a, b in zip(fast, slow):
+        assert a.shape == b.shape and a.dtype == b.dtype == torch.float32
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    t16 = [{"a": t["a"].bfloat16()} for t in trees]
+    assert tu._native_fold(tu._client_table(t16)[1], packed, tu._inverse(15.0)) is None
+    base = torch.randn(5, 1001, generator=g).to(cuda)
+    odd = [{"a": base[k, 1:]} for k in range(5)]  # 4-byte offset: not 16-byte aligned
+    rows_odd = tu._client_table(odd)[1]
+    assert isinstance(rows_odd, tu._Table)
+    assert tu._native_fold(rows_odd, packed, tu._inverse(15.0)) is None
+    m = tu.tree_mean(zip(odd, w))  # the Python path handles it
+    assert torch.equal(m["a"], tu.tree_mean(zip([{"a": base[k, 1:].clone()} for k in range(5)], w))["a"])
