@@ -37,8 +37,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 # N>1 auto-tune: 1 = no overlap; more = shorter exposed reduce tail; tapered relative sizes
-# (fd.bucket_edges) hide each reduce behind the next, smaller fold and expose only the last
-BUCKET_CANDIDATES = (1, 2, 4, 8, (3, 1), (7, 1), (4, 2, 1), (8, 4, 2, 1))
+# (fd.bucket_edges) hide each reduce behind the next, smaller fold and expose only the last.
+# Tapers whose buckets are whole multiples of 1 Mi f32 keep every bucket's fold on a full
+# grid (2:1:1 of 4 Mi = 2 Mi + 1 Mi + 1 Mi); 3:1 or 7:1 cut buckets the balanced grid
+# covers with part-empty tiles (profiles/r01t_probe_bucket.jsonl, r01t_shard_rehearsal.jsonl)
+BUCKET_CANDIDATES = (1, 2, 4, 8, (2, 1, 1), (4, 2, 1, 1))
 METRIC = "device-resident aggregated client-delta GB/s, K clients × P fp32 params"
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 WORKLOADS = {  # name: (clients, params, dtype, description)
