@@ -49,6 +49,7 @@ _SIGNATURES = {
     "fjagg_wsum_dense": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _i32, _i32, _vp, _i64, _vp]),
     "fjagg_split_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_ptrs_plan": (_i64, [_i32, _i32, _vp, _i32, _vp, _i64]),
+    "fjagg_ptrs_plan_leaves": (_i64, [_i32, _i32, _vp, _vp, _i32, _vp, _i64]),
     "fjagg_wsum_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _i32, _vp]),
     "fjagg_wsum_l2_ptrs_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_wsum_l2_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _vp, _i32, _vp, _i64, _vp]),

@@ -587,12 +587,47 @@ __global__ __launch_bounds__(kThreads) void k_dense_opt(
   }
 }
 
+// Walks the unit range [u0, u1) of one leaf (units of VV elements): in groups of
+// kThreads*8 units (E=8, U=4: the dense default; lanes past the range are masked)
+// when the range gives a lane more than one unit, else in groups of kThreads units
+// (E=1, U=8).
+template <int IN, class ACC, int OUT, int VV, bool NT, bool BURST, class RowFn, class NORM, class EPI>
+__device__ __forceinline__ void walk_units(RowFn row, uint32_t row_bytes, int64_t K, int64_t u0, int64_t u1,
+                                           uint8_t* ob, const typename ACC::T* __restrict__ w, bool dsc,
+                                           float scale, bool acm, NORM nrm, const EPI& epi) {
+  constexpr int IB = Elem<IN>::B;
+  const int tid = threadIdx.x;
+  if (u1 - u0 > (int64_t)kThreads) {
+    for (int64_t g = u0; g < u1; g += (int64_t)kThreads * 8) {
+      uint32_t off[8];
+      bool valid[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        int64_t u = g + j * kThreads + tid;
+        valid[j] = u < u1;
+        if (!valid[j]) u = u1 - 1;
+        off[j] = (uint32_t)(u * (VV * IB));
+      }
+      fold<IN, ACC, OUT, VV, 8, 4, NT, BURST>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm, epi);
+    }
+    return;
+  }
+  for (int64_t g = u0; g < u1; g += kThreads) {
+    int64_t u = g + tid;
+    const bool valid[1] = {u < u1};
+    if (!valid[0]) u = u1 - 1;
+    const uint32_t off[1] = {(uint32_t)(u * (VV * IB))};
+    fold<IN, ACC, OUT, VV, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm, epi);
+  }
+}
+
 // Pytree path. image = in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk].
-// Block b: word 0 = first unit (bits 0..39) | leaf (40..61) | tail flag (62);
-// word 1 = end unit (exclusive). A workgroup walks its unit range of one leaf in
-// groups of kThreads*8 units (E=8, U=4: the dense default; lanes past the range
-// are masked) when the range gives a lane more than one unit, else in groups of
-// kThreads units (E=1, U=8).
+// Block b: word 0 = first unit (bits 0..39) | leaf (40..61) | tail flag (62) |
+// element flag (63); word 1 = end unit (exclusive). A workgroup walks its unit range
+// of one leaf with walk_units. Units are V elements, or single elements when the
+// element flag is set: a leaf whose client or output pointers are not 16-byte
+// aligned (fjagg_ptrs_plan_leaves) takes element units without pulling the other
+// leaves of the launch off the 16-byte path.
 template <int IN, class ACC, int OUT, int V, bool NT, bool L2 = false, bool BURST = true>
 __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ img, int L,
                                                    int64_t K,
@@ -608,6 +643,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   const int64_t be = blk[0];
   const int leaf = (int)((be >> 40) & 0x3fffff);
   const bool tail = (be >> 62) & 1;
+  const bool elem = ((uint64_t)be >> 63) != 0;
   const int64_t u0 = be & ((1ll << 40) - 1);
   const int64_t u1 = blk[1];
   const int64_t n = leaf_n[leaf];
@@ -633,34 +669,10 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
       const bool valid[1] = {active};
       fold<IN, ACC, OUT, 1, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm);
     }
+  } else if (V > 1 && elem) {
+    walk_units<IN, ACC, OUT, 1, NT, BURST>(row, row_bytes, K, u0, u1, ob, w, dsc, scale, acm, nrm, PlainEpi());
   } else {
-    bool done = false;
-    if constexpr (V > 1) {
-      if (u1 - u0 > (int64_t)kThreads) {  // more than one unit per lane: E=8 groups, masked
-        for (int64_t g = u0; g < u1; g += (int64_t)kThreads * 8) {
-          uint32_t off[8];
-          bool valid[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            int64_t u = g + j * kThreads + tid;
-            valid[j] = u < u1;
-            if (!valid[j]) u = u1 - 1;
-            off[j] = (uint32_t)(u * (V * IB));
-          }
-          fold<IN, ACC, OUT, V, 8, 4, NT, BURST>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm);
-        }
-        done = true;
-      }
-    }
-    if (!done) {
-      for (int64_t g = u0; g < u1; g += kThreads) {
-        int64_t u = g + tid;
-        const bool valid[1] = {u < u1};
-        if (!valid[0]) u = u1 - 1;
-        const uint32_t off[1] = {(uint32_t)(u * (V * IB))};
-        fold<IN, ACC, OUT, V, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm);
-      }
-    }
+    walk_units<IN, ACC, OUT, V, NT, BURST>(row, row_bytes, K, u0, u1, ob, w, dsc, scale, acm, nrm, PlainEpi());
   }
   if constexpr (L2) {
     __syncthreads();
@@ -690,6 +702,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict
   const int64_t be = blk[0];
   const int leaf = (int)((be >> 40) & 0x3fffff);
   const bool tail = (be >> 62) & 1;
+  const bool elem = ((uint64_t)be >> 63) != 0;
   const int64_t u0 = be & ((1ll << 40) - 1);
   const int64_t u1 = blk[1];
   const int64_t n = leaf_n[leaf];
@@ -707,32 +720,12 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict
     }
     return;
   }
-  if constexpr (V > 1) {
-    if (u1 - u0 > (int64_t)kThreads) {  // E=8 groups, masked (as k_ptrs)
-      for (int64_t g = u0; g < u1; g += (int64_t)kThreads * 8) {
-        uint32_t off[8];
-        bool valid[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          int64_t u = g + j * kThreads + tid;
-          valid[j] = u < u1;
-          if (!valid[j]) u = u1 - 1;
-          off[j] = (uint32_t)(u * (V * IB));
-        }
-        fold<IN, AccF, FJAGG_F32, V, 8, 4, NT>(row, row_bytes, K, off, nullptr, valid, w, true, scale, false,
-                                               NoNorm(), epi);
-      }
-      return;
-    }
-  }
-  for (int64_t g = u0; g < u1; g += kThreads) {
-    int64_t u = g + tid;
-    const bool valid[1] = {u < u1};
-    if (!valid[0]) u = u1 - 1;
-    const uint32_t off[1] = {(uint32_t)(u * (V * IB))};
-    fold<IN, AccF, FJAGG_F32, V, 1, 8, NT>(row, row_bytes, K, off, nullptr, valid, w, true, scale, false,
-                                           NoNorm(), epi);
-  }
+  if (V > 1 && elem)
+    walk_units<IN, AccF, FJAGG_F32, 1, NT, true>(row, row_bytes, K, u0, u1, nullptr, w, true, scale, false, NoNorm(),
+                                                 epi);
+  else
+    walk_units<IN, AccF, FJAGG_F32, V, NT, true>(row, row_bytes, K, u0, u1, nullptr, w, true, scale, false, NoNorm(),
+                                                 epi);
 }
 
 // Per-client sum of squares: grid (nb, K); ws[k*nb + b] = block partial (f32),
@@ -1288,6 +1281,11 @@ int fjagg_wsum_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_d
 
 int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, int64_t* blocks,
                         int64_t blocks_cap) {
+  return fjagg_ptrs_plan_leaves(in_dtype, flags, leaf_n, nullptr, L, blocks, blocks_cap);
+}
+
+int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, const uint8_t* leaf_elem, int L,
+                               int64_t* blocks, int64_t blocks_cap) {
   g_err[0] = 0;
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16 && in_dtype != FJAGG_I32)
     return fail(FJAGG_EINVAL, "bad dtype %d", in_dtype);
@@ -1298,7 +1296,7 @@ int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, i
     const int64_t n = leaf_n[l];
     if (n < 0 || n * elem_bytes(in_dtype) > kMaxRowBytes)
       return fail(FJAGG_EINVAL, "leaf %d: %lld elements unsupported", l, (long long)n);
-    total += n / V;
+    total += (leaf_elem && leaf_elem[l]) ? (n + V - 1) / V : n / V;  // balance by bytes
   }
   // balanced unit share per workgroup, as for the dense path (balanced_grid): the
   // same number of E=8 workgroups on every CU, at most kPlanPerCU of them per CU
@@ -1323,11 +1321,19 @@ int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, i
     }
     ++nblk;
   };
+  // element-unit leaves (V > 1 only): units are single elements, ranges of S of them.
+  // A workgroup's time is set by its sequential walks over the K clients (one per
+  // group of kThreads*8 units), not by its bytes, so element ranges keep the unit
+  // count of the vector ranges: S*V elements would take V times as many walks.
+  auto is_elem = [&](int l) { return V > 1 && leaf_elem && leaf_elem[l]; };
   for (int l = 0; l < L; ++l)  // tails first: latency-bound, start them early
-    if (leaf_n[l] % V) put(((int64_t)l << 40) | (1ll << 62), 0);
+    if (!is_elem(l) && leaf_n[l] % V) put(((int64_t)l << 40) | (1ll << 62), 0);
   for (int l = 0; l < L; ++l) {
-    const int64_t nunits = leaf_n[l] / V;
-    for (int64_t u = 0; u < nunits; u += S) put(((int64_t)l << 40) | u, (u + S < nunits) ? u + S : nunits);
+    const bool el = is_elem(l);
+    const int64_t nunits = el ? leaf_n[l] : leaf_n[l] / V, step = S;
+    const int64_t flag = el ? (int64_t)(1ull << 63) : 0;
+    for (int64_t u = 0; u < nunits; u += step)
+      put(flag | ((int64_t)l << 40) | u, (u + step < nunits) ? u + step : nunits);
   }
   return nblk;
 }

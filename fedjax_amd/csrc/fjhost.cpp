@@ -224,8 +224,8 @@ PyObject* fold_weights(PyObject*, PyObject* args) {
   return result;
 }
 
-// fjagg_ptrs_plan / fjagg_wsum_ptrs of libfjagg.so (include/fjagg.h), passed in by address
-typedef int64_t (*PlanFn)(int, int, const int64_t*, int, int64_t*, int64_t);
+// fjagg_ptrs_plan_leaves / fjagg_wsum_ptrs of libfjagg.so (include/fjagg.h), passed in by address
+typedef int64_t (*PlanFn)(int, int, const int64_t*, const uint8_t*, int, int64_t*, int64_t);
 typedef int (*WsumFn)(int, int, int, const int64_t*, int, int64_t, int64_t, const void*, float, int, void*);
 constexpr int kF32 = 0, kScale = 1, kNontemporal = 4;  // fjagg.h enums
 
@@ -257,26 +257,32 @@ PyObject* fold_table(PyObject*, PyObject* args) {
   const auto* in = static_cast<const int64_t*>(bp.buf);
   try {
     // fast case only: float32 leaves (fold type and output type are then float32 for any
-    // weights), every pointer 16-byte aligned (the vector plan)
+    // weights). A leaf with a client pointer off 16 bytes walks element units (per-leaf
+    // plan); the outputs are fresh allocations, so aligned.
     std::vector<int64_t> leaf_n(L);
-    int64_t orbits = 0, total = 0;
+    int64_t total = 0;
     for (Py_ssize_t l = 0; l < L; ++l) {
       const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(row0, l));
       if (t.scalar_type() != at::kFloat) Py_RETURN_NONE;
       leaf_n[l] = t.numel();
       total += leaf_n[l];
     }
-    for (int64_t i = 0; i < K * L; ++i) orbits |= in[i];
+    std::vector<int64_t> lbits(L, 0);
+    for (int64_t k = 0; k < K; ++k)
+      for (Py_ssize_t l = 0; l < L; ++l) lbits[l] |= in[k * L + l];
     std::vector<at::Tensor> outs;
     outs.reserve(L);
+    std::vector<uint8_t> elem(L, 0);
+    bool any_elem = false;
     for (Py_ssize_t l = 0; l < L; ++l) {
       const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(row0, l));
       outs.push_back(at::empty(t.sizes(), t.options()));
-      orbits |= reinterpret_cast<int64_t>(outs.back().data_ptr());
+      elem[l] = ((lbits[l] | reinterpret_cast<int64_t>(outs.back().data_ptr())) & 15) != 0;
+      any_elem = any_elem || elem[l];
     }
-    if (orbits & 15) Py_RETURN_NONE;
     auto plan = reinterpret_cast<PlanFn>(plan_addr);
-    const int64_t nblk = plan(kF32, 0, leaf_n.data(), static_cast<int>(L), nullptr, 0);
+    const uint8_t* mask = any_elem ? elem.data() : nullptr;
+    const int64_t nblk = plan(kF32, 0, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);
     if (nblk < 0) Py_RETURN_NONE;
     // plan image (fjagg.h): in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk] | f32 weights
     const int64_t nw = (K + 1) / 2, n = K * L + 2 * L + 2 * nblk + nw;
@@ -287,7 +293,7 @@ PyObject* fold_table(PyObject*, PyObject* args) {
       p[K * L + l] = reinterpret_cast<int64_t>(outs[l].data_ptr());
       p[K * L + L + l] = leaf_n[l];
     }
-    if (plan(kF32, 0, leaf_n.data(), static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) Py_RETURN_NONE;
+    if (plan(kF32, 0, leaf_n.data(), mask, static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) Py_RETURN_NONE;
     p[n - 1] = 0;
     std::memcpy(p + n - nw, bw.buf, 4 * K);
     at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);

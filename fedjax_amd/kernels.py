@@ -152,16 +152,28 @@ def split_workspace_bytes(K: int, P: int) -> int:
     return int(_lib.load().fjagg_split_workspace_bytes(K, P))
 
 
-def ptrs_plan(in_code: int, leaf_n: Sequence[int], unaligned: bool) -> np.ndarray:
-    """Workgroup table of the pytree kernel (host int64 array, 2 words per workgroup)."""
+def ptrs_plan(in_code: int, leaf_n: Sequence[int], unaligned) -> np.ndarray:
+    """Workgroup table of the pytree kernel (host int64 array, 2 words per workgroup).
+
+    ``unaligned``: a bool for the whole launch (True = element units everywhere; launch
+    with ``unaligned=True``), or a per-leaf boolean array: the marked leaves take
+    element units, the others 16-byte units (``fjagg_ptrs_plan_leaves``; launch with
+    ``unaligned=False``)."""
     lib = _lib.load()
     n = np.ascontiguousarray(leaf_n, dtype=np.int64)
-    flags = _lib.UNALIGNED if unaligned else 0
-    need = lib.fjagg_ptrs_plan(in_code, flags, n.ctypes.data, len(n), None, 0)
-    _lib.check(0 if need >= 0 else int(need), "fjagg_ptrs_plan")
+    if isinstance(unaligned, (bool, np.bool_)):
+        flags, mask = (_lib.UNALIGNED if unaligned else 0), None
+    else:
+        mask = np.ascontiguousarray(unaligned, dtype=np.uint8)
+        if mask.shape != n.shape:
+            raise ValueError(f"per-leaf mask of {mask.shape[0] if mask.ndim else 0} entries for {n.size} leaves")
+        flags = 0
+    mp = mask.ctypes.data if mask is not None else None
+    need = lib.fjagg_ptrs_plan_leaves(in_code, flags, n.ctypes.data, mp, len(n), None, 0)
+    _lib.check(0 if need >= 0 else int(need), "fjagg_ptrs_plan_leaves")
     blocks = np.empty(2 * max(need, 1), dtype=np.int64)
-    got = lib.fjagg_ptrs_plan(in_code, flags, n.ctypes.data, len(n), blocks.ctypes.data, need)
-    _lib.check(0 if got >= 0 else int(got), "fjagg_ptrs_plan")
+    got = lib.fjagg_ptrs_plan_leaves(in_code, flags, n.ctypes.data, mp, len(n), blocks.ctypes.data, need)
+    _lib.check(0 if got >= 0 else int(got), "fjagg_ptrs_plan_leaves")
     return blocks[:2 * need]
 
 

@@ -158,8 +158,7 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
     for i, ls in enumerate((m, v, mo)):
         if ls is not None:
             st[i * L:(i + 1) * L] = [x.data_ptr() for x in ls]
-    unaligned = bool((in_ptrs % 16).any() or (out_ptrs % 16).any() or (st % 16).any())
-    blocks = tree_util._ptrs_plan(in_c, leaf_n, unaligned, device)
+    blocks, unaligned = tree_util._leaf_plan(in_c, leaf_n, in_ptrs, out_ptrs, st.reshape(3, L), device)
     w32 = weights.f32 if isinstance(weights, tree_util._Weights) else np.array(
         [np.float32(w) for w in weights], np.float32)
     w_words = np.zeros((K + 1) // 2, dtype=np.int64)

@@ -241,8 +241,7 @@ def _fold(rows, weights, *, scale=None,
         else:
             in_ptrs = np.array([[rows[k][l].data_ptr() for l in ls] for k in range(K)], dtype=np.int64)
         out_ptrs = np.array([outs[l].data_ptr() for l in ls], dtype=np.int64)
-        unaligned = bool((int(np.bitwise_or.reduce(in_ptrs, axis=None)) | int(np.bitwise_or.reduce(out_ptrs))) & 15)
-        blocks = _ptrs_plan(in_c, leaf_n, unaligned, device)
+        blocks, unaligned = _leaf_plan(in_c, leaf_n, in_ptrs, out_ptrs, device)
         if packed is not None:
             w_host = packed.f32 if acc_c == _lib.F32 else packed.i32
         elif acc_c == _lib.F32:
@@ -272,19 +271,19 @@ def _fold(rows, weights, *, scale=None,
     return outs
 
 
-_ENTRY_ADDRS = None  # (fjagg_ptrs_plan, fjagg_wsum_ptrs) addresses for fjhost.fold_table
+_ENTRY_ADDRS = None  # (fjagg_ptrs_plan_leaves, fjagg_wsum_ptrs) addresses for fjhost.fold_table
 
 
 def _native_fold(table: "_Table", packed: "_Weights", scale) -> Optional[List[torch.Tensor]]:
     """The common case of :func:`_fold` in one native call (fjhost.fold_table): float32
-    leaves, aligned pointers, Python-number weights, fresh outputs. It builds the same plan
+    leaves, Python-number weights, fresh outputs (misaligned leaves get the per-leaf plan). It builds the same plan
     image and launches the same kernel as the Python path below; None when the case does
     not hold (nothing launched)."""
     global _ENTRY_ADDRS
     if _ENTRY_ADDRS is None:
         lib = _lib.load()
         _ENTRY_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
-                             for f in ("fjagg_ptrs_plan", "fjagg_wsum_ptrs"))
+                             for f in ("fjagg_ptrs_plan_leaves", "fjagg_wsum_ptrs"))
     dev = table.row0[0].device
     if dev.type != "cuda":
         return None
@@ -302,14 +301,31 @@ def _native_fold(table: "_Table", packed: "_Weights", scale) -> Optional[List[to
 _PLANS = {}  # (in dtype, leaf sizes, unaligned) -> workgroup table (the device is fixed per process)
 
 
-def _ptrs_plan(in_c: int, leaf_n: np.ndarray, unaligned: bool, device: torch.device) -> np.ndarray:
-    key = (in_c, leaf_n.tobytes(), unaligned, device)
+def _ptrs_plan(in_c: int, leaf_n: np.ndarray, unaligned, device: torch.device) -> np.ndarray:
+    """Cached :func:`kernels.ptrs_plan`; ``unaligned`` is a bool or a per-leaf mask."""
+    key = (in_c, leaf_n.tobytes(), unaligned if isinstance(unaligned, bool) else
+           np.asarray(unaligned, dtype=np.uint8).tobytes(), device)
     blocks = _PLANS.get(key)
     if blocks is None:
         blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)
         if len(_PLANS) < 1024:
             _PLANS[key] = blocks
     return blocks
+
+
+def _leaf_plan(in_c: int, leaf_n: np.ndarray, in_ptrs: np.ndarray, *more_ptrs) -> tuple:
+    """Plan for a [K, L] table of client leaf pointers plus per-leaf output pointers
+    (``more_ptrs``: [L] or [m, L] int64 arrays, then the device). Leaves whose pointers
+    are not all 16-byte aligned walk element units; the others keep 16-byte units
+    (fjagg_ptrs_plan_leaves). Returns (blocks, launch-wide UNALIGNED flag) — the flag is
+    never needed now that the choice is per leaf, so it is always False."""
+    *arrs, device = more_ptrs
+    bits = np.bitwise_or.reduce(in_ptrs, axis=0) if in_ptrs.shape[0] else np.zeros(len(leaf_n), np.int64)
+    for a in arrs:
+        a = np.asarray(a, dtype=np.int64).reshape(-1, len(leaf_n))
+        bits = bits | np.bitwise_or.reduce(a, axis=0)
+    bad = (bits & 15) != 0
+    return _ptrs_plan(in_c, leaf_n, bad if bad.any() else False, device), False
 
 
 class _Table:

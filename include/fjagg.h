@@ -112,7 +112,7 @@ int64_t fjagg_split_workspace_bytes(int64_t K, int64_t P);
  *     out_ptrs[L]
  *     leaf_n  [L]      elements per leaf
  *     blocks  [2*nblk] from fjagg_ptrs_plan(): per workgroup (first unit | leaf | tail
- *                      flag, end unit), unit ranges balanced across the CUs
+ *                      flag | element flag, end unit), unit ranges balanced across the CUs
  * Replaces: jax.tree.map over leaves inside tree_weight/tree_add,
  * fedjax/core/tree_util.py:32,50, for the whole tree_mean loop :85-96.
  */
@@ -122,6 +122,17 @@ int64_t fjagg_split_workspace_bytes(int64_t K, int64_t P);
  * output pointer is not 16-byte aligned (the same flag must go to the launch). */
 int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, int64_t* blocks,
                         int64_t blocks_cap);
+/* fjagg_ptrs_plan with a per-leaf choice of unit: leaf_elem[l] != 0 marks a leaf whose
+ * client or output pointers are not all 16-byte aligned. Its workgroups walk single
+ * elements (the element flag, bit 63 of block word 0; ranges of as many units as the
+ * vector ranges, since a workgroup's time is its walks over the K clients) while every other leaf keeps
+ * 16-byte units, so one misaligned leaf does not slow the whole launch. Launch the
+ * plan WITHOUT FJAGG_UNALIGNED. leaf_elem == NULL is fjagg_ptrs_plan. Replaces the same
+ * reference loop as fjagg_ptrs_plan (tree_util.py:85-96); a caller-held pytree may be
+ * views into one buffer at any element offset (e.g. deserialized msgpack leaves,
+ * fedjax/core/serialization.py:79-87). */
+int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, const uint8_t* leaf_elem,
+                               int L, int64_t* blocks, int64_t blocks_cap);
 int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev,
                     int L, int64_t K, int64_t nblk, const void* w_dev, float scale,
                     int flags, void* stream);

@@ -256,6 +256,47 @@ def test_pytree_unaligned_and_mixed_leaves(cuda, coracle):
     assert np.array_equal(bits(got), bits(want))
 
 
+EMNIST = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "conv2_d_1": {"b": (64,), "w": (3, 3, 32, 64)},
+          "linear": {"b": (128,), "w": (9216, 128)}, "linear_1": {"b": (62,), "w": (128, 62)}}
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_pytree_mixed_alignment_per_leaf_units(cuda, coracle, dtype):
+    """Client pytrees that are views into one slab at EMNIST-CNN leaf offsets: linear_1/w
+    sits 8 bytes off a 16-byte boundary (f32), so that leaf walks element units while
+    the others keep 16-byte units (fjagg_ptrs_plan_leaves). Bitwise equal to the oracle
+    and to the same leaves cloned into aligned allocations; with l2 norms and with the
+    fused server step too."""
+    template = pytree_map(lambda s: np.zeros(s, np.float32), EMNIST)
+    K = 12
+    slab = fedjax_amd.ClientDeltaSlab(template, K, dtype=dtype, device=cuda).fill_synthetic(seed=21)
+    views = [slab.client(k) for k in range(K)]
+    ptrs = [x.data_ptr() % 16 for x in fedjax_amd.pytree.leaves_of(views[1])]
+    assert any(ptrs) and not all(ptrs)  # mixed alignment
+    clones = [pytree_map(lambda v: v.clone(), t) for t in views]
+    wi = [int(v) for v in ref.fedavg_weights(K, seed=22)]
+    m_v, m_c = tu.tree_mean(zip(views, wi)), tu.tree_mean(zip(clones, wi))
+    flat_v = torch.cat([v.reshape(-1) for v in fedjax_amd.pytree.leaves_of(m_v)])
+    flat_c = torch.cat([v.reshape(-1) for v in fedjax_amd.pytree.leaves_of(m_c)])
+    assert torch.equal(flat_v, flat_c)
+    if dtype == torch.float32:
+        xh = coracle.synth_f32(K, slab.num_params, seed=21)
+        want = coracle.wsum_f32(xh, np.float32(wi), scale=ref.mean_scale(wi))
+        assert np.array_equal(bits(host(flat_v)), bits(want))
+        mv, nv = tu.tree_mean_with_l2_norms(zip(views, wi))
+        mc, nc = tu.tree_mean_with_l2_norms(zip(clones, wi))
+        assert torch.equal(torch.cat([v.reshape(-1) for v in fedjax_amd.pytree.leaves_of(mv)]), flat_c)
+        npt.assert_allclose(host(nv), host(nc), rtol=2e-6)
+        from fedjax_amd import server
+        opt = server.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)
+        outs = []
+        for clients in (views, clones):
+            params = pytree_map(lambda v: torch.zeros(v.shape, device=cuda), clients[0])
+            st = server.fused_tree_mean_update(zip(clients, wi), opt, params, opt.init(params))
+            outs.append(torch.cat([v.reshape(-1) for v in fedjax_amd.pytree.leaves_of(params)]))
+        assert torch.equal(outs[0], outs[1])
+
+
 def test_slab_mean_equals_tree_mean_equals_oracle(cuda, coracle):
     shapes = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "linear": {"b": (128,), "w": (100, 128)}}
     template = pytree_map(lambda s: np.zeros(s, np.float32), shapes)
@@ -689,8 +730,9 @@ def test_native_table_declines_mixed_clients(cuda):
 
 
 def test_native_fold_table_is_used_and_declines(cuda):
-    """fjhost.fold_table (the native rest of tree_mean) launches for float32, aligned
-    tables and gives the Python path's bits; bf16 leaves and unaligned views decline it."""
+    """fjhost.fold_table (the native rest of tree_mean) launches for float32 tables, with
+    misaligned leaves on element units, and gives the Python path's bits; bf16 leaves
+    decline it."""
     g = torch.Generator(device="cpu").manual_seed(3)
     trees = [{"a": torch.randn(1000, generator=g).to(cuda), "b": torch.randn(7, generator=g).to(cuda)}
              for _ in range(5)]
@@ -710,6 +752,9 @@ def test_native_fold_table_is_used_and_declines(cuda):
     odd = [{"a": base[k, 1:]} for k in range(5)]  # 4-byte offset: not 16-byte aligned
     rows_odd = tu._client_table(odd)[1]
     assert isinstance(rows_odd, tu._Table)
-    assert tu._native_fold(rows_odd, packed, tu._inverse(15.0)) is None
-    m = tu.tree_mean(zip(odd, w))  # the Python path handles it
+    fast_odd = tu._native_fold(rows_odd, packed, tu._inverse(15.0))  # per-leaf element units
+    assert fast_odd is not None
+    slow_odd = tu._fold([[t["a"]] for t in odd], w, scale=tu._inverse(15.0), validated=True)
+    assert torch.equal(fast_odd[0].view(torch.int32), slow_odd[0].view(torch.int32))
+    m = tu.tree_mean(zip(odd, w))
     assert torch.equal(m["a"], tu.tree_mean(zip([{"a": base[k, 1:].clone()} for k in range(5)], w))["a"])

@@ -89,6 +89,34 @@ def test_ptrs_plan_covers_every_unit_once(unaligned):
     assert S % 64 == 0 and all(sz <= S for sz in sizes)
 
 
+def test_ptrs_plan_per_leaf_units():
+    """fjagg_ptrs_plan_leaves: marked leaves walk element units (flag bit 63, no tail
+    block, ranges of at most S elements); the other leaves keep 16-byte units and tails."""
+    leaf_n = [32, 288, 64, 18432, 128, 1179648, 62, 7936, 5, 3]
+    mask = np.array([0, 0, 0, 1, 0, 1, 1, 0, 0, 1], dtype=bool)
+    blocks = kernels.ptrs_plan(_lib.F32, leaf_n, mask).reshape(-1, 2)
+    elem = (blocks[:, 0].view(np.uint64) >> np.uint64(63)).astype(bool)
+    w0 = blocks[:, 0] & ((1 << 63) - 1)
+    dec = _decode(np.stack([w0, blocks[:, 1]], 1).ravel())
+    first_main = next(i for i, d in enumerate(dec) if not d[1])
+    assert all(d[1] for d in dec[:first_main]) and not any(d[1] for d in dec[first_main:])
+    S = max(u1 - u0 for (_, t, u0, u1), e in zip(dec, elem) if not t and not e)
+    for l, n in enumerate(leaf_n):
+        mine = [(d, e) for d, e in zip(dec, elem) if d[0] == l]
+        assert all(e == mask[l] for _, e in mine)
+        tails = [d for d, _ in mine if d[1]]
+        r = sorted((d[2], d[3]) for d, _ in mine if not d[1])
+        units = n if mask[l] else n // 4
+        assert len(tails) == (0 if mask[l] else int(n % 4 != 0))
+        assert r[0][0] == 0 and r[-1][1] == units and all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        assert all(u1 - u0 <= S for u0, u1 in r)  # element ranges keep the unit count
+    # no marked leaf: the same table as the launch-wide aligned plan
+    assert np.array_equal(kernels.ptrs_plan(_lib.F32, leaf_n, np.zeros(len(leaf_n), bool)),
+                          kernels.ptrs_plan(_lib.F32, leaf_n, False))
+    with pytest.raises(ValueError):
+        kernels.ptrs_plan(_lib.F32, leaf_n, mask[:-1])
+
+
 def test_ptrs_plan_bf16_units():
     blocks = kernels.ptrs_plan(_lib.BF16, [17], False)
     dec = _decode(blocks)
