@@ -48,26 +48,39 @@ class RunningMean:
         self.total_weight: Any = 0.0  # fed_avg.py:133 (num_examples_sum = 0.)
         self.num_clients = 0
         self.buffer_clients = max(1, int(buffer_clients))
-        self._rows: List[List[torch.Tensor]] = []
+        self._trees: List[PyTree] = []
         self._weights: List[Any] = []
 
     def add(self, delta: PyTree, weight) -> None:
-        """tree_add(sum, tree_weight(delta, weight)); fed_avg.py:137-139."""
+        """tree_add(sum, tree_weight(delta, weight)); fed_avg.py:137-139. The delta is
+        buffered by reference; its leaves are read when the buffer is folded."""
         w = tree_util._host_weight(weight)
-        row = [tree_util._device_leaf(x, self.device) for x in pytree.flatten_as(self.treedef, delta)]
-        self._rows.append(row)
+        self._trees.append(delta)
         self._weights.append(w)
         self.total_weight += w
         self.num_clients += 1
-        if len(self._rows) >= self.buffer_clients:
+        if len(self._trees) >= self.buffer_clients:
             self.flush()
 
     def flush(self) -> None:
-        if not self._rows:
+        """Fold the buffered clients into the running sum: ONE pytree-kernel launch in
+        accumulate mode. The K x L pointer table comes from the native gather
+        (tree_util._client_table) when every buffered delta is already a pytree of
+        contiguous device tensors shaped like the sum; otherwise each delta is
+        flattened against the template and copied to the device first."""
+        if not self._trees:
             return
-        if self._sum:  # dtype rules checked by _fold (the sum has the template's dtypes)
-            tree_util._fold(self._rows, self._weights, out=self._sum, accumulate=True)
-        self._rows, self._weights = [], []
+        trees, weights = self._trees, self._weights
+        self._trees, self._weights = [], []
+        if not self._sum:  # dtype rules checked by _fold (the sum has the template's dtypes)
+            return
+        td, rows = tree_util._client_table(trees)
+        if not (td == self.treedef and isinstance(rows, tree_util._Table)
+                and rows.row0[0].device == self.device):
+            rows = [[tree_util._device_leaf(x, self.device) for x in pytree.flatten_as(self.treedef, t)]
+                    for t in trees]
+        packed = tree_util._pack_weights(weights)
+        tree_util._fold(rows, packed if packed is not None else weights, out=self._sum, accumulate=True)
 
     def sum(self) -> PyTree:
         """The running weighted sum (flushes pending clients)."""

@@ -30,7 +30,7 @@
 //       None when any weight is something else (numpy scalar, tensor, bool, |w| >=
 //       2**53, ...): the caller then uses the Python path.
 //   fold_table(row0, ptrs, w_f32, scale, has_scale, nt_min_bytes, dev_index, stream,
-//              plan_fn, wsum_fn) -> (rc, outputs) | None
+//              plan_fn, wsum_fn[, outs, accumulate]) -> (rc, outputs) | None
 //       The rest of tree_mean's host work for a gathered table (ptrs from gather_rows,
 //       weights from fold_weights) when every leaf is float32 and every pointer is
 //       16-byte aligned: fresh output leaves shaped like row0, the plan image of
@@ -227,17 +227,19 @@ PyObject* fold_weights(PyObject*, PyObject* args) {
 // fjagg_ptrs_plan_leaves / fjagg_wsum_ptrs of libfjagg.so (include/fjagg.h), passed in by address
 typedef int64_t (*PlanFn)(int, int, const int64_t*, const uint8_t*, int, int64_t*, int64_t);
 typedef int (*WsumFn)(int, int, int, const int64_t*, int, int64_t, int64_t, const void*, float, int, void*);
-constexpr int kF32 = 0, kScale = 1, kNontemporal = 4;  // fjagg.h enums
+constexpr int kF32 = 0, kScale = 1, kAccumulate = 2, kNontemporal = 4;  // fjagg.h enums
 
 PyObject* fold_table(PyObject*, PyObject* args) {
-  PyObject *row0, *ptrs, *wf;
+  PyObject *row0, *ptrs, *wf, *dst = Py_None;
   double scale, nt_min_bytes;
-  int has_scale, dev;
+  int has_scale, dev, accumulate = 0;
   unsigned long long stream, plan_addr, wsum_addr;
-  if (!PyArg_ParseTuple(args, "O!OOdidiKKK", &PyList_Type, &row0, &ptrs, &wf, &scale, &has_scale, &nt_min_bytes,
-                        &dev, &stream, &plan_addr, &wsum_addr))
+  if (!PyArg_ParseTuple(args, "O!OOdidiKKK|Oi", &PyList_Type, &row0, &ptrs, &wf, &scale, &has_scale, &nt_min_bytes,
+                        &dev, &stream, &plan_addr, &wsum_addr, &dst, &accumulate))
     return nullptr;
   const Py_ssize_t L = PyList_GET_SIZE(row0);
+  if (dst != Py_None && (!PyList_Check(dst) || PyList_GET_SIZE(dst) != L)) Py_RETURN_NONE;
+  if (accumulate && dst == Py_None) Py_RETURN_NONE;
   Py_buffer bp, bw;
   if (PyObject_GetBuffer(ptrs, &bp, PyBUF_C_CONTIGUOUS) != 0) return nullptr;
   if (PyObject_GetBuffer(wf, &bw, PyBUF_C_CONTIGUOUS) != 0) {
@@ -276,7 +278,16 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     bool any_elem = false;
     for (Py_ssize_t l = 0; l < L; ++l) {
       const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(row0, l));
-      outs.push_back(at::empty(t.sizes(), t.options()));
+      if (dst != Py_None) {  // caller's destinations: float32, contiguous, row0's shape and device
+        PyObject* o = PyList_GET_ITEM(dst, l);
+        if (!THPVariable_Check(o)) Py_RETURN_NONE;
+        const at::Tensor& d = THPVariable_Unpack(o);
+        if (d.scalar_type() != at::kFloat || !d.is_contiguous() || d.sizes() != t.sizes() || d.device() != t.device())
+          Py_RETURN_NONE;
+        outs.push_back(d);
+      } else {
+        outs.push_back(at::empty(t.sizes(), t.options()));
+      }
       elem[l] = ((lbits[l] | reinterpret_cast<int64_t>(outs.back().data_ptr())) & 15) != 0;
       any_elem = any_elem || elem[l];
     }
@@ -298,7 +309,7 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     std::memcpy(p + n - nw, bw.buf, 4 * K);
     at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);
     const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
-    const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0);
+    const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0);
     const int64_t* dp = dimg.data_ptr<int64_t>();
     const int rc = reinterpret_cast<WsumFn>(wsum_addr)(kF32, kF32, kF32, dp, static_cast<int>(L), K, nblk,
                                                        dp + (n - nw), static_cast<float>(scale), flags,

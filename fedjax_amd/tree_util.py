@@ -186,9 +186,9 @@ def _fold(rows, weights, *, scale=None,
     if accumulate and out is None:
         raise ValueError("accumulate needs out")
     table = rows if isinstance(rows, _Table) else None
-    if (table is not None and out is None and not accumulate and l2sq is None and nontemporal is None
+    if (table is not None and l2sq is None and nontemporal is None
             and isinstance(weights, _Weights) and table.row0):
-        outs = _native_fold(table, weights, scale)
+        outs = _native_fold(table, weights, scale, out, accumulate)
         if outs is not None:
             return outs
     if table is not None:
@@ -274,9 +274,11 @@ def _fold(rows, weights, *, scale=None,
 _ENTRY_ADDRS = None  # (fjagg_ptrs_plan_leaves, fjagg_wsum_ptrs) addresses for fjhost.fold_table
 
 
-def _native_fold(table: "_Table", packed: "_Weights", scale) -> Optional[List[torch.Tensor]]:
+def _native_fold(table: "_Table", packed: "_Weights", scale, out=None,
+                 accumulate: bool = False) -> Optional[List[torch.Tensor]]:
     """The common case of :func:`_fold` in one native call (fjhost.fold_table): float32
-    leaves, Python-number weights, fresh outputs (misaligned leaves get the per-leaf plan). It builds the same plan
+    leaves, Python-number weights, fresh outputs or the caller's float32 ``out`` leaves
+    (``accumulate`` folds into them; misaligned leaves get the per-leaf plan). It builds the same plan
     image and launches the same kernel as the Python path below; None when the case does
     not hold (nothing launched)."""
     global _ENTRY_ADDRS
@@ -290,7 +292,7 @@ def _native_fold(table: "_Table", packed: "_Weights", scale) -> Optional[List[to
     sc = float(np.float32(scale)) if scale is not None else 1.0
     got = _lib.host().fold_table(table.row0, table.ptrs, packed.f32, sc, scale is not None,
                                  float(NONTEMPORAL_MIN_BYTES), dev.index, torch.cuda.current_stream(dev).cuda_stream,
-                                 *_ENTRY_ADDRS)
+                                 *_ENTRY_ADDRS, list(out) if out is not None else None, 1 if accumulate else 0)
     if got is None:
         return None
     rc, outs = got

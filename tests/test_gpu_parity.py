@@ -381,6 +381,43 @@ def test_running_mean_equals_library_fedavg_loop(buffer_clients, cuda, coracle):
     assert rm.num_clients == K and rm.total_weight == W
 
 
+def test_running_mean_native_flush_host_deltas_and_errors(cuda):
+    """RunningMean folds a buffer through the native table (fjhost.fold_table into the
+    running sum, accumulate mode): bitwise equal to the Python fold; host (numpy)
+    deltas take the flatten-and-copy path with the same bits; a delta whose structure
+    differs from the template raises when the buffer is folded."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    K = 11
+    trees = [{"a": torch.randn(1003, generator=g), "b": torch.randn(4, 6, generator=g)} for _ in range(K)]
+    w = [int(v) for v in torch.randint(1, 500, (K,), generator=g)]
+    dev_trees = [{k: v.to(cuda) for k, v in t.items()} for t in trees]
+    host_trees = [{k: v.numpy() for k, v in t.items()} for t in trees]
+    results = []
+    for clients in (dev_trees, host_trees):
+        rm = fedjax_amd.aggregators.RunningMean(dev_trees[0], buffer_clients=4, device=cuda)
+        for c, wk in zip(clients, w):
+            rm.add(c, wk)
+        results.append(rm.result())
+    s = [torch.zeros(1003, device=cuda), torch.zeros(4, 6, device=cuda)]
+    for k0 in range(0, K, 4):  # the Python fold of the same buffers
+        rows = [[t["a"], t["b"]] for t in dev_trees[k0:k0 + 4]]
+        tu._fold(rows, w[k0:k0 + 4], out=s, accumulate=True)
+    W = float(sum(w))
+    want = tu.tree_inverse_weight({"a": s[0], "b": s[1]}, W)
+    for r in results:
+        for key in ("a", "b"):
+            assert torch.equal(r[key].view(torch.int32), want[key].view(torch.int32))
+    # the native table path is the one taken for device deltas
+    _, rows = tu._client_table(dev_trees[:4])
+    out = [torch.zeros(1003, device=cuda), torch.zeros(4, 6, device=cuda)]
+    got = tu._native_fold(rows, tu._pack_weights(w[:4]), None, out, True)
+    assert got is not None and got[0] is out[0] and got[1] is out[1]
+    rm = fedjax_amd.aggregators.RunningMean(dev_trees[0], buffer_clients=2, device=cuda)
+    rm.add(dev_trees[0], 1)
+    with pytest.raises(ValueError):
+        rm.add({"a": dev_trees[1]["a"]}, 1)
+
+
 # ------------------------------------------------------------ fused fold + l2 norms
 @pytest.mark.parametrize("K,P,dt", [(1, 7, "f32"), (37, 10007, "f32"), (128, 1206590, "f32"),
                                     (300, 65536 + 5, "f32"), (64, 20000, "bf16"), (5, 3, "f32")])
