@@ -433,12 +433,20 @@ def _client_rows(trees: Sequence[PyTree], first=None) -> Tuple[pytree.TreeDef, L
 
 
 # ------------------------------------------------------------------------ public API
-def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
-    """Weights tree leaves by weight (tree_util.py:29-32)."""
-    td, rows = _client_rows([pytree_])
+def _fold_trees(trees: Sequence[PyTree], weights: List[Any]) -> PyTree:
+    """Fold of whole pytrees with host weights: the native table and weight packing
+    (fjhost) when they apply, the Python fold otherwise (same kernel, same bits)."""
+    td, rows = _client_table(trees)
     if not rows[0]:
         return pytree.unflatten(td, [])
-    return pytree.unflatten(td, _fold(rows, [_host_weight(weight)], validated=True))
+    packed = _pack_weights(weights)
+    return pytree.unflatten(td, _fold(rows, packed if packed is not None else [_host_weight(w) for w in weights],
+                                      validated=True))
+
+
+def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
+    """Weights tree leaves by weight (tree_util.py:29-32)."""
+    return _fold_trees([pytree_], [_host_weight(weight)])
 
 
 def tree_inverse_weight(pytree_: PyTree, weight: float) -> PyTree:
@@ -463,10 +471,7 @@ def tree_zeros_like(pytree_: PyTree) -> PyTree:
 def tree_add(left: PyTree, right: PyTree) -> PyTree:
     """Adds two trees together (tree_util.py:47-50): x*1 is exact, so a K=2 fold
     with unit weights is the reference's ``jnp.add``."""
-    td, rows = _client_rows([left, right])
-    if not rows[0]:
-        return pytree.unflatten(td, [])
-    return pytree.unflatten(td, _fold(rows, [1, 1], validated=True))
+    return _fold_trees([left, right], [1, 1])
 
 
 def tree_sum(pytrees: Iterable[PyTree]) -> PyTree:
@@ -474,10 +479,7 @@ def tree_sum(pytrees: Iterable[PyTree]) -> PyTree:
     trees = list(pytrees)
     if not trees:
         return None
-    td, rows = _client_table(trees)
-    if not rows[0]:
-        return pytree.unflatten(td, [])
-    return pytree.unflatten(td, _fold(rows, [1] * len(trees), validated=True))
+    return _fold_trees(trees, [1] * len(trees))
 
 
 def _collect_pairs(pairs):

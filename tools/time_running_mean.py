@@ -56,6 +56,18 @@ def main(K=128, reps=20):
         res[f"B{B}_ms"] = round(ms, 4)
         res[f"B{B}_GBs"] = round(K * P * 4 / ms / 1e6, 1)
         res[f"B{B}_bitwise_eq_tree_mean"] = same
+    # the reference loop itself, through this package's tree_util (fed_avg.py:132-146)
+    def literal():
+        s = tu.tree_zeros_like(tmpl)
+        n = 0.
+        for c, w in zip(clients, weights):
+            s = tu.tree_add(s, tu.tree_weight(c, w))
+            n += w
+        return tu.tree_inverse_weight(s, n)
+    res["literal_loop_ms"] = round(wall(literal, 5), 4)
+    out = literal()
+    res["literal_loop_bitwise_eq_tree_mean"] = all(
+        torch.equal(a, b) for a, b in zip(fedjax_amd.pytree.leaves_of(out), fedjax_amd.pytree.leaves_of(ref)))
     print(json.dumps(res), flush=True)
 
 
