@@ -121,7 +121,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time host-resident deltas (H2D + fold + D2H)")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse N>1 on one GPU")
-    ap.add_argument("--all-ranks", action="store_true", help="all_reduce instead of reduce to rank 0")
+    ap.add_argument("--all-ranks", action="store_true",
+                    help="every rank needs the mean: all_reduce only (default: the mean is needed on rank 0, and "
+                         "the auto-tune may still pick all_reduce when RCCL runs it faster than reduce)")
     ap.add_argument("--engine", choices=["auto", "native", "torch"], default="auto",
                     help="N>1 exchange: native RCCL pipeline (include/fjcomm.h), torch.distributed, or the "
                          "faster of the two measured during warmup")
@@ -226,6 +228,7 @@ def main():
     buckets = (tuple(float(v) for v in args.buckets.split(":")) if ":" in args.buckets
                else int(args.buckets)) or 1
     root = 0
+    collective = "all_reduce" if args.all_ranks else "reduce"  # the exchange of the partials
 
     def step(events=None):
         wd = torch.from_numpy(np.float32(w_local)).pin_memory().to(dev, non_blocking=True)
@@ -248,15 +251,15 @@ def main():
             evs, spans = None, fd.bucket_edges(P, buckets)
             if events is not None:
                 evs = [kernels.Event() for _ in range(2 * len(spans))]
-            fd.sharded_weighted_mean(x, wd, W, buckets=buckets, out=out, all_ranks=args.all_ranks, comm=comm,
-                                     nontemporal=nt, fold_events=evs)
+            fd.sharded_weighted_mean(x, wd, W, buckets=buckets, out=out, all_ranks=collective == "all_reduce",
+                                     comm=comm, nontemporal=nt, fold_events=evs)
             if evs is not None:
                 for i, (p0, p1) in enumerate(spans):
                     events.append((evs[2 * i], evs[2 * i + 1], Kl * (p1 - p0) * esize))
         else:
-            fd.sharded_weighted_mean(x, wd, W, buckets=buckets, out=out, all_ranks=args.all_ranks,
+            fd.sharded_weighted_mean(x, wd, W, buckets=buckets, out=out, all_ranks=collective == "all_reduce",
                                      partial_fn=lambda xs, wdd, sc, o: fold(xs, wdd, o, events))
-        if sharded and final is not None and (rank == root or args.all_ranks):  # f32 mean -> leaf dtype
+        if sharded and final is not None and (rank == root or collective == "all_reduce"):  # f32 mean -> leaf dtype
             kernels.weighted_sum_dense(out.view(1, P), ones, out=final)
 
     def wall(nsteps):
@@ -275,18 +278,24 @@ def main():
     tune = {}
     if sharded and args.buckets == "0":
         # every rank measures every candidate and sees the same max-over-ranks times,
-        # so all ranks pick the same (engine, buckets) without another exchange
+        # so all ranks pick the same (engine, collective, buckets) without another exchange.
+        # The mean is needed on rank 0 only, so all_reduce is a candidate next to reduce:
+        # RCCL may run it faster (its all-reduce algorithms are the most tuned), and it
+        # leaves the same mean on rank 0 (within the tolerance of DESIGN.md §4).
         engines = ["native", "torch"] if comm is not None and args.engine == "auto" else [engine]
+        colls = ["all_reduce"] if args.all_ranks else ["reduce", "all_reduce"]
         for eng in engines:
-            for b in BUCKET_CANDIDATES:
-                if len(fd.bucket_edges(P, b)) < (b if isinstance(b, int) else len(b)):
-                    continue  # P too small for that many aligned buckets
-                engine, buckets = eng, b
-                wall(2)
-                tune[(eng, b)] = wall(5) / 5 * 1e3
-        engine, buckets = min(tune, key=tune.get)
-        tune = {f"{e}/{fd.bucket_name(b)}": t for (e, b), t in tune.items()}
-        log(f"exchange auto-tune (ms/step, max over ranks): {tune} -> {engine}/{fd.bucket_name(buckets)}")
+            for col in colls:
+                for b in BUCKET_CANDIDATES:
+                    if len(fd.bucket_edges(P, b)) < (b if isinstance(b, int) else len(b)):
+                        continue  # P too small for that many aligned buckets
+                    engine, collective, buckets = eng, col, b
+                    wall(2)
+                    tune[(eng, col, b)] = wall(5) / 5 * 1e3
+        engine, collective, buckets = min(tune, key=tune.get)
+        tune = {f"{e}/{c}/{fd.bucket_name(b)}": t for (e, c, b), t in tune.items()}
+        log(f"exchange auto-tune (ms/step, max over ranks): {tune} -> "
+            f"{engine}/{collective}/{fd.bucket_name(buckets)}")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -347,11 +356,12 @@ def main():
             "config": {"workload": desc, "clients": K, "params": P, "clients_per_gpu": Kl,
                        "parallelism": f"client-sharded x{nshard}" + (
                            f" + {'RCCL' if args.backend == 'nccl' else args.backend} "
-                           f"{'all_reduce' if args.all_ranks else 'reduce'}" if sharded else "") + (
+                           f"{collective}" if sharded else "") + (
                            " (REHEARSAL: one GPU runs rank 0's share, RCCL world 1)" if nshard != world else ""),
                        "buckets": (buckets if isinstance(buckets, int) else fd.bucket_name(buckets))
                        if sharded else 1,
                        "exchange_engine": engine if sharded else None,
+                       "exchange_collective": collective if sharded else None,
                        "exchange_autotune_ms": {k: round(t, 4) for k, t in tune.items()} or None,
                        "nontemporal": nt,
                        "variant": args.variant, "fused_l2_norms": bool(args.with_norms),
