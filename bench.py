@@ -136,6 +136,12 @@ def main():
     ap.add_argument("--with-norms", action="store_true",
                     help="fuse every client's delta l2 norm into the fold (examples/fed_avg.py:79-81)")
     args = ap.parse_args()
+    # stdout carries exactly one line, rank 0's JSON: native libraries write banners to fd 1
+    # (RCCL's version block, gloo's connection notes), so fd 1 is pointed at stderr for the
+    # rest of the run and the JSON goes to a saved copy of the original stdout
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -381,7 +387,7 @@ def main():
             res["rehearsal_projected_whole_job_GBs"] = round(value * nshard, 2)
         if not sharded and not args.no_cpu_baseline and dtype == torch.float32:
             res["cpu_baseline"] = cpu_baseline(K)
-        print(json.dumps(res), flush=True)
+        os.write(json_fd, (json.dumps(res) + "\n").encode())
     if comm is not None:
         torch.cuda.synchronize()
         comm.close()
