@@ -262,11 +262,18 @@ class DeltaIngestor:
     enqueued so far.
     """
 
-    def __init__(self, slab: ClientDeltaSlab, depth: int = 4):
+    def __init__(self, slab: ClientDeltaSlab, depth: Optional[int] = None, copy_threads: int = 4):
         self.slab = slab
+        # host threads of the staging copy: the DMA engine reads host memory at the same
+        # time, and a copy on every OpenMP thread slows it (128 x 16 MiB rows on MI355X:
+        # 46 GB/s end to end with 16 threads, 53 GB/s with 4 = 98 % of the 54 GB/s of
+        # back-to-back pinned row copies; profiles/r01zi_ingest_stages.jsonl)
+        self.copy_threads = max(1, int(copy_threads))
         self.device = slab.device
         self.stream = torch.cuda.Stream(self.device)
         self.row_bytes = slab.num_params * slab.storage.element_size()
+        if depth is None:  # 8 rows in flight (51-52 GB/s vs 46-47 with 4), at most ~1 GiB pinned
+            depth = max(2, min(8, (1 << 30) // max(1, self.row_bytes)))
         self.staging = [torch.empty(max(1, self.row_bytes), dtype=torch.uint8).pin_memory()
                         for _ in range(max(1, depth))]
         self.events: List[Optional[torch.cuda.Event]] = [None] * len(self.staging)
@@ -280,22 +287,14 @@ class DeltaIngestor:
         i = self.n % len(self.staging)
         if self.events[i] is not None:
             self.events[i].synchronize()  # the DMA that last used this row has finished
-        row = self.staging[i]
-        off = 0
-        for x, size in zip(leaves, self.slab.sizes):
-            a = _host_view(x, self.slab.dtype)
-            if a.size != size * self.slab.storage.element_size():
-                raise ValueError(f"client {k}: leaf of {a.size} bytes, slab expects "
-                                 f"{size * self.slab.storage.element_size()}")
-            if a.size:  # torch's host copy is multithreaded for large buffers
-                if a.flags.writeable:
-                    src = torch.from_numpy(a)
-                else:  # a read-only view into the payload: only ever read here
-                    with warnings.catch_warnings():
-                        warnings.simplefilter("ignore", UserWarning)
-                        src = torch.frombuffer(a, dtype=torch.uint8)
-                row[off:off + a.size].copy_(src)
-            off += a.size
+        prev_threads = torch.get_num_threads()
+        if prev_threads != self.copy_threads:
+            torch.set_num_threads(self.copy_threads)
+        try:
+            self._stage(k, leaves, self.staging[i])
+        finally:
+            if prev_threads != self.copy_threads:
+                torch.set_num_threads(prev_threads)
         dst = self.slab.storage[k].view(torch.uint8)[: self.row_bytes]
         if not self._after_compute:  # earlier kernels may still read the slab rows
             self.stream.wait_stream(torch.cuda.current_stream(self.device))
@@ -306,6 +305,24 @@ class DeltaIngestor:
             ev.record(self.stream)
         self.events[i] = ev
         self.n += 1
+
+    def _stage(self, k: int, leaves, row: torch.Tensor) -> None:
+        """Pack client k's leaves back to back into the pinned staging row."""
+        off = 0
+        for x, size in zip(leaves, self.slab.sizes):
+            a = _host_view(x, self.slab.dtype)
+            if a.size != size * self.slab.storage.element_size():
+                raise ValueError(f"client {k}: leaf of {a.size} bytes, slab expects "
+                                 f"{size * self.slab.storage.element_size()}")
+            if a.size:  # torch's host copy runs on copy_threads threads for large buffers
+                if a.flags.writeable:
+                    src = torch.from_numpy(a)
+                else:  # a read-only view into the payload: only ever read here
+                    with warnings.catch_warnings():
+                        warnings.simplefilter("ignore", UserWarning)
+                        src = torch.frombuffer(a, dtype=torch.uint8)
+                row[off:off + a.size].copy_(src)
+            off += a.size
 
     def ready(self) -> None:
         """Order the current stream after every enqueued copy (call before the fold)."""
