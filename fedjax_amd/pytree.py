@@ -104,17 +104,41 @@ def _node(tree) -> Tuple[str, Any, List[Any]]:
     return "leaf", None, []
 
 
+_INTERNED = {}  # (kind, aux, children) -> TreeDef: one object per structure (capped)
+
+
+def _intern(kind, aux, children) -> TreeDef:
+    """The TreeDef of (kind, aux, children), shared by every flatten of that structure, so
+    equality is identity and per-structure caches (compiled accessors, native specs) are
+    hit without rehashing the structure. Unhashable aux data (registered classes) is not
+    interned."""
+    key = (kind, aux, children)
+    try:
+        td = _INTERNED.get(key)
+    except TypeError:
+        return TreeDef(kind, aux, children)
+    if td is None:
+        td = TreeDef(kind, aux, children)
+        if len(_INTERNED) < 4096:
+            _INTERNED[key] = td
+    return td
+
+
 def flatten(tree) -> Tuple[List[Any], TreeDef]:
     leaves: List[Any] = []
+    leaf_types = _LEAF_TYPES
 
     def rec(x) -> TreeDef:
+        if type(x) in leaf_types:  # tensors / arrays: skip the node classification
+            leaves.append(x)
+            return _LEAF
         kind, aux, children = _node(x)
         if kind == "leaf":
             leaves.append(x)
             return _LEAF
         if kind == "none":
             return _NONE
-        return TreeDef(kind, aux, tuple([rec(c) for c in children]))
+        return _intern(kind, aux, tuple([rec(c) for c in children]))
 
     td = rec(tree)
     return leaves, td
