@@ -30,7 +30,8 @@
 //       None when any weight is something else (numpy scalar, tensor, bool, |w| >=
 //       2**53, ...): the caller then uses the Python path.
 //   fold_table(row0, ptrs, w_f32, scale, has_scale, nt_min_bytes, dev_index, stream,
-//              plan_fn, wsum_fn[, outs, accumulate]) -> (rc, outputs) | None
+//              plan_fn, wsum_fn[, outs, accumulate, wsum_l2_fn, l2_ws_bytes_fn, l2sq])
+//       -> (rc, outputs) | None   (l2sq: float32 [K] device tensor -> fjagg_wsum_l2_ptrs)
 //       The rest of tree_mean's host work for a gathered table (ptrs from gather_rows,
 //       weights from fold_weights) when every leaf is float32 and every pointer is
 //       16-byte aligned: fresh output leaves shaped like row0, the plan image of
@@ -227,16 +228,22 @@ PyObject* fold_weights(PyObject*, PyObject* args) {
 // fjagg_ptrs_plan_leaves / fjagg_wsum_ptrs of libfjagg.so (include/fjagg.h), passed in by address
 typedef int64_t (*PlanFn)(int, int, const int64_t*, const uint8_t*, int, int64_t*, int64_t);
 typedef int (*WsumFn)(int, int, int, const int64_t*, int, int64_t, int64_t, const void*, float, int, void*);
+typedef int64_t (*L2WsFn)(int64_t, int64_t);
+typedef int (*WsumL2Fn)(int, int, int, const int64_t*, int, int64_t, int64_t, const void*, float, float*, int, void*,
+                        int64_t, void*);
 constexpr int kF32 = 0, kScale = 1, kAccumulate = 2, kNontemporal = 4;  // fjagg.h enums
 
 PyObject* fold_table(PyObject*, PyObject* args) {
-  PyObject *row0, *ptrs, *wf, *dst = Py_None;
+  PyObject *row0, *ptrs, *wf, *dst = Py_None, *l2sq = Py_None;
   double scale, nt_min_bytes;
   int has_scale, dev, accumulate = 0;
-  unsigned long long stream, plan_addr, wsum_addr;
-  if (!PyArg_ParseTuple(args, "O!OOdidiKKK|Oi", &PyList_Type, &row0, &ptrs, &wf, &scale, &has_scale, &nt_min_bytes,
-                        &dev, &stream, &plan_addr, &wsum_addr, &dst, &accumulate))
+  unsigned long long stream, plan_addr, wsum_addr, l2_addr = 0, l2ws_addr = 0;
+  if (!PyArg_ParseTuple(args, "O!OOdidiKKK|OiKKO", &PyList_Type, &row0, &ptrs, &wf, &scale, &has_scale,
+                        &nt_min_bytes, &dev, &stream, &plan_addr, &wsum_addr, &dst, &accumulate, &l2_addr,
+                        &l2ws_addr, &l2sq))
     return nullptr;
+  const bool with_l2 = l2sq != Py_None;
+  if (with_l2 && (!THPVariable_Check(l2sq) || !l2_addr || !l2ws_addr)) Py_RETURN_NONE;
   const Py_ssize_t L = PyList_GET_SIZE(row0);
   if (dst != Py_None && (!PyList_Check(dst) || PyList_GET_SIZE(dst) != L)) Py_RETURN_NONE;
   if (accumulate && dst == Py_None) Py_RETURN_NONE;
@@ -258,6 +265,12 @@ PyObject* fold_table(PyObject*, PyObject* args) {
   if (K < 1 || bw.len < 4 * K) Py_RETURN_NONE;
   const auto* in = static_cast<const int64_t*>(bp.buf);
   try {
+    if (with_l2) {
+      const at::Tensor& q = THPVariable_Unpack(l2sq);
+      if (q.scalar_type() != at::kFloat || q.numel() != K || !q.is_contiguous() || !q.is_cuda() ||
+          q.get_device() != dev)
+        Py_RETURN_NONE;
+    }
     // fast case only: float32 leaves (fold type and output type are then float32 for any
     // weights). A leaf with a client pointer off 16 bytes walks element units (per-leaf
     // plan); the outputs are fresh allocations, so aligned.
@@ -269,6 +282,7 @@ PyObject* fold_table(PyObject*, PyObject* args) {
       leaf_n[l] = t.numel();
       total += leaf_n[l];
     }
+    if (total == 0) Py_RETURN_NONE;  // only empty leaves: the Python path (no launch at all)
     std::vector<int64_t> lbits(L, 0);
     for (int64_t k = 0; k < K; ++k)
       for (Py_ssize_t l = 0; l < L; ++l) lbits[l] |= in[k * L + l];
@@ -311,9 +325,19 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
     const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0);
     const int64_t* dp = dimg.data_ptr<int64_t>();
-    const int rc = reinterpret_cast<WsumFn>(wsum_addr)(kF32, kF32, kF32, dp, static_cast<int>(L), K, nblk,
-                                                       dp + (n - nw), static_cast<float>(scale), flags,
-                                                       reinterpret_cast<void*>(stream));
+    int rc;
+    if (with_l2) {  // fused per-client squared l2 norms (fjagg_wsum_l2_ptrs), workspace from torch's allocator
+      const at::Tensor& q = THPVariable_Unpack(l2sq);
+      const int64_t need = reinterpret_cast<L2WsFn>(l2ws_addr)(K, nblk);
+      if (need < 0) Py_RETURN_NONE;
+      at::Tensor ws = at::empty({need > 4 ? need : 4}, dimg.options().dtype(at::kByte));
+      rc = reinterpret_cast<WsumL2Fn>(l2_addr)(kF32, kF32, kF32, dp, static_cast<int>(L), K, nblk, dp + (n - nw),
+                                               static_cast<float>(scale), q.data_ptr<float>(), flags,
+                                               ws.data_ptr(), ws.numel(), reinterpret_cast<void*>(stream));
+    } else {
+      rc = reinterpret_cast<WsumFn>(wsum_addr)(kF32, kF32, kF32, dp, static_cast<int>(L), K, nblk, dp + (n - nw),
+                                               static_cast<float>(scale), flags, reinterpret_cast<void*>(stream));
+    }
     PyObject* list = PyList_New(L);
     if (!list) return nullptr;
     for (Py_ssize_t l = 0; l < L; ++l) PyList_SET_ITEM(list, l, THPVariable_Wrap(std::move(outs[l])));

@@ -186,9 +186,8 @@ def _fold(rows, weights, *, scale=None,
     if accumulate and out is None:
         raise ValueError("accumulate needs out")
     table = rows if isinstance(rows, _Table) else None
-    if (table is not None and l2sq is None and nontemporal is None
-            and isinstance(weights, _Weights) and table.row0):
-        outs = _native_fold(table, weights, scale, out, accumulate)
+    if (table is not None and nontemporal is None and isinstance(weights, _Weights) and table.row0):
+        outs = _native_fold(table, weights, scale, out, accumulate, l2sq)
         if outs is not None:
             return outs
     if table is not None:
@@ -271,28 +270,31 @@ def _fold(rows, weights, *, scale=None,
     return outs
 
 
-_ENTRY_ADDRS = None  # (fjagg_ptrs_plan_leaves, fjagg_wsum_ptrs) addresses for fjhost.fold_table
+_ENTRY_ADDRS = None  # (plan_leaves, wsum_ptrs, wsum_l2_ptrs, l2 workspace bytes) addresses for fjhost.fold_table
 
 
 def _native_fold(table: "_Table", packed: "_Weights", scale, out=None,
-                 accumulate: bool = False) -> Optional[List[torch.Tensor]]:
+                 accumulate: bool = False, l2sq: Optional[torch.Tensor] = None) -> Optional[List[torch.Tensor]]:
     """The common case of :func:`_fold` in one native call (fjhost.fold_table): float32
     leaves, Python-number weights, fresh outputs or the caller's float32 ``out`` leaves
-    (``accumulate`` folds into them; misaligned leaves get the per-leaf plan). It builds the same plan
+    (``accumulate`` folds into them; misaligned leaves get the per-leaf plan); with ``l2sq``
+    also every client's squared l2 norm (fjagg_wsum_l2_ptrs). It builds the same plan
     image and launches the same kernel as the Python path below; None when the case does
     not hold (nothing launched)."""
     global _ENTRY_ADDRS
     if _ENTRY_ADDRS is None:
         lib = _lib.load()
         _ENTRY_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
-                             for f in ("fjagg_ptrs_plan_leaves", "fjagg_wsum_ptrs"))
+                             for f in ("fjagg_ptrs_plan_leaves", "fjagg_wsum_ptrs", "fjagg_wsum_l2_ptrs",
+                                       "fjagg_wsum_l2_ptrs_workspace_bytes"))
     dev = table.row0[0].device
     if dev.type != "cuda":
         return None
     sc = float(np.float32(scale)) if scale is not None else 1.0
     got = _lib.host().fold_table(table.row0, table.ptrs, packed.f32, sc, scale is not None,
                                  float(NONTEMPORAL_MIN_BYTES), dev.index, torch.cuda.current_stream(dev).cuda_stream,
-                                 *_ENTRY_ADDRS, list(out) if out is not None else None, 1 if accumulate else 0)
+                                 _ENTRY_ADDRS[0], _ENTRY_ADDRS[1], list(out) if out is not None else None,
+                                 1 if accumulate else 0, _ENTRY_ADDRS[2], _ENTRY_ADDRS[3], l2sq)
     if got is None:
         return None
     rc, outs = got

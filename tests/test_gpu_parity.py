@@ -795,3 +795,25 @@ def test_native_fold_table_is_used_and_declines(cuda):
     assert torch.equal(fast_odd[0].view(torch.int32), slow_odd[0].view(torch.int32))
     m = tu.tree_mean(zip(odd, w))
     assert torch.equal(m["a"], tu.tree_mean(zip([{"a": base[k, 1:].clone()} for k in range(5)], w))["a"])
+
+
+def test_native_fold_table_fused_l2(cuda):
+    """fjhost.fold_table with l2sq launches fjagg_wsum_l2_ptrs: the mean and norms are
+    bitwise those of the Python fused path, for aligned and misaligned leaves."""
+    g = torch.Generator(device="cpu").manual_seed(9)
+    base = torch.randn(7, 3001, generator=g).to(cuda)
+    for off in (0, 1):
+        trees = [{"a": base[k, off:off + 1000], "b": base[k, off + 1000:off + 3000]} for k in range(7)]
+        w = [3, 1, 4, 1, 5, 9, 2]
+        _, rows = tu._client_table(trees)
+        assert isinstance(rows, tu._Table)
+        q_fast = torch.empty(7, device=cuda)
+        fast = tu._native_fold(rows, tu._pack_weights(w), tu._inverse(25.0), None, False, q_fast)
+        assert fast is not None
+        q_slow = torch.empty(7, device=cuda)
+        slow = tu._fold([[t["a"], t["b"]] for t in trees], w, scale=tu._inverse(25.0), validated=True, l2sq=q_slow)
+        for a, b in zip(fast, slow):
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+        assert torch.equal(q_fast.view(torch.int32), q_slow.view(torch.int32))
+        m, n = tu.tree_mean_with_l2_norms(zip(trees, w))
+        assert torch.equal(m["a"], fast[0]) and torch.equal(n, torch.sqrt(q_fast))
