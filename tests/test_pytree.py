@@ -62,3 +62,26 @@ def test_aggregator_is_pytree_dataclass():
     leaves, _ = pytree.flatten(agg)
     assert len(leaves) == 2
     assert isinstance(agg.init(), fedjax_amd.aggregators.MeanAggregatorState)
+
+
+def test_treedefs_are_interned():
+    """Flattens of one structure share one TreeDef object (per-structure caches hit by
+    identity); different structures stay different; unhashable aux data is not interned."""
+    import numpy as np
+    a = {"b": {"w": np.zeros(3), "b": np.zeros(2)}, "a": [np.zeros(1), (np.zeros(1), None)]}
+    b = {"a": [np.ones(1), (np.ones(1), None)], "b": {"b": np.ones(2), "w": np.ones(3)}}
+    la, ta = pytree.flatten(a)
+    lb, tb = pytree.flatten(b)
+    assert ta is tb and len(la) == len(lb) == 4
+    _, tc = pytree.flatten({"a": [np.zeros(1), [np.zeros(1), None]], "b": {"w": 0, "b": 0}})
+    assert tc != ta and tc is not ta
+    assert pytree.unflatten(ta, lb)["b"]["w"] is b["b"]["w"]
+
+    class Box:
+        def __init__(self, v, meta):
+            self.v, self.meta = v, meta
+    pytree.register_pytree_node(Box, lambda x: ([x.v], x.meta), lambda aux, ch: Box(ch[0], aux))
+    t1 = pytree.flatten(Box(np.zeros(2), {"unhashable": 1}))[1]
+    t2 = pytree.flatten(Box(np.zeros(2), {"unhashable": 1}))[1]
+    assert t1 is not t2  # aux is a dict: built fresh each time
+    assert pytree.unflatten(t1, [np.ones(2)]).meta == {"unhashable": 1}
