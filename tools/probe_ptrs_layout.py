@@ -73,7 +73,13 @@ def main(K=128):
         "clones": [tmap(lambda v: v.clone(), slab.client(k)) for k in range(K)],
         "packed": [packed_copy(slab.client(k), dev) for k in range(K)],
     }
+    # is the gap in the big leaf or in the seven small ones? clones of linear/w alone vs its views
+    big = {"views_linear_w_only": [{"w": c["linear"]["w"]} for c in placements["views"]],
+           "clones_linear_w_only": [{"w": c["linear"]["w"]} for c in placements["clones"]]}
     res = {"workload": "configs[1] 128 x EMNIST-CNN, 8 leaves", "bytes": K * P * 4}
+    for name, clients in big.items():
+        pairs = list(zip(clients, weights))
+        res[name] = {"ms": round(gpu_ms(lambda: tu.tree_mean(pairs)), 4)}
     ref = None
     for name, clients in placements.items():
         pairs = list(zip(clients, weights))
