@@ -2,6 +2,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2] [--e2e]
 
+``--gpus N`` > 1 works bare (this process spawns N ranks through a
+``torch.distributed.run`` child and forwards rank 0's JSON line) or under an
+outer ``torch.distributed.run`` (WORLD_SIZE set: this process is one rank).
+
 One step = one weighted mean of the round's client deltas, already resident in
 HBM: host W and f32 weights (4 KiB pinned H2D) + the fold kernel, exactly what
 ``ClientDeltaSlab.mean`` / ``sharded_weighted_mean`` do per round.
@@ -64,11 +68,21 @@ def fedavg_weights(K, seed=1):
     return np.random.RandomState(seed).randint(1, 501, size=K).tolist()
 
 
-def cpu_baseline(K, seconds=8.0):
-    """Reference op sequence (per client: fresh w*x buffer, in-place add; final
-    scale) on the host, 1 thread and all usable cores, bounded sample."""
-    import ctypes
+def _cgroup_cpus():
+    """CPUs the cgroup quota grants this process (cpu.max), or None without a quota."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else max(1, int(round(int(quota) / int(period))))
+    except (OSError, ValueError):
+        return None
 
+
+def cpu_baseline(K, seconds=6.0):
+    """Reference op sequence (per client: fresh w*x buffer, in-place add; final
+    scale) on the host, bounded sample, timed at 1 thread, at the cgroup's CPU
+    share and at every core this process may run on (os.sched_getaffinity, SURVEY
+    §8(d)). ``value`` / ``cores`` are the all-cores run; ``sweep`` holds the others."""
     from tests import coracle as co
 
     lib_path = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
@@ -80,22 +94,68 @@ def cpu_baseline(K, seconds=8.0):
     x = o.synth_f32(K, Ps, seed=0)
     w = np.float32(fedavg_weights(K))
     r = np.float32(1.0 / float(sum(fedavg_weights(K))))
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores = len(os.sched_getaffinity(0))
+    share = _cgroup_cpus()
     res = {}
-    for nt in sorted({1, cores}):
+    for nt in sorted({1, cores} | ({min(share, cores)} if share else set())):
         reps, t = 0, 0.0
-        while t < seconds / 2 or reps < 2:
+        while t < seconds / 3 or reps < 2:
             t0 = time.perf_counter()
             o.refseq_f32(x, w, r, nthreads=nt)
             t += time.perf_counter() - t0
             reps += 1
         res[nt] = K * Ps * 4 * reps / t / 1e9
-    del ctypes
     return {"value": round(res[cores], 2), "unit": "GB/s", "cores": cores, "kind": "port",
             "single_thread_value": round(res[1], 2),
+            "sweep": {str(n): round(v, 2) for n, v in sorted(res.items())},
+            "cgroup_cpu_share": share,
             "sample": f"{K} clients x {Ps} params fp32 ({K * Ps * 4 / 2**30:.2f} GiB), reference op "
                       f"sequence (tree_util.py:85-96) restated in C, oracle/fold_ref.c; "
-                      f"{os.uname().machine} host, {cores} of {len(os.sched_getaffinity(0))} visible cores"}
+                      f"{os.uname().machine} host, {cores} threads = every core in sched_getaffinity"
+                      + (f" (cgroup quota: {share} CPUs)" if share else "")}
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(nproc: int, argv, script: str = None, timeout: float = None) -> int:
+    """Run ``script argv`` as ``nproc`` ranks of one node and forward rank 0's JSON line.
+
+    A bare ``python bench.py --gpus N`` (no WORLD_SIZE in the environment) lands here
+    before anything touches the GPU. The ranks are children of this process
+    (``python -m torch.distributed.run``, rendezvous on 127.0.0.1): nothing is exec'd.
+    Every rank's stderr passes through; stdout is collected and only the JSON line
+    (rank 0's) is printed. Returns the launcher's exit status, non-zero if any rank
+    failed or no JSON line came back."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script or os.path.abspath(__file__),
+           *argv]
+    env = dict(os.environ, FJ_BENCH_LAUNCHER="bench.py -> torch.distributed.run child")
+    log("+", " ".join(cmd))
+    try:
+        proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        log(f"spawned ranks did not finish within {timeout} s")
+        return 124
+    lines = [ln for ln in proc.stdout.decode(errors="replace").splitlines() if ln.startswith("{")]
+    if proc.returncode != 0:
+        log(f"rank launcher exited with status {proc.returncode}")
+        return proc.returncode
+    if len(lines) != 1:
+        log(f"expected one JSON line from rank 0, got {len(lines)}")
+        return 1
+    sys.stdout.write(lines[0] + "\n")
+    sys.stdout.flush()
+    return 0
 
 
 def load_traffic(workload):
@@ -136,6 +196,13 @@ def main():
     ap.add_argument("--with-norms", action="store_true",
                     help="fuse every client's delta l2 norm into the fold (examples/fed_avg.py:79-81)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # bare `python bench.py --gpus N`: one rank per GPU as child processes (no GPU
+        # call has happened in this process, and nothing is exec'd)
+        if args.backend == "nccl" and torch.cuda.device_count() < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} needs {args.gpus} visible GPUs for RCCL "
+                             f"(found {torch.cuda.device_count()}); --backend gloo rehearses on fewer")
+        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:]))
     # stdout carries exactly one line, rank 0's JSON: native libraries write banners to fd 1
     # (RCCL's version block, gloo's connection notes), so fd 1 is pointed at stderr for the
     # rest of the run and the JSON goes to a saved copy of the original stdout
@@ -350,6 +417,10 @@ def main():
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
+            "ranks": world,
+            "rccl_ranks": world if (sharded and args.backend == "nccl" and nshard == world) else 0,
+            "launcher": os.environ.get("FJ_BENCH_LAUNCHER",
+                                       "torch.distributed.run" if "WORLD_SIZE" in os.environ else "direct"),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 from typing import Any, List, Optional
 
+import numpy as np
 import torch
 
 from fedjax_amd import pytree, tree_util
@@ -34,12 +35,20 @@ class RunningMean:
     """Running weighted sum of client deltas with the structure of ``template``.
 
     ``add(delta, weight)`` may be called with device or host pytrees; deltas are
-    buffered (references only) and folded ``buffer_clients`` at a time. ``result()``
-    returns ``tree_inverse_weight(sum, total_weight)`` (tree_util.py:35-38).
+    buffered and folded ``buffer_clients`` at a time. ``result()`` returns
+    ``tree_inverse_weight(sum, total_weight)`` (tree_util.py:35-38).
+
+    Buffering holds references, not copies. The reference's loop reads each delta at
+    its ``tree_add``, so a caller that updates a delta tensor in place after ``add()``
+    (reusing one buffer for every client, as torch loops often do) would change the
+    sum here but not there. Each tensor leaf's in-place version counter is recorded
+    at ``add()`` and checked before the buffer is read: a changed leaf raises
+    ``RuntimeError``. ``copy_on_add=True`` clones every delta at ``add()`` instead
+    (one extra device copy per client; safe for any reuse).
     """
 
     def __init__(self, template: PyTree, *, buffer_clients: int = 8,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, copy_on_add: bool = False):
         leaves, self.treedef = pytree.flatten(template)
         self.device = device or tree_util._find_device(leaves)
         zeros = tree_util.tree_zeros_like(pytree.unflatten(self.treedef, [
@@ -50,11 +59,35 @@ class RunningMean:
         self.buffer_clients = max(1, int(buffer_clients))
         self._trees: List[PyTree] = []
         self._weights: List[Any] = []
+        self._versions: List[Any] = []
+        self.copy_on_add = bool(copy_on_add)
+        self._spec = pytree.native_spec(self.treedef)
+        self._nleaves = len(self._sum)
+
+    def _leaf_versions(self, trees: List[PyTree]):
+        """int64 [len(trees), L] in-place version counters of every tensor leaf (-1 for
+        host arrays and scalars, which carry none); ValueError on a structure mismatch."""
+        L = self._nleaves
+        v = np.empty((len(trees), L), dtype=np.int64)
+        if self._spec is not None:
+            from fedjax_amd import _lib
+            if _lib.host().leaf_versions(trees, self._spec, L, v) == 0:
+                return v
+        for k, t in enumerate(trees):  # other leaf types or node kinds; raises on mismatch
+            v[k] = [x._version if isinstance(x, torch.Tensor) else -1
+                    for x in pytree.flatten_as(self.treedef, t)]
+        return v
 
     def add(self, delta: PyTree, weight) -> None:
         """tree_add(sum, tree_weight(delta, weight)); fed_avg.py:137-139. The delta is
-        buffered by reference; its leaves are read when the buffer is folded."""
+        buffered by reference (a clone with ``copy_on_add``); its leaves are read when
+        the buffer is folded, after checking that none was modified in place since."""
         w = tree_util._host_weight(weight)
+        if self.copy_on_add:
+            delta = pytree.unflatten(self.treedef, [
+                x.clone() if isinstance(x, torch.Tensor) else x for x in pytree.flatten_as(self.treedef, delta)])
+        else:
+            self._versions.append(self._leaf_versions([delta])[0])
         self._trees.append(delta)
         self._weights.append(w)
         self.total_weight += w
@@ -70,10 +103,14 @@ class RunningMean:
         flattened against the template and copied to the device first."""
         if not self._trees:
             return
-        trees, weights = self._trees, self._weights
-        self._trees, self._weights = [], []
+        trees, weights, versions = self._trees, self._weights, self._versions
+        self._trees, self._weights, self._versions = [], [], []
         if not self._sum:  # dtype rules checked by _fold (the sum has the template's dtypes)
             return
+        if versions and not np.array_equal(self._leaf_versions(trees), np.stack(versions)):
+            raise RuntimeError("a buffered client delta was modified in place after RunningMean.add(); "
+                               "the reference would have summed its value at add() time. Add a copy, "
+                               "or construct RunningMean(..., copy_on_add=True)")
         td, rows = tree_util._client_table(trees)
         if not (td == self.treedef and isinstance(rows, tree_util._Table)
                 and rows.row0[0].device == self.device):

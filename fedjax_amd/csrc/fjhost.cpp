@@ -21,6 +21,11 @@
 //       cuda:dev_index (-1: host tensors, for the CPU tests), strided and contiguous,
 //       with row0[l]'s dtype and shape. Also writes row0's pointers to row 0 when k0 == 1.
 //       Returns 0, or -(k+1) for the first client k that does not match.
+//   leaf_versions(trees, spec, L, out) -> int
+//       out[k*L + l] = Tensor._version of client k's leaf l (torch's in-place modification
+//       counter), walking every tree against `spec`; any tensor type. 0, or -(k+1) for the
+//       first client whose structure differs. RunningMean records these at add() and checks
+//       them before the buffered deltas are read (a delta updated in place after add()).
 //   fold_weights(weights, f32_out, i32_out_or_None) -> (W, kinds) | None
 //       For weights that are all Python int / float (not bool): f32_out[k] =
 //       float32(w_k) (numpy's np.float32(w) rounding), i32_out[k] = the int32 wrap of an
@@ -53,17 +58,23 @@
 namespace {
 
 struct Walk {
-  const std::vector<at::ScalarType>* dtypes;
+  const std::vector<at::ScalarType>* dtypes;  // nullptr: record versions only (leaf_versions)
   const std::vector<c10::IntArrayRef>* sizes;
   c10::DeviceIndex dev;
-  int64_t* out;  // row of L pointers
+  int64_t* out;  // row of L pointers (or L versions)
   size_t leaf;
+  size_t cap = 0;  // leaf_versions: slots in the row
 };
 
 enum { kLeaf = 0, kNone = 1, kDict = 2, kList = 3, kTuple = 4 };
 
 // 0: matches; 1: mismatch (no Python error set); -1: Python error set.
 int leaf(PyObject* x, Walk& w) {
+  if (w.dtypes == nullptr) {  // leaf_versions: any tensor, its in-place modification counter
+    if (!THPVariable_Check(x) || w.leaf >= w.cap) return 1;
+    w.out[w.leaf++] = static_cast<int64_t>(THPVariable_Unpack(x)._version());
+    return 0;
+  }
   if (Py_TYPE(x) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) return 1;
   size_t l = w.leaf++;
   if (l >= w.dtypes->size()) return 1;
@@ -164,6 +175,32 @@ PyObject* gather_rows(PyObject*, PyObject* args) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
   }
+}
+
+PyObject* leaf_versions(PyObject*, PyObject* args) {
+  PyObject *trees, *spec, *vers;
+  Py_ssize_t L;
+  if (!PyArg_ParseTuple(args, "O!OnO", &PyList_Type, &trees, &spec, &L, &vers)) return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(trees);
+  Py_buffer buf;
+  if (PyObject_GetBuffer(vers, &buf, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) != 0) return nullptr;
+  struct Release {
+    Py_buffer* b;
+    ~Release() { PyBuffer_Release(b); }
+  } release{&buf};
+  if (L < 0 || buf.len < static_cast<Py_ssize_t>(sizeof(int64_t)) * K * L) {
+    PyErr_SetString(PyExc_ValueError, "leaf_versions: version buffer smaller than K*L int64");
+    return nullptr;
+  }
+  Walk w{nullptr, nullptr, 0, nullptr, 0, static_cast<size_t>(L)};
+  for (Py_ssize_t k = 0; k < K; ++k) {
+    w.out = static_cast<int64_t*>(buf.buf) + k * L;
+    w.leaf = 0;
+    int rc = walk(spec, PyList_GET_ITEM(trees, k), w);
+    if (rc < 0) return nullptr;
+    if (rc > 0 || w.leaf != static_cast<size_t>(L)) return PyLong_FromSsize_t(-(k + 1));
+  }
+  return PyLong_FromLong(0);
 }
 
 PyObject* fold_weights(PyObject*, PyObject* args) {
@@ -350,6 +387,7 @@ PyObject* fold_table(PyObject*, PyObject* args) {
 
 PyMethodDef kMethods[] = {
     {"gather_rows", gather_rows, METH_VARARGS, "pointer table of K client pytrees (see fjhost.cpp)"},
+    {"leaf_versions", leaf_versions, METH_VARARGS, "torch in-place version counters of K pytrees' leaves"},
     {"fold_weights", fold_weights, METH_VARARGS, "f32/i32 weights and W of Python-number weights"},
     {"fold_table", fold_table, METH_VARARGS, "plan image + output leaves + fjagg_wsum_ptrs launch (see fjhost.cpp)"},
     {nullptr, nullptr, 0, nullptr},

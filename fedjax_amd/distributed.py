@@ -35,7 +35,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from fedjax_amd import _lib, kernels, tree_util
+from fedjax_amd import _lib, kernels, pytree, tree_util
 
 # bucket edges are multiples of this many elements (keeps 16-byte alignment)
 BUCKET_ALIGN = 1024
@@ -212,38 +212,76 @@ def sharded_weighted_mean(x_local: torch.Tensor, w_local: torch.Tensor, W_total,
 
 
 def sharded_tree_mean(local_pytrees_and_weights, *, W_total=None, group=None, dst: int = 0,
-                      all_ranks: bool = False):
+                      all_ranks: bool = False, template=None):
     """``tree_mean`` over the union of every rank's clients.
 
     Each rank folds its own (pytree, weight) pairs in one pytree-kernel launch
     (already scaled by f32(1/W)); the float32 partial leaves are packed into one
-    buffer and summed across ranks. Returns the mean pytree (float32 leaves) on
-    ``dst`` (on every rank with ``all_ranks``), ``None`` elsewhere or when no rank
-    has a client.
+    buffer and summed across ranks. Returns the mean pytree (float32 leaves) on the
+    global rank ``dst`` (on every rank with ``all_ranks``), ``None`` elsewhere.
+
+    A rank may hold no clients (``shard_range`` gives some ranks none when K < world
+    size): it contributes a zero partial, so every rank reaches the same collectives.
+    One small all_gather of (local W, partial size) runs first; it gives every rank
+    W (when ``W_total`` is None) and lets all ranks agree on the partial's size — or
+    raise together when the ranks' trees disagree. A rank that must return the mean
+    but has no clients needs ``template`` (any pytree with the clients' structure and
+    leaf shapes, e.g. the server params) for the structure of the result. Returns
+    ``None`` on every rank when no rank has a client.
     """
     pairs = list(local_pytrees_and_weights)
     trees = [t for t, _ in pairs]
     weights = [tree_util._host_weight(w) for _, w in pairs]
+    W_local = 0.0
+    for w in weights:
+        W_local += w  # tree_util.py:95 on this rank's share
+    nccl = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
+    td, views, sizes = None, None, None
+    if trees:
+        td, rows = tree_util._client_table(trees)
+        row0 = rows[0]
+        if any(x.dtype != torch.float32 for x in row0):
+            raise TypeError("sharded_tree_mean needs float32 leaves")
+        sizes = [x.numel() for x in row0]
+        shapes = [x.shape for x in row0]
+        dev = row0[0].device if row0 else dev
+    elif template is not None:
+        leaves, td = pytree.flatten(template)
+        shapes = [tuple(tree_util._to_tensor(x).shape) for x in leaves]
+        sizes = [int(np.prod(s, dtype=np.int64)) for s in shapes]
+    P = sum(sizes) if sizes is not None else -1
+    hdr = torch.tensor([float(W_local), float(P), float(len(trees))], dtype=torch.float64,
+                       device=dev if nccl else None)
+    world = dist.get_world_size(group)
+    got = [torch.empty_like(hdr) for _ in range(world)]
+    dist.all_gather(got, hdr, group=group)
+    got = [t.cpu().numpy() for t in got]
     if W_total is None:
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else None
-        W_total = total_weight(weights, group=group, device=dev)
-    if not trees:
-        raise ValueError("every rank needs at least one client (use shard_range)")
-    td, rows = tree_util._client_table(trees)
-    row0 = rows[0]
-    sizes = [x.numel() for x in row0]
-    flat = torch.empty(sum(sizes), dtype=torch.float32, device=row0[0].device)
-    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-    views = [flat[o:o + n].view(x.shape) for o, n, x in zip(offs[:-1], sizes, row0)]
-    if any(x.dtype != torch.float32 for x in row0):
-        raise TypeError("sharded_tree_mean needs float32 leaves")
-    tree_util._fold(rows, weights, scale=tree_util._inverse(W_total), out=views, accumulate=False,
-                    validated=True)
+        W_total = 0.0
+        for g in got:
+            W_total += float(g[0])  # rank order: the same W on every rank
+    if sum(int(g[2]) for g in got) == 0:
+        return None  # no rank has a client (tree_util.py:96)
+    Ps = {int(g[1]) for g in got} - {-1}
+    if len(Ps) != 1:  # every rank sees the same header, so all of them raise here together
+        raise ValueError(f"ranks disagree on the number of parameters: {sorted(Ps)}")
+    flat = torch.zeros(Ps.pop(), dtype=torch.float32, device=dev)
+    if trees:
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        views = [flat[o:o + n].view(sh) for o, n, sh in zip(offs[:-1], sizes, shapes)]
+        tree_util._fold(rows, weights, scale=tree_util._inverse(W_total), out=views, accumulate=False,
+                        validated=True)
+    elif td is not None:
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        views = [flat[o:o + n].view(sh) for o, n, sh in zip(offs[:-1], sizes, shapes)]
     if all_ranks:
         dist.all_reduce(flat, group=group)
     else:
-        dist.reduce(flat, dst=dst, group=group)
-    if all_ranks or dist.get_rank(group) == dst:
-        from fedjax_amd import pytree
+        dist.reduce(flat, dst=dst, group=group)  # dst is a global rank (torch.distributed)
+    if all_ranks or dist.get_rank() == dst:
+        if views is None:
+            raise ValueError("this rank holds no clients and must return the mean: pass template= "
+                             "(a pytree with the clients' structure) to shape the result")
         return pytree.unflatten(td, views)
     return None

@@ -189,6 +189,7 @@ def _compile(td: TreeDef):
     ``td`` (then flatten_as takes the general walk, which also builds the error). Other
     node kinds are not compiled (returns None)."""
     lines, names = [], []
+    consts: List[Any] = []  # dict keys, passed as objects (repr(key) need not be an expression)
     counter = [0]
 
     def var():
@@ -206,15 +207,18 @@ def _compile(td: TreeDef):
             return True
         if k == "dict":
             lines.append(f"if type({ref}) is not dict or len({ref}) != {len(t.aux)}: return None")
-            keys = list(t.aux)
+            keys = []
+            for key in t.aux:
+                keys.append(f"C[{len(consts)}]")
+                consts.append(key)
         elif k in ("list", "tuple"):
             lines.append(f"if type({ref}) is not {k} or len({ref}) != {t.aux}: return None")
-            keys = list(range(t.aux))
+            keys = [str(i) for i in range(t.aux)]
         else:
             return False
         for key, c in zip(keys, t.children):
             v = var()
-            lines.append(f"{v} = {ref}[{key!r}]")
+            lines.append(f"{v} = {ref}[{key}]")
             if not emit(c, v):
                 return False
         return True
@@ -224,7 +228,7 @@ def _compile(td: TreeDef):
             return None
         body = "\n    ".join(lines + [f"return [{', '.join(names)}]"])
         src = f"def fast(x):\n  try:\n    {body}\n  except (KeyError, IndexError, TypeError):\n    return None\n"
-        ns = {"LT": _LEAF_TYPES}
+        ns = {"LT": _LEAF_TYPES, "C": tuple(consts)}
         exec(compile(src, f"<pytree accessor {len(names)} leaves>", "exec"), ns)  # noqa: S102 - generated
         return ns["fast"]
     except (SyntaxError, RecursionError, ValueError):

@@ -154,11 +154,17 @@ static void* refseq_worker(void* arg) {
 int oracle_tree_mean_refseq_f32(const float* x, int64_t ld, int64_t K, int64_t P,
                                 const float* w, float scale, float* y, int nthreads) {
   if (nthreads < 1) nthreads = 1;
-  if (nthreads > 256) nthreads = 256;
-  pthread_t th[256];
-  struct refseq_job jobs[256];
+  if (nthreads > 4096) nthreads = 4096;
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  struct refseq_job* jobs = (struct refseq_job*)calloc((size_t)nthreads, sizeof(struct refseq_job));
+  int* spawned = (int*)calloc((size_t)nthreads, sizeof(int));
+  if (!th || !jobs || !spawned) {
+    free(th);
+    free(jobs);
+    free(spawned);
+    return -1;
+  }
   const int64_t chunk = ((P + nthreads - 1) / nthreads + 15) / 16 * 16;
-  int spawned[256] = {0};
   for (int i = 0; i < nthreads; ++i) {
     int64_t p0 = (int64_t)i * chunk, p1 = p0 + chunk;
     if (p0 > P) p0 = P;
@@ -173,5 +179,8 @@ int oracle_tree_mean_refseq_f32(const float* x, int64_t ld, int64_t K, int64_t P
   refseq_worker(&jobs[0]);
   for (int i = 1; i < nthreads; ++i)
     if (spawned[i]) pthread_join(th[i], NULL);
+  free(th);
+  free(jobs);
+  free(spawned);
   return 0;
 }

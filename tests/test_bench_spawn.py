@@ -1,0 +1,68 @@
+"""bench.py's rank launcher (CPU): a bare ``python bench.py --gpus N`` spawns N ranks
+through a ``torch.distributed.run`` child and forwards rank 0's single JSON line.
+
+The rank script here stands in for bench.py's GPU body: it joins a world-size-N gloo
+group (the same rendezvous the real ranks use), all-reduces its rank, and rank 0
+prints the JSON line; the launcher logic under test is bench.spawn_ranks itself."""
+import json
+import os
+import textwrap
+
+import pytest
+
+import bench
+
+RANK_SCRIPT = textwrap.dedent("""
+    import json, os, sys
+    import torch, torch.distributed as dist
+    fail_rank = int(sys.argv[1])
+    dist.init_process_group("gloo")
+    r, n = dist.get_rank(), dist.get_world_size()
+    t = torch.tensor([float(r)])
+    dist.all_reduce(t)
+    print(f"rank {r} banner on stdout")  # native libraries print banners; only JSON is forwarded
+    if r == fail_rank:
+        sys.exit(3)
+    if r == 0:
+        print(json.dumps({"n_gpus": n, "ranksum": t.item(),
+                          "launcher": os.environ.get("FJ_BENCH_LAUNCHER")}))
+    dist.destroy_process_group()
+""")
+
+
+@pytest.fixture()
+def rank_script(tmp_path):
+    p = tmp_path / "rank.py"
+    p.write_text(RANK_SCRIPT)
+    return str(p)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_spawn_forwards_rank0_json(rank_script, capfd, n):
+    rc = bench.spawn_ranks(n, ["-1"], script=rank_script, timeout=180)
+    out = capfd.readouterr().out
+    assert rc == 0
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1, out
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["ranksum"] == sum(range(n))
+    assert d["launcher"].startswith("bench.py")
+
+
+def test_spawn_propagates_rank_failure(rank_script, capfd):
+    rc = bench.spawn_ranks(2, ["1"], script=rank_script, timeout=180)
+    assert rc != 0
+    assert capfd.readouterr().out.strip() == ""
+
+
+def test_bare_bench_refuses_nccl_without_gpus():
+    """--gpus 2 on a box without 2 GPUs and the RCCL backend: a clear error, no spawn."""
+    import subprocess
+    import sys
+
+    if bench.torch.cuda.device_count() >= 2:
+        pytest.skip("this host has the GPUs")
+    p = subprocess.run([sys.executable, os.path.join(bench.ROOT, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0
+    assert "visible GPUs" in p.stderr

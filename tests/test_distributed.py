@@ -114,3 +114,33 @@ def test_ragged_shards_world3_gloo():
     x = ref.synth(7, 999, seed=4)
     want = ref.wsum_dense(x, np.float32(weights), scale=ref.mean_scale(weights))
     np.testing.assert_allclose(res[0][1], want, rtol=2e-6, atol=1e-9)
+
+
+def _worker_empty(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fedjax_amd import distributed as fd
+        tmpl = {"w": torch.zeros(3, 2), "b": torch.zeros(2)}
+        # no rank holds a client: every rank returns None, nobody blocks in a collective
+        a = fd.sharded_tree_mean([], template=tmpl if rank == 0 else None)
+        b = fd.sharded_tree_mean(iter([]), all_ranks=True)
+        q.put((rank, a is None and b is None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_tree_mean_without_clients_world3_gloo():
+    """ranks without clients must reach the same collectives (no hang)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_empty, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: True, 1: True, 2: True}

@@ -45,8 +45,14 @@ def _worker(rank, world, port, q):
         y = fd.sharded_weighted_mean(x, wl, W, buckets=3, all_ranks=True)
         trees = [({"a": x[i, :1000], "b": x[i, 1000:]}, weights[k0 + i]) for i in range(k1 - k0)]
         m = fd.sharded_tree_mean(trees, all_ranks=True)
+        # K < world size: rank 1 holds no client and contributes zeros (template shapes the result)
+        tmpl = {"a": torch.zeros(1000), "b": torch.zeros(P - 1000)}
+        m1 = fd.sharded_tree_mean(trees[:1] if rank == 0 else [], all_ranks=True, template=tmpl)
+        # dst is a global rank: only rank 1 (which holds the clients this time) gets the mean
+        m2 = fd.sharded_tree_mean(trees if rank == 1 else [], dst=1)
         torch.cuda.synchronize()
-        q.put((rank, y.cpu().numpy(), torch.cat([m["a"], m["b"]]).cpu().numpy()))
+        flat = lambda t: None if t is None else torch.cat([t["a"], t["b"]]).cpu().numpy()  # noqa: E731
+        q.put((rank, y.cpu().numpy(), flat(m), (flat(m1), flat(m2), k0, k1)))
     finally:
         dist.destroy_process_group()
 
@@ -58,7 +64,8 @@ def test_sharded_mean_world2_on_gpu(cuda, coracle):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = {r: (y, m) for r, y, m in (q.get(timeout=300) for _ in procs)}
+    got = {r: (y, m, extra) for r, y, m, extra in (q.get(timeout=300) for _ in procs)}
+    res = {r: v[:2] for r, v in got.items()}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -68,8 +75,17 @@ def test_sharded_mean_world2_on_gpu(cuda, coracle):
     want = coracle.wsum_f32(x, np.float32(weights), scale=r)
     bound = coracle.bound_f32(x, np.float32(weights), r, want) * (K + 4) / (K + 2)
     for rank in (0, 1):
-        for got in res[rank]:
-            assert np.all(np.abs(got.astype(np.float64) - want) <= bound)
+        for y in res[rank]:
+            assert np.all(np.abs(y.astype(np.float64) - want) <= bound)
+    # one rank's partial + the other rank's zeros: bitwise the single-rank exact fold
+    want1 = coracle.wsum_f32(x[:1], np.float32(weights[:1]), scale=ref.mean_scale(weights[:1]))
+    for rank in (0, 1):
+        assert np.array_equal(got[rank][2][0].view(np.uint32), want1.astype(np.float32).view(np.uint32))
+    k0, k1 = got[1][2][2:]
+    want2 = coracle.wsum_f32(np.ascontiguousarray(x[k0:k1]), np.float32(weights[k0:k1]),
+                             scale=ref.mean_scale(weights[k0:k1]))
+    assert got[0][2][1] is None
+    assert np.array_equal(got[1][2][1].view(np.uint32), want2.astype(np.float32).view(np.uint32))
 
 
 def _native_worker(port, q):

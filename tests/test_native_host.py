@@ -106,3 +106,25 @@ def test_collect_pairs_consumes_a_generator_once():
     assert got_trees == trees and W == 6.0 and isinstance(weights, tu._Weights)
     _, weights, W = tu._collect_pairs(zip(trees, [np.float32(1), np.float32(2), np.float32(0.5)]))
     assert isinstance(weights, list) and isinstance(W, np.float32) and W == np.float32(3.5)
+
+
+def test_leaf_versions_track_in_place_updates():
+    """fjhost.leaf_versions (RunningMean's reuse guard): torch's version counters in
+    flatten order; an in-place update bumps exactly that leaf; structure mismatch is
+    reported at the first bad client."""
+    trees = [_tree(k) for k in range(3)]
+    leaves0, td = pytree.flatten(trees[0])
+    spec, L = pytree.native_spec(td), len(leaves0)
+    v0 = np.empty((3, L), dtype=np.int64)
+    assert H.leaf_versions(trees, spec, L, v0) == 0
+    assert v0.tolist() == [[x._version for x in pytree.flatten(t)[0]] for t in trees]
+    trees[1]["b"]["w"].add_(1.0)
+    v1 = np.empty((3, L), dtype=np.int64)
+    assert H.leaf_versions(trees, spec, L, v1) == 0
+    changed = np.argwhere(v1 != v0).tolist()
+    pos = [i for i, x in enumerate(pytree.flatten(trees[1])[0]) if x is trees[1]["b"]["w"]][0]
+    assert changed == [[1, pos]]
+    trees[2]["b"].pop("w")
+    assert H.leaf_versions(trees, spec, L, v1) == -3
+    with pytest.raises(ValueError):
+        H.leaf_versions(trees, spec, L, np.empty(2, dtype=np.int64))

@@ -85,3 +85,28 @@ def test_treedefs_are_interned():
     t2 = pytree.flatten(Box(np.zeros(2), {"unhashable": 1}))[1]
     assert t1 is not t2  # aux is a dict: built fresh each time
     assert pytree.unflatten(t1, [np.ones(2)]).meta == {"unhashable": 1}
+
+
+def test_flatten_as_keys_without_expression_repr():
+    """dict keys whose repr is not a Python expression (numpy strings, enums)
+    go through the compiled accessor as objects."""
+    import enum
+
+    import numpy as np
+
+    from fedjax_amd import pytree
+
+    class Color(enum.Enum):
+        RED = 1
+
+    t = {np.str_("a"): np.zeros(2), Color.RED: np.ones(1)}
+    try:
+        leaves, td = pytree.flatten(t)
+    except TypeError:  # unorderable mixed keys: jax refuses such dicts too
+        t = {np.str_("a"): np.zeros(2), np.str_("b"): np.ones(1)}
+        leaves, td = pytree.flatten(t)
+    got = pytree.flatten_as(td, t)
+    assert all(a is b for a, b in zip(got, leaves))
+    t2 = {np.str_("a"): np.zeros(2), np.str_("b"): np.ones(1)}
+    leaves2, td2 = pytree.flatten(t2)
+    assert [x is y for x, y in zip(pytree.flatten_as(td2, t2), leaves2)] == [True, True]
