@@ -418,6 +418,38 @@ def test_running_mean_native_flush_host_deltas_and_errors(cuda):
         rm.add({"a": dev_trees[1]["a"]}, 1)
 
 
+def test_running_mean_detects_in_place_reuse(cuda):
+    """a torch loop that reuses one delta buffer for every client.
+    The reference sums each delta at its tree_add; a buffered reference would sum the
+    last value K times. RunningMean raises instead; copy_on_add gives the reference's
+    sum (bitwise the eager loop)."""
+    K = 5
+    g = torch.Generator(device="cpu").manual_seed(9)
+    vals = [torch.randn(2000, generator=g).to(cuda) for _ in range(K)]
+    tmpl = {"d": torch.zeros(2000, device=cuda)}
+    buf = torch.empty(2000, device=cuda)
+    rm = fedjax_amd.aggregators.RunningMean(tmpl, buffer_clients=8, device=cuda)
+    for k in range(K):
+        buf.copy_(vals[k])  # in place: bumps the version counter
+        rm.add({"d": buf}, k + 1)
+    with pytest.raises(RuntimeError, match="modified in place"):
+        rm.result()
+    rc = fedjax_amd.aggregators.RunningMean(tmpl, buffer_clients=8, device=cuda, copy_on_add=True)
+    for k in range(K):
+        buf.copy_(vals[k])
+        rc.add({"d": buf}, k + 1)
+    s = torch.zeros(2000, device=cuda)
+    for k in range(K):
+        s = s + vals[k] * float(np.float32(k + 1))
+    want = s * float(np.float32(1.0 / 15.0))
+    assert torch.equal(rc.result()["d"].view(torch.int32), want.view(torch.int32))
+    # untouched deltas (the common case) fold without a copy
+    ru = fedjax_amd.aggregators.RunningMean(tmpl, buffer_clients=2, device=cuda)
+    for k in range(K):
+        ru.add({"d": vals[k]}, k + 1)
+    assert torch.equal(ru.result()["d"].view(torch.int32), want.view(torch.int32))
+
+
 # ------------------------------------------------------------ fused fold + l2 norms
 @pytest.mark.parametrize("K,P,dt", [(1, 7, "f32"), (37, 10007, "f32"), (128, 1206590, "f32"),
                                     (300, 65536 + 5, "f32"), (64, 20000, "bf16"), (5, 3, "f32")])
