@@ -1,6 +1,7 @@
 """ctypes binding of ``libfjagg.so`` — the C ABI declared in ``include/fjagg.h``
 (aggregation), ``include/fjcomp.h`` (compression aggregators) and
-``include/fjcomm.h`` (client-sharded aggregation over RCCL, timing events).
+``include/fjcomm.h`` (client-sharded aggregation over RCCL, timing events) and
+``include/fjtree.h`` (per-call tree ops, leaf table in the kernel arguments).
 
 The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950) into
 ``fedjax_amd/_build/libfjagg.so``. It links against the HIP runtime by soname
@@ -35,6 +36,9 @@ COMP_ABI_VERSION = 1
 COMM_ABI_VERSION = 1
 COMM_ID_BYTES = 128
 COMM_MAX_BUCKETS = 64
+TREE_ABI_VERSION = 1
+TREE_MAX_LEAVES, TREE_MAX_OPERANDS = 64, 2
+TREE_NORM, TREE_NO_OUT = 1 << 8, 1 << 9
 # include/fjcomp.h
 COMP_UNIFORM, COMP_TERNGRAD, COMP_BINARY = 1, 2, 3
 WHT_PLAIN, WHT_ROTATE, WHT_UNROTATE, WHT_UNROTATE_DRIVE = 0, 1, 2, 3
@@ -89,6 +93,10 @@ _SIGNATURES = {
     "fjagg_event_destroy": (_i32, [_vp]),
     "fjagg_event_record": (_i32, [_vp, _vp]),
     "fjagg_event_elapsed_ms": (_i32, [_vp, _vp, _vp]),
+    # include/fjtree.h
+    "fjtree_abi_version": (_i32, []),
+    "fjtree_workspace_bytes": (_i64, [_vp]),
+    "fjtree_fold_leaves": (_i32, [_vp, _vp]),
 }
 SYMBOLS = tuple(_SIGNATURES)
 
@@ -102,6 +110,15 @@ class ServerOpt(ctypes.Structure):
 
 
 OPT_SGD, OPT_MOMENTUM, OPT_ADAM = 1, 2, 3
+
+
+class TreeLeaves(ctypes.Structure):
+    """struct fjtree_leaves (include/fjtree.h)."""
+    _fields_ = [("K", ctypes.c_int), ("L", ctypes.c_int),
+                ("x", (ctypes.c_void_p * 64) * 2), ("out", ctypes.c_void_p * 64), ("n", ctypes.c_int64 * 64),
+                ("w", ctypes.c_float * 2), ("scale", ctypes.c_float), ("flags", ctypes.c_int),
+                ("norm_operand", ctypes.c_int), ("norm_out", ctypes.c_void_p), ("ws", ctypes.c_void_p),
+                ("ws_bytes", ctypes.c_int64)]
 
 
 class FjaggError(RuntimeError):
@@ -143,9 +160,11 @@ def load() -> ctypes.CDLL:
             if fn is None:
                 raise FjaggError(f"{LIB_PATH} does not export {name}")
             fn.restype, fn.argtypes = res, args
-        got = (lib.fjagg_abi_version(), lib.fjcomp_abi_version(), lib.fjcomm_abi_version())
-        if got != (ABI_VERSION, COMP_ABI_VERSION, COMM_ABI_VERSION):
-            raise FjaggError(f"ABI mismatch: library {got} != {(ABI_VERSION, COMP_ABI_VERSION, COMM_ABI_VERSION)}")
+        got = (lib.fjagg_abi_version(), lib.fjcomp_abi_version(), lib.fjcomm_abi_version(),
+               lib.fjtree_abi_version())
+        want = (ABI_VERSION, COMP_ABI_VERSION, COMM_ABI_VERSION, TREE_ABI_VERSION)
+        if got != want:
+            raise FjaggError(f"ABI mismatch: library {got} != {want}")
         runtimes = hip_runtimes_mapped()
         if len(runtimes) > 1:
             raise FjaggError(f"two HIP runtimes mapped into one process: {runtimes}")

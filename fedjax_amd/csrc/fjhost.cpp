@@ -49,11 +49,18 @@
 #include <Python.h>
 
 #include <ATen/ATen.h>
+#include <c10/hip/HIPFunctions.h>
+#include <c10/hip/HIPStream.h>
 #include <torch/csrc/autograd/python_variable.h>
 
+#include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
+
+#include "fjagg.h"
+#include "fjtree.h"
 
 namespace {
 
@@ -385,10 +392,351 @@ PyObject* fold_table(PyObject*, PyObject* args) {
   }
 }
 
+// ------------------------------------------------------------------ per-call tree ops
+// (include/fjtree.h). The K operand trees are walked in parallel, driven by tree 0:
+// exact dict (keys sorted, as jax flattens) / list / tuple / None nodes, exact
+// torch.Tensor leaves. Anything else is "not the fast case" (None to the caller).
+
+struct PWalk {
+  int K = 0;
+  std::vector<PyObject*> leaves[FJTREE_MAX_OPERANDS];  // borrowed, flatten order
+  std::vector<PyObject*> keys;                         // owned sorted key lists, pre-order
+  ~PWalk() {
+    for (PyObject* k : keys) Py_DECREF(k);
+  }
+};
+
+// 0: walked; 1: not the fast case / structures differ; -1: Python error set.
+int pwalk(PyObject* const* xs, PWalk& w, int depth) {
+  if (depth > 64) return 1;
+  PyObject* x0 = xs[0];
+  const int K = w.K;
+  PyTypeObject* tt = reinterpret_cast<PyTypeObject*>(THPVariableClass);
+  if (Py_TYPE(x0) == tt) {
+    for (int k = 0; k < K; ++k) {
+      if (Py_TYPE(xs[k]) != tt) return 1;
+      if (w.leaves[k].size() >= FJTREE_MAX_LEAVES) return 1;
+      w.leaves[k].push_back(xs[k]);
+    }
+    return 0;
+  }
+  if (x0 == Py_None) {
+    for (int k = 1; k < K; ++k)
+      if (xs[k] != Py_None) return 1;
+    return 0;
+  }
+  PyObject* vals[FJTREE_MAX_OPERANDS];
+  if (PyDict_CheckExact(x0)) {
+    const Py_ssize_t n = PyDict_GET_SIZE(x0);
+    for (int k = 1; k < K; ++k)
+      if (!PyDict_CheckExact(xs[k]) || PyDict_GET_SIZE(xs[k]) != n) return 1;
+    PyObject* keys = PyDict_Keys(x0);
+    if (!keys) return -1;
+    w.keys.push_back(keys);
+    if (PyList_Sort(keys) != 0) {  // unorderable keys: the Python path decides
+      PyErr_Clear();
+      return 1;
+    }
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      PyObject* key = PyList_GET_ITEM(keys, i);
+      for (int k = 0; k < K; ++k) {
+        vals[k] = PyDict_GetItemWithError(xs[k], key);
+        if (!vals[k]) {
+          if (PyErr_Occurred()) PyErr_Clear();
+          return 1;
+        }
+      }
+      if (int rc = pwalk(vals, w, depth + 1)) return rc;
+    }
+    return 0;
+  }
+  const bool is_list = PyList_CheckExact(x0), is_tuple = PyTuple_CheckExact(x0);
+  if (!is_list && !is_tuple) return 1;
+  const Py_ssize_t n = Py_SIZE(x0);
+  for (int k = 1; k < K; ++k)
+    if (Py_TYPE(xs[k]) != Py_TYPE(x0) || Py_SIZE(xs[k]) != n) return 1;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    for (int k = 0; k < K; ++k) vals[k] = is_list ? PyList_GET_ITEM(xs[k], i) : PyTuple_GET_ITEM(xs[k], i);
+    if (int rc = pwalk(vals, w, depth + 1)) return rc;
+  }
+  return 0;
+}
+
+// A new tree shaped like x0 whose leaves are outs[i++] (stolen references), dict keys
+// in sorted order (jax's unflatten of a dict); key lists from the walk, in pre-order.
+PyObject* rebuild(PyObject* x0, PyObject** outs, size_t& i, const std::vector<PyObject*>& keys, size_t& ki) {
+  if (Py_TYPE(x0) == reinterpret_cast<PyTypeObject*>(THPVariableClass)) {
+    PyObject* o = outs[i];
+    outs[i++] = nullptr;
+    return o;
+  }
+  if (x0 == Py_None) {
+    Py_INCREF(Py_None);
+    return Py_None;
+  }
+  if (PyDict_CheckExact(x0)) {
+    PyObject* kl = keys[ki++];
+    PyObject* d = PyDict_New();
+    if (!d) return nullptr;
+    for (Py_ssize_t j = 0; j < PyList_GET_SIZE(kl); ++j) {
+      PyObject* key = PyList_GET_ITEM(kl, j);
+      PyObject* v = rebuild(PyDict_GetItem(x0, key), outs, i, keys, ki);
+      if (!v || PyDict_SetItem(d, key, v) != 0) {
+        Py_XDECREF(v);
+        Py_DECREF(d);
+        return nullptr;
+      }
+      Py_DECREF(v);
+    }
+    return d;
+  }
+  const bool is_list = PyList_CheckExact(x0);
+  const Py_ssize_t n = Py_SIZE(x0);
+  PyObject* c = is_list ? PyList_New(n) : PyTuple_New(n);
+  if (!c) return nullptr;
+  for (Py_ssize_t j = 0; j < n; ++j) {
+    PyObject* v = rebuild(is_list ? PyList_GET_ITEM(x0, j) : PyTuple_GET_ITEM(x0, j), outs, i, keys, ki);
+    if (!v) {
+      Py_DECREF(c);
+      return nullptr;
+    }
+    if (is_list) PyList_SET_ITEM(c, j, v);
+    else PyTuple_SET_ITEM(c, j, v);
+  }
+  return c;
+}
+
+// float32 of a Python int / float weight as numpy rounds it; false for anything else.
+bool f32_weight(PyObject* w, float* out) {
+  if (PyLong_CheckExact(w)) {
+    int overflow = 0;
+    long long v = PyLong_AsLongLongAndOverflow(w, &overflow);
+    if (overflow || v >= (1LL << 53) || v <= -(1LL << 53)) {
+      if (PyErr_Occurred()) PyErr_Clear();
+      return false;
+    }
+    *out = static_cast<float>(static_cast<double>(v));
+    return true;
+  }
+  if (PyFloat_CheckExact(w)) {
+    *out = static_cast<float>(PyFloat_AS_DOUBLE(w));
+    return true;
+  }
+  return false;
+}
+
+// Leaves of operand k: float32, strided, contiguous, on cuda:dev, leaf l shaped like
+// operand 0's. Fills the version sum. false: not the fast case.
+bool check_leaves(const PWalk& w, int k, c10::DeviceIndex dev, int64_t* vsum) {
+  int64_t vs = 0;
+  for (size_t l = 0; l < w.leaves[k].size(); ++l) {
+    const at::Tensor& t = THPVariable_Unpack(w.leaves[k][l]);
+    if (t.layout() != c10::kStrided || t.scalar_type() != at::kFloat || !t.is_cuda() || t.get_device() != dev ||
+        !t.is_contiguous())
+      return false;
+    if (k > 0 && t.sizes() != THPVariable_Unpack(w.leaves[0][l]).sizes()) return false;
+    vs += static_cast<int64_t>(t._version());
+  }
+  *vsum = vs;
+  return true;
+}
+
+struct WsKey {
+  int dev;
+  uint64_t stream;
+  bool operator==(const WsKey& o) const { return dev == o.dev && stream == o.stream; }
+};
+struct WsHash {
+  size_t operator()(const WsKey& k) const { return std::hash<uint64_t>()(k.stream ^ (uint64_t(k.dev) << 56)); }
+};
+// Norm workspace per (device, stream): its completion counter must start at 0, and each
+// launch leaves it at 0, so launches on one stream can share it (include/fjtree.h).
+std::unordered_map<WsKey, at::Tensor, WsHash>& workspaces() {
+  static auto* m = new std::unordered_map<WsKey, at::Tensor, WsHash>();
+  return *m;
+}
+
+typedef int (*TreeFoldFn)(const fjtree_leaves*, void*);
+typedef int64_t (*TreeWsFn)(const fjtree_leaves*);
+constexpr int kStale = -100;
+
+// capture(tree, dev) -> (leaves_tuple, version_sum) | None   (dev = -1: the first leaf's)
+//     tree_weight's lazy result holds its input's leaves (strong references, flatten order)
+//     and their version sum, so tree_add can check that nothing changed in between.
+PyObject* capture(PyObject*, PyObject* args) {
+  PyObject* tree;
+  int dev;
+  if (!PyArg_ParseTuple(args, "Oi", &tree, &dev)) return nullptr;
+  try {
+    PWalk w;
+    w.K = 1;
+    int rc = pwalk(&tree, w, 0);
+    if (rc < 0) return nullptr;
+    int64_t vs = 0;
+    if (rc > 0 || w.leaves[0].empty()) Py_RETURN_NONE;
+    if (dev < 0) {
+      const at::Tensor& t0 = THPVariable_Unpack(w.leaves[0][0]);
+      if (!t0.is_cuda()) Py_RETURN_NONE;
+      dev = t0.get_device();
+    }
+    if (!check_leaves(w, 0, static_cast<c10::DeviceIndex>(dev), &vs)) Py_RETURN_NONE;
+    const Py_ssize_t L = static_cast<Py_ssize_t>(w.leaves[0].size());
+    PyObject* tup = PyTuple_New(L);
+    if (!tup) return nullptr;
+    for (Py_ssize_t l = 0; l < L; ++l) {
+      Py_INCREF(w.leaves[0][l]);
+      PyTuple_SET_ITEM(tup, l, w.leaves[0][l]);
+    }
+    return Py_BuildValue("(NL)", tup, static_cast<long long>(vs));
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
+// matches(tree, leaves_tuple, version_sum) -> bool: the same leaf objects, unmodified.
+PyObject* matches(PyObject*, PyObject* args) {
+  PyObject *tree, *tup;
+  long long vsum;
+  if (!PyArg_ParseTuple(args, "OO!L", &tree, &PyTuple_Type, &tup, &vsum)) return nullptr;
+  try {
+    PWalk w;
+    w.K = 1;
+    int rc = pwalk(&tree, w, 0);
+    if (rc < 0) return nullptr;
+    if (rc > 0 || static_cast<Py_ssize_t>(w.leaves[0].size()) != PyTuple_GET_SIZE(tup)) Py_RETURN_FALSE;
+    int64_t vs = 0;
+    for (size_t l = 0; l < w.leaves[0].size(); ++l) {
+      if (w.leaves[0][l] != PyTuple_GET_ITEM(tup, l)) Py_RETURN_FALSE;
+      vs += static_cast<int64_t>(THPVariable_Unpack(w.leaves[0][l])._version());
+    }
+    if (vs != vsum) Py_RETURN_FALSE;
+    Py_RETURN_TRUE;
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
+// leaf_fold(trees, weights, caps, scale, flags, norm_operand, dev, stream, fold_fn, ws_fn)
+//     -> (rc, out_tree | None, l2sq | None, l2 | None) | None
+// dev = -1: the first leaf's device; stream = 0: torch's current stream on it.
+// One fjtree_fold_leaves launch over K = len(trees) operand trees (include/fjtree.h):
+// out = [fl(] sum_k fl(x_k * f32(w_k)) [* scale)], plus the l2 norm of operand
+// norm_operand with FJTREE_NORM (0-d float32 views of a fresh [2] tensor). caps[k] is
+// None or (leaves_tuple, version_sum) from capture(): operand k must still hold exactly
+// those leaf objects, unmodified, else rc = -100 (nothing launched). None: not the fast
+// case (float32 leaves, <= FJTREE_MAX_LEAVES of them, Python-number weights, matching
+// structures), nothing launched.
+PyObject* leaf_fold(PyObject*, PyObject* args) {
+  PyObject *trees, *weights, *caps;
+  double scale;
+  int flags, norm_operand, dev;
+  unsigned long long stream, fold_addr, ws_addr;
+  if (!PyArg_ParseTuple(args, "O!O!O!diiiKKK", &PyList_Type, &trees, &PyList_Type, &weights, &PyList_Type, &caps,
+                        &scale, &flags, &norm_operand, &dev, &stream, &fold_addr, &ws_addr))
+    return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(trees);
+  if (K < 1 || K > FJTREE_MAX_OPERANDS || PyList_GET_SIZE(weights) != K || PyList_GET_SIZE(caps) != K)
+    Py_RETURN_NONE;
+  try {
+    fjtree_leaves t;
+    std::memset(&t, 0, sizeof(t));
+    for (Py_ssize_t k = 0; k < K; ++k)
+      if (!f32_weight(PyList_GET_ITEM(weights, k), &t.w[k])) Py_RETURN_NONE;
+    PWalk w;
+    w.K = static_cast<int>(K);
+    PyObject* xs[FJTREE_MAX_OPERANDS];
+    for (Py_ssize_t k = 0; k < K; ++k) xs[k] = PyList_GET_ITEM(trees, k);
+    int rc = pwalk(xs, w, 0);
+    if (rc < 0) return nullptr;
+    if (rc > 0 || w.leaves[0].empty()) Py_RETURN_NONE;
+    if (dev < 0) {  // the first leaf's device, and the caller's current stream on it
+      const at::Tensor& t0 = THPVariable_Unpack(w.leaves[0][0]);
+      if (!t0.is_cuda()) Py_RETURN_NONE;
+      dev = t0.get_device();
+    }
+    if (stream == 0) stream = reinterpret_cast<unsigned long long>(c10::hip::getCurrentHIPStream(dev).stream());
+    const c10::DeviceIndex di = static_cast<c10::DeviceIndex>(dev);
+    for (Py_ssize_t k = 0; k < K; ++k) {
+      int64_t vs = 0;
+      if (!check_leaves(w, static_cast<int>(k), di, &vs)) Py_RETURN_NONE;
+      PyObject* cap = PyList_GET_ITEM(caps, k);
+      if (cap == Py_None) continue;
+      PyObject* tup = PyTuple_GET_ITEM(cap, 0);
+      long long cv = PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1));
+      bool same = PyTuple_GET_SIZE(tup) == static_cast<Py_ssize_t>(w.leaves[k].size()) && cv == vs;
+      for (size_t l = 0; same && l < w.leaves[k].size(); ++l) same = w.leaves[k][l] == PyTuple_GET_ITEM(tup, l);
+      if (!same) return Py_BuildValue("(iOOO)", kStale, Py_None, Py_None, Py_None);
+    }
+    const int L = static_cast<int>(w.leaves[0].size());
+    const bool norm = flags & FJTREE_NORM, out = !(flags & FJTREE_NO_OUT);
+    t.K = static_cast<int>(K);
+    t.L = L;
+    t.scale = static_cast<float>(scale);
+    t.flags = flags;
+    t.norm_operand = norm_operand;
+    std::vector<at::Tensor> outs;
+    outs.reserve(L);
+    for (int l = 0; l < L; ++l) {
+      const at::Tensor& x0 = THPVariable_Unpack(w.leaves[0][l]);
+      for (Py_ssize_t k = 0; k < K; ++k)
+        t.x[k][l] = static_cast<const float*>(THPVariable_Unpack(w.leaves[k][l]).data_ptr());
+      t.n[l] = x0.numel();
+      if (out) {
+        outs.push_back(at::empty(x0.sizes(), x0.options()));
+        t.out[l] = outs.back().data_ptr<float>();
+      }
+    }
+    at::Tensor nrm;
+    if (norm) {
+      nrm = at::empty({2}, THPVariable_Unpack(w.leaves[0][0]).options());
+      t.norm_out = nrm.data_ptr<float>();
+      const int64_t need = reinterpret_cast<TreeWsFn>(ws_addr)(&t);
+      at::Tensor& ws = workspaces()[WsKey{dev, stream}];
+      if (!ws.defined() || ws.numel() < need)
+        ws = at::zeros({need > 4096 ? need * 2 : 8192}, nrm.options().dtype(at::kByte));
+      t.ws = ws.data_ptr();
+      t.ws_bytes = ws.numel();
+    }
+    rc = reinterpret_cast<TreeFoldFn>(fold_addr)(&t, reinterpret_cast<void*>(stream));
+    PyObject* tree_out = Py_None;
+    Py_INCREF(Py_None);
+    if (out && rc == 0) {
+      std::vector<PyObject*> objs(L);
+      for (int l = 0; l < L; ++l) objs[l] = THPVariable_Wrap(std::move(outs[l]));
+      size_t i = 0, ki = 0;
+      PyObject* r = rebuild(xs[0], objs.data(), i, w.keys, ki);
+      for (PyObject* o : objs) Py_XDECREF(o);
+      if (!r) {
+        Py_DECREF(Py_None);
+        return nullptr;
+      }
+      Py_DECREF(Py_None);
+      tree_out = r;
+    }
+    PyObject *sq = Py_None, *l2 = Py_None;
+    if (norm && rc == 0) {
+      sq = THPVariable_Wrap(nrm.select(0, 0));
+      l2 = THPVariable_Wrap(nrm.select(0, 1));
+    } else {
+      Py_INCREF(Py_None);
+      Py_INCREF(Py_None);
+    }
+    return Py_BuildValue("(iNNN)", rc, tree_out, sq, l2);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 PyMethodDef kMethods[] = {
     {"gather_rows", gather_rows, METH_VARARGS, "pointer table of K client pytrees (see fjhost.cpp)"},
     {"leaf_versions", leaf_versions, METH_VARARGS, "torch in-place version counters of K pytrees' leaves"},
     {"fold_weights", fold_weights, METH_VARARGS, "f32/i32 weights and W of Python-number weights"},
+    {"capture", capture, METH_VARARGS, "leaves + version sum of a tree for a lazy tree_weight"},
+    {"matches", matches, METH_VARARGS, "tree holds exactly the captured leaves, unmodified"},
+    {"leaf_fold", leaf_fold, METH_VARARGS, "fjtree_fold_leaves over 1-2 operand trees (see fjhost.cpp)"},
     {"fold_table", fold_table, METH_VARARGS, "plan image + output leaves + fjagg_wsum_ptrs launch (see fjhost.cpp)"},
     {nullptr, nullptr, 0, nullptr},
 };

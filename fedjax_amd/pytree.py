@@ -22,6 +22,14 @@ import collections
 from typing import Any, Callable, Dict, List, Tuple
 
 _REGISTRY: Dict[type, Tuple[Callable, Callable]] = {}
+# lazy values (tree_util.WeightedTree): type -> fn(x) returning the pytree they stand for;
+# every walk here materializes them where they appear
+_LAZY: Dict[type, Callable] = {}
+
+
+def register_lazy_type(cls: type, materialize: Callable) -> None:
+    """Instances of ``cls`` stand for the pytree ``materialize(x)`` returns."""
+    _LAZY[cls] = materialize
 
 
 def register_pytree_node(cls: type, flatten_fn: Callable, unflatten_fn: Callable) -> None:
@@ -132,6 +140,8 @@ def flatten(tree) -> Tuple[List[Any], TreeDef]:
         if type(x) in leaf_types:  # tensors / arrays: skip the node classification
             leaves.append(x)
             return _LEAF
+        if type(x) in _LAZY:
+            return rec(_LAZY[type(x)](x))
         kind, aux, children = _node(x)
         if kind == "leaf":
             leaves.append(x)
@@ -265,6 +275,8 @@ def _spec(td: TreeDef):
 
 
 def _collect(td: TreeDef, x, out: List[Any]) -> None:
+    if type(x) in _LAZY:
+        x = _LAZY[type(x)](x)
     k = td.kind
     if k == "leaf":
         if not _is_leaf(x):
@@ -289,6 +301,7 @@ def _collect(td: TreeDef, x, out: List[Any]) -> None:
         if kind != k or aux != td.aux or len(vals) != len(td.children):
             raise _Mismatch
     if td.leafy:
+        vals = [_LAZY[type(v)](v) if type(v) in _LAZY else v for v in vals]
         for v in vals:
             if not _is_leaf(v):
                 raise _Mismatch

@@ -37,7 +37,7 @@ from fedjax_amd.typing import PyTree
 __all__ = [
     "tree_weight", "tree_inverse_weight", "tree_zeros_like", "tree_add", "tree_sum",
     "tree_mean", "tree_size", "tree_l2_squared", "tree_l2_norm", "tree_clip_by_global_norm",
-    "tree_l2_norms", "tree_mean_with_l2_norms",
+    "tree_l2_norms", "tree_mean_with_l2_norms", "WeightedTree",
 ]
 
 # Non-temporal loads pay off once the deltas cannot stay in the 256 MiB Infinity
@@ -446,14 +446,131 @@ def _fold_trees(trees: Sequence[PyTree], weights: List[Any]) -> PyTree:
                                       validated=True))
 
 
+# ------------------------------------------------------- per-call tree ops (fjtree.h)
+# The running-sum loop of FedJAX's algorithms (fedjax/algorithms/fed_avg.py:132-146 and
+# six others) calls tree_add(s, tree_weight(delta, n)) and tree_l2_norm(delta) once per
+# client. For pytrees of float32 device tensors (<= 64 leaves) each call is ONE launch of
+# fjtree_fold_leaves with the leaf table in the kernel arguments (fjhost.leaf_fold):
+# tree_weight is deferred (WeightedTree) and folded into the tree_add that consumes it,
+# and that launch also sums the squares of the weighted delta, which tree_l2_norm of the
+# same, unmodified delta then returns without another pass.
+_TREE_ADDRS = None
+_STALE = -100  # fjhost.leaf_fold: a captured operand changed since tree_weight
+_NORMS: "collections.deque" = None  # (capture, l2sq, l2) of the last fused tree_add calls
+
+
+def _tree_addrs():
+    global _TREE_ADDRS, _NORMS
+    if _TREE_ADDRS is None:
+        import collections
+        lib = _lib.load()
+        _NORMS = collections.deque(maxlen=2)
+        _TREE_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
+                            for f in ("fjtree_fold_leaves", "fjtree_workspace_bytes"))
+    return _TREE_ADDRS
+
+
+def _leaf_fold(trees, weights, caps, scale=None, norm_operand=-1, no_out=False):
+    """fjhost.leaf_fold: (out_tree, l2sq, l2) from one fjtree launch; None when the call
+    is not the fast case (nothing launched). Raises when a captured operand is stale."""
+    fold, ws = _TREE_ADDRS or _tree_addrs()
+    flags = ((_lib.SCALE if scale is not None else 0) | (_lib.TREE_NORM if norm_operand >= 0 else 0)
+             | (_lib.TREE_NO_OUT if no_out else 0))
+    got = _lib.host().leaf_fold(trees, weights, caps, 1.0 if scale is None else float(scale), flags,
+                                max(norm_operand, 0), -1, 0, fold, ws)
+    if got is None:
+        return None
+    rc, out, sq, l2 = got
+    if rc == _STALE:
+        raise RuntimeError("a pytree passed to tree_weight was modified (a leaf replaced or updated in "
+                           "place) before its weighted value was used; the reference computes "
+                           "tree_weight eagerly")
+    _lib.check(rc, "fjtree_fold_leaves")
+    return out, sq, l2
+
+
+class WeightedTree:
+    """``tree_weight(tree, w)`` of a pytree of float32 device tensors, not yet computed.
+
+    The multiply is deferred so that ``tree_add(s, tree_weight(x, n))`` — the running sum
+    of fed_avg.py:137-138 — is one fused launch (bitwise ``fl(s + fl(x * f32(n)))``). Any
+    other use computes it: indexing, iteration, attribute access and every pytree walk of
+    this package (``pytree.flatten``, ``tree_util.*``) see the weighted pytree itself, and
+    ``materialize()`` returns it. The input's leaf objects and their in-place versions are
+    captured at ``tree_weight``: if a leaf is replaced or modified before the weighted
+    value is used, using it raises RuntimeError (the reference's arrays are immutable).
+    ``isinstance(w, dict)`` is False: call ``materialize()`` where the concrete container
+    type matters.
+    """
+
+    __slots__ = ("_tree", "_weight", "_cap", "_value")
+
+    def __init__(self, tree, weight, cap):
+        self._tree, self._weight, self._cap, self._value = tree, weight, cap, None
+
+    def materialize(self) -> PyTree:
+        if self._value is None:
+            got = _leaf_fold([self._tree], [self._weight], [self._cap])
+            if got is None:
+                raise RuntimeError("the pytree passed to tree_weight changed structure before use")
+            self._value = got[0]
+            self._tree = self._cap = None
+        return self._value
+
+    def __getitem__(self, key):
+        return self.materialize()[key]
+
+    def __iter__(self):
+        return iter(self.materialize())
+
+    def __len__(self):
+        return len(self.materialize())
+
+    def __contains__(self, key):
+        return key in self.materialize()
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        return getattr(self.materialize(), name)
+
+    def __repr__(self):
+        return f"WeightedTree({self.materialize()!r})"
+
+
+pytree.register_lazy_type(WeightedTree, WeightedTree.materialize)
+_F32_EXACT_INT = 1 << 53
+
+
 def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
-    """Weights tree leaves by weight (tree_util.py:29-32)."""
-    return _fold_trees([pytree_], [_host_weight(weight)])
+    """Weights tree leaves by weight (tree_util.py:29-32).
+
+    Float32 device pytrees (<= 64 leaves) with a Python-number weight give a
+    :class:`WeightedTree` (deferred, fused into the tree_add that consumes it);
+    anything else is computed now by the pytree kernel."""
+    w = _host_weight(weight)
+    if (type(w) is float or (type(w) is int and -_F32_EXACT_INT < w < _F32_EXACT_INT)):
+        if _TREE_ADDRS is None:
+            _tree_addrs()
+        cap = _lib.host().capture(pytree_, -1)
+        if cap is not None:
+            return WeightedTree(pytree_, w, cap)
+    return _fold_trees([pytree_], [w])
+
+
+def _eager(t):
+    return t.materialize() if type(t) is WeightedTree else t
 
 
 def tree_inverse_weight(pytree_: PyTree, weight: float) -> PyTree:
-    """Weights tree leaves by ``1 / weight`` (tree_util.py:35-38)."""
-    return tree_weight(pytree_, _inverse(_host_weight(weight)))
+    """Weights tree leaves by ``1 / weight`` (tree_util.py:35-38); computed now."""
+    inv = _inverse(_host_weight(weight))
+    pytree_ = _eager(pytree_)
+    if type(inv) is float:
+        got = _leaf_fold([pytree_], [inv], [None])
+        if got is not None:
+            return got[0]
+    return _fold_trees([pytree_], [inv])
 
 
 def tree_zeros_like(pytree_: PyTree) -> PyTree:
@@ -472,8 +589,26 @@ def tree_zeros_like(pytree_: PyTree) -> PyTree:
 
 def tree_add(left: PyTree, right: PyTree) -> PyTree:
     """Adds two trees together (tree_util.py:47-50): x*1 is exact, so a K=2 fold
-    with unit weights is the reference's ``jnp.add``."""
-    return _fold_trees([left, right], [1, 1])
+    with unit weights is the reference's ``jnp.add``. A :class:`WeightedTree` operand
+    is folded in the same launch (``fl(s + fl(x * f32(n)))``), which also sums the
+    squares of its input for a following ``tree_l2_norm`` of that input."""
+    tl, tr = type(left) is WeightedTree, type(right) is WeightedTree
+    if tl or tr:
+        ops = [left._tree if tl else left, right._tree if tr else right]
+        if ops[0] is None or ops[1] is None:  # already materialized
+            return _fold_trees([_eager(left), _eager(right)], [1, 1])
+        ws = [left._weight if tl else 1, right._weight if tr else 1]
+        caps = [left._cap if tl else None, right._cap if tr else None]
+        norm_op = 1 if tr else 0
+    else:
+        ops, ws, caps, norm_op = [left, right], [1, 1], [None, None], -1
+    got = _leaf_fold(ops, ws, caps, norm_operand=norm_op)
+    if got is not None:
+        out, sq, l2 = got
+        if norm_op >= 0:
+            _NORMS.appendleft((caps[norm_op], sq, l2))
+        return out
+    return _fold_trees([_eager(left), _eager(right)], [1, 1])
 
 
 def tree_sum(pytrees: Iterable[PyTree]) -> PyTree:
@@ -565,8 +700,26 @@ def _l2_rows(rows: List[List[torch.Tensor]], take_sqrt: bool) -> torch.Tensor:
     return out
 
 
+def _l2_fast(pytree_, which: int):
+    """(l2sq, l2)[which] of a float32 device pytree: the fused value of a preceding
+    tree_add(s, tree_weight(pytree_, n)) when pytree_ is unchanged since, else one
+    fjtree launch (same reduction order, so the same bits). None: not the fast case."""
+    if _TREE_ADDRS is None:
+        _tree_addrs()
+    host = _lib.host()
+    for cap, sq, l2 in _NORMS:
+        if host.matches(pytree_, cap[0], cap[1]):
+            return sq if which == 0 else l2
+    got = _leaf_fold([pytree_], [1], [None], norm_operand=0, no_out=True)
+    return None if got is None else got[1 + which]
+
+
 def tree_l2_squared(pytree_: PyTree) -> torch.Tensor:
     """Returns squared l2 norm of tree (tree_util.py:105-108), a 0-d float32 tensor."""
+    pytree_ = _eager(pytree_)
+    got = _l2_fast(pytree_, 0)
+    if got is not None:
+        return got
     _, rows = _client_rows([pytree_])
     if not rows[0]:
         return torch.zeros((), dtype=torch.float32, device=_default_device())
@@ -575,6 +728,10 @@ def tree_l2_squared(pytree_: PyTree) -> torch.Tensor:
 
 def tree_l2_norm(pytree_: PyTree) -> torch.Tensor:
     """Returns l2 norm of tree (tree_util.py:111-114), a 0-d float32 tensor."""
+    pytree_ = _eager(pytree_)
+    got = _l2_fast(pytree_, 1)
+    if got is not None:
+        return got
     _, rows = _client_rows([pytree_])
     if not rows[0]:
         return torch.zeros((), dtype=torch.float32, device=_default_device())
@@ -598,4 +755,4 @@ def tree_clip_by_global_norm(pytree_: PyTree, max_norm: float) -> PyTree:
     norm = np.float32(tree_l2_norm(pytree_).item())
     with np.errstate(divide="ignore", invalid="ignore"):
         scale = np.minimum(np.float32(1), np.float32(max_norm) / norm)
-    return tree_weight(pytree_, np.float32(scale))
+    return _eager(tree_weight(pytree_, np.float32(scale)))

@@ -13,14 +13,14 @@ import torch
 from fedjax_amd import _lib, kernels
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("fjagg.h", "fjcomp.h", "fjcomm.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("fjagg.h", "fjcomp.h", "fjcomm.h", "fjtree.h")]
 
 
 def header_symbols():
     syms = set()
     for h in HEADERS:
         src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
-        syms |= set(re.findall(r"\b(fj(?:agg|comp|comm)_\w+)\s*\(", src))
+        syms |= set(re.findall(r"\b(fj(?:agg|comp|comm|tree)_\w+)\s*\(", src))
     return syms
 
 
@@ -31,7 +31,7 @@ def test_header_and_binding_agree():
 def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
-    exported = set(re.findall(r"\bT (fj(?:agg|comp|comm)_\w+)", out))
+    exported = set(re.findall(r"\bT (fj(?:agg|comp|comm|tree)_\w+)", out))
     assert header_symbols() <= exported, header_symbols() - exported
 
 
@@ -115,3 +115,22 @@ def test_comm_host_side_validation_without_gpu():
     assert b"communicator" in lib.fjagg_last_error()
     assert lib.fjcomm_init(None, None, 1, 0) in (-1, -3)  # null handle / RCCL absent
     assert lib.fjcomm_destroy(None) == 0
+
+
+def test_tree_table_layout_and_validation():
+    """include/fjtree.h: the ctypes mirror has the C layout (static_assert in fjtree.hip), and
+    bad tables are refused before any HIP call."""
+    import ctypes
+    assert ctypes.sizeof(_lib.TreeLeaves) == 2104
+    lib = _lib.load()
+    t = _lib.TreeLeaves()
+    t.K, t.L = 3, 1
+    assert lib.fjtree_fold_leaves(ctypes.byref(t), None) == -1 and b"K must be" in lib.fjagg_last_error()
+    t.K, t.L = 1, 65
+    assert lib.fjtree_fold_leaves(ctypes.byref(t), None) == -1
+    t.L, t.n[0] = 1, 10
+    assert lib.fjtree_fold_leaves(ctypes.byref(t), None) == -1 and b"null operand" in lib.fjagg_last_error()
+    t.flags = _lib.TREE_NORM
+    assert lib.fjtree_workspace_bytes(ctypes.byref(t)) == 256 + 4
+    t.n[0] = 4097
+    assert lib.fjtree_workspace_bytes(ctypes.byref(t)) == 256 + 8
