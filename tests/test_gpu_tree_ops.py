@@ -1,0 +1,199 @@
+"""Per-call tree ops on the GPU (include/fjtree.h, fedjax_amd/csrc/fjtree.hip): the running
+sum of fedjax/algorithms/fed_avg.py:132-146 called literally —
+
+    s = tree_zeros_like(params)
+    for each client: s = tree_add(s, tree_weight(delta, n)); tree_l2_norm(delta)
+    mean = tree_inverse_weight(s, sum n)
+
+— must be bitwise the reference's op sequence (numpy restatement: fl(s + fl(x * f32(n))),
+then fl(s * f32(1/W))), with tree_weight deferred into the tree_add that consumes it and
+the delta's l2 norm taken from that launch. Edge cases: unaligned views, empty leaves,
+more leaves than one launch holds, non-float32 leaves, structure mismatch, a delta
+modified between tree_weight and tree_add.
+"""
+import numpy as np
+import pytest
+import torch
+
+import fedjax_amd
+from fedjax_amd import pytree, tree_util as tu
+from oracle import tree_util_ref as ref
+
+pytestmark = pytest.mark.gpu
+EMNIST = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "conv2_d_1": {"b": (64,), "w": (3, 3, 32, 64)},
+          "linear": {"b": (128,), "w": (9216, 128)}, "linear_1": {"b": (62,), "w": (128, 62)}}
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def tmap(fn, t):
+    return {k: tmap(fn, v) for k, v in t.items()} if isinstance(t, dict) else fn(t)
+
+
+def rand_tree(shapes, g, scale=0.01):
+    return tmap(lambda s: (torch.rand(s, generator=g) * 2 - 1) * scale, shapes)
+
+
+def to_dev(t, dev):
+    return tmap(lambda x: x.to(dev), t)
+
+
+def to_np(t):
+    return tmap(lambda x: x.detach().cpu().numpy(), t)
+
+
+def leaves_np(t):
+    return [x.detach().cpu().numpy().reshape(-1) for x in pytree.leaves_of(t)]
+
+
+def literal_loop(tu_mod, params, deltas, weights, with_norm=True):
+    """fedjax/algorithms/fed_avg.py:132-146 written against a tree_util module."""
+    s = tu_mod.tree_zeros_like(params)
+    n_sum = 0.
+    norms = []
+    for d, n in zip(deltas, weights):
+        s = tu_mod.tree_add(s, tu_mod.tree_weight(d, n))
+        n_sum += n
+        if with_norm:
+            norms.append(tu_mod.tree_l2_norm(d))
+    return tu_mod.tree_inverse_weight(s, n_sum), norms
+
+
+def test_literal_running_sum_bitwise_emnist(cuda):
+    g = torch.Generator().manual_seed(3)
+    K = 24
+    deltas_h = [rand_tree(EMNIST, g) for _ in range(K)]
+    weights = [int(v) for v in ref.fedavg_weights(K, seed=4)]
+    weights[5] = 2.5  # a float weight in the middle (weak float)
+    params = to_dev(tmap(lambda s: torch.zeros(s), EMNIST), cuda)
+    deltas = [to_dev(d, cuda) for d in deltas_h]
+    mean, norms = literal_loop(tu, params, deltas, weights)
+    # the reference's op sequence in numpy (oracle/tree_util_ref.py restates tree_util.py:29-61)
+    s = tmap(lambda s: np.zeros(s, np.float32), EMNIST)
+    n_sum = 0.
+    for d, n in zip(deltas_h, weights):
+        s = ref.tree_add(s, ref.tree_weight(to_np(d), n))
+        n_sum += n
+    want = ref.tree_inverse_weight(s, n_sum)
+    for got, w in zip(leaves_np(mean), [x.reshape(-1) for x in pytree.leaves_of(want)]):
+        assert np.array_equal(bits(got), bits(w))
+    # the cached fused norms are the standalone norms' bits, and within f32 rounding of f64
+    for d, nrm in zip(deltas, norms):
+        alone = tu._leaf_fold([d], [1], [None], norm_operand=0, no_out=True)[2]
+        assert torch.equal(nrm.view(torch.int32), alone.view(torch.int32))
+        x64 = np.concatenate([x.astype(np.float64) for x in leaves_np(d)])
+        np.testing.assert_allclose(float(nrm), np.sqrt((x64 * x64).sum()), rtol=2e-6)
+
+
+def test_weighted_tree_is_deferred_and_fused(cuda, monkeypatch):
+    """tree_weight returns a WeightedTree; tree_add consumes it in ONE fjtree launch
+    (no materialization), and tree_l2_norm of the same delta reuses that launch."""
+    g = torch.Generator().manual_seed(5)
+    d = to_dev(rand_tree({"a": (1000,), "b": (7, 3)}, g), cuda)
+    s = to_dev(rand_tree({"a": (1000,), "b": (7, 3)}, g), cuda)
+    wt = tu.tree_weight(d, 7)
+    assert type(wt) is tu.WeightedTree and wt._value is None
+    calls = []
+    real = tu._leaf_fold
+    monkeypatch.setattr(tu, "_leaf_fold", lambda *a, **k: calls.append(a) or real(*a, **k))
+    out = tu.tree_add(s, wt)
+    nrm = tu.tree_l2_norm(d)
+    assert len(calls) == 1 and wt._value is None  # fused: one launch, never materialized
+    want = {k: to_np(s)[k] + to_np(d)[k] * np.float32(7) for k in ("a", "b")}
+    for k in ("a", "b"):
+        assert np.array_equal(bits(out[k].cpu().numpy()), bits(want[k]))
+    x64 = np.concatenate([to_np(d)[k].astype(np.float64).reshape(-1) for k in ("a", "b")])
+    np.testing.assert_allclose(float(nrm), np.sqrt((x64 ** 2).sum()), rtol=2e-6)
+    assert float(tu.tree_l2_squared(d)) == pytest.approx(float(nrm) ** 2, rel=1e-6)
+
+
+def test_weighted_tree_materializes_on_use(cuda):
+    g = torch.Generator().manual_seed(6)
+    d = to_dev(rand_tree({"a": (33,), "b": {"c": (5, 5)}}, g), cuda)
+    wt = tu.tree_weight(d, 3)
+    want = {"a": to_np(d)["a"] * np.float32(3), "c": to_np(d)["b"]["c"] * np.float32(3)}
+    assert np.array_equal(bits(wt["a"].cpu().numpy()), bits(want["a"]))  # indexing
+    assert sorted(wt) == ["a", "b"] and len(wt) == 2 and "b" in wt and list(wt.keys()) == ["a", "b"]
+    leaves = pytree.leaves_of(wt)  # pytree walks see the weighted tree
+    assert np.array_equal(bits(leaves[1].cpu().numpy()), bits(want["c"]))
+    # tree_mean / tree_sum / tree_inverse_weight over deferred trees
+    m = tu.tree_mean([(tu.tree_weight(d, 2), 1), (tu.tree_weight(d, 4), 3)])
+    wm = (to_np(d)["a"] * np.float32(2) * np.float32(1) + to_np(d)["a"] * np.float32(4) * np.float32(3)) \
+        * np.float32(1 / 4)
+    assert np.array_equal(bits(m["a"].cpu().numpy()), bits(wm))
+    iw = tu.tree_inverse_weight(tu.tree_weight(d, 3), 3.0)
+    assert np.array_equal(bits(iw["a"].cpu().numpy()), bits(want["a"] * np.float32(1 / 3.0)))
+    # both operands deferred
+    both = tu.tree_add(tu.tree_weight(d, 2), tu.tree_weight(d, 5))
+    wb = to_np(d)["a"] * np.float32(2) + to_np(d)["a"] * np.float32(5)
+    assert np.array_equal(bits(both["a"].cpu().numpy()), bits(wb))
+
+
+def test_modified_delta_raises(cuda):
+    d = {"a": torch.ones(100, device=cuda)}
+    s = {"a": torch.zeros(100, device=cuda)}
+    wt = tu.tree_weight(d, 2)
+    d["a"].add_(1.0)  # in place, before the weighted value is used
+    with pytest.raises(RuntimeError, match="modified"):
+        tu.tree_add(s, wt)
+    wt = tu.tree_weight(d, 2)
+    d["a"] = torch.zeros(100, device=cuda)  # leaf replaced
+    with pytest.raises(RuntimeError, match="modified"):
+        tu.tree_add(s, wt)
+    # the fused-norm cache does not answer for a modified delta
+    d = {"a": torch.ones(100, device=cuda)}
+    tu.tree_add(s, tu.tree_weight(d, 2))
+    d["a"].mul_(2.0)
+    assert float(tu.tree_l2_norm(d)) == pytest.approx(20.0)
+
+
+def test_fast_path_edges(cuda):
+    # unaligned views (scalar loads), empty leaves, alias-free outputs
+    base = torch.arange(1, 4001, dtype=torch.float32, device=cuda) / 1000
+    d = {"u": base[1:3002], "e": base[:0], "v": base[3002:3999]}
+    s = {"u": base[:3001].clone(), "e": base[:0].clone(), "v": base[3:1000].clone()}
+    out = tu.tree_add(s, tu.tree_weight(d, 3))
+    for k in ("u", "v"):
+        want = s[k].cpu().numpy() + d[k].cpu().numpy() * np.float32(3)
+        assert np.array_equal(bits(out[k].cpu().numpy()), bits(want))
+    assert out["e"].numel() == 0
+    x64 = np.concatenate([d[k].cpu().numpy().astype(np.float64) for k in ("e", "u", "v")])
+    np.testing.assert_allclose(float(tu.tree_l2_norm(d)), np.sqrt((x64 ** 2).sum()), rtol=2e-6)
+    assert float(tu.tree_l2_norm({"e": base[:0]})) == 0.0
+    # more leaves than one fjtree launch holds: the pytree kernel path, same bits
+    many = {f"l{i:03d}": torch.full((3,), float(i), device=cuda) for i in range(70)}
+    got = tu.tree_add(many, tu.tree_weight(many, 2))
+    assert all(torch.equal(got[k], many[k] * 3) for k in many)
+    # bf16 leaves and int leaves: computed eagerly by the pytree kernel
+    hb = {"a": torch.ones(10, dtype=torch.bfloat16, device=cuda)}
+    assert type(tu.tree_weight(hb, 3)) is not tu.WeightedTree
+    hi = {"a": torch.arange(10, dtype=torch.int32, device=cuda)}
+    r = tu.tree_add(hi, tu.tree_weight(hi, 2))
+    assert r["a"].dtype == torch.int32 and torch.equal(r["a"], hi["a"] * 3)
+    # structure mismatch raises like jax.tree.map
+    with pytest.raises(ValueError):
+        tu.tree_add({"a": torch.ones(3, device=cuda)}, tu.tree_weight({"b": torch.ones(3, device=cuda)}, 2))
+    with pytest.raises(ValueError):
+        tu.tree_add({"a": torch.ones(3, device=cuda)}, tu.tree_weight({"a": torch.ones(4, device=cuda)}, 2))
+
+
+@pytest.mark.parametrize("K", [128])
+def test_literal_loop_configs1_bitwise_and_host_cost(K, cuda):
+    """configs[1] shape (EMNIST-CNN, 1,206,590 params): the literal loop over K=128 clients
+    is bitwise RunningMean / tree_mean and costs one launch per client (timed in
+    tools/time_literal_loop.py)."""
+    g = torch.Generator(device=cuda).manual_seed(8)
+    deltas = [tmap(lambda s: (torch.rand(s, device=cuda, generator=g) - 0.5) * 0.02, EMNIST) for _ in range(K)]
+    weights = [int(v) for v in ref.fedavg_weights(K, seed=9)]
+    params = tmap(lambda s: torch.zeros(s, device=cuda), EMNIST)
+    mean, norms = literal_loop(tu, params, deltas, weights)
+    rm = fedjax_amd.aggregators.RunningMean(params, buffer_clients=16, device=cuda)
+    for d, n in zip(deltas, weights):
+        rm.add(d, n)
+    want = rm.result()
+    for a, b in zip(pytree.leaves_of(mean), pytree.leaves_of(want)):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    nn = tu.tree_l2_norms(deltas)
+    np.testing.assert_allclose(torch.stack(norms).cpu().numpy(), nn.cpu().numpy(), rtol=2e-6)

@@ -64,7 +64,22 @@ def main(K=128, reps=20):
             s = tu.tree_add(s, tu.tree_weight(c, w))
             n += w
         return tu.tree_inverse_weight(s, n)
-    res["literal_loop_ms"] = round(wall(literal, 5), 4)
+    res["literal_loop_ms"] = round(wall(literal, 10), 4)
+
+    def literal_norms():  # + the per-client delta_l2_norm diagnostic of fed_avg.py:142-144
+        s = tu.tree_zeros_like(tmpl)
+        n, norms = 0., []
+        for c, w in zip(clients, weights):
+            s = tu.tree_add(s, tu.tree_weight(c, w))
+            n += w
+            norms.append(tu.tree_l2_norm(c))
+        return tu.tree_inverse_weight(s, n)
+    res["literal_loop_with_l2_norms_ms"] = round(wall(literal_norms, 10), 4)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    literal_norms()
+    res["literal_loop_with_l2_norms_host_issue_ms"] = round((time.perf_counter() - t0) * 1e3, 4)
+    torch.cuda.synchronize()
     out = literal()
     res["literal_loop_bitwise_eq_tree_mean"] = all(
         torch.equal(a, b) for a, b in zip(fedjax_amd.pytree.leaves_of(out), fedjax_amd.pytree.leaves_of(ref)))
