@@ -193,9 +193,14 @@ def main():
                     help="one GPU, world 1: run rank 0's share of an N-way shard through the full sharded "
                          "step (RCCL communicator of one rank). Timing rehearsal only: no cross-GPU traffic")
     ap.add_argument("--clients", type=int, default=0, help="override the workload's client count (experiments)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="N GPUs driven by ONE process (fjcomm_init_all / fjcomm_multi_wsum_dense, grouped RCCL "
+                         "reduce): the shape of FedJAX's server over jax.local_devices(); no launcher")
     ap.add_argument("--with-norms", action="store_true",
                     help="fuse every client's delta l2 norm into the fold (examples/fed_avg.py:79-81)")
     args = ap.parse_args()
+    if args.single_process:
+        return single_process(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # bare `python bench.py --gpus N`: one rank per GPU as child processes (no GPU
         # call has happened in this process, and nothing is exec'd)
@@ -464,6 +469,70 @@ def main():
         comm.close()
     if sharded:
         dist.destroy_process_group()
+
+
+def single_process(args):
+    """``--single-process``: one process folds each GPU's client share and sums the
+    partials with one grouped RCCL reduce per bucket (include/fjcomm.h,
+    fjcomm_multi_wsum_dense). Strong scaling over the same 1024 x 4 Mi workload."""
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+    from fedjax_amd import distributed as fd, kernels, tree_util as tu
+
+    N = args.gpus
+    if torch.cuda.device_count() < N:
+        raise SystemExit(f"--single-process --gpus {N}: only {torch.cuda.device_count()} GPUs visible")
+    K, P, dtype, desc = WORKLOADS[args.workload]
+    if args.clients:
+        K = args.clients
+    esize = torch.empty((), dtype=dtype).element_size()
+    weights = fedavg_weights(K)
+    W = 0.0
+    for w in weights:
+        W += w
+    devs = [torch.device("cuda", d) for d in range(N)]
+    xs, ws = [], []
+    for d, dev in enumerate(devs):
+        k0, k1 = fd.shard_range(K, d, N)
+        vw = 16 // esize
+        x = torch.empty(k1 - k0, (P + vw - 1) // vw * vw, dtype=dtype, device=dev)[:, :P]
+        kernels.fill_synth(x, seed=0, k0=k0)
+        xs.append(x)
+        ws.append(torch.tensor(np.float32(weights[k0:k1]), device=dev))
+    comm = fd.MultiDeviceCommunicator(devs)
+    outs = [torch.empty(P, dtype=torch.float32, device=dev) for dev in devs]
+    buckets = (tuple(float(v) for v in args.buckets.split(":")) if ":" in args.buckets
+               else int(args.buckets)) or 1
+
+    def sync():
+        for dev in devs:
+            torch.cuda.synchronize(dev)
+
+    def step():
+        fd.multi_device_weighted_mean(xs, ws, W, comm=comm, buckets=buckets, outs=outs,
+                                      all_devices=args.all_ranks)
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    comm.close()
+    res = {"metric": METRIC, "value": round(K * P * esize * args.steps / elapsed / 1e9, 2), "unit": "GB/s",
+           "n_gpus": N, "ranks": 1, "rccl_ranks": N, "launcher": "single process (fjcomm_init_all)",
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+           "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
+           "data": "synthetic: counter-hash client deltas 0.01*u[-1,1), integer weights in [1,500]",
+           "config": {"workload": desc, "clients": K, "params": P,
+                      "parallelism": f"client-sharded x{N}, one process, grouped RCCL "
+                                     f"{'all_reduce' if args.all_ranks else 'reduce'}",
+                      "buckets": fd.bucket_name(buckets)}}
+    os.write(json_fd, (json.dumps(res) + "\n").encode())
 
 
 if __name__ == "__main__":

@@ -36,6 +36,7 @@ COMP_ABI_VERSION = 1
 COMM_ABI_VERSION = 1
 COMM_ID_BYTES = 128
 COMM_MAX_BUCKETS = 64
+COMM_MAX_DEVICES = 16
 TREE_ABI_VERSION = 1
 TREE_MAX_LEAVES, TREE_MAX_OPERANDS = 64, 2
 TREE_NORM, TREE_NO_OUT = 1 << 8, 1 << 9
@@ -89,6 +90,9 @@ _SIGNATURES = {
                                          _vp]),
     "fjcomm_sharded_wsum_dense_edges": (_i32, [_vp, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i32, _i32,
                                                _i32, _vp, _vp]),
+    "fjcomm_init_all": (_i32, [_vp, _i32, _vp]),
+    "fjcomm_multi_wsum_dense": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _i64, _vp, _f32, _vp, _vp, _i32, _i32, _i32,
+                                       _vp]),
     "fjagg_event_create": (_i32, [_vp]),
     "fjagg_event_destroy": (_i32, [_vp]),
     "fjagg_event_record": (_i32, [_vp, _vp]),

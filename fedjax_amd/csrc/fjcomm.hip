@@ -46,6 +46,9 @@ constexpr int kNcclSum = 0;
 struct Rccl {
   int (*get_unique_id)(NcclId*) = nullptr;
   int (*comm_init_rank)(NcclComm*, int, NcclId, int) = nullptr;
+  int (*comm_init_all)(NcclComm*, int, const int*) = nullptr;
+  int (*group_start)() = nullptr;
+  int (*group_end)() = nullptr;
   int (*comm_destroy)(NcclComm) = nullptr;
   int (*reduce)(const void*, void*, size_t, int, int, int, NcclComm, hipStream_t) = nullptr;
   int (*all_reduce)(const void*, void*, size_t, int, int, NcclComm, hipStream_t) = nullptr;
@@ -64,10 +67,14 @@ const Rccl& rccl() {
     t.get_unique_id = reinterpret_cast<decltype(t.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
     t.comm_init_rank = reinterpret_cast<decltype(t.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
     t.comm_destroy = reinterpret_cast<decltype(t.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    t.comm_init_all = reinterpret_cast<decltype(t.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+    t.group_start = reinterpret_cast<decltype(t.group_start)>(dlsym(h, "ncclGroupStart"));
+    t.group_end = reinterpret_cast<decltype(t.group_end)>(dlsym(h, "ncclGroupEnd"));
     t.reduce = reinterpret_cast<decltype(t.reduce)>(dlsym(h, "ncclReduce"));
     t.all_reduce = reinterpret_cast<decltype(t.all_reduce)>(dlsym(h, "ncclAllReduce"));
     t.error_string = reinterpret_cast<decltype(t.error_string)>(dlsym(h, "ncclGetErrorString"));
-    t.ok = t.get_unique_id && t.comm_init_rank && t.comm_destroy && t.reduce && t.all_reduce && t.error_string;
+    t.ok = t.get_unique_id && t.comm_init_rank && t.comm_destroy && t.reduce && t.all_reduce && t.error_string &&
+           t.comm_init_all && t.group_start && t.group_end;
     return t;
   }();
   return r;
@@ -100,6 +107,41 @@ hipError_t make_dep_event(hipEvent_t* e) {
   return rc;
 }
 
+// The communicator's own stream (highest priority) and its events, on the current device.
+hipError_t make_comm_resources(Comm* c) {
+  hipError_t e = hipGetDevice(&c->device);
+  int lo = 0, hi = 0;
+  if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, hi);
+  for (int b = 0; e == hipSuccess && b < FJCOMM_MAX_BUCKETS; ++b) e = make_dep_event(&c->ready[b]);
+  if (e == hipSuccess) e = make_dep_event(&c->done);
+  return e;
+}
+
+// Restores the calling thread's current HIP device on scope exit.
+struct DeviceGuard {
+  int saved = -1;
+  DeviceGuard() { (void)hipGetDevice(&saved); }
+  ~DeviceGuard() {
+    if (saved >= 0) (void)hipSetDevice(saved);
+  }
+};
+
+int check_edges(const int64_t* edges, int nbuckets, int64_t P) {
+  if (nbuckets < 1 || nbuckets > FJCOMM_MAX_BUCKETS)
+    return fail(FJAGG_EINVAL, "nbuckets must be in [1, %d]", FJCOMM_MAX_BUCKETS);
+  if (!edges) return fail(FJAGG_EINVAL, "null edges");
+  if (edges[0] != 0 || edges[nbuckets] != P)
+    return fail(FJAGG_EINVAL, "edges must run from 0 to P = %lld", (long long)P);
+  for (int b = 0; b < nbuckets; ++b) {
+    if (edges[b + 1] <= edges[b]) return fail(FJAGG_EINVAL, "edges must increase strictly (bucket %d)", b);
+    if (edges[b] % FJCOMM_BUCKET_ALIGN)
+      return fail(FJAGG_EINVAL, "edge %lld is not a multiple of %d elements", (long long)edges[b],
+                  FJCOMM_BUCKET_ALIGN);
+  }
+  return FJAGG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -124,12 +166,7 @@ int fjcomm_init(void** comm, const uint8_t* id, int nranks, int rank) {
   Comm* c = new Comm();
   c->nranks = nranks;
   c->rank = rank;
-  hipError_t e = hipGetDevice(&c->device);
-  int lo = 0, hi = 0;
-  if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-  if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, hi);
-  for (int b = 0; e == hipSuccess && b < FJCOMM_MAX_BUCKETS; ++b) e = make_dep_event(&c->ready[b]);
-  if (e == hipSuccess) e = make_dep_event(&c->done);
+  hipError_t e = make_comm_resources(c);
   if (e != hipSuccess) {
     int rc = hip_fail(e, "fjcomm_init");
     fjcomm_destroy(c);
@@ -150,6 +187,8 @@ int fjcomm_init(void** comm, const uint8_t* id, int nranks, int rank) {
 int fjcomm_destroy(void* comm) {
   Comm* c = reinterpret_cast<Comm*>(comm);
   if (!c) return FJAGG_OK;
+  DeviceGuard guard;  // the communicator's resources live on its device
+  (void)hipSetDevice(c->device);
   if (c->cs) (void)hipStreamSynchronize(c->cs);
   if (c->nc && rccl().ok) rccl().comm_destroy(c->nc);
   for (hipEvent_t& e : c->ready)
@@ -193,15 +232,7 @@ int fjcomm_sharded_wsum_dense_edges(void* comm, int in_dtype, const void* x_dev,
     return fail(FJAGG_EINVAL, "nbuckets must be in [1, %d]", FJCOMM_MAX_BUCKETS);
   if (root >= c->nranks) return fail(FJAGG_EINVAL, "root %d >= nranks %d", root, c->nranks);
   if (P == 0) return FJAGG_OK;
-  if (!edges) return fail(FJAGG_EINVAL, "null edges");
-  if (edges[0] != 0 || edges[nbuckets] != P)
-    return fail(FJAGG_EINVAL, "edges must run from 0 to P = %lld", (long long)P);
-  for (int b = 0; b < nbuckets; ++b) {
-    if (edges[b + 1] <= edges[b]) return fail(FJAGG_EINVAL, "edges must increase strictly (bucket %d)", b);
-    if (edges[b] % FJCOMM_BUCKET_ALIGN)
-      return fail(FJAGG_EINVAL, "edge %lld is not a multiple of %d elements", (long long)edges[b],
-                  FJCOMM_BUCKET_ALIGN);
-  }
+  if (int rc = check_edges(edges, nbuckets, P)) return rc;
   if (!out_dev || (K > 0 && (!x_dev || !w_dev))) return fail(FJAGG_EINVAL, "null pointer argument");
   if (flags & ~(FJAGG_NONTEMPORAL | FJAGG_VARIANT(0xff)))
     return fail(FJAGG_EINVAL, "flags may hold FJAGG_NONTEMPORAL and FJAGG_VARIANT bits only");
@@ -244,6 +275,116 @@ int fjcomm_sharded_wsum_dense_edges(void* comm, int in_dtype, const void* x_dev,
                        ? rccl().reduce(seg, seg, (size_t)n, kNcclFloat32, kNcclSum, root, c->nc, rs)
                        : rccl().all_reduce(seg, seg, (size_t)n, kNcclFloat32, kNcclSum, c->nc, rs);
     if (rc != kNcclSuccess) return nccl_fail(rc, root >= 0 ? "ncclReduce" : "ncclAllReduce");
+  }
+  return FJAGG_OK;
+}
+
+int fjcomm_init_all(void** comms, int ndev, const int* devs) {
+  fjagg_g_err[0] = 0;
+  if (int rc = need_rccl()) return rc;
+  if (!comms || !devs) return fail(FJAGG_EINVAL, "null argument");
+  if (ndev < 1 || ndev > FJCOMM_MAX_DEVICES) return fail(FJAGG_EINVAL, "ndev must be in [1, %d]", FJCOMM_MAX_DEVICES);
+  for (int d = 0; d < ndev; ++d) {
+    comms[d] = nullptr;
+    for (int e = 0; e < d; ++e)
+      if (devs[e] == devs[d]) return fail(FJAGG_EINVAL, "device %d listed twice", devs[d]);
+  }
+  DeviceGuard guard;
+  Comm* cs[FJCOMM_MAX_DEVICES] = {};
+  NcclComm nc[FJCOMM_MAX_DEVICES] = {};
+  int rc = FJAGG_OK;
+  for (int d = 0; d < ndev && rc == FJAGG_OK; ++d) {
+    cs[d] = new Comm();
+    cs[d]->nranks = ndev;
+    cs[d]->rank = d;
+    hipError_t e = hipSetDevice(devs[d]);
+    if (e == hipSuccess) e = make_comm_resources(cs[d]);
+    if (e != hipSuccess) rc = hip_fail(e, "fjcomm_init_all");
+  }
+  if (rc == FJAGG_OK) {
+    if (int nr = rccl().comm_init_all(nc, ndev, devs)) rc = nccl_fail(nr, "ncclCommInitAll");
+  }
+  if (rc != FJAGG_OK) {
+    for (int d = 0; d < ndev; ++d)
+      if (cs[d]) {
+        cs[d]->nc = nc[d];
+        (void)hipSetDevice(cs[d]->device);
+        fjcomm_destroy(cs[d]);
+      }
+    return rc;
+  }
+  for (int d = 0; d < ndev; ++d) {
+    cs[d]->nc = nc[d];
+    comms[d] = cs[d];
+  }
+  return FJAGG_OK;
+}
+
+int fjcomm_multi_wsum_dense(void* const* comms, int ndev, int in_dtype, const void* const* x_dev,
+                            const int64_t* ld, const int64_t* K, int64_t P, const void* const* w_dev, float scale,
+                            float* const* out_dev, const int64_t* edges, int nbuckets, int root, int flags,
+                            void* const* streams) {
+  fjagg_g_err[0] = 0;
+  if (!comms || !x_dev || !ld || !K || !w_dev || !out_dev || !streams) return fail(FJAGG_EINVAL, "null argument");
+  if (ndev < 1 || ndev > FJCOMM_MAX_DEVICES) return fail(FJAGG_EINVAL, "ndev must be in [1, %d]", FJCOMM_MAX_DEVICES);
+  if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16) return fail(FJAGG_EINVAL, "in_dtype must be F32 or BF16");
+  if (P < 0) return fail(FJAGG_EINVAL, "P < 0");
+  if (root >= ndev) return fail(FJAGG_EINVAL, "root %d >= ndev %d", root, ndev);
+  if (flags & ~(FJAGG_NONTEMPORAL | FJAGG_VARIANT(0xff)))
+    return fail(FJAGG_EINVAL, "flags may hold FJAGG_NONTEMPORAL and FJAGG_VARIANT bits only");
+  Comm* cs[FJCOMM_MAX_DEVICES];
+  for (int d = 0; d < ndev; ++d) {
+    cs[d] = reinterpret_cast<Comm*>(comms[d]);
+    if (!cs[d] || !cs[d]->nc) return fail(FJAGG_EINVAL, "comms[%d] is not an initialised communicator", d);
+    if (cs[d]->rank != d || cs[d]->nranks != ndev)
+      return fail(FJAGG_EINVAL, "comms[%d] is rank %d of %d, not %d of %d (pass fjcomm_init_all's handles in order)",
+                  d, cs[d]->rank, cs[d]->nranks, d, ndev);
+    if (K[d] < 0 || ld[d] < P || !out_dev[d] || (K[d] > 0 && (!x_dev[d] || !w_dev[d])))
+      return fail(FJAGG_EINVAL, "device %d: need K >= 0, ld >= P and non-null pointers", d);
+  }
+  if (P == 0) return FJAGG_OK;
+  if (int rc = check_edges(edges, nbuckets, P)) return rc;
+  DeviceGuard guard;
+  const int64_t esz = in_dtype == FJAGG_BF16 ? 2 : 4;
+  const int nb = nbuckets;
+  for (int b = 0; b < nb; ++b) {
+    const int64_t p0 = edges[b], n = edges[b + 1] - p0;
+    // every device folds its clients' share of bucket b on its own stream, then signals
+    // its communicator stream (all but the last bucket, as in the one-rank-per-process path)
+    for (int d = 0; d < ndev; ++d) {
+      Comm* c = cs[d];
+      hipStream_t s = reinterpret_cast<hipStream_t>(streams[d]);
+      if (hipError_t e = hipSetDevice(c->device)) return hip_fail(e, "hipSetDevice");
+      float* seg = out_dev[d] + p0;
+      if (K[d] > 0) {
+        const uint8_t* xb = reinterpret_cast<const uint8_t*>(x_dev[d]) + p0 * esz;
+        if (int rc = fjagg_wsum_dense(in_dtype, FJAGG_F32, FJAGG_F32, xb, ld[d], K[d], n, w_dev[d], scale, seg,
+                                      flags | FJAGG_SCALE, FJAGG_MODE_EXACT, nullptr, 0, s))
+          return rc;
+      } else if (hipError_t e = hipMemsetAsync(seg, 0, n * sizeof(float), s)) {
+        return hip_fail(e, "hipMemsetAsync");
+      }
+      if (b + 1 < nb) {
+        if (hipError_t e = hipEventRecord(c->ready[b], s)) return hip_fail(e, "hipEventRecord");
+        if (hipError_t e = hipStreamWaitEvent(c->cs, c->ready[b], 0)) return hip_fail(e, "hipStreamWaitEvent");
+      } else if (nb > 1) {
+        if (hipError_t e = hipEventRecord(c->done, c->cs)) return hip_fail(e, "hipEventRecord");
+        if (hipError_t e = hipStreamWaitEvent(s, c->done, 0)) return hip_fail(e, "hipStreamWaitEvent");
+      }
+    }
+    // one process drives every device: the collectives of a bucket are one RCCL group
+    if (int r = rccl().group_start()) return nccl_fail(r, "ncclGroupStart");
+    int rc = kNcclSuccess;
+    for (int d = 0; d < ndev && rc == kNcclSuccess; ++d) {
+      Comm* c = cs[d];
+      hipStream_t rs = b + 1 < nb ? c->cs : reinterpret_cast<hipStream_t>(streams[d]);
+      float* seg = out_dev[d] + p0;
+      rc = root >= 0 ? rccl().reduce(seg, seg, (size_t)n, kNcclFloat32, kNcclSum, root, c->nc, rs)
+                     : rccl().all_reduce(seg, seg, (size_t)n, kNcclFloat32, kNcclSum, c->nc, rs);
+    }
+    const int ge = rccl().group_end();
+    if (rc != kNcclSuccess) return nccl_fail(rc, root >= 0 ? "ncclReduce" : "ncclAllReduce");
+    if (ge != kNcclSuccess) return nccl_fail(ge, "ncclGroupEnd");
   }
   return FJAGG_OK;
 }

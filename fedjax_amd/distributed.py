@@ -285,3 +285,98 @@ def sharded_tree_mean(local_pytrees_and_weights, *, W_total=None, group=None, ds
                              "(a pytree with the clients' structure) to shape the result")
         return pytree.unflatten(td, views)
     return None
+
+
+# ------------------------------------------------------------- one process, several GPUs
+class MultiDeviceCommunicator:
+    """RCCL communicators over several GPUs of ONE process (``fjcomm_init_all`` =
+    ``ncclCommInitAll``): the shape of FedJAX's server, one Python process over
+    ``jax.local_devices()`` (fedjax/core/for_each_client.py:266-357). No launcher and no
+    torch.distributed process group are involved. ``close()`` destroys the handles."""
+
+    def __init__(self, devices: Sequence):
+        lib = _lib.load()
+        self.devices = [torch.device(d) if not isinstance(d, torch.device) else d for d in devices]
+        idx = []
+        for d in self.devices:
+            if d.type != "cuda":
+                raise ValueError(f"{d} is not a GPU")
+            idx.append(d.index if d.index is not None else torch.cuda.current_device())
+        n = len(idx)
+        if not 1 <= n <= _lib.COMM_MAX_DEVICES:
+            raise ValueError(f"need 1..{_lib.COMM_MAX_DEVICES} devices, got {n}")
+        if len(set(idx)) != n:
+            raise ValueError(f"devices must be distinct, got {idx}")
+        self.indices = idx
+        handles = (ctypes.c_void_p * n)()
+        _lib.check(lib.fjcomm_init_all(handles, n, (ctypes.c_int * n)(*idx)), "fjcomm_init_all")
+        self.handles = handles
+
+    def __len__(self):
+        return len(self.indices)
+
+    def close(self) -> None:
+        hs = getattr(self, "handles", None)
+        if hs is not None:
+            lib = _lib.load()
+            for h in hs:
+                if h:
+                    lib.fjcomm_destroy(ctypes.c_void_p(h))
+            self.handles = None
+
+    __del__ = close
+
+
+def multi_device_weighted_mean(xs: Sequence[torch.Tensor], ws: Sequence[torch.Tensor], W_total, *,
+                               comm: MultiDeviceCommunicator, root: int = 0, all_devices: bool = False,
+                               buckets: Union[int, Sequence[float]] = 1,
+                               outs: Optional[Sequence[torch.Tensor]] = None,
+                               nontemporal: Optional[bool] = None) -> List[torch.Tensor]:
+    """Weighted mean over clients spread across the GPUs of this process.
+
+    xs[d]: the client slab [K_d, P] (unit column stride, float32 or bfloat16) on
+    ``comm.devices[d]``; ws[d]: its float32 weights [K_d] there; W_total: the sum of ALL
+    clients' weights (tree_util.py:86,95, host value). Each device folds its clients into
+    a float32 partial already scaled by f32(1/W); the partials are summed by one grouped
+    RCCL reduce per bucket (all-reduce with ``all_devices``). Returns the per-device
+    float32 [P] buffers: the mean is in ``outs[root]`` (in every one with
+    ``all_devices``). Asynchronous on each device's current stream. Numerics as
+    :func:`sharded_weighted_mean`; with one device, bitwise the exact fold.
+    """
+    n = len(comm)
+    if len(xs) != n or len(ws) != n:
+        raise ValueError(f"need one slab and one weight vector per device ({n})")
+    P = xs[0].shape[1]
+    dt = xs[0].dtype
+    for d, (x, w, dev) in enumerate(zip(xs, ws, comm.devices)):
+        if x.dim() != 2 or x.shape[1] != P or x.dtype != dt or dt not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"device {d}: slabs must be [K_d, {P}] of one float dtype")
+        if x.shape[0] and x.stride(1) != 1:
+            raise ValueError(f"device {d}: client rows need unit column stride")
+        if x.device != dev or w.device != dev:
+            raise ValueError(f"device {d}: slab and weights must be on {dev}")
+        if w.dtype != torch.float32 or w.numel() != x.shape[0]:
+            raise ValueError(f"device {d}: weights must be float32 [K_d]")
+    if outs is None:
+        outs = [torch.empty(P, dtype=torch.float32, device=dev) for dev in comm.devices]
+    for d, (o, dev) in enumerate(zip(outs, comm.devices)):
+        if o.dtype != torch.float32 or o.numel() != P or not o.is_contiguous() or o.device != dev:
+            raise ValueError(f"device {d}: out must be a contiguous float32 [P] tensor on {dev}")
+    spans = bucket_edges(P, buckets)
+    if not spans:
+        return list(outs)
+    if len(spans) > _lib.COMM_MAX_BUCKETS:
+        raise ValueError(f"at most {_lib.COMM_MAX_BUCKETS} buckets")
+    edges = np.array([p0 for p0, _ in spans] + [P], dtype=np.int64)
+    nbytes = max(x.shape[0] for x in xs) * P * xs[0].element_size()
+    nt = (nbytes >= tree_util.NONTEMPORAL_MIN_BYTES) if nontemporal is None else nontemporal
+    scale = float(np.float32(tree_util._inverse(W_total)))
+    vp = ctypes.c_void_p * n
+    i64 = ctypes.c_int64 * n
+    _lib.call("fjcomm_multi_wsum_dense", comm.handles, n, kernels.dtype_code(dt),
+              vp(*[x.data_ptr() if x.shape[0] else None for x in xs]),
+              i64(*[x.stride(0) if x.shape[0] > 1 else P for x in xs]), i64(*[x.shape[0] for x in xs]), P,
+              vp(*[w.data_ptr() if w.numel() else None for w in ws]), scale, vp(*[o.data_ptr() for o in outs]),
+              edges.ctypes.data, len(spans), -1 if all_devices else int(root), _lib.NONTEMPORAL if nt else 0,
+              vp(*[torch.cuda.current_stream(dev).cuda_stream for dev in comm.devices]))
+    return list(outs)

@@ -81,6 +81,32 @@ int fjcomm_sharded_wsum_dense_edges(void* comm, int in_dtype, const void* x_dev,
                                     const int64_t* edges, int nbuckets, int root, int flags, void* stream,
                                     void* const* fold_events);
 
+/*
+ * Single process, several GPUs. FedJAX's server is ONE Python process over
+ * jax.local_devices() (fedjax/core/for_each_client.py:266-357, devices at :289-293);
+ * these entry points give such a process the sharded aggregation without a launcher:
+ *
+ * fjcomm_init_all: ncclCommInitAll over devs[0..ndev) (distinct HIP device ordinals);
+ * comms[d] is the handle of devs[d] (rank d), with its own stream and events on that
+ * device. Destroy each handle with fjcomm_destroy. The calling thread's current device
+ * is restored on return.
+ *
+ * fjcomm_multi_wsum_dense: one round over all devices, issued from one thread. Device d
+ * folds its client slab (x_dev[d]: K[d] rows of ld[d] elements, w_dev[d] float[K[d]],
+ * both on devs[d]) into out_dev[d] (float32 [P] on devs[d]) scaled by `scale`, on
+ * streams[d]; the partials are then summed by ncclReduce to device `root` (ncclAllReduce
+ * when root < 0), bucket by bucket over `edges` as in fjcomm_sharded_wsum_dense_edges.
+ * The collectives of one bucket are one ncclGroupStart/End group (required when one
+ * thread drives several ranks). streams[d] waits for the last collective of device d.
+ * K[d] may be 0 (device d contributes zeros).
+ */
+#define FJCOMM_MAX_DEVICES 16
+int fjcomm_init_all(void** comms, int ndev, const int* devs);
+int fjcomm_multi_wsum_dense(void* const* comms, int ndev, int in_dtype, const void* const* x_dev,
+                            const int64_t* ld, const int64_t* K, int64_t P, const void* const* w_dev, float scale,
+                            float* const* out_dev, const int64_t* edges, int nbuckets, int root, int flags,
+                            void* const* streams);
+
 /* Timing events without the system-scope fence (hipEventDisableSystemFence): recording
  * one costs no cache write-back, so bracketing every launch does not perturb it. */
 int fjagg_event_create(void** ev);

@@ -134,3 +134,25 @@ def test_tree_table_layout_and_validation():
     assert lib.fjtree_workspace_bytes(ctypes.byref(t)) == 256 + 4
     t.n[0] = 4097
     assert lib.fjtree_workspace_bytes(ctypes.byref(t)) == 256 + 8
+
+
+def test_multi_device_entry_points_validate_without_gpu():
+    """include/fjcomm.h single-process entry points refuse bad arguments before any HIP or
+    RCCL work (no GPU here)."""
+    import ctypes
+    lib = _lib.load()
+    h = (ctypes.c_void_p * 2)()
+    assert lib.fjcomm_init_all(h, 0, (ctypes.c_int * 1)(0)) != 0
+    assert lib.fjcomm_init_all(h, 2, (ctypes.c_int * 2)(0, 0)) != 0  # a device listed twice
+    assert lib.fjcomm_init_all(None, 1, (ctypes.c_int * 1)(0)) != 0
+    vp = ctypes.c_void_p * 1
+    i64 = ctypes.c_int64 * 1
+    rc = lib.fjcomm_multi_wsum_dense(None, 1, _lib.F32, vp(16), i64(4), i64(1), 4, vp(16), 1.0, vp(16),
+                                     None, 1, 0, 0, vp(0))
+    assert rc == -1 and b"null argument" in lib.fjagg_last_error()
+    rc = lib.fjcomm_multi_wsum_dense(h, 1, _lib.F32, vp(16), i64(4), i64(1), 4, vp(16), 1.0, vp(16),
+                                     None, 1, 0, 0, vp(0))
+    assert rc == -1 and b"not an initialised communicator" in lib.fjagg_last_error()
+    rc = lib.fjcomm_multi_wsum_dense(h, 0, _lib.F32, vp(16), i64(4), i64(1), 4, vp(16), 1.0, vp(16),
+                                     None, 1, 0, 0, vp(0))
+    assert rc == -1 and b"ndev" in lib.fjagg_last_error()

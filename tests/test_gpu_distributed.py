@@ -157,3 +157,57 @@ def test_native_rccl_pipeline_world1(cuda, coracle):
     xb = (coracle.synth_bf16(K, P, seed=9).astype(np.uint32) << 16).view(np.float32)  # bf16 -> f32 exactly
     want_b = coracle.wsum_f32(np.ascontiguousarray(xb), np.float32(weights), scale=r)
     assert np.array_equal(yb.view(np.uint32), want_b.astype(np.float32).view(np.uint32))
+
+
+def _multi_device_worker(q):
+    """One process over its GPUs (here the box's one GPU): fjcomm_init_all +
+    fjcomm_multi_wsum_dense, no launcher, no process group."""
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    from fedjax_amd import distributed as fd, kernels
+    weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
+    W = 0.0
+    for w in weights:
+        W += w
+    comm = fd.MultiDeviceCommunicator([dev])
+    x = torch.empty(K, P + 5, dtype=torch.float32, device=dev)[:, :P]
+    kernels.fill_synth(x, seed=9)
+    wl = torch.tensor(np.float32(weights), device=dev)
+    res = {}
+    for buckets, alld in ((1, False), (3, False), ((4, 2, 1), True)):
+        outs = fd.multi_device_weighted_mean([x], [wl], W, comm=comm, buckets=buckets, all_devices=alld)
+        torch.cuda.synchronize()
+        res[(fd.bucket_name(buckets), alld)] = outs[0].cpu().numpy()
+    z = fd.multi_device_weighted_mean([x[:0]], [wl[:0]], W, comm=comm)[0]  # a device without clients
+    torch.cuda.synchronize()
+    errs = []
+    for bad in (lambda: fd.multi_device_weighted_mean([x, x], [wl, wl], W, comm=comm),
+                lambda: fd.multi_device_weighted_mean([x], [wl[:3]], W, comm=comm),
+                lambda: fd.MultiDeviceCommunicator([dev, dev])):
+        try:
+            bad()
+            errs.append(None)
+        except (ValueError, RuntimeError) as e:
+            errs.append(type(e).__name__)
+    comm.close()
+    q.put((res, z.cpu().numpy(), errs))
+
+
+def test_single_process_multi_device_ndev1(cuda, coracle):
+    """the single-process entry point at ndev = 1 is bitwise the exact
+    fold (a one-rank reduce is the identity) for equal and tapered buckets, reduce and
+    all-reduce; a device without clients contributes zeros; bad inputs are refused."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_multi_device_worker, args=(q,))
+    p.start()
+    res, z, errs = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
+    x = coracle.synth_f32(K, P, seed=9)
+    want = coracle.wsum_f32(x, np.float32(weights), scale=ref.mean_scale(weights))
+    for key, y in res.items():
+        assert np.array_equal(y.view(np.uint32), want.astype(np.float32).view(np.uint32)), key
+    assert np.all(z == 0)
+    assert errs == ["ValueError", "ValueError", "ValueError"]
