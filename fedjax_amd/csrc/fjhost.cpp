@@ -560,7 +560,7 @@ typedef int (*TreeFoldFn)(const fjtree_leaves*, void*);
 typedef int64_t (*TreeWsFn)(const fjtree_leaves*);
 constexpr int kStale = -100;
 
-// capture(tree, dev) -> (leaves_tuple, version_sum) | None   (dev = -1: the first leaf's)
+// capture(tree, dev) -> (leaves_tuple, version_sum, nbytes) | None   (dev = -1: the first leaf's)
 //     tree_weight's lazy result holds its input's leaves (strong references, flatten order)
 //     and their version sum, so tree_add can check that nothing changed in between.
 PyObject* capture(PyObject*, PyObject* args) {
@@ -583,11 +583,13 @@ PyObject* capture(PyObject*, PyObject* args) {
     const Py_ssize_t L = static_cast<Py_ssize_t>(w.leaves[0].size());
     PyObject* tup = PyTuple_New(L);
     if (!tup) return nullptr;
+    int64_t nbytes = 0;
     for (Py_ssize_t l = 0; l < L; ++l) {
       Py_INCREF(w.leaves[0][l]);
       PyTuple_SET_ITEM(tup, l, w.leaves[0][l]);
+      nbytes += 4 * THPVariable_Unpack(w.leaves[0][l]).numel();
     }
-    return Py_BuildValue("(NL)", tup, static_cast<long long>(vs));
+    return Py_BuildValue("(NLL)", tup, static_cast<long long>(vs), static_cast<long long>(nbytes));
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
@@ -612,6 +614,71 @@ PyObject* matches(PyObject*, PyObject* args) {
     }
     if (vs != vsum) Py_RETURN_FALSE;
     Py_RETURN_TRUE;
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
+// compatible(a, b) -> bool: the two trees have the same structure (the fast walk's node
+// kinds, dict keys, lengths) and float32 device leaves of equal shapes on one device,
+// i.e. tree_add(a, b) is the fast case. Nothing is launched.
+PyObject* compatible(PyObject*, PyObject* args) {
+  PyObject *a, *b;
+  if (!PyArg_ParseTuple(args, "OO", &a, &b)) return nullptr;
+  try {
+    PWalk w;
+    w.K = 2;
+    PyObject* xs[2] = {a, b};
+    int rc = pwalk(xs, w, 0);
+    if (rc < 0) return nullptr;
+    if (rc > 0 || w.leaves[0].empty()) Py_RETURN_FALSE;
+    const at::Tensor& t0 = THPVariable_Unpack(w.leaves[0][0]);
+    if (!t0.is_cuda()) Py_RETURN_FALSE;
+    int64_t vs;
+    if (!check_leaves(w, 0, t0.get_device(), &vs) || !check_leaves(w, 1, t0.get_device(), &vs)) Py_RETURN_FALSE;
+    Py_RETURN_TRUE;
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
+// table_from_caps(caps, ptrs) -> int
+//     caps: list of K captures (leaves_tuple, version_sum) of L leaves each; writes leaf l of
+//     capture k's device pointer to ptrs[k*L + l] (int64 buffer). Returns -1 when every
+//     capture is unchanged (same versions), else the index of the first stale one.
+PyObject* table_from_caps(PyObject*, PyObject* args) {
+  PyObject *caps, *ptrs;
+  if (!PyArg_ParseTuple(args, "O!O", &PyList_Type, &caps, &ptrs)) return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(caps);
+  if (K == 0) return PyLong_FromLong(-1);
+  const Py_ssize_t L = PyTuple_GET_SIZE(PyTuple_GET_ITEM(PyList_GET_ITEM(caps, 0), 0));
+  Py_buffer buf;
+  if (PyObject_GetBuffer(ptrs, &buf, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) != 0) return nullptr;
+  struct Release {
+    Py_buffer* b;
+    ~Release() { PyBuffer_Release(b); }
+  } release{&buf};
+  if (buf.len < static_cast<Py_ssize_t>(sizeof(int64_t)) * K * L) {
+    PyErr_SetString(PyExc_ValueError, "table_from_caps: pointer buffer smaller than K*L int64");
+    return nullptr;
+  }
+  auto* out = static_cast<int64_t*>(buf.buf);
+  try {
+    for (Py_ssize_t k = 0; k < K; ++k) {
+      PyObject* cap = PyList_GET_ITEM(caps, k);
+      PyObject* tup = PyTuple_GET_ITEM(cap, 0);
+      if (PyTuple_GET_SIZE(tup) != L) return PyLong_FromSsize_t(k);
+      int64_t vs = 0;
+      for (Py_ssize_t l = 0; l < L; ++l) {
+        const at::Tensor& t = THPVariable_Unpack(PyTuple_GET_ITEM(tup, l));
+        vs += static_cast<int64_t>(t._version());
+        out[k * L + l] = reinterpret_cast<int64_t>(t.data_ptr());
+      }
+      if (vs != PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1))) return PyLong_FromSsize_t(k);
+    }
+    return PyLong_FromLong(-1);
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
@@ -736,6 +803,8 @@ PyMethodDef kMethods[] = {
     {"fold_weights", fold_weights, METH_VARARGS, "f32/i32 weights and W of Python-number weights"},
     {"capture", capture, METH_VARARGS, "leaves + version sum of a tree for a lazy tree_weight"},
     {"matches", matches, METH_VARARGS, "tree holds exactly the captured leaves, unmodified"},
+    {"compatible", compatible, METH_VARARGS, "tree_add(a, b) is the fast case (structure, float32 leaves)"},
+    {"table_from_caps", table_from_caps, METH_VARARGS, "pointer table of captured leaves, version check"},
     {"leaf_fold", leaf_fold, METH_VARARGS, "fjtree_fold_leaves over 1-2 operand trees (see fjhost.cpp)"},
     {"fold_table", fold_table, METH_VARARGS, "plan image + output leaves + fjagg_wsum_ptrs launch (see fjhost.cpp)"},
     {nullptr, nullptr, 0, nullptr},

@@ -17,7 +17,7 @@
 //     __fmul_rn / __fadd_rn and -ffp-contract=off;
 //   * the optional l2 norm reads the operand the fold already loaded: per-lane partials
 //     in element order, xor butterfly, waves in order, then the last workgroup to finish
-//     (completion counter, agent-scope fences) adds the workgroup partials in order and
+//     (completion counter, agent-scope stores and loads) adds the workgroup partials in order and
 //     resets the counter. The lane -> element map is the same on both paths, so the norm
 //     does not depend on alignment.
 #include <hip/hip_runtime.h>
@@ -71,8 +71,12 @@ __global__ __launch_bounds__(kThreads) void k_leaves(const Args a) {
   __shared__ float wsum[kThreads / 64];
   __shared__ int last;
   const int b = blockIdx.x;
+  // leaf of this workgroup: blk0 is non-decreasing and padded with INT32_MAX, so counting
+  // the entries <= b needs no data-dependent loop (the scalar unit loads blk0 in a few
+  // wide independent loads instead of one dependent load per leaf)
   int l = 0;
-  while (l + 1 < a.L && a.blk0[l + 1] <= b) ++l;  // uniform: kernarg scalar loads
+#pragma unroll
+  for (int i = 1; i < FJTREE_MAX_LEAVES; ++i) l += a.blk0[i] <= b;
   const int64_t n = a.n[l];
   const int64_t e0 = (int64_t)(b - a.blk0[l]) * kChunk;
   const int64_t e1 = e0 + kChunk < n ? e0 + kChunk : n;
@@ -153,14 +157,19 @@ __global__ __launch_bounds__(kThreads) void k_leaves(const Args a) {
       float p = wsum[0];
 #pragma unroll
       for (int w = 1; w < kThreads / 64; ++w) p = __fadd_rn(p, wsum[w]);
+      // Publish the partial, then count it. An agent-scope store is written through this
+      // XCD's L2, and waiting for it to be acknowledged orders it before the count, so no
+      // release fence is needed: on gfx950 that fence writes back the whole L2 (the
+      // outputs this kernel just wrote included), which tripled the launch time.
       __hip_atomic_store(a.partials + b, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence();  // release: the partial before the count
-      const unsigned old = atomicAdd(a.counter, 1u);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_s_waitcnt(0);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      const unsigned old = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last = old == (unsigned)(a.nblk - 1);
     }
     __syncthreads();
-    if (last && j < 64) {
-      __threadfence();  // acquire: every workgroup's partial is visible
+    if (last && j < 64) {  // agent-scope loads read the partials past the (per-XCD) L2
       float t = 0.f;
       for (int q = j; q < a.nblk; q += 64)
         t = __fadd_rn(t, __hip_atomic_load(a.partials + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -181,7 +190,9 @@ int64_t blocks_of(const fjtree_leaves* t, int32_t* blk0) {
     if (blk0) blk0[l] = (int32_t)nb;
     nb += (t->n[l] + kChunk - 1) / kChunk;
   }
-  if (blk0) blk0[t->L] = (int32_t)nb;
+  // entries past the last leaf never count (see k_leaves); blk0[L] == nb is not read
+  if (blk0)
+    for (int l = t->L; l <= FJTREE_MAX_LEAVES; ++l) blk0[l] = INT32_MAX;
   return nb;
 }
 

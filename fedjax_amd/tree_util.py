@@ -37,7 +37,7 @@ from fedjax_amd.typing import PyTree
 __all__ = [
     "tree_weight", "tree_inverse_weight", "tree_zeros_like", "tree_add", "tree_sum",
     "tree_mean", "tree_size", "tree_l2_squared", "tree_l2_norm", "tree_clip_by_global_norm",
-    "tree_l2_norms", "tree_mean_with_l2_norms", "WeightedTree",
+    "tree_l2_norms", "tree_mean_with_l2_norms", "WeightedTree", "PendingSum", "set_deferred_sums",
 ]
 
 # Non-temporal loads pay off once the deltas cannot stay in the 256 MiB Infinity
@@ -541,6 +541,138 @@ class WeightedTree:
 pytree.register_lazy_type(WeightedTree, WeightedTree.materialize)
 _F32_EXACT_INT = 1 << 53
 
+# Deferred running sums (PendingSum): on by default; see set_deferred_sums.
+_DEFER = {"enabled": True, "budget_bytes": 4 << 30, "max_clients": 4096}
+
+
+def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = None,
+                      max_clients: Optional[int] = None) -> None:
+    """Configure how ``tree_add(s, tree_weight(x, n))`` runs.
+
+    Enabled (default): the sum is deferred (:class:`PendingSum`) and folded by ONE
+    pytree-kernel launch when it is used, at most ``budget_bytes`` of pending deltas or
+    ``max_clients`` clients per launch (an older part of the chain is folded first when a
+    limit would be passed, so memory stays bounded). Disabled: every call is one fused
+    launch (fjtree_fold_leaves), which also suits loops that update delta tensors in place
+    between clients. Both give the reference's bits."""
+    _DEFER["enabled"] = bool(enabled)
+    if budget_bytes is not None:
+        _DEFER["budget_bytes"] = int(budget_bytes)
+    if max_clients is not None:
+        _DEFER["max_clients"] = max(1, int(max_clients))
+
+
+class PendingSum:
+    """``s = tree_add(s, tree_weight(x, n))`` repeated over clients, not yet computed.
+
+    FedJAX's algorithms build the round's running sum this way, one client at a time
+    (fedjax/algorithms/fed_avg.py:132-146). Each ``tree_add`` here appends the client's
+    delta (its leaves, captured at ``tree_weight``) and weight to a chain in O(1) host
+    work; the chain is folded when the sum is used — by ``tree_inverse_weight`` (which
+    also applies the ``1/W`` scale in the same launch), by indexing, iteration, attribute
+    access, ``materialize()`` or any pytree walk of this package. The fold is the pytree
+    kernel over [base, x_1 .. x_k] with weights [1, n_1 .. n_k]: per element
+    ``fl(...fl(fl(base*1) + fl(x_1 n_1)) ... + fl(x_k n_k))``, the reference's sequence of
+    ``jnp.add`` calls, bit for bit.
+
+    The deltas stay referenced until the fold (bounded by :func:`set_deferred_sums`). A
+    delta modified in place after it was added makes the fold raise RuntimeError (the
+    reference's arrays are immutable); loops that reuse delta buffers should call
+    ``set_deferred_sums(False)``. ``isinstance(s, dict)`` is False: call
+    ``materialize()`` where the concrete container type matters.
+    """
+
+    __slots__ = ("_root", "_parent", "_cap", "_weight", "_n", "_bytes", "_value")
+
+    def __init__(self, root, parent, cap, weight):
+        self._root, self._parent, self._cap, self._weight, self._value = root, parent, cap, weight, None
+        self._n = 1 + (parent._n if parent is not None and parent._value is None else 0)
+        self._bytes = cap[2] + (parent._bytes if parent is not None and parent._value is None else 0)
+
+    def _base_tree(self):
+        p = self
+        while p._parent is not None and p._value is None:
+            p = p._parent
+        return p._value if p._value is not None else p._root
+
+    def _chain(self):
+        """(base tree, captures, weights) from the nearest folded ancestor or the root."""
+        caps, ws = [], []
+        p = self
+        while p is not None and p._value is None:
+            caps.append(p._cap)
+            ws.append(p._weight)
+            if p._parent is None:
+                base = p._root
+            p = p._parent
+        if p is not None:
+            base = p._value
+        caps.reverse()
+        ws.reverse()
+        return base, caps, ws
+
+    def materialize(self) -> PyTree:
+        if self._value is None:
+            base, caps, ws = self._chain()
+            self._value = _fold_chain(base, caps, ws, None)
+            self._root = self._parent = self._cap = None  # the deltas can go
+        return self._value
+
+    __getitem__ = WeightedTree.__getitem__
+    __iter__ = WeightedTree.__iter__
+    __len__ = WeightedTree.__len__
+    __contains__ = WeightedTree.__contains__
+    __getattr__ = WeightedTree.__getattr__
+
+    def __repr__(self):
+        return f"PendingSum({self.materialize()!r})"
+
+
+pytree.register_lazy_type(PendingSum, PendingSum.materialize)
+
+
+def _fold_chain(base, caps, weights, scale):
+    """fl(...fl(fl(base*1) + fl(x_1 w_1)) ... + fl(x_k w_k)) [* f32(scale)]: one pytree-kernel
+    launch over the base tree's leaves and the captured leaves of every client."""
+    leaves0, td = pytree.flatten(base)
+    L = len(leaves0)
+    ptrs = np.empty((1 + len(caps), L), dtype=np.int64)
+    ptrs[0] = [x.data_ptr() for x in leaves0]
+    bad = _lib.host().table_from_caps(caps, ptrs[1:])
+    if bad >= 0:
+        raise RuntimeError(f"client {bad} of a pending tree_add sum was modified (a leaf updated in place) "
+                           "after it was added; the reference sums each delta's value at tree_add. Add "
+                           "copies, or call fedjax_amd.tree_util.set_deferred_sums(False)")
+    packed = _pack_weights([1] + list(weights))
+    outs = _fold(_Table(list(leaves0), ptrs), packed, scale=scale, validated=True)
+    return pytree.unflatten(td, outs)
+
+
+def _defer(sum_side, item, item_weight, item_cap):
+    """PendingSum for tree_add(sum_side, weighted item), or None when not applicable."""
+    if type(sum_side) is PendingSum:
+        if sum_side._value is not None:
+            ref, parent, root = sum_side._value, sum_side, None
+        else:
+            ref, parent, root = sum_side._base_tree(), sum_side, None
+    else:
+        ref, parent, root = sum_side, None, sum_side
+    host = _lib.host()
+    if item_cap is None:
+        item_cap = host.capture(item, -1)
+        if item_cap is None:
+            return None
+    elif not host.matches(item, item_cap[0], item_cap[1]):
+        raise RuntimeError("a pytree passed to tree_weight was modified (a leaf replaced or updated in "
+                           "place) before its weighted value was used; the reference computes "
+                           "tree_weight eagerly")
+    if not host.compatible(ref, item):
+        return None
+    if parent is not None and parent._value is None and (
+            parent._n + 1 > _DEFER["max_clients"] or parent._bytes + item_cap[2] > _DEFER["budget_bytes"]):
+        parent.materialize()  # bound the chain: fold what is pending, continue from it
+    return PendingSum(root, parent, item_cap, item_weight)
+
 
 def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
     """Weights tree leaves by weight (tree_util.py:29-32).
@@ -559,12 +691,17 @@ def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
 
 
 def _eager(t):
-    return t.materialize() if type(t) is WeightedTree else t
+    return t.materialize() if type(t) is WeightedTree or type(t) is PendingSum else t
 
 
 def tree_inverse_weight(pytree_: PyTree, weight: float) -> PyTree:
-    """Weights tree leaves by ``1 / weight`` (tree_util.py:35-38); computed now."""
+    """Weights tree leaves by ``1 / weight`` (tree_util.py:35-38); computed now. A
+    :class:`PendingSum` is folded with the ``1/W`` scale in the same launch
+    (``fl(s * f32(1/W))``, the reference's bits) — fed_avg.py:145-146 in one pass."""
     inv = _inverse(_host_weight(weight))
+    if type(pytree_) is PendingSum and pytree_._value is None:
+        base, caps, ws = pytree_._chain()
+        return _fold_chain(base, caps, ws, inv)
     pytree_ = _eager(pytree_)
     if type(inv) is float:
         got = _leaf_fold([pytree_], [inv], [None])
@@ -593,6 +730,22 @@ def tree_add(left: PyTree, right: PyTree) -> PyTree:
     is folded in the same launch (``fl(s + fl(x * f32(n)))``), which also sums the
     squares of its input for a following ``tree_l2_norm`` of that input."""
     tl, tr = type(left) is WeightedTree, type(right) is WeightedTree
+    pl, pr = type(left) is PendingSum, type(right) is PendingSum
+    if _DEFER["enabled"] and (tl != tr or pl != pr) and not (pl and pr):
+        # the running-sum pattern: defer (x + y == y + x exactly, so the sum may be either side)
+        if tr and right._tree is not None and not tl:
+            got = _defer(left, right._tree, right._weight, right._cap)
+        elif tl and left._tree is not None and not tr:
+            got = _defer(right, left._tree, left._weight, left._cap)
+        elif pl and not tr:
+            got = _defer(left, right, 1, None)
+        elif pr and not tl:
+            got = _defer(right, left, 1, None)
+        else:
+            got = None
+        if got is not None:
+            return got
+    left, right = (left.materialize() if pl else left), (right.materialize() if pr else right)
     if tl or tr:
         ops = [left._tree if tl else left, right._tree if tr else right]
         if ops[0] is None or ops[1] is None:  # already materialized

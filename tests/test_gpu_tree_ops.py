@@ -20,6 +20,17 @@ from fedjax_amd import pytree, tree_util as tu
 from oracle import tree_util_ref as ref
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["deferred", "eager"], autouse=True)
+def sum_mode(request):
+    """Every test runs with deferred running sums (PendingSum, the default) and with one
+    fused launch per tree_add (set_deferred_sums(False))."""
+    tu.set_deferred_sums(request.param == "deferred")
+    yield request.param
+    tu.set_deferred_sums(True)
+
+
 EMNIST = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "conv2_d_1": {"b": (64,), "w": (3, 3, 32, 64)},
           "linear": {"b": (128,), "w": (9216, 128)}, "linear_1": {"b": (62,), "w": (128, 62)}}
 
@@ -87,9 +98,11 @@ def test_literal_running_sum_bitwise_emnist(cuda):
         np.testing.assert_allclose(float(nrm), np.sqrt((x64 * x64).sum()), rtol=2e-6)
 
 
-def test_weighted_tree_is_deferred_and_fused(cuda, monkeypatch):
-    """tree_weight returns a WeightedTree; tree_add consumes it in ONE fjtree launch
-    (no materialization), and tree_l2_norm of the same delta reuses that launch."""
+def test_weighted_tree_is_deferred_and_fused(cuda, monkeypatch, sum_mode):
+    """tree_weight returns a WeightedTree that is never computed on its own. Eager mode:
+    tree_add consumes it in ONE fjtree launch and tree_l2_norm of the same delta reuses
+    that launch. Deferred mode: tree_add launches nothing (a PendingSum), the norm is one
+    norm-only launch, and the sum is folded when read."""
     g = torch.Generator().manual_seed(5)
     d = to_dev(rand_tree({"a": (1000,), "b": (7, 3)}, g), cuda)
     s = to_dev(rand_tree({"a": (1000,), "b": (7, 3)}, g), cuda)
@@ -99,8 +112,10 @@ def test_weighted_tree_is_deferred_and_fused(cuda, monkeypatch):
     real = tu._leaf_fold
     monkeypatch.setattr(tu, "_leaf_fold", lambda *a, **k: calls.append(a) or real(*a, **k))
     out = tu.tree_add(s, wt)
+    assert type(out) is (tu.PendingSum if sum_mode == "deferred" else dict)
+    assert len(calls) == (0 if sum_mode == "deferred" else 1)
     nrm = tu.tree_l2_norm(d)
-    assert len(calls) == 1 and wt._value is None  # fused: one launch, never materialized
+    assert len(calls) == 1 and wt._value is None  # one launch either way, never materialized
     want = {k: to_np(s)[k] + to_np(d)[k] * np.float32(7) for k in ("a", "b")}
     for k in ("a", "b"):
         assert np.array_equal(bits(out[k].cpu().numpy()), bits(want[k]))
@@ -180,7 +195,7 @@ def test_fast_path_edges(cuda):
 
 
 @pytest.mark.parametrize("K", [128])
-def test_literal_loop_configs1_bitwise_and_host_cost(K, cuda):
+def test_literal_loop_configs1_bitwise_and_host_cost(K, cuda, sum_mode):
     """configs[1] shape (EMNIST-CNN, 1,206,590 params): the literal loop over K=128 clients
     is bitwise RunningMean / tree_mean and costs one launch per client (timed in
     tools/time_literal_loop.py)."""
@@ -197,3 +212,51 @@ def test_literal_loop_configs1_bitwise_and_host_cost(K, cuda):
         assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     nn = tu.tree_l2_norms(deltas)
     np.testing.assert_allclose(torch.stack(norms).cpu().numpy(), nn.cpu().numpy(), rtol=2e-6)
+
+
+def test_pending_sum_chain_semantics(cuda, sum_mode):
+    """PendingSum keeps every intermediate sum valid (s1 stays s0 + x1 after s2 is built),
+    folds in bounded chunks under the budget, applies tree_inverse_weight's scale in the
+    same launch, and refuses a delta modified after it was added."""
+    if sum_mode != "deferred":
+        pytest.skip("deferred mode only")
+    g = torch.Generator().manual_seed(11)
+    shapes = {"a": (1001,), "b": {"c": (6, 7)}}
+    xs = [to_dev(rand_tree(shapes, g), cuda) for _ in range(9)]
+    z = tu.tree_zeros_like(xs[0])
+    s1 = tu.tree_add(z, tu.tree_weight(xs[0], 3))
+    s2 = tu.tree_add(s1, tu.tree_weight(xs[1], 5))
+    s3 = tu.tree_add(tu.tree_weight(xs[2], 0.5), s2)  # the sum on the right
+    assert all(type(v) is tu.PendingSum for v in (s1, s2, s3))
+    npz = [to_np(x) for x in xs]
+
+    def want(ks, ws, inv=None):
+        acc = tmap(lambda s: np.zeros(s, np.float32), shapes)
+        for k, w in zip(ks, ws):
+            acc = ref.tree_add(acc, ref.tree_weight(npz[k], w))
+        return acc if inv is None else ref.tree_inverse_weight(acc, inv)
+
+    def same(got, w):
+        return all(np.array_equal(bits(a), bits(b.reshape(-1)))
+                   for a, b in zip(leaves_np(got), pytree.leaves_of(w)))
+    assert same(s3, want([0, 1, 2], [3, 5, 0.5]))
+    assert same(s1, want([0], [3]))  # an older link, folded after a newer one
+    assert same(tu.tree_inverse_weight(s2, 8.0), want([0, 1], [3, 5], 8.0))
+    # a plain tree added to a pending sum (weight 1), then more clients after a fold
+    s4 = tu.tree_add(s3, xs[3])
+    s5 = tu.tree_add(s4, tu.tree_weight(xs[4], 2))
+    assert same(s5, want([0, 1, 2, 3, 4], [3, 5, 0.5, 1, 2]))
+    # budget: at most 3 pending clients per fold, same bits
+    tu.set_deferred_sums(True, max_clients=3)
+    try:
+        s = z
+        for k in range(9):
+            s = tu.tree_add(s, tu.tree_weight(xs[k], k + 1))
+        assert same(s, want(range(9), [k + 1 for k in range(9)]))
+    finally:
+        tu.set_deferred_sums(True, max_clients=4096)
+    # a delta updated in place after it joined the chain: the fold refuses
+    s = tu.tree_add(z, tu.tree_weight(xs[5], 2))
+    xs[5]["a"].add_(1.0)
+    with pytest.raises(RuntimeError, match="modified"):
+        s.materialize()
