@@ -644,6 +644,70 @@ PyObject* compatible(PyObject*, PyObject* args) {
   }
 }
 
+// append_check(ref, item, cap) -> cap | None | -100
+//     One walk for tree_add(sum, weighted item) in deferred mode: `item` must have ref's
+//     structure and float32 device leaves of ref's shapes on ref's device (else None: not the
+//     fast case). cap None: returns a new capture of item (leaves_tuple, version_sum,
+//     nbytes); cap given (from tree_weight): item must still hold exactly those leaves,
+//     unmodified (else -100), and cap is returned.
+PyObject* append_check(PyObject*, PyObject* args) {
+  PyObject *ref, *item, *cap;
+  if (!PyArg_ParseTuple(args, "OOO", &ref, &item, &cap)) return nullptr;
+  try {
+    PWalk w;
+    w.K = 2;
+    PyObject* xs[2] = {ref, item};
+    int rc = pwalk(xs, w, 0);
+    if (rc < 0) return nullptr;
+    if (rc > 0 || w.leaves[0].empty()) Py_RETURN_NONE;
+    const at::Tensor& t0 = THPVariable_Unpack(w.leaves[0][0]);
+    if (!t0.is_cuda()) Py_RETURN_NONE;
+    int64_t vs0, vs;
+    if (!check_leaves(w, 0, t0.get_device(), &vs0) || !check_leaves(w, 1, t0.get_device(), &vs)) Py_RETURN_NONE;
+    const Py_ssize_t L = static_cast<Py_ssize_t>(w.leaves[1].size());
+    if (cap != Py_None) {
+      if (!PyTuple_Check(cap) || PyTuple_GET_SIZE(cap) < 2) Py_RETURN_NONE;
+      PyObject* tup = PyTuple_GET_ITEM(cap, 0);
+      bool same = PyTuple_GET_SIZE(tup) == L && PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1)) == vs;
+      for (Py_ssize_t l = 0; same && l < L; ++l) same = w.leaves[1][l] == PyTuple_GET_ITEM(tup, l);
+      if (!same) return PyLong_FromLong(kStale);
+      Py_INCREF(cap);
+      return cap;
+    }
+    PyObject* tup = PyTuple_New(L);
+    if (!tup) return nullptr;
+    int64_t nbytes = 0;
+    for (Py_ssize_t l = 0; l < L; ++l) {
+      Py_INCREF(w.leaves[1][l]);
+      PyTuple_SET_ITEM(tup, l, w.leaves[1][l]);
+      nbytes += 4 * THPVariable_Unpack(w.leaves[1][l]).numel();
+    }
+    return Py_BuildValue("(NLL)", tup, static_cast<long long>(vs), static_cast<long long>(nbytes));
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
+// norm_view(buf, row, index, type) -> 0-d tensor of `type` (a torch.Tensor subclass) viewing
+// buf[row, index]: the lazy l2-norm values of deferred sums (tree_util._NormView).
+PyObject* norm_view(PyObject*, PyObject* args) {
+  PyObject *buf, *type;
+  long long row, index;
+  if (!PyArg_ParseTuple(args, "OLLO", &buf, &row, &index, &type)) return nullptr;
+  if (!THPVariable_Check(buf) || !PyType_Check(type)) {
+    PyErr_SetString(PyExc_TypeError, "norm_view(tensor, row, index, type)");
+    return nullptr;
+  }
+  try {
+    const at::Tensor& b = THPVariable_Unpack(buf);
+    return THPVariable_Wrap(b.select(0, row).select(0, index), reinterpret_cast<PyTypeObject*>(type));
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 // table_from_caps(caps, ptrs) -> int
 //     caps: list of K captures (leaves_tuple, version_sum) of L leaves each; writes leaf l of
 //     capture k's device pointer to ptrs[k*L + l] (int64 buffer). Returns -1 when every
@@ -804,6 +868,8 @@ PyMethodDef kMethods[] = {
     {"capture", capture, METH_VARARGS, "leaves + version sum of a tree for a lazy tree_weight"},
     {"matches", matches, METH_VARARGS, "tree holds exactly the captured leaves, unmodified"},
     {"compatible", compatible, METH_VARARGS, "tree_add(a, b) is the fast case (structure, float32 leaves)"},
+    {"append_check", append_check, METH_VARARGS, "deferred tree_add: structure + capture check in one walk"},
+    {"norm_view", norm_view, METH_VARARGS, "0-d view of buf[row, index] as a tensor subclass"},
     {"table_from_caps", table_from_caps, METH_VARARGS, "pointer table of captured leaves, version check"},
     {"leaf_fold", leaf_fold, METH_VARARGS, "fjtree_fold_leaves over 1-2 operand trees (see fjhost.cpp)"},
     {"fold_table", fold_table, METH_VARARGS, "plan image + output leaves + fjagg_wsum_ptrs launch (see fjhost.cpp)"},

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import ctypes
 import numbers
+import weakref
 from typing import Any, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -542,7 +543,7 @@ pytree.register_lazy_type(WeightedTree, WeightedTree.materialize)
 _F32_EXACT_INT = 1 << 53
 
 # Deferred running sums (PendingSum): on by default; see set_deferred_sums.
-_DEFER = {"enabled": True, "budget_bytes": 4 << 30, "max_clients": 4096}
+_DEFER = {"enabled": True, "budget_bytes": 4 << 30, "max_clients": 4095}
 
 
 def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = None,
@@ -551,15 +552,70 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
 
     Enabled (default): the sum is deferred (:class:`PendingSum`) and folded by ONE
     pytree-kernel launch when it is used, at most ``budget_bytes`` of pending deltas or
-    ``max_clients`` clients per launch (an older part of the chain is folded first when a
-    limit would be passed, so memory stays bounded). Disabled: every call is one fused
-    launch (fjtree_fold_leaves), which also suits loops that update delta tensors in place
-    between clients. Both give the reference's bits."""
+    ``max_clients`` (<= 4095) clients per launch (an older part of the chain is folded
+    first when a limit would be passed, so memory stays bounded). Disabled: every call is
+    one fused launch (fjtree_fold_leaves), which also suits loops that update delta
+    tensors in place between clients. Both give the reference's bits."""
     _DEFER["enabled"] = bool(enabled)
     if budget_bytes is not None:
         _DEFER["budget_bytes"] = int(budget_bytes)
     if max_clients is not None:
-        _DEFER["max_clients"] = max(1, int(max_clients))
+        _DEFER["max_clients"] = min(4095, max(1, int(max_clients)))
+
+
+class _Chain:
+    """The linear run of PendingSum links one norm buffer serves: float32 [2, n] on the
+    device, row 0 = squared l2 norms, row 1 = l2 norms of the clients, by link index."""
+
+    __slots__ = ("tip", "buf")
+
+    def __init__(self):
+        self.tip, self.buf = None, None
+
+
+class _Ticket:
+    """What a lazy norm view needs to get its value: the link whose fold writes it
+    (dropped once written, so views never keep client deltas alive)."""
+
+    __slots__ = ("node",)
+
+    def __init__(self, node):
+        self.node = node
+
+
+class _NormView(torch.Tensor):
+    """0-d float32 l2 norm (or its square) of a client delta added to a deferred sum: a
+    view into the chain's norm buffer, written by the chain's fold. Every torch function
+    or method that touches it (``float(v)``, ``v.item()``, ``print(v)``, ``torch.stack``,
+    arithmetic) first runs that fold if it has not run, then computes on plain tensors —
+    so no read can see the buffer before the value is there."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        _flush_views(args)
+        if kwargs:
+            _flush_views(kwargs)
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **(kwargs or {}))
+
+    def __format__(self, spec):
+        _flush_views(self)
+        with torch._C.DisableTorchFunctionSubclass():
+            return self.item().__format__(spec) if self.dim() == 0 else torch.Tensor.__format__(self, spec)
+
+
+def _flush_views(x) -> None:
+    t = type(x)
+    if t is _NormView:
+        ticket = x.__dict__.get("_ticket")
+        if ticket is not None and ticket.node is not None:
+            ticket.node._chain.tip.materialize()  # folds every pending link of the chain
+    elif t is list or t is tuple:
+        for y in x:
+            _flush_views(y)
+    elif t is dict:
+        for y in x.values():
+            _flush_views(y)
 
 
 class PendingSum:
@@ -573,7 +629,9 @@ class PendingSum:
     access, ``materialize()`` or any pytree walk of this package. The fold is the pytree
     kernel over [base, x_1 .. x_k] with weights [1, n_1 .. n_k]: per element
     ``fl(...fl(fl(base*1) + fl(x_1 n_1)) ... + fl(x_k n_k))``, the reference's sequence of
-    ``jnp.add`` calls, bit for bit.
+    ``jnp.add`` calls, bit for bit. ``tree_l2_norm(x)`` of the delta just added returns a
+    lazy view whose value the same fold computes (fjagg_wsum_l2_ptrs): the per-client
+    ``delta_l2_norm`` of fed_avg.py:142-144 without another pass over the delta.
 
     The deltas stay referenced until the fold (bounded by :func:`set_deferred_sums`). A
     delta modified in place after it was added makes the fold raise RuntimeError (the
@@ -582,12 +640,20 @@ class PendingSum:
     ``materialize()`` where the concrete container type matters.
     """
 
-    __slots__ = ("_root", "_parent", "_cap", "_weight", "_n", "_bytes", "_value")
+    __slots__ = ("_root", "_parent", "_cap", "_weight", "_n", "_bytes", "_value", "_chain", "_idx", "_ticket",
+                 "__weakref__")
 
     def __init__(self, root, parent, cap, weight):
         self._root, self._parent, self._cap, self._weight, self._value = root, parent, cap, weight, None
-        self._n = 1 + (parent._n if parent is not None and parent._value is None else 0)
-        self._bytes = cap[2] + (parent._bytes if parent is not None and parent._value is None else 0)
+        self._ticket = None
+        live = parent is not None and parent._value is None
+        self._n = 1 + (parent._n if live else 0)
+        self._bytes = cap[2] + (parent._bytes if live else 0)
+        if live and parent._chain.tip is parent:
+            self._chain, self._idx = parent._chain, parent._idx + 1
+        else:
+            self._chain, self._idx = _Chain(), 0
+        self._chain.tip = self
 
     def _base_tree(self):
         p = self
@@ -595,26 +661,24 @@ class PendingSum:
             p = p._parent
         return p._value if p._value is not None else p._root
 
-    def _chain(self):
-        """(base tree, captures, weights) from the nearest folded ancestor or the root."""
-        caps, ws = [], []
+    def _links(self):
+        """(base tree, the unfolded links from the nearest folded ancestor, in order)."""
+        links = []
         p = self
         while p is not None and p._value is None:
-            caps.append(p._cap)
-            ws.append(p._weight)
+            links.append(p)
             if p._parent is None:
                 base = p._root
             p = p._parent
         if p is not None:
             base = p._value
-        caps.reverse()
-        ws.reverse()
-        return base, caps, ws
+        links.reverse()
+        return base, links
 
     def materialize(self) -> PyTree:
         if self._value is None:
-            base, caps, ws = self._chain()
-            self._value = _fold_chain(base, caps, ws, None)
+            base, links = self._links()
+            self._value = _fold_chain(base, links, None)
             self._root = self._parent = self._cap = None  # the deltas can go
         return self._value
 
@@ -629,13 +693,16 @@ class PendingSum:
 
 
 pytree.register_lazy_type(PendingSum, PendingSum.materialize)
+_LAST = None  # weakref to the most recent PendingSum link (tree_l2_norm of its delta is lazy)
 
 
-def _fold_chain(base, caps, weights, scale):
+def _fold_chain(base, links, scale):
     """fl(...fl(fl(base*1) + fl(x_1 w_1)) ... + fl(x_k w_k)) [* f32(scale)]: one pytree-kernel
-    launch over the base tree's leaves and the captured leaves of every client."""
+    launch over the base tree's leaves and the captured leaves of every link; with the
+    per-client squared norms from the same pass when a lazy norm view waits on a link."""
     leaves0, td = pytree.flatten(base)
     L = len(leaves0)
+    caps = [n._cap for n in links]
     ptrs = np.empty((1 + len(caps), L), dtype=np.int64)
     ptrs[0] = [x.data_ptr() for x in leaves0]
     bad = _lib.host().table_from_caps(caps, ptrs[1:])
@@ -643,35 +710,70 @@ def _fold_chain(base, caps, weights, scale):
         raise RuntimeError(f"client {bad} of a pending tree_add sum was modified (a leaf updated in place) "
                            "after it was added; the reference sums each delta's value at tree_add. Add "
                            "copies, or call fedjax_amd.tree_util.set_deferred_sums(False)")
-    packed = _pack_weights([1] + list(weights))
-    outs = _fold(_Table(list(leaves0), ptrs), packed, scale=scale, validated=True)
+    packed = _pack_weights([1] + [n._weight for n in links])
+    waiting = [n for n in links if n._ticket is not None and n._ticket.node is not None]
+    l2sq = None
+    if waiting:
+        l2sq = torch.empty(1 + len(links), dtype=torch.float32, device=leaves0[0].device)
+    outs = _fold(_Table(list(leaves0), ptrs), packed, scale=scale, validated=True, l2sq=l2sq)
+    if waiting:
+        # per chain, the links form one run of consecutive indices: two small launches each
+        j = 0
+        while j < len(links):
+            ch, j0 = links[j]._chain, j
+            while j < len(links) and links[j]._chain is ch and links[j]._idx == links[j0]._idx + (j - j0):
+                j += 1
+            if ch.buf is not None:
+                i0, i1 = links[j0]._idx, links[j0]._idx + (j - j0)
+                ch.buf[0, i0:i1].copy_(l2sq[1 + j0:1 + j])
+                torch.sqrt(l2sq[1 + j0:1 + j], out=ch.buf[1, i0:i1])
+        for n in waiting:
+            n._ticket.node = None
+            n._ticket = None
     return pytree.unflatten(td, outs)
+
+
+def _lazy_norm(pytree_, row: int):
+    """A _NormView of the delta just added to a deferred sum, or None."""
+    node = _LAST() if _LAST is not None else None
+    if node is None or node._value is not None or node._cap is None:
+        return None
+    host = _lib.host()
+    if not host.matches(pytree_, node._cap[0], node._cap[1]):
+        return None
+    ch = node._chain
+    if ch.buf is None:
+        ch.buf = torch.empty((2, _DEFER["max_clients"] + 1), dtype=torch.float32, device=node._cap[0][0].device)
+    if node._idx >= ch.buf.shape[1]:
+        return None
+    if node._ticket is None:
+        node._ticket = _Ticket(node)
+    v = host.norm_view(ch.buf, row, node._idx, _NormView)
+    v._ticket = node._ticket
+    return v
 
 
 def _defer(sum_side, item, item_weight, item_cap):
     """PendingSum for tree_add(sum_side, weighted item), or None when not applicable."""
+    global _LAST
     if type(sum_side) is PendingSum:
-        if sum_side._value is not None:
-            ref, parent, root = sum_side._value, sum_side, None
-        else:
-            ref, parent, root = sum_side._base_tree(), sum_side, None
+        parent, root = sum_side, None
+        ref = sum_side._value if sum_side._value is not None else sum_side._base_tree()
     else:
         ref, parent, root = sum_side, None, sum_side
-    host = _lib.host()
-    if item_cap is None:
-        item_cap = host.capture(item, -1)
-        if item_cap is None:
-            return None
-    elif not host.matches(item, item_cap[0], item_cap[1]):
+    cap = _lib.host().append_check(ref, item, item_cap)
+    if cap is None:
+        return None
+    if type(cap) is int:
         raise RuntimeError("a pytree passed to tree_weight was modified (a leaf replaced or updated in "
                            "place) before its weighted value was used; the reference computes "
                            "tree_weight eagerly")
-    if not host.compatible(ref, item):
-        return None
     if parent is not None and parent._value is None and (
-            parent._n + 1 > _DEFER["max_clients"] or parent._bytes + item_cap[2] > _DEFER["budget_bytes"]):
+            parent._n + 1 > _DEFER["max_clients"] or parent._bytes + cap[2] > _DEFER["budget_bytes"]):
         parent.materialize()  # bound the chain: fold what is pending, continue from it
-    return PendingSum(root, parent, item_cap, item_weight)
+    node = PendingSum(root, parent, cap, item_weight)
+    _LAST = weakref.ref(node)
+    return node
 
 
 def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
@@ -700,8 +802,8 @@ def tree_inverse_weight(pytree_: PyTree, weight: float) -> PyTree:
     (``fl(s * f32(1/W))``, the reference's bits) — fed_avg.py:145-146 in one pass."""
     inv = _inverse(_host_weight(weight))
     if type(pytree_) is PendingSum and pytree_._value is None:
-        base, caps, ws = pytree_._chain()
-        return _fold_chain(base, caps, ws, inv)
+        base, links = pytree_._links()
+        return _fold_chain(base, links, inv)
     pytree_ = _eager(pytree_)
     if type(inv) is float:
         got = _leaf_fold([pytree_], [inv], [None])
@@ -859,6 +961,10 @@ def _l2_fast(pytree_, which: int):
     fjtree launch (same reduction order, so the same bits). None: not the fast case."""
     if _TREE_ADDRS is None:
         _tree_addrs()
+    if _DEFER["enabled"]:
+        v = _lazy_norm(pytree_, which)
+        if v is not None:
+            return v
     host = _lib.host()
     for cap, sq, l2 in _NORMS:
         if host.matches(pytree_, cap[0], cap[1]):

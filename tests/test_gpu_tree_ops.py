@@ -72,7 +72,7 @@ def literal_loop(tu_mod, params, deltas, weights, with_norm=True):
     return tu_mod.tree_inverse_weight(s, n_sum), norms
 
 
-def test_literal_running_sum_bitwise_emnist(cuda):
+def test_literal_running_sum_bitwise_emnist(cuda, sum_mode):
     g = torch.Generator().manual_seed(3)
     K = 24
     deltas_h = [rand_tree(EMNIST, g) for _ in range(K)]
@@ -90,10 +90,15 @@ def test_literal_running_sum_bitwise_emnist(cuda):
     want = ref.tree_inverse_weight(s, n_sum)
     for got, w in zip(leaves_np(mean), [x.reshape(-1) for x in pytree.leaves_of(want)]):
         assert np.array_equal(bits(got), bits(w))
-    # the cached fused norms are the standalone norms' bits, and within f32 rounding of f64
+    # eager mode: the fused norms are the standalone fjtree norms' bits; deferred mode: the
+    # fold's fused per-client norms (another fixed order). Both within f32 rounding of f64.
     for d, nrm in zip(deltas, norms):
         alone = tu._leaf_fold([d], [1], [None], norm_operand=0, no_out=True)[2]
-        assert torch.equal(nrm.view(torch.int32), alone.view(torch.int32))
+        if sum_mode == "eager":
+            assert torch.equal(nrm.view(torch.int32), alone.view(torch.int32))
+        else:
+            assert type(nrm) is tu._NormView
+            np.testing.assert_allclose(float(nrm), float(alone), rtol=2e-6)
         x64 = np.concatenate([x.astype(np.float64) for x in leaves_np(d)])
         np.testing.assert_allclose(float(nrm), np.sqrt((x64 * x64).sum()), rtol=2e-6)
 
@@ -115,7 +120,8 @@ def test_weighted_tree_is_deferred_and_fused(cuda, monkeypatch, sum_mode):
     assert type(out) is (tu.PendingSum if sum_mode == "deferred" else dict)
     assert len(calls) == (0 if sum_mode == "deferred" else 1)
     nrm = tu.tree_l2_norm(d)
-    assert len(calls) == 1 and wt._value is None  # one launch either way, never materialized
+    # eager: one fused launch gave the sum and the norm; deferred: nothing launched yet
+    assert len(calls) == (0 if sum_mode == "deferred" else 1) and wt._value is None
     want = {k: to_np(s)[k] + to_np(d)[k] * np.float32(7) for k in ("a", "b")}
     for k in ("a", "b"):
         assert np.array_equal(bits(out[k].cpu().numpy()), bits(want[k]))
@@ -260,3 +266,57 @@ def test_pending_sum_chain_semantics(cuda, sum_mode):
     xs[5]["a"].add_(1.0)
     with pytest.raises(RuntimeError, match="modified"):
         s.materialize()
+
+
+def test_lazy_norms_of_a_deferred_sum(cuda, sum_mode):
+    """tree_l2_norm of the delta just added to a deferred sum is a _NormView that the sum's
+    fold fills: reading it first runs the fold (any torch function or method), reading it
+    after tree_inverse_weight needs nothing more, and once filled the view no longer keeps
+    the chain (or its deltas) alive."""
+    if sum_mode != "deferred":
+        pytest.skip("deferred mode only")
+    import gc
+    import weakref
+    g = torch.Generator().manual_seed(12)
+    shapes = {"a": (5000,), "b": {"c": (33, 3)}}
+    xs = [to_dev(rand_tree(shapes, g), cuda) for _ in range(6)]
+
+    def f64norm(t):
+        x = np.concatenate([v.astype(np.float64) for v in leaves_np(t)])
+        return np.sqrt((x * x).sum())
+    # read before the sum is used: the read runs the fold
+    s = tu.tree_zeros_like(xs[0])
+    views = []
+    for k, x in enumerate(xs):
+        s = tu.tree_add(s, tu.tree_weight(x, k + 1))
+        views.append((tu.tree_l2_norm(x), tu.tree_l2_squared(x)))
+    assert all(type(v) is tu._NormView for pair in views for v in pair)
+    assert s._value is None
+    got = torch.stack([v for v, _ in views]).cpu().numpy()  # one flush covers the chain
+    assert s._value is not None
+    np.testing.assert_allclose(got, [f64norm(x) for x in xs], rtol=2e-6)
+    np.testing.assert_allclose([float(q) for _, q in views], [f64norm(x) ** 2 for x in xs], rtol=4e-6)
+    assert f"{views[0][0]:.4f}" == f"{float(views[0][0]):.4f}"
+    # read after tree_inverse_weight: the fold that produced the mean filled them
+    s = tu.tree_zeros_like(xs[0])
+    norms = {}
+    for k, x in enumerate(xs):
+        s = tu.tree_add(s, tu.tree_weight(x, 2))
+        norms[k] = {"delta_l2_norm": tu.tree_l2_norm(x)}
+    link = weakref.ref(s)
+    mean = tu.tree_inverse_weight(s, 12.0)
+    del s
+    gc.collect()
+    assert link() is None  # the filled views hold no link (nor the deltas it captured)
+    np.testing.assert_allclose([float(norms[k]["delta_l2_norm"]) for k in range(6)],
+                               [f64norm(x) for x in xs], rtol=2e-6)
+    want = tmap(lambda s: np.zeros(s, np.float32), shapes)
+    for x in xs:
+        want = ref.tree_add(want, ref.tree_weight(to_np(x), 2))
+    want = ref.tree_inverse_weight(want, 12.0)
+    for a, b in zip(leaves_np(mean), pytree.leaves_of(want)):
+        assert np.array_equal(bits(a), bits(b.reshape(-1)))
+    # a norm of a delta that is not the last one added is computed at once (not lazy)
+    s = tu.tree_add(tu.tree_zeros_like(xs[0]), tu.tree_weight(xs[0], 1))
+    s = tu.tree_add(s, tu.tree_weight(xs[1], 1))
+    assert type(tu.tree_l2_norm(xs[0])) is not tu._NormView
