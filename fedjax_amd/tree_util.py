@@ -641,10 +641,11 @@ class PendingSum:
     """
 
     __slots__ = ("_root", "_parent", "_cap", "_weight", "_n", "_bytes", "_value", "_chain", "_idx", "_ticket",
-                 "__weakref__")
+                 "_ref", "__weakref__")
 
-    def __init__(self, root, parent, cap, weight):
+    def __init__(self, root, parent, cap, weight, ref):
         self._root, self._parent, self._cap, self._weight, self._value = root, parent, cap, weight, None
+        self._ref = ref  # a tree with the sum's structure (the chain's base): O(1) structure checks
         self._ticket = None
         live = parent is not None and parent._value is None
         self._n = 1 + (parent._n if live else 0)
@@ -654,12 +655,6 @@ class PendingSum:
         else:
             self._chain, self._idx = _Chain(), 0
         self._chain.tip = self
-
-    def _base_tree(self):
-        p = self
-        while p._parent is not None and p._value is None:
-            p = p._parent
-        return p._value if p._value is not None else p._root
 
     def _links(self):
         """(base tree, the unfolded links from the nearest folded ancestor, in order)."""
@@ -679,7 +674,7 @@ class PendingSum:
         if self._value is None:
             base, links = self._links()
             self._value = _fold_chain(base, links, None)
-            self._root = self._parent = self._cap = None  # the deltas can go
+            self._root = self._parent = self._cap = self._ref = None  # the deltas can go
         return self._value
 
     __getitem__ = WeightedTree.__getitem__
@@ -758,7 +753,7 @@ def _defer(sum_side, item, item_weight, item_cap):
     global _LAST
     if type(sum_side) is PendingSum:
         parent, root = sum_side, None
-        ref = sum_side._value if sum_side._value is not None else sum_side._base_tree()
+        ref = sum_side._value if sum_side._value is not None else sum_side._ref
     else:
         ref, parent, root = sum_side, None, sum_side
     cap = _lib.host().append_check(ref, item, item_cap)
@@ -771,7 +766,7 @@ def _defer(sum_side, item, item_weight, item_cap):
     if parent is not None and parent._value is None and (
             parent._n + 1 > _DEFER["max_clients"] or parent._bytes + cap[2] > _DEFER["budget_bytes"]):
         parent.materialize()  # bound the chain: fold what is pending, continue from it
-    node = PendingSum(root, parent, cap, item_weight)
+    node = PendingSum(root, parent, cap, item_weight, ref)
     _LAST = weakref.ref(node)
     return node
 
@@ -832,6 +827,11 @@ def tree_add(left: PyTree, right: PyTree) -> PyTree:
     is folded in the same launch (``fl(s + fl(x * f32(n)))``), which also sums the
     squares of its input for a following ``tree_l2_norm`` of that input."""
     tl, tr = type(left) is WeightedTree, type(right) is WeightedTree
+    if tr and not tl and right._tree is not None and _DEFER["enabled"]:
+        # the running sum of fed_avg.py:137-138: s = tree_add(s, tree_weight(x, n))
+        got = _defer(left, right._tree, right._weight, right._cap)
+        if got is not None:
+            return got
     pl, pr = type(left) is PendingSum, type(right) is PendingSum
     if _DEFER["enabled"] and (tl != tr or pl != pr) and not (pl and pr):
         # the running-sum pattern: defer (x + y == y + x exactly, so the sum may be either side)
