@@ -108,6 +108,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint8_t* base, 
 
 // One unit of a client row via buffer_load with a 32-bit lane offset: no per-load
 // address VGPRs (aux 2 = nt).
+// Bytes a rebased row descriptor covers: what is left of the row, capped to the
+// descriptor's 31-bit record count (a workgroup never reaches that far).
+__device__ __forceinline__ uint32_t row_range(int64_t bytes) {
+  return (uint32_t)(bytes < 0x7fffffffll ? bytes : 0x7fffffffll);
+}
+
 template <int IN, int V, bool NT>
 __device__ __forceinline__ typename Unit<IN, V>::Raw load_unit(__amdgpu_buffer_rsrc_t r,
                                                                uint32_t off) {
@@ -648,9 +654,12 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   const int64_t u1 = blk[1];
   const int64_t n = leaf_n[leaf];
   const int64_t nunits = n / V;
-  uint8_t* ob = reinterpret_cast<uint8_t*>(out_ptrs[leaf]);
-  auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]); };
-  const uint32_t row_bytes = (uint32_t)(n * IB);
+  // Rebase every row at this workgroup's first element: lane offsets stay 32-bit for a
+  // leaf of any size (a workgroup's range is a few MB at most).
+  const int64_t e_base = tail ? nunits * V : ((V > 1 && elem) ? u0 : u0 * V);
+  uint8_t* ob = reinterpret_cast<uint8_t*>(out_ptrs[leaf]) + e_base * Elem<OUT>::B;
+  auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]) + e_base * IB; };
+  const uint32_t row_bytes = row_range((n - e_base) * IB);
   const bool dsc = do_scale != 0, acm = accumulate != 0;
   // L2: per-client squared norms of this block's units, (kThreads/64) x K floats in LDS
   extern __shared__ __attribute__((aligned(16))) float l2lds[];
@@ -664,15 +673,15 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   if (tail) {
     const bool active = tid < n - nunits * V;
     if (L2 || active) {  // with L2 every lane joins the per-client wave reductions
-      const int64_t e = nunits * V + (active ? tid : 0);
+      const int64_t e = active ? tid : 0;
       const uint32_t off[1] = {(uint32_t)(e * IB)};
       const bool valid[1] = {active};
       fold<IN, ACC, OUT, 1, 1, 8, NT>(row, row_bytes, K, off, ob, valid, w, dsc, scale, acm, nrm);
     }
   } else if (V > 1 && elem) {
-    walk_units<IN, ACC, OUT, 1, NT, BURST>(row, row_bytes, K, u0, u1, ob, w, dsc, scale, acm, nrm, PlainEpi());
+    walk_units<IN, ACC, OUT, 1, NT, BURST>(row, row_bytes, K, 0, u1 - u0, ob, w, dsc, scale, acm, nrm, PlainEpi());
   } else {
-    walk_units<IN, ACC, OUT, V, NT, BURST>(row, row_bytes, K, u0, u1, ob, w, dsc, scale, acm, nrm, PlainEpi());
+    walk_units<IN, ACC, OUT, V, NT, BURST>(row, row_bytes, K, 0, u1 - u0, ob, w, dsc, scale, acm, nrm, PlainEpi());
   }
   if constexpr (L2) {
     __syncthreads();
@@ -707,13 +716,15 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict
   const int64_t u1 = blk[1];
   const int64_t n = leaf_n[leaf];
   const int64_t nunits = n / V;
-  const OptEpi epi{opt, reinterpret_cast<float*>(out_ptrs[leaf]), reinterpret_cast<float*>(state[leaf]),
-                   reinterpret_cast<float*>(state[L + leaf]), reinterpret_cast<float*>(state[2 * L + leaf])};
-  auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]); };
-  const uint32_t row_bytes = (uint32_t)(n * IB);
+  // rebased at the workgroup's first element, as in k_ptrs (the epilogue's element index too)
+  const int64_t e_base = tail ? nunits * V : ((V > 1 && elem) ? u0 : u0 * V);
+  auto at = [=](int64_t p) { return p ? reinterpret_cast<float*>(p) + e_base : nullptr; };
+  const OptEpi epi{opt, at(out_ptrs[leaf]), at(state[leaf]), at(state[L + leaf]), at(state[2 * L + leaf])};
+  auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]) + e_base * IB; };
+  const uint32_t row_bytes = row_range((n - e_base) * IB);
   if (tail) {
     if (tid < n - nunits * V) {
-      const uint32_t off[1] = {(uint32_t)((nunits * V + tid) * IB)};
+      const uint32_t off[1] = {(uint32_t)(tid * IB)};
       const bool valid[1] = {true};
       fold<IN, AccF, FJAGG_F32, 1, 1, 8, NT>(row, row_bytes, K, off, nullptr, valid, w, true, scale, false,
                                              NoNorm(), epi);
@@ -721,11 +732,11 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict
     return;
   }
   if (V > 1 && elem)
-    walk_units<IN, AccF, FJAGG_F32, 1, NT, true>(row, row_bytes, K, u0, u1, nullptr, w, true, scale, false, NoNorm(),
-                                                 epi);
+    walk_units<IN, AccF, FJAGG_F32, 1, NT, true>(row, row_bytes, K, 0, u1 - u0, nullptr, w, true, scale, false,
+                                                 NoNorm(), epi);
   else
-    walk_units<IN, AccF, FJAGG_F32, V, NT, true>(row, row_bytes, K, u0, u1, nullptr, w, true, scale, false, NoNorm(),
-                                                 epi);
+    walk_units<IN, AccF, FJAGG_F32, V, NT, true>(row, row_bytes, K, 0, u1 - u0, nullptr, w, true, scale, false,
+                                                 NoNorm(), epi);
 }
 
 // Per-client sum of squares: grid (nb, K); ws[k*nb + b] = block partial (f32),
@@ -1294,7 +1305,8 @@ int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, c
   int64_t total = 0;
   for (int l = 0; l < L; ++l) {
     const int64_t n = leaf_n[l];
-    if (n < 0 || n * elem_bytes(in_dtype) > kMaxRowBytes)
+    // unit offsets are 40-bit in the block words; rows are rebased per workgroup
+    if (n < 0 || n >= (1ll << 40))
       return fail(FJAGG_EINVAL, "leaf %d: %lld elements unsupported", l, (long long)n);
     total += (leaf_elem && leaf_elem[l]) ? (n + V - 1) / V : n / V;  // balance by bytes
   }

@@ -892,13 +892,28 @@ def _collect_pairs(pairs):
     return trees, weights, sum_weight
 
 
+# tree_mean over a one-shot iterable holds at most this many bytes of client deltas
+# (float32 leaves) before folding them into the running sum (see tree_mean).
+STREAM_BUDGET_BYTES = 4 << 30
+
+
 def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
     """Returns (weighted) mean of input trees and weights (tree_util.py:76-96).
 
     All K clients are folded by ONE kernel launch per leaf-dtype group; the result
     is bitwise equal to the reference's sequential jit fold for float32 leaves.
     The iterable is consumed once (it may be a generator, compression.py:191).
+
+    A list or tuple is folded in one launch (its deltas are resident anyway). Any other
+    iterable of float32 pytrees is consumed in chunks of at most
+    :data:`STREAM_BUDGET_BYTES` of deltas, each folded into the running sum in
+    accumulate mode (the same per-element sequence, so the same bits), with the ``1/W``
+    scale fused into the last chunk's launch. Like the reference, which holds one client
+    at a time, a generator of host-resident or freshly produced deltas therefore never
+    needs all K deltas on the GPU at once; below the budget it is still one launch.
     """
+    if type(pytrees_and_weights) is not list and type(pytrees_and_weights) is not tuple:
+        return _tree_mean_stream(iter(pytrees_and_weights))
     trees, weights, sum_weight = _collect_pairs(pytrees_and_weights)
     if not trees:
         return None  # tree_util.py:96 maps over None
@@ -907,6 +922,60 @@ def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
         return pytree.unflatten(td, [])
     inv = _inverse(sum_weight)
     return pytree.unflatten(td, _fold(rows, weights, scale=inv, validated=True))
+
+
+def _f32_tree_bytes(tree) -> Optional[int]:
+    """4 x elements of a pytree whose leaves are all float32 (tensors or arrays), else None."""
+    n = 0
+    for x in pytree.leaves_of(tree):
+        dt = getattr(x, "dtype", None)
+        if dt is not torch.float32 and dt != np.float32:
+            return None
+        n += x.numel() if isinstance(x, torch.Tensor) else int(np.size(x))
+    return 4 * n
+
+
+def _tree_mean_stream(it) -> PyTree:
+    first = next(it, None)
+    if first is None:
+        return None
+    tree0, _ = first
+    per_client = _f32_tree_bytes(tree0)
+    if not per_client:  # other dtypes (whose fold type may depend on every weight): all at once
+        return tree_mean([first] + list(it))
+    B = max(1, STREAM_BUDGET_BYTES // per_client)
+    chunk, out, td, sum_weight = [first], None, None, 0.0
+    while True:
+        done = False
+        while len(chunk) < B:
+            nxt = next(it, None)
+            if nxt is None:
+                done = True
+                break
+            chunk.append(nxt)
+        trees = [t for t, _ in chunk]
+        weights = [w for _, w in chunk]
+        for i, w in enumerate(weights):
+            w = weights[i] = _host_weight(w)
+            sum_weight += w  # tree_util.py:95, in arrival order across chunks
+        ctd, rows = _client_table(trees)
+        if td is None:
+            td = ctd
+            if not rows[0]:
+                list(it)  # consume the rest, as the reference's loop does
+                return pytree.unflatten(td, [])
+        elif ctd != td:
+            raise ValueError(f"pytree structure mismatch: expected {td!r}, got {ctd!r}")
+        packed = _pack_weights(weights)
+        out = _fold(rows, packed if packed is not None else weights, out=out, accumulate=out is not None,
+                    scale=_inverse(sum_weight) if done else None, validated=True)
+        if done:
+            return pytree.unflatten(td, out)
+        chunk = []
+        nxt = next(it, None)
+        if nxt is None:  # the iterable ended exactly at a chunk boundary: scale what was folded
+            return tree_inverse_weight(pytree.unflatten(td, out), sum_weight)
+        chunk.append(nxt)
 
 
 def tree_mean_with_l2_norms(pytrees_and_weights: Iterable[Tuple[PyTree, float]]):

@@ -564,9 +564,30 @@ def test_empty_and_scalar_leaves(cuda):
     npt.assert_allclose(host(m["v"]), [want] * 3, rtol=1e-7)
 
 
-def test_oversize_leaf_is_rejected():
+def test_leaf_over_one_gib_through_the_pytree_kernel(cuda):
+    """a leaf of 300 M float32 (1.2 GB) per client folds through tree_mean (the
+    pytree kernel rebases every row at its workgroup's first element, so lane offsets stay
+    32-bit), bitwise vs the oracle at columns on both sides of the 1 GiB and 2 GiB marks;
+    with fused l2 norms too. A plan beyond 40-bit unit offsets is refused."""
+    K, P = 2, 300_000_000
+    x = torch.empty(K, P + 5, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(x[:, :P], seed=57)
+    trees = [{"big": x[k, :P].clone(), "small": x[k, P:P + 5].clone()} for k in range(K)]
+    del x
+    wi = [3, 5]
+    m = tu.tree_mean(zip(trees, wi))
+    cols = np.array([0, 1, 2, 3, 268435455, 268435456, 268435457, 536870911 // 2, P - 2, P - 1])
+    want = ref.wsum_dense(synth_cols(K, cols, 57), np.float32(wi), scale=ref.mean_scale(wi))
+    assert np.array_equal(bits(host(m["big"])[cols]), bits(want))
+    m2, norms = tu.tree_mean_with_l2_norms(zip(trees, wi))
+    assert torch.equal(m2["big"].view(torch.int32), m["big"].view(torch.int32))
+    for k in range(K):
+        npt.assert_allclose(float(norms[k]), float(torch.linalg.vector_norm(
+            torch.cat([trees[k]["big"], trees[k]["small"]]).double())), rtol=2e-6)
+    del trees, m, m2
+    torch.cuda.empty_cache()
     with pytest.raises(_lib.FjaggError):
-        kernels.ptrs_plan(_lib.F32, [300_000_000], False)
+        kernels.ptrs_plan(_lib.F32, [1 << 41], False)
 
 
 # ------------------------------------------------------- fused server optimizer step
@@ -849,3 +870,32 @@ def test_native_fold_table_fused_l2(cuda):
         assert torch.equal(q_fast.view(torch.int32), q_slow.view(torch.int32))
         m, n = tu.tree_mean_with_l2_norms(zip(trees, w))
         assert torch.equal(m["a"], fast[0]) and torch.equal(n, torch.sqrt(q_fast))
+
+
+def test_tree_mean_streams_one_shot_iterables(cuda, monkeypatch):
+    """a generator is consumed in chunks under STREAM_BUDGET_BYTES (accumulate
+    mode, scale fused into the last chunk) — bitwise the one-launch fold of the same list,
+    for host (numpy) and device deltas, chunk boundaries landing anywhere (incl. exactly
+    at the end), and only one chunk of host deltas is ever copied to the GPU."""
+    K = 23
+    g = np.random.RandomState(3)
+    host_trees = [{"a": g.uniform(-1, 1, 1001).astype(np.float32), "b": g.uniform(-1, 1, (3, 4)).astype(np.float32)}
+                  for _ in range(K)]
+    wi = [int(v) for v in ref.fedavg_weights(K, seed=5)]
+    wi[4] = 0.25
+    want = tu.tree_mean(list(zip([{k: torch.from_numpy(v).to(cuda) for k, v in t.items()} for t in host_trees], wi)))
+    per = 4 * (1001 + 12)
+    for B in (1, 5, 23, 24, 100):
+        monkeypatch.setattr(tu, "STREAM_BUDGET_BYTES", B * per)
+        for trees in (host_trees, [{k: torch.from_numpy(v).to(cuda) for k, v in t.items()} for t in host_trees]):
+            got = tu.tree_mean((t, w) for t, w in zip(trees, wi))
+            for k in ("a", "b"):
+                assert torch.equal(got[k].view(torch.int32), want[k].view(torch.int32)), (B, k)
+    # the aggregator's lazy map goes through the same path
+    monkeypatch.setattr(tu, "STREAM_BUDGET_BYTES", 4 * per)
+    agg = fedjax_amd.aggregators.mean_aggregator()
+    got, _ = agg.apply(((f"c{i}", t, w) for i, (t, w) in enumerate(zip(host_trees, wi))), agg.init())
+    assert torch.equal(got["a"].view(torch.int32), want["a"].view(torch.int32))
+    with pytest.raises(ValueError):
+        tu.tree_mean(iter([({"a": np.zeros(3, np.float32)}, 1)] * 5 + [({"b": np.zeros(3, np.float32)}, 1)]))
+    assert tu.tree_mean(iter([])) is None
