@@ -992,9 +992,35 @@ def tree_mean_with_l2_norms(pytrees_and_weights: Iterable[Tuple[PyTree, float]])
     td, rows = _client_table(trees)
     if not rows[0]:
         return pytree.unflatten(td, []), torch.zeros(len(trees), dtype=torch.float32, device=_default_device())
+    float_one = len({x.dtype for x in rows[0]}) == 1 and rows[0][0].dtype in (torch.float32, torch.bfloat16)
+    if len(trees) > _L2_MAX_CLIENTS or not float_one:
+        # the fused pass keeps K partial norms per workgroup in LDS (K <= 4096) and sums one
+        # float dtype: otherwise the mean and the norms take one pass each
+        outs = _fold(rows, weights, scale=_inverse(sum_weight), validated=True)
+        return pytree.unflatten(td, outs), tree_l2_norms(trees)
     l2sq = torch.empty(len(trees), dtype=torch.float32, device=rows[0][0].device)
     outs = _fold(rows, weights, scale=_inverse(sum_weight), validated=True, l2sq=l2sq)
     return pytree.unflatten(td, outs), torch.sqrt(l2sq)
+
+
+_L2_MAX_CLIENTS = 4096  # fjagg_wsum_l2_ptrs (kL2MaxClients in fjagg.hip)
+
+
+def _l2sq_mixed(row: List[torch.Tensor]) -> torch.Tensor:
+    """``sum(jnp.vdot(x, x) for x in leaves)`` (tree_util.py:105-108) for leaves of mixed or
+    integer dtypes: int32 leaves square and sum in wrapping int32 (exact in any order,
+    computed mod 2**32), float leaves in float32; the per-leaf values are added in leaf
+    order from Python's int 0 with jnp's promotion (int32 + float32 -> float32)."""
+    acc = None
+    for x in row:
+        if x.dtype == torch.int32:
+            v = (x.long() * x.long()).sum() & 0xFFFFFFFF
+            v = torch.where(v >= 2 ** 31, v - 2 ** 32, v).to(torch.int32)
+        else:
+            xf = x.float()
+            v = torch.dot(xf.reshape(-1), xf.reshape(-1))
+        acc = v if acc is None else acc + v
+    return acc if acc is not None else torch.zeros((), dtype=torch.int32)
 
 
 def tree_size(pytree_: PyTree) -> int:
@@ -1051,6 +1077,8 @@ def tree_l2_squared(pytree_: PyTree) -> torch.Tensor:
     _, rows = _client_rows([pytree_])
     if not rows[0]:
         return torch.zeros((), dtype=torch.float32, device=_default_device())
+    if len({x.dtype for x in rows[0]}) > 1 or rows[0][0].dtype == torch.int32:
+        return _l2sq_mixed(rows[0])
     return _l2_rows(rows, take_sqrt=False).reshape(())
 
 
@@ -1063,6 +1091,8 @@ def tree_l2_norm(pytree_: PyTree) -> torch.Tensor:
     _, rows = _client_rows([pytree_])
     if not rows[0]:
         return torch.zeros((), dtype=torch.float32, device=_default_device())
+    if len({x.dtype for x in rows[0]}) > 1 or rows[0][0].dtype == torch.int32:
+        return torch.sqrt(_l2sq_mixed(rows[0]).float())  # jnp.sqrt of an int32 sum is float32
     return _l2_rows(rows, take_sqrt=True).reshape(())
 
 
@@ -1071,6 +1101,8 @@ def tree_l2_norms(pytrees: Sequence[PyTree]) -> torch.Tensor:
     ``delta_l2_norm`` diagnostic of examples/fed_avg.py:79-81 batched."""
     trees = list(pytrees)
     _, rows = _client_rows(trees)
+    if len({x.dtype for x in rows[0]}) > 1 or rows[0][0].dtype == torch.int32:
+        return torch.stack([torch.sqrt(_l2sq_mixed(r).float()) for r in rows])
     return _l2_rows(rows, take_sqrt=True)
 
 

@@ -899,3 +899,23 @@ def test_tree_mean_streams_one_shot_iterables(cuda, monkeypatch):
     with pytest.raises(ValueError):
         tu.tree_mean(iter([({"a": np.zeros(3, np.float32)}, 1)] * 5 + [({"b": np.zeros(3, np.float32)}, 1)]))
     assert tu.tree_mean(iter([])) is None
+
+
+def test_l2_of_int_and_mixed_leaves_and_many_clients(cuda):
+    """tree_l2_squared / tree_l2_norm accept int32 and mixed-dtype pytrees like
+    the reference's sum(jnp.vdot(x, x)) (int32 squares wrap), and tree_mean_with_l2_norms
+    takes K > 4096 clients (two passes instead of the fused one)."""
+    t = {"i": torch.tensor([3, 4], dtype=torch.int32, device=cuda), "f": torch.tensor([1.5], device=cuda)}
+    sq = tu.tree_l2_squared(t)
+    assert sq.dtype == torch.float32 and float(sq) == 27.25
+    npt.assert_allclose(float(tu.tree_l2_norm(t)), np.sqrt(27.25), rtol=1e-7)
+    ti = {"i": torch.tensor([46341, 1], dtype=torch.int32, device=cuda)}  # 46341^2 > 2^31: wraps
+    want = np.int32(np.int64(46341) ** 2 + 1 - 2 ** 32)
+    got = tu.tree_l2_squared(ti)
+    assert got.dtype == torch.int32 and int(got) == int(want)
+    K = 4100
+    trees = [{"w": torch.full((3,), float(k % 7), device=cuda)} for k in range(K)]
+    m, norms = tu.tree_mean_with_l2_norms(zip(trees, [1] * K))
+    assert norms.shape == (K,)
+    npt.assert_allclose(host(norms)[:8], [np.sqrt(3) * (k % 7) for k in range(8)], rtol=1e-6)
+    assert torch.equal(m["w"], tu.tree_mean(list(zip(trees, [1] * K)))["w"])
