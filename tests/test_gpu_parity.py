@@ -709,10 +709,11 @@ def test_tree_mean_with_l2_norms_edges(cuda):
     m, n = tu.tree_mean_with_l2_norms([({"x": a}, 1), ({"x": 2 * a}, 3)])
     npt.assert_allclose(host(n), [np.sqrt(30.0), np.sqrt(120.0)], rtol=1e-6)
     npt.assert_array_equal(host(m["x"]), host(tu.tree_mean([({"x": a}, 1), ({"x": 2 * a}, 3)])["x"]))
-    with pytest.raises(TypeError):
-        tu.tree_mean_with_l2_norms([({"x": torch.ones(3, dtype=torch.int32, device=cuda)}, 1)])
-    with pytest.raises(TypeError):
-        tu.tree_mean_with_l2_norms([({"x": a, "y": a.bfloat16()}, 1)])
+    # int and mixed-dtype leaves: the mean and the norms in two passes
+    mi, ni = tu.tree_mean_with_l2_norms([({"x": torch.full((3,), 2, dtype=torch.int32, device=cuda)}, 1)])
+    assert mi["x"].dtype == torch.float32 and host(ni).tolist() == [np.float32(np.sqrt(12.0))]
+    mm, nm = tu.tree_mean_with_l2_norms([({"x": a, "y": a.bfloat16()}, 1)])
+    npt.assert_allclose(host(nm), [np.sqrt(60.0)], rtol=1e-6)
 
 
 @pytest.mark.parametrize("make", [lambda s: s.sgd(0.5), lambda s: s.sgd(0.1, momentum=0.9),
