@@ -28,6 +28,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <mutex>
 #include <type_traits>
@@ -597,6 +598,18 @@ __global__ __launch_bounds__(kThreads) void k_dense_opt(
 // kThreads*8 units (E=8, U=4: the dense default; lanes past the range are masked)
 // when the range gives a lane more than one unit, else in groups of kThreads units
 // (E=1, U=8).
+// XCD-aware order of the pytree plan's workgroups. MI355X hands workgroup p to XCD p % 8
+// (round robin); remapped, XCD x runs the consecutive plan entries [x*q + min(x, r),
+// +q + (x < r)) of the n = 8q + r, i.e. one contiguous eighth of every leaf instead of
+// strided slices of all of it. Each XCD has its own L2 and translation caches: with one
+// allocation per (client, leaf) (128 rows of 4.7 MB at configs[1]) an XCD then touches
+// ~1-2 of each row's 2 MiB pages instead of all of them (profiles/r02e_*).
+__device__ __forceinline__ int64_t xcd_block(int64_t p, int64_t n, int remap) {
+  if (!remap) return p;
+  const int64_t q = n / 8, r = n % 8, x = p % 8, i = p / 8;
+  return x * q + (x < r ? x : r) + i;
+}
+
 template <int IN, class ACC, int OUT, int VV, bool NT, bool BURST, class RowFn, class NORM, class EPI>
 __device__ __forceinline__ void walk_units(RowFn row, uint32_t row_bytes, int64_t K, int64_t u0, int64_t u1,
                                            uint8_t* ob, const typename ACC::T* __restrict__ w, bool dsc,
@@ -639,13 +652,14 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
                                                    int64_t K,
                                                    const typename ACC::T* __restrict__ w,
                                                    float scale, int do_scale, int accumulate,
-                                                   float* __restrict__ ws = nullptr) {
+                                                   float* __restrict__ ws, int remap) {
   constexpr int IB = Elem<IN>::B;
   const int tid = threadIdx.x;
   const int64_t* in_ptrs = img;
   const int64_t* out_ptrs = img + K * L;
   const int64_t* leaf_n = out_ptrs + L;
-  const int64_t* blk = leaf_n + L + 2 * (int64_t)blockIdx.x;
+  const int64_t bid = xcd_block(blockIdx.x, gridDim.x, remap);
+  const int64_t* blk = leaf_n + L + 2 * bid;
   const int64_t be = blk[0];
   const int leaf = (int)((be >> 40) & 0x3fffff);
   const bool tail = (be >> 62) & 1;
@@ -689,7 +703,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
       float t = l2lds[k];
 #pragma unroll
       for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, l2lds[i * K + k]);
-      ws[(int64_t)blockIdx.x * K + k] = t;
+      ws[bid * K + k] = t;  // plan order: the combine adds the partials in that order
     }
   }
 }
@@ -701,13 +715,14 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
 template <int IN, int V, bool NT>
 __global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict__ img, int L, int64_t K,
                                                        const float* __restrict__ w, float scale,
-                                                       fjagg_server_opt opt, const int64_t* __restrict__ state) {
+                                                       fjagg_server_opt opt, const int64_t* __restrict__ state,
+                                                       int remap) {
   constexpr int IB = Elem<IN>::B;
   const int tid = threadIdx.x;
   const int64_t* in_ptrs = img;
   const int64_t* out_ptrs = img + K * L;
   const int64_t* leaf_n = out_ptrs + L;
-  const int64_t* blk = leaf_n + L + 2 * (int64_t)blockIdx.x;
+  const int64_t* blk = leaf_n + L + 2 * xcd_block(blockIdx.x, gridDim.x, remap);
   const int64_t be = blk[0];
   const int leaf = (int)((be >> 40) & 0x3fffff);
   const bool tail = (be >> 62) & 1;
@@ -1119,6 +1134,16 @@ int dense_exact_chunked(int in, int acc, int out, const uint8_t* x, int64_t ld_b
   return FJAGG_OK;
 }
 
+// XCD-aware plan order in the pytree kernels (xcd_block); FJAGG_PTRS_REMAP=0 turns it
+// off for A/B runs.
+int ptrs_remap() {
+  static const int on = [] {
+    const char* e = getenv("FJAGG_PTRS_REMAP");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+
 template <int IN, class ACC, int OUT, int V>
 int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w,
                   float scale, int do_scale, int accumulate, float* ws, float* l2, hipStream_t s) {
@@ -1128,10 +1153,10 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
       const size_t smem = (size_t)(kThreads / 64) * K * sizeof(float);
       if (nt)
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true>), dim3((unsigned)nblk), dim3(kThreads), smem, s,
-                           img, L, K, wt, scale, do_scale, accumulate, ws);
+                           img, L, K, wt, scale, do_scale, accumulate, ws, ptrs_remap());
       else
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true>), dim3((unsigned)nblk), dim3(kThreads), smem,
-                           s, img, L, K, wt, scale, do_scale, accumulate, ws);
+                           s, img, L, K, wt, scale, do_scale, accumulate, ws, ptrs_remap());
       if (int rc = check_launch("k_ptrs (l2)")) return rc;
       hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s,
                          ws, nblk, K, l2);
@@ -1143,16 +1168,16 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
   const bool burst = nblk < 2 * (int64_t)residency(reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true>)).cus;
   if (nt && burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, ptrs_remap());
   else if (nt)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, ptrs_remap());
   else if (burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, ptrs_remap());
   else
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, ptrs_remap());
   return check_launch("k_ptrs");
 }
 
@@ -1406,10 +1431,10 @@ int fjagg_server_update_ptrs(int in_dtype, const int64_t* image_dev, int L, int6
   do {                                                                                               \
     if (nt)                                                                                          \
       hipLaunchKernelGGL((k_ptrs_opt<I, VV, true>), grid, block, 0, s, image_dev, L, K, w_dev, scale, \
-                         *opt, state_dev);                                                           \
+                         *opt, state_dev, ptrs_remap());                                             \
     else                                                                                             \
       hipLaunchKernelGGL((k_ptrs_opt<I, VV, false>), grid, block, 0, s, image_dev, L, K, w_dev, scale, \
-                         *opt, state_dev);                                                           \
+                         *opt, state_dev, ptrs_remap());                                             \
   } while (0)
   if (in_dtype == FJAGG_F32) {
     if (vec) FJ_OPT_LAUNCH(FJAGG_F32, 4); else FJ_OPT_LAUNCH(FJAGG_F32, 1);
