@@ -598,21 +598,6 @@ __global__ __launch_bounds__(kThreads) void k_dense_opt(
 // kThreads*8 units (E=8, U=4: the dense default; lanes past the range are masked)
 // when the range gives a lane more than one unit, else in groups of kThreads units
 // (E=1, U=8).
-// Start every client row's first access of this workgroup at once: one 1-byte load per
-// client (never past the workgroup's range), spread over the lanes. With one allocation per (client, leaf) each row sits in
-// its own pages, and the fold's walk (4 clients at a time) would otherwise discover the
-// K address translations a few at a time (configs[1], separate allocations: ~23 K
-// translation misses per launch, TCP_UTCL1_TRANSLATION_MISS, profiles/r02e_*). The bytes
-// are the first ones the walk reads, so nothing extra comes from HBM. The returned word
-// only feeds a store that cannot happen (K is never negative), which keeps the loads.
-template <class RowFn>
-__device__ __forceinline__ unsigned warm_rows(RowFn row, int64_t K) {
-  unsigned sink = 0;
-  for (int64_t k = threadIdx.x; k < K; k += kThreads)
-    sink |= __builtin_nontemporal_load(row(k));
-  return sink;
-}
-
 template <int IN, class ACC, int OUT, int VV, bool NT, bool BURST, class RowFn, class NORM, class EPI>
 __device__ __forceinline__ void walk_units(RowFn row, uint32_t row_bytes, int64_t K, int64_t u0, int64_t u1,
                                            uint8_t* ob, const typename ACC::T* __restrict__ w, bool dsc,
@@ -655,7 +640,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
                                                    int64_t K,
                                                    const typename ACC::T* __restrict__ w,
                                                    float scale, int do_scale, int accumulate,
-                                                   float* __restrict__ ws, int prefetch) {
+                                                   float* __restrict__ ws) {
   constexpr int IB = Elem<IN>::B;
   const int tid = threadIdx.x;
   const int64_t* in_ptrs = img;
@@ -687,7 +672,6 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
     __syncthreads();
     nrm = LdsNorm{l2lds + (tid >> 6) * K, 0.f};
   }
-  const unsigned warm = prefetch && !tail ? warm_rows(row, K) : 0u;
   if (tail) {
     const bool active = tid < n - nunits * V;
     if (L2 || active) {  // with L2 every lane joins the per-client wave reductions
@@ -701,7 +685,6 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   } else {
     walk_units<IN, ACC, OUT, V, NT, BURST>(row, row_bytes, K, 0, u1 - u0, ob, w, dsc, scale, acm, nrm, PlainEpi());
   }
-  if (warm == 0x1ffu && K < 0) ob[0] = 0;  // never taken: keeps warm_rows' loads
   if constexpr (L2) {
     __syncthreads();
     for (int64_t k = tid; k < K; k += kThreads) {
@@ -720,8 +703,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
 template <int IN, int V, bool NT>
 __global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict__ img, int L, int64_t K,
                                                        const float* __restrict__ w, float scale,
-                                                       fjagg_server_opt opt, const int64_t* __restrict__ state,
-                                                       int prefetch) {
+                                                       fjagg_server_opt opt, const int64_t* __restrict__ state) {
   constexpr int IB = Elem<IN>::B;
   const int tid = threadIdx.x;
   const int64_t* in_ptrs = img;
@@ -742,8 +724,6 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict
   const OptEpi epi{opt, at(out_ptrs[leaf]), at(state[leaf]), at(state[L + leaf]), at(state[2 * L + leaf])};
   auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]) + e_base * IB; };
   const uint32_t row_bytes = row_range((n - e_base) * IB);
-  const unsigned warm = prefetch && !tail ? warm_rows(row, K) : 0u;
-  if (warm == 0x1ffu && K < 0) epi.params[0] = 0.f;  // never taken: keeps warm_rows' loads
   if (tail) {
     if (tid < n - nunits * V) {
       const uint32_t off[1] = {(uint32_t)(tid * IB)};
@@ -1141,16 +1121,6 @@ int dense_exact_chunked(int in, int acc, int out, const uint8_t* x, int64_t ld_b
   return FJAGG_OK;
 }
 
-// Translation warm-up in the pytree kernels (warm_rows); FJAGG_PTRS_PREFETCH=0 turns it
-// off for A/B runs.
-int ptrs_prefetch() {
-  static const int on = [] {
-    const char* e = getenv("FJAGG_PTRS_PREFETCH");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on;
-}
-
 template <int IN, class ACC, int OUT, int V>
 int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w,
                   float scale, int do_scale, int accumulate, float* ws, float* l2, hipStream_t s) {
@@ -1160,10 +1130,10 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
       const size_t smem = (size_t)(kThreads / 64) * K * sizeof(float);
       if (nt)
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true>), dim3((unsigned)nblk), dim3(kThreads), smem, s,
-                           img, L, K, wt, scale, do_scale, accumulate, ws, ptrs_prefetch());
+                           img, L, K, wt, scale, do_scale, accumulate, ws);
       else
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true>), dim3((unsigned)nblk), dim3(kThreads), smem,
-                           s, img, L, K, wt, scale, do_scale, accumulate, ws, ptrs_prefetch());
+                           s, img, L, K, wt, scale, do_scale, accumulate, ws);
       if (int rc = check_launch("k_ptrs (l2)")) return rc;
       hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s,
                          ws, nblk, K, l2);
@@ -1175,16 +1145,16 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
   const bool burst = nblk < 2 * (int64_t)residency(reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true>)).cus;
   if (nt && burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr, ptrs_prefetch());
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
   else if (nt)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr, ptrs_prefetch());
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
   else if (burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr, ptrs_prefetch());
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
   else
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr, ptrs_prefetch());
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
   return check_launch("k_ptrs");
 }
 
@@ -1438,10 +1408,10 @@ int fjagg_server_update_ptrs(int in_dtype, const int64_t* image_dev, int L, int6
   do {                                                                                               \
     if (nt)                                                                                          \
       hipLaunchKernelGGL((k_ptrs_opt<I, VV, true>), grid, block, 0, s, image_dev, L, K, w_dev, scale, \
-                         *opt, state_dev, ptrs_prefetch());                                             \
+                         *opt, state_dev);                                             \
     else                                                                                             \
       hipLaunchKernelGGL((k_ptrs_opt<I, VV, false>), grid, block, 0, s, image_dev, L, K, w_dev, scale, \
-                         *opt, state_dev, ptrs_prefetch());                                             \
+                         *opt, state_dev);                                             \
   } while (0)
   if (in_dtype == FJAGG_F32) {
     if (vec) FJ_OPT_LAUNCH(FJAGG_F32, 4); else FJ_OPT_LAUNCH(FJAGG_F32, 1);
