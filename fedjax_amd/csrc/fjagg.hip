@@ -1297,6 +1297,29 @@ int64_t fjagg_ptrs_plan(int in_dtype, int flags, const int64_t* leaf_n, int L, i
   return fjagg_ptrs_plan_leaves(in_dtype, flags, leaf_n, nullptr, L, blocks, blocks_cap);
 }
 
+}  // extern "C"
+
+namespace {
+// CUs of the current device, queried once per device (the plan is rebuilt per call).
+int cu_count() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  int c = __atomic_load_n(&cached[dev], __ATOMIC_RELAXED);
+  if (c <= 0) {
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) c = 256;
+    (void)hipGetLastError();
+    __atomic_store_n(&cached[dev], c, __ATOMIC_RELAXED);
+  }
+  return c;
+}
+}  // namespace
+
+extern "C" {
+
 int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, const uint8_t* leaf_elem, int L,
                                int64_t* blocks, int64_t blocks_cap) {
   g_err[0] = 0;
@@ -1314,11 +1337,7 @@ int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, c
   }
   // balanced unit share per workgroup, as for the dense path (balanced_grid): the
   // same number of E=8 workgroups on every CU, at most kPlanPerCU of them per CU
-  int cus = 256, dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-    cus = 256;
-  (void)hipGetLastError();
+  const int cus = cu_count();
   constexpr int64_t kPlanPerCU = 3;  // E=8 x U=4 fold: 3 workgroups per CU (VGPR-limited)
   const int64_t tile = (int64_t)kThreads * 8;
   const int64_t ntiles = (total + tile - 1) / tile;

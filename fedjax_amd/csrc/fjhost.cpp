@@ -53,6 +53,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/csrc/autograd/python_variable.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -63,6 +64,20 @@
 #include "fjtree.h"
 
 namespace {
+
+// Host phase timers of fold_table (host_timers() reads and resets them): where the
+// per-call host time of tree_mean goes (tools/prof_tree_mean_host.py).
+enum { kTChecks, kTOutputs, kTPlan, kTImage, kTUpload, kTLaunch, kTWrap, kTPhases };
+double g_timers[kTPhases] = {};
+long long g_timer_calls = 0;
+struct Stamp {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(int phase) {
+    auto n = std::chrono::steady_clock::now();
+    g_timers[phase] += std::chrono::duration<double, std::micro>(n - t).count();
+    t = n;
+  }
+};
 
 struct Walk {
   const std::vector<at::ScalarType>* dtypes;  // nullptr: record versions only (leaf_versions)
@@ -308,6 +323,8 @@ PyObject* fold_table(PyObject*, PyObject* args) {
   const int64_t K = bp.len / (8 * L);
   if (K < 1 || bw.len < 4 * K) Py_RETURN_NONE;
   const auto* in = static_cast<const int64_t*>(bp.buf);
+  Stamp st;
+  ++g_timer_calls;
   try {
     if (with_l2) {
       const at::Tensor& q = THPVariable_Unpack(l2sq);
@@ -330,6 +347,7 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     std::vector<int64_t> lbits(L, 0);
     for (int64_t k = 0; k < K; ++k)
       for (Py_ssize_t l = 0; l < L; ++l) lbits[l] |= in[k * L + l];
+    st.lap(kTChecks);
     std::vector<at::Tensor> outs;
     outs.reserve(L);
     std::vector<uint8_t> elem(L, 0);
@@ -349,12 +367,14 @@ PyObject* fold_table(PyObject*, PyObject* args) {
       elem[l] = ((lbits[l] | reinterpret_cast<int64_t>(outs.back().data_ptr())) & 15) != 0;
       any_elem = any_elem || elem[l];
     }
+    st.lap(kTOutputs);
     auto plan = reinterpret_cast<PlanFn>(plan_addr);
     const uint8_t* mask = any_elem ? elem.data() : nullptr;
     const int64_t nblk = plan(kF32, 0, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);
     if (nblk < 0) Py_RETURN_NONE;
     // plan image (fjagg.h): in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk] | f32 weights
     const int64_t nw = (K + 1) / 2, n = K * L + 2 * L + 2 * nblk + nw;
+    st.lap(kTPlan);
     at::Tensor img = at::empty({n}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
     int64_t* p = img.data_ptr<int64_t>();
     std::memcpy(p, in, sizeof(int64_t) * K * L);
@@ -365,7 +385,9 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     if (plan(kF32, 0, leaf_n.data(), mask, static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) Py_RETURN_NONE;
     p[n - 1] = 0;
     std::memcpy(p + n - nw, bw.buf, 4 * K);
+    st.lap(kTImage);
     at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);
+    st.lap(kTUpload);
     const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
     const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0);
     const int64_t* dp = dimg.data_ptr<int64_t>();
@@ -382,9 +404,11 @@ PyObject* fold_table(PyObject*, PyObject* args) {
       rc = reinterpret_cast<WsumFn>(wsum_addr)(kF32, kF32, kF32, dp, static_cast<int>(L), K, nblk, dp + (n - nw),
                                                static_cast<float>(scale), flags, reinterpret_cast<void*>(stream));
     }
+    st.lap(kTLaunch);
     PyObject* list = PyList_New(L);
     if (!list) return nullptr;
     for (Py_ssize_t l = 0; l < L; ++l) PyList_SET_ITEM(list, l, THPVariable_Wrap(std::move(outs[l])));
+    st.lap(kTWrap);
     return Py_BuildValue("(iN)", rc, list);
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
@@ -861,7 +885,25 @@ PyObject* leaf_fold(PyObject*, PyObject* args) {
   }
 }
 
+PyObject* host_timers(PyObject*, PyObject*) {
+  static const char* names[kTPhases] = {"checks", "outputs", "plan", "image", "upload", "launch", "wrap"};
+  PyObject* d = PyDict_New();
+  if (!d) return nullptr;
+  for (int i = 0; i < kTPhases; ++i) {
+    PyObject* v = PyFloat_FromDouble(g_timer_calls ? g_timers[i] / g_timer_calls : 0.0);
+    PyDict_SetItemString(d, names[i], v);
+    Py_DECREF(v);
+    g_timers[i] = 0.0;
+  }
+  PyObject* c = PyLong_FromLongLong(g_timer_calls);
+  PyDict_SetItemString(d, "calls", c);
+  Py_DECREF(c);
+  g_timer_calls = 0;
+  return d;
+}
+
 PyMethodDef kMethods[] = {
+    {"host_timers", host_timers, METH_NOARGS, "mean per-call microseconds of fold_table's phases (resets)"},
     {"gather_rows", gather_rows, METH_VARARGS, "pointer table of K client pytrees (see fjhost.cpp)"},
     {"leaf_versions", leaf_versions, METH_VARARGS, "torch in-place version counters of K pytrees' leaves"},
     {"fold_weights", fold_weights, METH_VARARGS, "f32/i32 weights and W of Python-number weights"},

@@ -48,8 +48,11 @@ def main(K=128, reps=200):
         if i % 50 == 0:
             torch.cuda.synchronize()
     torch.cuda.synchronize()
+    from fedjax_amd import _lib
+    inner = {k: round(v, 2) for k, v in _lib.host().host_timers().items()}
     print(json.dumps({"workload": "configs[1] tree_mean host phases (us, median)",
-                      **{k: round(float(np.median(v)), 2) for k, v in ph.items()}}), flush=True)
+                      **{k: round(float(np.median(v)), 2) for k, v in ph.items()},
+                      "fold_table_phases_us_mean": inner}), flush=True)
 
 
 if __name__ == "__main__":
