@@ -741,6 +741,99 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict
                                                  NoNorm(), epi);
 }
 
+// Narrow parameter axis, many clients (exact mode). The exact fold walks the clients in
+// order per element, so the only parallelism is the parameter axis: at 16 Ki-128 Ki f32
+// params the 16-byte-unit kernels above have 4 K-32 K lanes for the whole chip and keep
+// too few loads in flight (0.7-4.3 TB/s, profiles/r02i_*). Here a workgroup owns 64
+// consecutive elements; all four waves load client rows into an LDS tile (each wave a
+// quarter of the tile's clients, kNarrowTile/4 loads in flight per lane), and wave 0
+// folds the previous tile from LDS in client order while the next tile is in flight
+// (double buffer). One element per lane, so 64-element rows of 256 B per wave-load and
+// 4x the lanes of the 16-byte path; any alignment. Same op sequence as fold(): bitwise.
+constexpr int kNarrowCols = 64;
+constexpr int kNarrowTile = 128;  // clients per LDS tile (2 x 128 x 64 x 4 B = 64 KiB LDS)
+
+template <int IN, class ACC, int OUT, bool NT>
+__global__ __launch_bounds__(kThreads) void k_dense_narrow(const uint8_t* __restrict__ x, int64_t ld_bytes,
+                                                           int64_t K, int64_t P,
+                                                           const typename ACC::T* __restrict__ w, float scale,
+                                                           int do_scale, int accumulate, uint8_t* __restrict__ out) {
+  using T = typename ACC::T;
+  constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
+  constexpr int PER = kNarrowTile / (kThreads / 64);  // client rows per wave per tile
+  __shared__ unsigned tile[2][kNarrowTile][kNarrowCols];
+  __shared__ T wt[2][kNarrowTile];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * kNarrowCols + lane;
+  const bool active = col < P;
+  const uint32_t coff = (uint32_t)((active ? col : P - 1) * IB);
+  const int64_t ntiles = (K + kNarrowTile - 1) / kNarrowTile;
+  unsigned r[PER];
+  T wr = T(0);
+  auto load = [&](int64_t t) {  // this wave's rows of tile t -> registers (+ the tile's weights)
+    const int64_t k0 = t * kNarrowTile;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int64_t k = k0 + wave + (int64_t)(kThreads / 64) * i;
+      k = k < K ? k : K - 1;
+      const uint8_t* p = x + k * ld_bytes + coff;
+      if constexpr (IB == 4) {
+        r[i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p))
+                  : *reinterpret_cast<const unsigned*>(p);
+      } else {
+        r[i] = NT ? (unsigned)__builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(p))
+                  : (unsigned)*reinterpret_cast<const unsigned short*>(p);
+      }
+    }
+    if (threadIdx.x < kNarrowTile) {
+      const int64_t k = k0 + threadIdx.x;
+      wr = w[k < K ? k : K - 1];
+    }
+  };
+  auto store = [&](int64_t t) {  // registers -> LDS buffer t & 1
+    unsigned(*b)[kNarrowCols] = tile[t & 1];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) b[wave + (kThreads / 64) * i][lane] = r[i];
+    if (threadIdx.x < kNarrowTile) wt[t & 1][threadIdx.x] = wr;
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  T acc = T(0);
+  for (int64_t t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) load(t + 1);  // in flight while wave 0 folds tile t
+    if (wave == 0) {
+      const unsigned(*b)[kNarrowCols] = tile[t & 1];
+      const T* wk = wt[t & 1];
+      const int64_t k0 = t * kNarrowTile;
+      const int n = (int)(K - k0 < kNarrowTile ? K - k0 : kNarrowTile);
+      int j = 0;
+      if (t == 0) {  // client 0: s_0 = t_0, or out + t_0 (running sum)
+        T v[1];
+        decode<IN, ACC, 1>(b[0][lane], v);
+        acc = ACC::mul(v[0], wk[0]);
+        if (accumulate && active) {
+          unsigned ob[1];
+          load_out_unit<OUT, 1>(out + col * OB, ob);
+          acc = ACC::add(init_from<OUT, ACC>(ob[0]), acc);
+        }
+        j = 1;
+      }
+      for (; j < n; ++j) {
+        T v[1];
+        decode<IN, ACC, 1>(b[j][lane], v);
+        acc = ACC::add(acc, ACC::mul(v[0], wk[j]));
+      }
+    }
+    if (t + 1 < ntiles) store(t + 1);  // buffer (t+1)&1 was last read in iteration t-1
+    __syncthreads();
+  }
+  if (wave == 0 && active) {
+    const unsigned b[1] = {finish<OUT, ACC>(acc, do_scale != 0, scale)};
+    store_unit<OUT, 1>(out + col * OB, b);
+  }
+}
+
 // Per-client sum of squares: grid (nb, K); ws[k*nb + b] = block partial (f32),
 // then k_l2sq_combine sums the nb partials of each client in block order.
 template <int IN>
@@ -965,7 +1058,8 @@ constexpr VariantShape kVariants[] = {{0, 0, 0},  {2, 8, 0},  {1, 8, 0},  {1, 16
                                       {2, 8, 8},  {2, 4, 8},  {1, 16, 8}, {4, 4, 4},
                                       {8, 4, 0},  {8, 8, 0},  {4, 16, 0}, {4, 12, 0},
                                       {8, 4, 0} /* 16: E8U4 burst */, {8, 4, 0} /* 17: E8U4 interleaved */};
-constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+constexpr int kNarrowVariant = 18;  // k_dense_narrow (LDS-staged, one element per lane)
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]) + 1;
 
 // Default shape: E=8 x U=4 (8 units = 128 B per lane per client, 4 clients = 32
 // loads in flight per lane, 3 workgroups per CU) on the balanced grid: fastest or
@@ -1074,6 +1168,37 @@ int validate_common(int in, int acc, int out, int64_t K, int flags, float scale)
 }
 
 // One dense launch over elements [0, P) of rows that start at x (row stride ld_bytes).
+template <int IN, class ACC, int OUT>
+int launch_narrow_t(const uint8_t* x, int64_t ld_bytes, int64_t K, int64_t P, const void* w, float scale,
+                    uint8_t* y, int flags, hipStream_t s) {
+  const dim3 grid((unsigned)((P + kNarrowCols - 1) / kNarrowCols));
+  const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
+  const int dsc = (flags & FJAGG_SCALE) ? 1 : 0, acm = (flags & FJAGG_ACCUMULATE) ? 1 : 0;
+  if (flags & FJAGG_NONTEMPORAL)
+    hipLaunchKernelGGL((k_dense_narrow<IN, ACC, OUT, true>), grid, dim3(kThreads), 0, s, x, ld_bytes, K, P, wt,
+                       scale, dsc, acm, y);
+  else
+    hipLaunchKernelGGL((k_dense_narrow<IN, ACC, OUT, false>), grid, dim3(kThreads), 0, s, x, ld_bytes, K, P, wt,
+                       scale, dsc, acm, y);
+  return check_launch("k_dense_narrow");
+}
+
+int launch_narrow(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, int64_t K, int64_t P,
+                  const void* w, float scale, uint8_t* y, int flags, hipStream_t s) {
+  if (K < 1 || P < 1) return FJAGG_OK;
+#define FJ_CASE(I, A, O, ACCT) \
+  if (in == I && acc == A && out == O) return launch_narrow_t<I, ACCT, O>(x, ld_bytes, K, P, w, scale, y, flags, s);
+  FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_BF16, AccF)
+  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_BF16, AccF)
+  FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
+  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
+  FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
+#undef FJ_CASE
+  return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination (%d,%d,%d)", in, acc, out);
+}
+
 int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, int64_t K,
                 int64_t P, const void* w, float scale, uint8_t* y, int flags, hipStream_t s,
                 int64_t kchunk, int64_t gy, int64_t y_ystride) {
@@ -1084,6 +1209,7 @@ int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, in
   int variant = (flags >> 8) & 0xff;
   if (variant >= kNumVariants) return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
   if (variant == 0) variant = pick_variant(P / V, K);
+  if (variant == kNarrowVariant && gy == 1) return launch_narrow(in, acc, out, x, ld_bytes, K, P, w, scale, y, flags, s);
   DenseArgs a;
   a.x = x;
   a.ld_bytes = ld_bytes;

@@ -164,10 +164,38 @@ def test_dense_all_variants_bitwise(K, P, cuda, coracle):
     r = ref.mean_scale(wi)
     want = coracle.wsum_f32(xh, np.float32(wi), scale=r)
     w = torch.tensor(np.float32(wi), device=cuda)
-    for variant in range(16):
+    for variant in list(range(18)) + [18]:  # 18: k_dense_narrow (LDS-staged, one element per lane)
         for nt, bal in ((False, True), (True, True), (True, False)):
             y = kernels.weighted_sum_dense(x, w, scale=float(r), variant=variant, nontemporal=nt, balanced=bal)
             assert np.array_equal(bits(host(y)), bits(want)), (variant, nt, bal)
+
+
+@pytest.mark.parametrize("K,P,dt,offset", [(300, 65536 + 7, "f32", 1), (129, 200, "bf16", 0), (1024, 4096, "f32", 0),
+                                           (2, 70, "i32", 3), (257, 33, "f32", 2)])
+def test_narrow_fold_bitwise_every_dtype_and_alignment(K, P, dt, offset, cuda, coracle):
+    """k_dense_narrow (variant 18): clients not a multiple of its 128-client tile, columns
+    not a multiple of its 64-element stripe, rows at odd element offsets (any alignment),
+    accumulate mode, bf16 in/out, wrapping int32 — bitwise the other variants' fold."""
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "i32": torch.int32}[dt]
+    base = torch.empty(K, P + offset + 5, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(base, seed=K + P)
+    if dt == "i32":
+        x = (base * 1e6).to(torch.int32)[:, offset:offset + P]
+        w = torch.tensor([int(v) for v in ref.fedavg_weights(K, seed=3)], dtype=torch.int32, device=cuda)
+    else:
+        x = base.to(tdt)[:, offset:offset + P]
+        w = torch.tensor(np.float32(ref.fedavg_weights(K, seed=3)), device=cuda)
+    scale = None if dt == "i32" else 0.125
+    for acc in (False, True):
+        outs = []
+        for variant in (2, 18):
+            o = torch.full((P,), 3, dtype=x.dtype, device=cuda) if acc else None
+            outs.append(kernels.weighted_sum_dense(x, w, scale=scale, variant=variant, out=o, accumulate=acc))
+        assert torch.equal(outs[0].view(torch.uint8), outs[1].view(torch.uint8)), (dt, acc)
+    if dt == "f32" and offset == 1:  # and against the oracle
+        want = coracle.wsum_f32(np.ascontiguousarray(host(x)), host(w), scale=np.float32(scale))
+        y18 = kernels.weighted_sum_dense(x, w, scale=scale, variant=18)
+        assert np.array_equal(bits(host(y18)), bits(want))
 
 
 def test_dense_accumulate_and_strided_rows(cuda, coracle):
