@@ -819,6 +819,23 @@ __global__ __launch_bounds__(kThreads) void k_dense_narrow(const uint8_t* __rest
         }
         j = 1;
       }
+      // 8 clients' LDS reads in flight before their folds: the chain of adds is serial,
+      // the reads are not (a read-fold-read loop waits out the LDS latency per client)
+      for (; j + 8 <= n; j += 8) {
+        unsigned raw[8];
+        T wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          raw[u] = b[j + u][lane];
+          wv[u] = wk[j + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          T v[1];
+          decode<IN, ACC, 1>(raw[u], v);
+          acc = ACC::add(acc, ACC::mul(v[0], wv[u]));
+        }
+      }
       for (; j < n; ++j) {
         T v[1];
         decode<IN, ACC, 1>(b[j][lane], v);
