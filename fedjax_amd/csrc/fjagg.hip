@@ -751,9 +751,11 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_opt(const int64_t* __restrict
 // (double buffer). One element per lane, so 64-element rows of 256 B per wave-load and
 // 4x the lanes of the 16-byte path; any alignment. Same op sequence as fold(): bitwise.
 constexpr int kNarrowCols = 64;
-constexpr int kNarrowTile = 128;  // clients per LDS tile (2 x 128 x 64 x 4 B = 64 KiB LDS)
 
-template <int IN, class ACC, int OUT, bool NT>
+// TILE clients per LDS tile: 128 (2 x 32 KiB buffers: two workgroups per CU) when the grid
+// has at least two stripes per CU, 256 (2 x 64 KiB: one per CU, twice the bytes in flight
+// per workgroup) below that.
+template <int IN, class ACC, int OUT, bool NT, int kNarrowTile>
 __global__ __launch_bounds__(kThreads) void k_dense_narrow(const uint8_t* __restrict__ x, int64_t ld_bytes,
                                                            int64_t K, int64_t P,
                                                            const typename ACC::T* __restrict__ w, float scale,
@@ -1185,18 +1187,25 @@ int validate_common(int in, int acc, int out, int64_t K, int flags, float scale)
 }
 
 // One dense launch over elements [0, P) of rows that start at x (row stride ld_bytes).
+int cu_count();
+
 template <int IN, class ACC, int OUT>
 int launch_narrow_t(const uint8_t* x, int64_t ld_bytes, int64_t K, int64_t P, const void* w, float scale,
                     uint8_t* y, int flags, hipStream_t s) {
-  const dim3 grid((unsigned)((P + kNarrowCols - 1) / kNarrowCols));
+  const int64_t stripes = (P + kNarrowCols - 1) / kNarrowCols;
+  const dim3 grid((unsigned)stripes);
   const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
   const int dsc = (flags & FJAGG_SCALE) ? 1 : 0, acm = (flags & FJAGG_ACCUMULATE) ? 1 : 0;
-  if (flags & FJAGG_NONTEMPORAL)
-    hipLaunchKernelGGL((k_dense_narrow<IN, ACC, OUT, true>), grid, dim3(kThreads), 0, s, x, ld_bytes, K, P, wt,
-                       scale, dsc, acm, y);
-  else
-    hipLaunchKernelGGL((k_dense_narrow<IN, ACC, OUT, false>), grid, dim3(kThreads), 0, s, x, ld_bytes, K, P, wt,
-                       scale, dsc, acm, y);
+  const bool nt = flags & FJAGG_NONTEMPORAL;
+  const bool wide = stripes < 2 * (int64_t)cu_count() && K > 128;
+#define FJ_NARROW(NTV, TILE)                                                                             \
+  hipLaunchKernelGGL((k_dense_narrow<IN, ACC, OUT, NTV, TILE>), grid, dim3(kThreads), 0, s, x, ld_bytes, K, P, \
+                     wt, scale, dsc, acm, y)
+  if (nt && wide) FJ_NARROW(true, 256);
+  else if (nt) FJ_NARROW(true, 128);
+  else if (wide) FJ_NARROW(false, 256);
+  else FJ_NARROW(false, 128);
+#undef FJ_NARROW
   return check_launch("k_dense_narrow");
 }
 
@@ -1225,6 +1234,9 @@ int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, in
   const int V = vec ? vw : 1;
   int variant = (flags >> 8) & 0xff;
   if (variant >= kNumVariants) return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
+  // a narrow parameter axis with many clients: the LDS-staged kernel (k_dense_narrow);
+  // from 256 Ki f32 up the 16-byte kernels keep enough loads in flight (profiles/r02i_*)
+  if (variant == 0 && gy == 1 && K >= 16 && P * ib <= (512 << 10)) variant = kNarrowVariant;
   if (variant == 0) variant = pick_variant(P / V, K);
   if (variant == kNarrowVariant && gy == 1) return launch_narrow(in, acc, out, x, ld_bytes, K, P, w, scale, y, flags, s);
   DenseArgs a;
