@@ -28,7 +28,7 @@ LIB_PATH = os.environ.get("FJAGG_LIB", os.path.join(_HERE, "_build", "libfjagg.s
 # enum fjagg_dtype
 F32, BF16, I32 = 0, 1, 2
 # enum fjagg_flags
-SCALE, ACCUMULATE, NONTEMPORAL, UNALIGNED, UNBALANCED = 1, 2, 4, 8, 16
+SCALE, ACCUMULATE, NONTEMPORAL, UNALIGNED, UNBALANCED, NARROW = 1, 2, 4, 8, 16, 32
 # enum fjagg_mode
 MODE_EXACT, MODE_SPLIT = 0, 1
 ABI_VERSION = 1

@@ -755,20 +755,20 @@ constexpr int kNarrowCols = 64;
 // TILE clients per LDS tile: 128 (2 x 32 KiB buffers: two workgroups per CU) when the grid
 // has at least two stripes per CU, 256 (2 x 64 KiB: one per CU, twice the bytes in flight
 // per workgroup) below that.
-template <int IN, class ACC, int OUT, bool NT, int kNarrowTile>
-__global__ __launch_bounds__(kThreads) void k_dense_narrow(const uint8_t* __restrict__ x, int64_t ld_bytes,
-                                                           int64_t K, int64_t P,
-                                                           const typename ACC::T* __restrict__ w, float scale,
-                                                           int do_scale, int accumulate, uint8_t* __restrict__ out) {
+template <int IN, class ACC, int OUT, bool NT, int kNarrowTile, class RowFn>
+__device__ __forceinline__ void narrow_fold(RowFn rowp, int64_t K, int64_t ncols,
+                                            const typename ACC::T* __restrict__ w, float scale, int do_scale,
+                                            int accumulate, uint8_t* __restrict__ out) {
+  // rowp(k): client k's row at this stripe's first element; ncols <= kNarrowCols valid
+  // elements; out: the stripe's first output element
   using T = typename ACC::T;
   constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
   constexpr int PER = kNarrowTile / (kThreads / 64);  // client rows per wave per tile
   __shared__ unsigned tile[2][kNarrowTile][kNarrowCols];
   __shared__ T wt[2][kNarrowTile];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * kNarrowCols + lane;
-  const bool active = col < P;
-  const uint32_t coff = (uint32_t)((active ? col : P - 1) * IB);
+  const bool active = lane < ncols;
+  const uint32_t coff = (uint32_t)((active ? lane : ncols - 1) * IB);
   const int64_t ntiles = (K + kNarrowTile - 1) / kNarrowTile;
   unsigned r[PER];
   T wr = T(0);
@@ -778,7 +778,7 @@ __global__ __launch_bounds__(kThreads) void k_dense_narrow(const uint8_t* __rest
     for (int i = 0; i < PER; ++i) {
       int64_t k = k0 + wave + (int64_t)(kThreads / 64) * i;
       k = k < K ? k : K - 1;
-      const uint8_t* p = x + k * ld_bytes + coff;
+      const uint8_t* p = rowp(k) + coff;
       if constexpr (IB == 4) {
         r[i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p))
                   : *reinterpret_cast<const unsigned*>(p);
@@ -816,7 +816,7 @@ __global__ __launch_bounds__(kThreads) void k_dense_narrow(const uint8_t* __rest
         acc = ACC::mul(v[0], wk[0]);
         if (accumulate && active) {
           unsigned ob[1];
-          load_out_unit<OUT, 1>(out + col * OB, ob);
+          load_out_unit<OUT, 1>(out + lane * OB, ob);
           acc = ACC::add(init_from<OUT, ACC>(ob[0]), acc);
         }
         j = 1;
@@ -849,8 +849,41 @@ __global__ __launch_bounds__(kThreads) void k_dense_narrow(const uint8_t* __rest
   }
   if (wave == 0 && active) {
     const unsigned b[1] = {finish<OUT, ACC>(acc, do_scale != 0, scale)};
-    store_unit<OUT, 1>(out + col * OB, b);
+    store_unit<OUT, 1>(out + lane * OB, b);
   }
+}
+
+template <int IN, class ACC, int OUT, bool NT, int kNarrowTile>
+__global__ __launch_bounds__(kThreads) void k_dense_narrow(const uint8_t* __restrict__ x, int64_t ld_bytes,
+                                                           int64_t K, int64_t P,
+                                                           const typename ACC::T* __restrict__ w, float scale,
+                                                           int do_scale, int accumulate, uint8_t* __restrict__ out) {
+  constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
+  const int64_t c0 = (int64_t)blockIdx.x * kNarrowCols;
+  const int64_t ncols = P - c0 < kNarrowCols ? P - c0 : kNarrowCols;
+  narrow_fold<IN, ACC, OUT, NT, kNarrowTile>([=](int64_t k) { return x + k * ld_bytes + c0 * IB; }, K, ncols, w,
+                                             scale, do_scale, accumulate, out + c0 * OB);
+}
+
+// The same over the pytree plan image (FJAGG_NARROW): block b's words give its leaf and a
+// range of at most kNarrowCols elements (fjagg_ptrs_plan_leaves with FJAGG_NARROW); the
+// client rows come from the K x L pointer table.
+template <int IN, class ACC, int OUT, bool NT, int kNarrowTile>
+__global__ __launch_bounds__(kThreads) void k_ptrs_narrow(const int64_t* __restrict__ img, int L, int64_t K,
+                                                          const typename ACC::T* __restrict__ w, float scale,
+                                                          int do_scale, int accumulate) {
+  constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
+  const int64_t* in_ptrs = img;
+  const int64_t* out_ptrs = img + K * L;
+  const int64_t* leaf_n = out_ptrs + L;
+  const int64_t* blk = leaf_n + L + 2 * (int64_t)blockIdx.x;
+  const int64_t be = blk[0];
+  const int leaf = (int)((be >> 40) & 0x3fffff);
+  const int64_t e0 = be & ((1ll << 40) - 1), e1 = blk[1];
+  uint8_t* ob = reinterpret_cast<uint8_t*>(out_ptrs[leaf]) + e0 * OB;
+  narrow_fold<IN, ACC, OUT, NT, kNarrowTile>(
+      [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]) + e0 * IB; }, K, e1 - e0, w,
+      scale, do_scale, accumulate, ob);
 }
 
 // Per-client sum of squares: grid (nb, K); ws[k*nb + b] = block partial (f32),
@@ -1314,6 +1347,23 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
 }
 
 template <int IN, class ACC, int OUT>
+int launch_ptrs_narrow(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w, float scale,
+                       int do_scale, int accumulate, hipStream_t s) {
+  const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
+  const bool wide = nblk < 2 * (int64_t)cu_count() && K > 128;  // as launch_narrow_t
+  const dim3 grid((unsigned)nblk);
+#define FJ_NARROW(NTV, TILE) \
+  hipLaunchKernelGGL((k_ptrs_narrow<IN, ACC, OUT, NTV, TILE>), grid, dim3(kThreads), 0, s, img, L, K, wt, scale, \
+                     do_scale, accumulate)
+  if (nt && wide) FJ_NARROW(true, 256);
+  else if (nt) FJ_NARROW(true, 128);
+  else if (wide) FJ_NARROW(false, 256);
+  else FJ_NARROW(false, 128);
+#undef FJ_NARROW
+  return check_launch("k_ptrs_narrow");
+}
+
+template <int IN, class ACC, int OUT>
 int launch_ptrs_io(bool vec, bool nt, const int64_t* img, int L, int64_t K, int64_t nblk,
                    const void* w, float scale, int do_scale, int accumulate, float* ws, float* l2,
                    hipStream_t s) {
@@ -1481,6 +1531,20 @@ int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, c
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16 && in_dtype != FJAGG_I32)
     return fail(FJAGG_EINVAL, "bad dtype %d", in_dtype);
   if (L < 0 || L >= (1 << 22)) return fail(FJAGG_EINVAL, "bad leaf count %d", L);
+  if (flags & FJAGG_NARROW) {  // stripes of kNarrowCols elements of every leaf (k_ptrs_narrow)
+    int64_t nblk = 0;
+    for (int l = 0; l < L; ++l) {
+      if (leaf_n[l] < 0 || leaf_n[l] >= (1ll << 40))
+        return fail(FJAGG_EINVAL, "leaf %d: %lld elements unsupported", l, (long long)leaf_n[l]);
+      for (int64_t e = 0; e < leaf_n[l]; e += kNarrowCols, ++nblk) {
+        if (nblk < blocks_cap) {
+          blocks[2 * nblk] = ((int64_t)l << 40) | e;
+          blocks[2 * nblk + 1] = e + kNarrowCols < leaf_n[l] ? e + kNarrowCols : leaf_n[l];
+        }
+      }
+    }
+    return nblk;
+  }
   const int64_t V = (flags & FJAGG_UNALIGNED) ? 1 : vwidth(in_dtype);
   int64_t total = 0;
   for (int l = 0; l < L; ++l) {
@@ -1534,6 +1598,20 @@ int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* im
   const bool vec = !(flags & FJAGG_UNALIGNED);
   const bool nt = (flags & FJAGG_NONTEMPORAL) != 0;
   const int ds = (flags & FJAGG_SCALE) ? 1 : 0, ac = (flags & FJAGG_ACCUMULATE) ? 1 : 0;
+  if (flags & FJAGG_NARROW) {
+    if (ws) return fail(FJAGG_EINVAL, "FJAGG_NARROW plans fold only (no fused norms)");
+#define FJ_CASE(I, A, O, ACCT)                                                                          \
+    if (in_dtype == I && acc_dtype == A && out_dtype == O)                                              \
+      return launch_ptrs_narrow<I, ACCT, O>(nt, image_dev, L, K, nblk, w_dev, scale, ds, ac, s);
+    FJ_CASE(FJAGG_F32, FJAGG_F32, FJAGG_F32, AccF)
+    FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_BF16, AccF)
+    FJ_CASE(FJAGG_BF16, FJAGG_F32, FJAGG_F32, AccF)
+    FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
+    FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
+    FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
+#undef FJ_CASE
+    return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination");
+  }
 #define FJ_CASE(I, A, O, ACCT)                                                                 \
   if (in_dtype == I && acc_dtype == A && out_dtype == O)                                       \
     return launch_ptrs_io<I, ACCT, O>(vec, nt, image_dev, L, K, nblk, w_dev, scale, ds, ac, ws, l2, s);

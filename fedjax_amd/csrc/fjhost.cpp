@@ -369,8 +369,12 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     }
     st.lap(kTOutputs);
     auto plan = reinterpret_cast<PlanFn>(plan_addr);
-    const uint8_t* mask = any_elem ? elem.data() : nullptr;
-    const int64_t nblk = plan(kF32, 0, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);
+    // a small delta and many clients: k_ptrs_narrow's LDS-staged stripes (any alignment;
+    // the rule of tree_util._narrow), not with fused norms
+    const bool narrow = !with_l2 && K >= 16 && total * 4 <= (512 << 10);
+    const uint8_t* mask = any_elem && !narrow ? elem.data() : nullptr;
+    const int pflags = narrow ? FJAGG_NARROW : 0;
+    const int64_t nblk = plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);
     if (nblk < 0) Py_RETURN_NONE;
     // plan image (fjagg.h): in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk] | f32 weights
     const int64_t nw = (K + 1) / 2, n = K * L + 2 * L + 2 * nblk + nw;
@@ -382,14 +386,15 @@ PyObject* fold_table(PyObject*, PyObject* args) {
       p[K * L + l] = reinterpret_cast<int64_t>(outs[l].data_ptr());
       p[K * L + L + l] = leaf_n[l];
     }
-    if (plan(kF32, 0, leaf_n.data(), mask, static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) Py_RETURN_NONE;
+    if (plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) Py_RETURN_NONE;
     p[n - 1] = 0;
     std::memcpy(p + n - nw, bw.buf, 4 * K);
     st.lap(kTImage);
     at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);
     st.lap(kTUpload);
     const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
-    const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0);
+    const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0) |
+                      (narrow ? FJAGG_NARROW : 0);
     const int64_t* dp = dimg.data_ptr<int64_t>();
     int rc;
     if (with_l2) {  // fused per-client squared l2 norms (fjagg_wsum_l2_ptrs), workspace from torch's allocator

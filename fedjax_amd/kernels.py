@@ -152,16 +152,19 @@ def split_workspace_bytes(K: int, P: int) -> int:
     return int(_lib.load().fjagg_split_workspace_bytes(K, P))
 
 
-def ptrs_plan(in_code: int, leaf_n: Sequence[int], unaligned) -> np.ndarray:
+def ptrs_plan(in_code: int, leaf_n: Sequence[int], unaligned, narrow: bool = False) -> np.ndarray:
     """Workgroup table of the pytree kernel (host int64 array, 2 words per workgroup).
 
     ``unaligned``: a bool for the whole launch (True = element units everywhere; launch
     with ``unaligned=True``), or a per-leaf boolean array: the marked leaves take
     element units, the others 16-byte units (``fjagg_ptrs_plan_leaves``; launch with
-    ``unaligned=False``)."""
+    ``unaligned=False``). ``narrow``: 64-element stripes for k_ptrs_narrow (any
+    alignment; launch with ``FJAGG_NARROW``)."""
     lib = _lib.load()
     n = np.ascontiguousarray(leaf_n, dtype=np.int64)
-    if isinstance(unaligned, (bool, np.bool_)):
+    if narrow:
+        flags, mask = _lib.NARROW, None
+    elif isinstance(unaligned, (bool, np.bool_)):
         flags, mask = (_lib.UNALIGNED if unaligned else 0), None
     else:
         mask = np.ascontiguousarray(unaligned, dtype=np.uint8)

@@ -241,7 +241,11 @@ def _fold(rows, weights, *, scale=None,
         else:
             in_ptrs = np.array([[rows[k][l].data_ptr() for l in ls] for k in range(K)], dtype=np.int64)
         out_ptrs = np.array([outs[l].data_ptr() for l in ls], dtype=np.int64)
-        blocks, unaligned = _leaf_plan(in_c, leaf_n, in_ptrs, out_ptrs, device)
+        narrow = _narrow(K, leaf_n, in_c) and l2sq is None
+        if narrow:
+            blocks, unaligned = _ptrs_plan(in_c, leaf_n, "narrow", device), False
+        else:
+            blocks, unaligned = _leaf_plan(in_c, leaf_n, in_ptrs, out_ptrs, device)
         if packed is not None:
             w_host = packed.f32 if acc_c == _lib.F32 else packed.i32
         elif acc_c == _lib.F32:
@@ -257,6 +261,7 @@ def _fold(rows, weights, *, scale=None,
         nt = (total_bytes >= NONTEMPORAL_MIN_BYTES) if nontemporal is None else nontemporal
         flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
         flags |= (_lib.UNALIGNED if unaligned else 0) | (_lib.NONTEMPORAL if nt else 0)
+        flags |= _lib.NARROW if narrow else 0
         nblk = len(blocks) // 2
         sc = float(np.float32(scale) if scale is not None else 1.0)
         stream = torch.cuda.current_stream(device).cuda_stream
@@ -306,13 +311,25 @@ def _native_fold(table: "_Table", packed: "_Weights", scale, out=None,
 _PLANS = {}  # (in dtype, leaf sizes, unaligned) -> workgroup table (the device is fixed per process)
 
 
+# A small client delta and many clients: the LDS-staged stripes of k_ptrs_narrow keep more
+# loads in flight than 16-byte units spread over the few lanes a narrow tree has (the
+# dense path's rule, fjagg.hip dense_exact: rows <= 512 KiB, K >= 16)
+_NARROW_MAX_BYTES = 512 << 10
+
+
+def _narrow(K: int, leaf_n: np.ndarray, in_c: int) -> bool:
+    return K >= 16 and int(leaf_n.sum()) * (2 if in_c == _lib.BF16 else 4) <= _NARROW_MAX_BYTES
+
+
 def _ptrs_plan(in_c: int, leaf_n: np.ndarray, unaligned, device: torch.device) -> np.ndarray:
-    """Cached :func:`kernels.ptrs_plan`; ``unaligned`` is a bool or a per-leaf mask."""
-    key = (in_c, leaf_n.tobytes(), unaligned if isinstance(unaligned, bool) else
+    """Cached :func:`kernels.ptrs_plan`; ``unaligned`` is a bool, a per-leaf mask, or
+    "narrow" (the k_ptrs_narrow stripes)."""
+    key = (in_c, leaf_n.tobytes(), unaligned if isinstance(unaligned, (bool, str)) else
            np.asarray(unaligned, dtype=np.uint8).tobytes(), device)
     blocks = _PLANS.get(key)
     if blocks is None:
-        blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)
+        blocks = (kernels.ptrs_plan(in_c, leaf_n, False, narrow=True) if unaligned == "narrow"
+                  else kernels.ptrs_plan(in_c, leaf_n, unaligned))
         if len(_PLANS) < 1024:
             _PLANS[key] = blocks
     return blocks

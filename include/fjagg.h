@@ -65,6 +65,9 @@ enum fjagg_flags {
   FJAGG_UNALIGNED = 1 << 3,   /* ptrs path: some pointer is not 16-byte aligned */
   FJAGG_UNBALANCED = 1 << 4,  /* dense path: one tile per workgroup instead of a balanced
                                  resident grid (tuning / A-B only) */
+  FJAGG_NARROW = 1 << 5,      /* pytree path, plan AND launch: 64-element stripes per workgroup,
+                                 client rows staged through LDS (k_ptrs_narrow) — for small
+                                 leaves and many clients; fold only (no fused norms) */
 };
 /* bits 8..15 of flags select a kernel shape of the dense path: 0 = automatic,
  * 1..11 = fixed (units per lane, clients in flight, waves/SIMD) for tuning; see fjagg.hip */
