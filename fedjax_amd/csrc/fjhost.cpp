@@ -55,6 +55,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <unordered_map>
@@ -371,7 +372,11 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     auto plan = reinterpret_cast<PlanFn>(plan_addr);
     // a small delta and many clients: k_ptrs_narrow's LDS-staged stripes (any alignment;
     // the rule of tree_util._narrow), not with fused norms
-    const bool narrow = !with_l2 && K >= 16 && total * 4 <= (512 << 10);
+    static const int64_t narrow_max = [] {  // FJAGG_NARROW_MAX_BYTES, as tree_util._NARROW_MAX_BYTES
+      const char* e = getenv("FJAGG_NARROW_MAX_BYTES");
+      return e ? (int64_t)atoll(e) : (int64_t)(512 << 10);
+    }();
+    const bool narrow = !with_l2 && K >= 16 && total * 4 <= narrow_max;
     const uint8_t* mask = any_elem && !narrow ? elem.data() : nullptr;
     const int pflags = narrow ? FJAGG_NARROW : 0;
     const int64_t nblk = plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import ctypes
 import numbers
+import os
 import weakref
 from typing import Any, Iterable, List, Optional, Sequence, Tuple
 
@@ -314,7 +315,7 @@ _PLANS = {}  # (in dtype, leaf sizes, unaligned) -> workgroup table (the device 
 # A small client delta and many clients: the LDS-staged stripes of k_ptrs_narrow keep more
 # loads in flight than 16-byte units spread over the few lanes a narrow tree has (the
 # dense path's rule, fjagg.hip dense_exact: rows <= 512 KiB, K >= 16)
-_NARROW_MAX_BYTES = 512 << 10
+_NARROW_MAX_BYTES = int(os.environ.get("FJAGG_NARROW_MAX_BYTES", 512 << 10))  # 0: never (A/B runs)
 
 
 def _narrow(K: int, leaf_n: np.ndarray, in_c: int) -> bool:
@@ -328,7 +329,7 @@ def _ptrs_plan(in_c: int, leaf_n: np.ndarray, unaligned, device: torch.device) -
            np.asarray(unaligned, dtype=np.uint8).tobytes(), device)
     blocks = _PLANS.get(key)
     if blocks is None:
-        blocks = (kernels.ptrs_plan(in_c, leaf_n, False, narrow=True) if unaligned == "narrow"
+        blocks = (kernels.ptrs_plan(in_c, leaf_n, False, narrow=True) if isinstance(unaligned, str)
                   else kernels.ptrs_plan(in_c, leaf_n, unaligned))
         if len(_PLANS) < 1024:
             _PLANS[key] = blocks
