@@ -755,12 +755,46 @@ constexpr int kNarrowCols = 64;
 // TILE clients per LDS tile: 128 (2 x 32 KiB buffers: two workgroups per CU) when the grid
 // has at least two stripes per CU, 256 (2 x 64 KiB: one per CU, twice the bytes in flight
 // per workgroup) below that.
-template <int IN, class ACC, int OUT, bool NT, int kNarrowTile, class RowFn>
-__device__ __forceinline__ void narrow_fold(RowFn rowp, int64_t K, int64_t ncols,
+// Client rows of a dense slab: computed, nothing to stage.
+struct SlabRows {
+  const uint8_t* base;  // client 0's row at the stripe's first element
+  int64_t ld_bytes;
+  __device__ __forceinline__ void fetch(int64_t, int64_t) {}
+  __device__ __forceinline__ void commit(int) {}
+  __device__ __forceinline__ const uint8_t* row(int, int64_t k, int64_t) const { return base + k * ld_bytes; }
+};
+
+// Client rows of the pytree plan: pointers from the K x L table, staged through LDS one
+// tile ahead of the data loads that use them (a per-row scalar load from the table would
+// put one more memory round trip in front of every tile's loads).
+template <int TILE>
+struct TableRows {
+  const int64_t* in_ptrs;
+  int L, leaf;
+  int64_t eoff;           // the stripe's first element, in bytes
+  unsigned long long* lds;  // [2][TILE] row pointers
+  unsigned long long pr;    // this thread's fetched pointer (threads < TILE)
+  __device__ __forceinline__ void fetch(int64_t k0, int64_t K) {
+    if (threadIdx.x < TILE) {
+      int64_t k = k0 + threadIdx.x;
+      k = k < K ? k : K - 1;
+      pr = (unsigned long long)in_ptrs[k * L + leaf];
+    }
+  }
+  __device__ __forceinline__ void commit(int slot) {
+    if (threadIdx.x < TILE) lds[slot * TILE + threadIdx.x] = pr;
+  }
+  __device__ __forceinline__ const uint8_t* row(int slot, int64_t k, int64_t k0) const {
+    return reinterpret_cast<const uint8_t*>(lds[slot * TILE + (k - k0)]) + eoff;
+  }
+};
+
+template <int IN, class ACC, int OUT, bool NT, int kNarrowTile, class Rows>
+__device__ __forceinline__ void narrow_fold(Rows rows, int64_t K, int64_t ncols,
                                             const typename ACC::T* __restrict__ w, float scale, int do_scale,
                                             int accumulate, uint8_t* __restrict__ out) {
-  // rowp(k): client k's row at this stripe's first element; ncols <= kNarrowCols valid
-  // elements; out: the stripe's first output element
+  // rows: client k's row at this stripe's first element (SlabRows / TableRows); ncols <=
+  // kNarrowCols valid elements; out: the stripe's first output element
   using T = typename ACC::T;
   constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
   constexpr int PER = kNarrowTile / (kThreads / 64);  // client rows per wave per tile
@@ -778,7 +812,7 @@ __device__ __forceinline__ void narrow_fold(RowFn rowp, int64_t K, int64_t ncols
     for (int i = 0; i < PER; ++i) {
       int64_t k = k0 + wave + (int64_t)(kThreads / 64) * i;
       k = k < K ? k : K - 1;
-      const uint8_t* p = rowp(k) + coff;
+      const uint8_t* p = rows.row((int)(t & 1), k, k0) + coff;
       if constexpr (IB == 4) {
         r[i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p))
                   : *reinterpret_cast<const unsigned*>(p);
@@ -798,12 +832,20 @@ __device__ __forceinline__ void narrow_fold(RowFn rowp, int64_t K, int64_t ncols
     for (int i = 0; i < PER; ++i) b[wave + (kThreads / 64) * i][lane] = r[i];
     if (threadIdx.x < kNarrowTile) wt[t & 1][threadIdx.x] = wr;
   };
+  rows.fetch(0, K);
+  rows.commit(0);
+  if (ntiles > 1) {
+    rows.fetch(kNarrowTile, K);
+    rows.commit(1);
+  }
+  __syncthreads();
   load(0);
   store(0);
   __syncthreads();
   T acc = T(0);
   for (int64_t t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) load(t + 1);  // in flight while wave 0 folds tile t
+    if (t + 2 < ntiles) rows.fetch((t + 2) * kNarrowTile, K);  // row pointers, one tile further
     if (wave == 0) {
       const unsigned(*b)[kNarrowCols] = tile[t & 1];
       const T* wk = wt[t & 1];
@@ -845,6 +887,7 @@ __device__ __forceinline__ void narrow_fold(RowFn rowp, int64_t K, int64_t ncols
       }
     }
     if (t + 1 < ntiles) store(t + 1);  // buffer (t+1)&1 was last read in iteration t-1
+    if (t + 2 < ntiles) rows.commit((int)(t & 1));  // tile t's pointers were used at iteration t-1
     __syncthreads();
   }
   if (wave == 0 && active) {
@@ -861,8 +904,8 @@ __global__ __launch_bounds__(kThreads) void k_dense_narrow(const uint8_t* __rest
   constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
   const int64_t c0 = (int64_t)blockIdx.x * kNarrowCols;
   const int64_t ncols = P - c0 < kNarrowCols ? P - c0 : kNarrowCols;
-  narrow_fold<IN, ACC, OUT, NT, kNarrowTile>([=](int64_t k) { return x + k * ld_bytes + c0 * IB; }, K, ncols, w,
-                                             scale, do_scale, accumulate, out + c0 * OB);
+  narrow_fold<IN, ACC, OUT, NT, kNarrowTile>(SlabRows{x + c0 * IB, ld_bytes}, K, ncols, w, scale, do_scale,
+                                             accumulate, out + c0 * OB);
 }
 
 // The same over the pytree plan image (FJAGG_NARROW): block b's words give its leaf and a
@@ -873,6 +916,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_narrow(const int64_t* __restr
                                                           const typename ACC::T* __restrict__ w, float scale,
                                                           int do_scale, int accumulate) {
   constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
+  __shared__ unsigned long long rowp[2 * kNarrowTile];
   const int64_t* in_ptrs = img;
   const int64_t* out_ptrs = img + K * L;
   const int64_t* leaf_n = out_ptrs + L;
@@ -881,9 +925,8 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_narrow(const int64_t* __restr
   const int leaf = (int)((be >> 40) & 0x3fffff);
   const int64_t e0 = be & ((1ll << 40) - 1), e1 = blk[1];
   uint8_t* ob = reinterpret_cast<uint8_t*>(out_ptrs[leaf]) + e0 * OB;
-  narrow_fold<IN, ACC, OUT, NT, kNarrowTile>(
-      [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]) + e0 * IB; }, K, e1 - e0, w,
-      scale, do_scale, accumulate, ob);
+  narrow_fold<IN, ACC, OUT, NT, kNarrowTile>(TableRows<kNarrowTile>{in_ptrs, L, leaf, e0 * IB, rowp, 0ull}, K,
+                                             e1 - e0, w, scale, do_scale, accumulate, ob);
 }
 
 // Per-client sum of squares: grid (nb, K); ws[k*nb + b] = block partial (f32),
