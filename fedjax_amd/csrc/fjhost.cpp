@@ -374,7 +374,7 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     // the rule of tree_util._narrow), not with fused norms
     static const int64_t narrow_max = [] {  // FJAGG_NARROW_MAX_BYTES, as tree_util._NARROW_MAX_BYTES
       const char* e = getenv("FJAGG_NARROW_MAX_BYTES");
-      return e ? (int64_t)atoll(e) : (int64_t)(512 << 10);
+      return e ? (int64_t)atoll(e) : (int64_t)(256 << 10);
     }();
     const bool narrow = !with_l2 && K >= 16 && total * 4 <= narrow_max;
     const uint8_t* mask = any_elem && !narrow ? elem.data() : nullptr;

@@ -313,9 +313,10 @@ _PLANS = {}  # (in dtype, leaf sizes, unaligned) -> workgroup table (the device 
 
 
 # A small client delta and many clients: the LDS-staged stripes of k_ptrs_narrow keep more
-# loads in flight than 16-byte units spread over the few lanes a narrow tree has (the
-# dense path's rule, fjagg.hip dense_exact: rows <= 512 KiB, K >= 16)
-_NARROW_MAX_BYTES = int(os.environ.get("FJAGG_NARROW_MAX_BYTES", 512 << 10))  # 0: never (A/B runs)
+# loads in flight than 16-byte units spread over the few lanes a narrow tree has. Up to
+# 256 KiB per client (a 48.7 K-param model at 1,024-4,096 clients: 0.44 -> 0.33 ms); at
+# ~430 KiB the balanced 16-byte plan is as fast or faster (profiles/r02k_narrow_pytree.txt).
+_NARROW_MAX_BYTES = int(os.environ.get("FJAGG_NARROW_MAX_BYTES", 256 << 10))  # 0: never (A/B runs)
 
 
 def _narrow(K: int, leaf_n: np.ndarray, in_c: int) -> bool:
