@@ -35,7 +35,8 @@ class RunningMean:
     """Running weighted sum of client deltas with the structure of ``template``.
 
     ``add(delta, weight)`` may be called with device or host pytrees; deltas are
-    buffered and folded ``buffer_clients`` at a time. ``result()`` returns
+    buffered and folded ``buffer_clients`` at a time (default: as many as fit
+    ``tree_util.STREAM_BUDGET_BYTES``, so usually once per round). ``result()`` returns
     ``tree_inverse_weight(sum, total_weight)`` (tree_util.py:35-38).
 
     Buffering holds references, not copies. The reference's loop reads each delta at
@@ -47,7 +48,7 @@ class RunningMean:
     (one extra device copy per client; safe for any reuse).
     """
 
-    def __init__(self, template: PyTree, *, buffer_clients: int = 8,
+    def __init__(self, template: PyTree, *, buffer_clients: Optional[int] = None,
                  device: Optional[torch.device] = None, copy_on_add: bool = False):
         leaves, self.treedef = pytree.flatten(template)
         self.device = device or tree_util._find_device(leaves)
@@ -56,6 +57,11 @@ class RunningMean:
         self._sum: List[torch.Tensor] = pytree.leaves_of(zeros)  # fed_avg.py:132
         self.total_weight: Any = 0.0  # fed_avg.py:133 (num_examples_sum = 0.)
         self.num_clients = 0
+        if buffer_clients is None:
+            # as many clients as tree_mean streams per launch (STREAM_BUDGET_BYTES of deltas,
+            # at most 4096): one fold per round for most models (configs[1]: 888 clients)
+            per = max(1, 4 * sum(int(x.numel()) for x in self._sum))
+            buffer_clients = min(4096, max(1, tree_util.STREAM_BUDGET_BYTES // per))
         self.buffer_clients = max(1, int(buffer_clients))
         self._trees: List[PyTree] = []
         self._weights: List[Any] = []

@@ -384,7 +384,7 @@ def test_full_size_configs(K, P, cuda):
 
 
 # ------------------------------------------------------------ streaming running sum
-@pytest.mark.parametrize("buffer_clients", [1, 5, 8])
+@pytest.mark.parametrize("buffer_clients", [1, 5, 8, None])
 def test_running_mean_equals_library_fedavg_loop(buffer_clients, cuda, coracle):
     """fedjax/algorithms/fed_avg.py:132-146 restated: s = 0; s = s + x_k*n_k; s * f32(1/W)."""
     K, P = 37, 3001

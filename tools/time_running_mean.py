@@ -44,7 +44,7 @@ def main(K=128, reps=20):
     res = {"workload": "configs[1] 128 x EMNIST-CNN through RunningMean (fed_avg.py:132-146)",
            "tree_mean_ms": round(wall(lambda: tu.tree_mean(zip(clients, weights)), reps), 4)}
     ref = tu.tree_mean(zip(clients, weights))
-    for B in (1, 8, 32, 128):
+    for B in (1, 8, 32, 128, None):
         def rnd():
             rm = aggregators.RunningMean(tmpl, buffer_clients=B, device=dev)
             for c, w in zip(clients, weights):
