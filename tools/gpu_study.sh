@@ -1,0 +1,73 @@
+#!/bin/bash
+# GPU-box studies behind DESIGN.md's numbers (run from the repo root on the box):
+#   bash tools/gpu_study.sh STUDY
+# STUDY:
+#   tree_ops      per-call tree-op tests, literal running-sum loop host costs and timing,
+#                 rocprofv3 kernel stats of the loop                   (profiles/r02c_*)
+#   placement     k_ptrs by leaf placement: kernel trace + UTCL1 / UTCL2 / TCC PMC passes
+#                                                                      (profiles/r02e_ptrs_placement)
+#   quant         k_quant_fold VALU counters                           (profiles/r02h_*)
+#   narrow        k_dense_narrow parity + variant sweep on narrow shapes (profiles/r02i_*)
+#   narrow_tree   k_ptrs_narrow vs k_ptrs on small models (FJAGG_NARROW_MAX_BYTES A/B, profiles/r02k_*)
+# Every GPU step runs under its own time limit; the script stops at the first failure.
+set -u
+STUDY=${1:?study name}
+O=gpurun_out/study_$STUDY
+mkdir -p "$O"
+export TMPDIR=/tmp
+die() { echo "$1 failed"; exit 1; }
+PT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
+case "$STUDY" in
+  tree_ops)
+    timeout -k 10 300 $PT tests/test_gpu_tree_ops.py > $O/tests.log 2>&1; rc=$?; tail -2 $O/tests.log; [ $rc -le 1 ] || exit $rc
+    timeout -k 10 300 python tools/prof_literal_loop.py > $O/loop.json 2> $O/loop.err || die loop
+    timeout -k 10 300 python tools/time_running_mean.py > $O/time.json 2> $O/time.err || die time
+    cat $O/loop.json $O/time.json
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
+      python tools/prof_literal_loop.py > $O/prof.log 2>&1 || die rocprof
+    rm -f $O/prof/run_kernel_trace.csv
+    ;;
+  placement)
+    for m in views clones rows2m bigseg; do
+      timeout -s KILL 90 rocprofv3 --kernel-trace -d $O/$m/trace -o run --output-format csv -- \
+        python tools/probe_ptrs_pmc.py $m 20 > $O/$m.log 2>&1 || die "trace $m"
+      timeout -s KILL 90 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
+        TCP_UTCL1_REQUEST_sum TCP_UTCL1_STALL_MULTI_MISS_sum -d $O/$m/pmcA -o run --output-format csv -- \
+        python tools/probe_ptrs_pmc.py $m 10 >> $O/$m.log 2>&1 || die "pmcA $m"
+      timeout -s KILL 90 rocprofv3 --pmc TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum \
+        TCP_UTCL1_STALL_INFLIGHT_MAX_sum TCP_UTCL1_PERMISSION_MISS_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE \
+        -d $O/$m/pmcB -o run --output-format csv -- python tools/probe_ptrs_pmc.py $m 10 >> $O/$m.log 2>&1 || die "pmcB $m"
+      timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_RDREQ TCC_TAG_STALL_sum TCC_EA0_RDREQ_DRAM_sum \
+        -d $O/$m/pmcC -o run --output-format csv -- python tools/probe_ptrs_pmc.py $m 10 >> $O/$m.log 2>&1 || die "pmcC $m"
+    done
+    python tools/pmc_table.py k_ptrs $O/table.json $O/views $O/clones $O/rows2m $O/bigseg
+    ;;
+  quant)
+    B="python tools/bench_compression.py --only uniform,terngrad --rounds 3 --warmup 1 --cpu-sample 0"
+    timeout -s KILL 120 rocprofv3 --kernel-trace -d $O/comp/trace -o run --output-format csv -- $B > $O.log 2>&1 || die trace
+    timeout -s KILL 120 rocprofv3 --pmc VALUBusy VALUUtilization -d $O/comp/pmc1 -o run --output-format csv -- $B >> $O.log 2>&1 || die pmc1
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VMEM_RD \
+      GRBM_GUI_ACTIVE -d $O/comp/pmc2 -o run --output-format csv -- $B >> $O.log 2>&1 || die pmc2
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+      SQ_ACTIVE_INST_VALU -d $O/comp/pmc3 -o run --output-format csv -- $B >> $O.log 2>&1 || die pmc3
+    python tools/pmc_table.py k_quant_fold $O/table.json $O/comp
+    ;;
+  narrow)
+    timeout -k 10 300 $PT tests/test_gpu_parity.py -k "variants_bitwise or narrow_fold or golden or split or bf16" \
+      > $O/tests.log 2>&1; rc=$?; tail -2 $O/tests.log; [ $rc -le 1 ] || exit $rc
+    for s in "1024 65536 f32" "4096 16384 f32" "512 131072 f32" "256 262144 f32" "2048 32768 f32" "64 65536 f32" \
+             "16384 4096 f32" "1024 131072 bf16" "4096 32768 bf16" "1024 4194304 f32"; do
+      SWEEP_VARIANTS=0,2,18 timeout -k 10 120 python tools/sweep.py $s 3 5 || die "sweep $s"
+    done > $O/sweep.jsonl
+    cat $O/sweep.jsonl
+    ;;
+  narrow_tree)
+    for m in 262144 0; do
+      FJAGG_NARROW_MAX_BYTES=$m timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $O/max_$m -o run \
+        --output-format csv -- python tools/time_narrow_pytree.py > $O/max_$m.jsonl 2>&1 || die "narrow $m"
+      rm -f $O/max_$m/run_kernel_trace.csv
+      grep '^{' $O/max_$m.jsonl
+    done
+    ;;
+  *) echo "unknown study $STUDY"; exit 2 ;;
+esac
