@@ -12,11 +12,15 @@ examples/fed_avg.py:64-101 for the part this project owns:
 Client training is JAX autodiff in the reference and out of scope here: synthetic
 deltas stand in for it (no datasets are downloadable in this environment).
 
-Two equivalent paths are run each round and checked against each other:
+Three equivalent paths are run each round and checked against each other:
   A. the reference surface: mean_aggregator().apply over per-client pytrees, then the
      server step on the mean;
   B. the fused slab path: ClientDeltaSlab + fjagg_server_update_dense (one kernel for
-     mean + Adam) and the norms from the same pass.
+     mean + Adam) and the norms from the same pass;
+  C. the library algorithm's loop written literally (fedjax/algorithms/fed_avg.py:132-146:
+     tree_zeros_like, tree_add(s, tree_weight(delta, n)), tree_l2_norm(delta),
+     tree_inverse_weight) through fedjax_amd.tree_util — deferred into one fold.
+     Its mean is a running sum from zeros, which equals A's tree_mean bit for bit.
 
 usage: python examples/emnist_fed_avg_rounds.py [rounds]
 """
@@ -80,15 +84,33 @@ def run(rounds=5, clients_per_round=10, seed=0, verbose=True):
         state_b = server.fused_mean_update(slab, weights, opt, params_b, state_b, mean_out=mean_b)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
+        # C: the library FedAvg loop, literally
+        s = tree_util.tree_zeros_like(slab.client(0))
+        n_sum, norms_c = 0., []
+        for k in range(clients_per_round):
+            delta = slab.client(k)
+            s = tree_util.tree_add(s, tree_util.tree_weight(delta, weights[k]))
+            n_sum += weights[k]
+            norms_c.append(tree_util.tree_l2_norm(delta))
+        mean_c = tree_util.tree_inverse_weight(s, n_sum)
+        mean_c_flat = torch.cat([x.reshape(-1) for x in fedjax_amd.pytree.leaves_of(mean_c)])
+        norms_c = torch.stack(norms_c)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
         same_mean = torch.equal(mean_b.view(torch.int32), mean_flat.view(torch.int32))
+        same_mean_c = torch.equal(mean_c_flat.view(torch.int32), mean_flat.view(torch.int32))
+        norm_rel_c = float(((norms_a - norms_c).abs() / norms_a).max())
         same_params = torch.equal(params_a.view(torch.int32), params_b.view(torch.int32))
         norm_rel = float(((norms_a - norms_b).abs() / norms_a).max())
         history.append({"round": rnd, "same_mean": same_mean, "same_params": same_params,
-                        "norm_rel_diff": norm_rel, "ms_reference_surface": (t1 - t0) * 1e3,
-                        "ms_fused": (t2 - t1) * 1e3})
+                        "same_mean_library_loop": same_mean_c, "norm_rel_diff": norm_rel,
+                        "norm_rel_diff_library_loop": norm_rel_c, "ms_reference_surface": (t1 - t0) * 1e3,
+                        "ms_fused": (t2 - t1) * 1e3, "ms_library_loop": (t3 - t2) * 1e3})
         if verbose:
             print(f"[round {rnd}] mean bitwise={same_mean} params bitwise={same_params} "
-                  f"norm rel diff={norm_rel:.1e}  surface {1e3 * (t1 - t0):.2f} ms  fused {1e3 * (t2 - t1):.2f} ms")
+                  f"library loop mean bitwise={same_mean_c} norm rel diff={max(norm_rel, norm_rel_c):.1e}  "
+                  f"surface {1e3 * (t1 - t0):.2f} ms  fused {1e3 * (t2 - t1):.2f} ms  "
+                  f"library loop {1e3 * (t3 - t2):.2f} ms")
     return history
 
 

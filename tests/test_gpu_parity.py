@@ -689,6 +689,7 @@ def test_emnist_fed_avg_rounds_example(cuda):
     spec.loader.exec_module(mod)
     hist = mod.run(rounds=3, verbose=False)
     assert all(h["same_mean"] and h["same_params"] and h["norm_rel_diff"] < 2e-6 for h in hist), hist
+    assert all(h["same_mean_library_loop"] and h["norm_rel_diff_library_loop"] < 2e-6 for h in hist), hist
 
 
 # ------------------------------------------------- fused l2 norms on the pytree path
