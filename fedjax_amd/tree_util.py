@@ -660,11 +660,12 @@ class PendingSum:
     """
 
     __slots__ = ("_root", "_parent", "_cap", "_weight", "_n", "_bytes", "_value", "_chain", "_idx", "_ticket",
-                 "_ref", "__weakref__")
+                 "_ref", "_bcap", "__weakref__")
 
-    def __init__(self, root, parent, cap, weight, ref):
+    def __init__(self, root, parent, cap, weight, ref, bcap=None):
         self._root, self._parent, self._cap, self._weight, self._value = root, parent, cap, weight, None
         self._ref = ref  # a tree with the sum's structure (the chain's base): O(1) structure checks
+        self._bcap = bcap  # capture of the base tree when this link starts a run (parent not pending)
         self._ticket = None
         live = parent is not None and parent._value is None
         self._n = 1 + (parent._n if live else 0)
@@ -693,7 +694,7 @@ class PendingSum:
         if self._value is None:
             base, links = self._links()
             self._value = _fold_chain(base, links, None)
-            self._root = self._parent = self._cap = self._ref = None  # the deltas can go
+            self._root = self._parent = self._cap = self._ref = self._bcap = None  # the deltas can go
         return self._value
 
     __getitem__ = WeightedTree.__getitem__
@@ -718,10 +719,24 @@ def _fold_chain(base, links, scale):
     L = len(leaves0)
     caps = [n._cap for n in links]
     ptrs = np.empty((1 + len(caps), L), dtype=np.int64)
-    ptrs[0] = [x.data_ptr() for x in leaves0]
-    bad = _lib.host().table_from_caps(caps, ptrs[1:])
-    if bad >= 0:
-        raise RuntimeError(f"client {bad} of a pending tree_add sum was modified (a leaf updated in place) "
+    bcap = links[0]._bcap
+    if bcap is not None:
+        # the base as it was at the first tree_add: its captured leaves, checked unmodified
+        if len(bcap[0]) != L:
+            bad = 0
+        else:
+            leaves0 = list(bcap[0])
+            bad = _lib.host().table_from_caps([bcap] + caps, ptrs)
+    else:
+        ptrs[0] = [x.data_ptr() for x in leaves0]
+        bad = _lib.host().table_from_caps(caps, ptrs[1:])
+        bad = bad + 1 if bad >= 0 else bad
+    if bad == 0:
+        raise RuntimeError("the running sum passed to tree_add was modified (a leaf replaced or updated in "
+                           "place) before the pending sum was used; the reference adds its value at tree_add. "
+                           "Call fedjax_amd.tree_util.set_deferred_sums(False) for loops that do this")
+    if bad > 0:
+        raise RuntimeError(f"client {bad - 1} of a pending tree_add sum was modified (a leaf updated in place) "
                            "after it was added; the reference sums each delta's value at tree_add. Add "
                            "copies, or call fedjax_amd.tree_util.set_deferred_sums(False)")
     packed = _pack_weights([1] + [n._weight for n in links])
@@ -785,7 +800,10 @@ def _defer(sum_side, item, item_weight, item_cap):
     if parent is not None and parent._value is None and (
             parent._n + 1 > _DEFER["max_clients"] or parent._bytes + cap[2] > _DEFER["budget_bytes"]):
         parent.materialize()  # bound the chain: fold what is pending, continue from it
-    node = PendingSum(root, parent, cap, item_weight, ref)
+    bcap = None
+    if parent is None or parent._value is not None:  # this link starts a run: capture its base
+        bcap = _lib.host().capture(root if parent is None else parent._value, -1)
+    node = PendingSum(root, parent, cap, item_weight, ref, bcap)
     _LAST = weakref.ref(node)
     return node
 

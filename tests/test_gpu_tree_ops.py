@@ -266,6 +266,17 @@ def test_pending_sum_chain_semantics(cuda, sum_mode):
     xs[5]["a"].add_(1.0)
     with pytest.raises(RuntimeError, match="modified"):
         s.materialize()
+    # the base of the chain: a leaf replaced after tree_add keeps the value the call saw
+    # (the reference's semantics); a leaf updated in place makes the fold refuse
+    base = tu.tree_zeros_like(xs[0])
+    s = tu.tree_add(base, tu.tree_weight(xs[6], 2))
+    base["a"] = torch.ones_like(base["a"])
+    assert same(s, want([6], [2]))
+    base = tu.tree_zeros_like(xs[0])
+    s = tu.tree_add(tu.tree_add(base, tu.tree_weight(xs[6], 2)), tu.tree_weight(xs[7], 3))
+    base["b"]["c"].add_(1.0)
+    with pytest.raises(RuntimeError, match="running sum passed to tree_add was modified"):
+        tu.tree_inverse_weight(s, 5.0)
 
 
 def test_lazy_norms_of_a_deferred_sum(cuda, sum_mode):
