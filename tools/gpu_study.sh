@@ -9,6 +9,8 @@
 #   quant         k_quant_fold VALU counters                           (profiles/r02h_*)
 #   narrow        k_dense_narrow parity + variant sweep on narrow shapes (profiles/r02i_*)
 #   narrow_tree   k_ptrs_narrow vs k_ptrs on small models (FJAGG_NARROW_MAX_BYTES A/B, profiles/r02k_*)
+#   ptrs_u        k_ptrs at configs[1] with 4 / 8 / 16 clients in flight (FJAGG_PTRS_U, an experiment build
+#                 of k_ptrs not kept in the tree; profiles/r02n_ptrs_u)
 # Every GPU step runs under its own time limit; the script stops at the first failure.
 set -u
 STUDY=${1:?study name}
@@ -68,6 +70,16 @@ case "$STUDY" in
       rm -f $O/max_$m/run_kernel_trace.csv
       grep '^{' $O/max_$m.jsonl
     done
+    ;;
+  ptrs_u)
+    for u in 4 8 16; do
+      for m in views clones; do
+        FJAGG_PTRS_U=$u timeout -s KILL 90 rocprofv3 --kernel-trace -d $O/u${u}_$m -o run --output-format csv -- \
+          python tools/probe_ptrs_pmc.py $m 30 > $O/u${u}_$m.log 2>&1 || die "trace u$u $m"
+      done
+    done
+    python tools/pmc_table.py k_ptrs $O/table.json $O/u4_views $O/u4_clones $O/u8_views $O/u8_clones \
+      $O/u16_views $O/u16_clones | grep -E '"u|duration'
     ;;
   *) echo "unknown study $STUDY"; exit 2 ;;
 esac
