@@ -198,9 +198,14 @@ def main():
                          "reduce): the shape of FedJAX's server over jax.local_devices(); no launcher")
     ap.add_argument("--with-norms", action="store_true",
                     help="fuse every client's delta l2 norm into the fold (examples/fed_avg.py:79-81)")
+    ap.add_argument("--reference-bf16", action="store_true",
+                    help="bf16 workloads: the reference's bf16 arithmetic (every product and sum rounded to bf16, "
+                         "tree_util.set_bf16_semantics('reference')) instead of the f32 fold")
     args = ap.parse_args()
     if args.single_process:
         return single_process(args)
+    if args.reference_bf16 and (WORKLOADS[args.workload][2] != torch.bfloat16 or args.gpus > 1 or args.with_norms):
+        raise SystemExit("--reference-bf16 runs a bf16 workload (c5s) at N=1 without fused norms")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # bare `python bench.py --gpus N`: one rank per GPU as child processes (no GPU
         # call has happened in this process, and nothing is exec'd)
@@ -278,7 +283,8 @@ def main():
             kernels.weighted_sum_l2_dense(xs, wd, scale=scale, out=o, l2sq=l2sq, nontemporal=nt,
                                           workspace=l2ws)
         else:
-            kernels.weighted_sum_dense(xs, wd, scale=scale, out=o, nontemporal=nt, variant=args.variant)
+            kernels.weighted_sum_dense(xs, wd, scale=scale, out=o, nontemporal=nt, variant=args.variant,
+                                       reference_bf16=args.reference_bf16)
         if events is not None:
             e1.record(stream)
             events.append((e0, e1, xs.shape[0] * xs.shape[1] * esize))
@@ -447,6 +453,8 @@ def main():
                        "exchange_autotune_ms": {k: round(t, 4) for k, t in tune.items()} or None,
                        "nontemporal": nt,
                        "variant": args.variant, "fused_l2_norms": bool(args.with_norms),
+                       "bf16_arithmetic": ("reference (every op rounded to bf16)" if args.reference_bf16 else
+                                           "f32 fold, one rounding") if dtype == torch.bfloat16 else None,
                        "fused_server_step": args.server},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4),

@@ -31,7 +31,7 @@ F32, BF16, I32 = 0, 1, 2
 SCALE, ACCUMULATE, NONTEMPORAL, UNALIGNED, UNBALANCED, NARROW = 1, 2, 4, 8, 16, 32
 # enum fjagg_mode
 MODE_EXACT, MODE_SPLIT = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 COMP_ABI_VERSION = 1
 COMM_ABI_VERSION = 1
 COMM_ID_BYTES = 128

@@ -71,19 +71,6 @@ template <> struct Elem<FJAGG_I32> { static constexpr int B = 4; };
 
 template <int IN> constexpr int vec_width() { return 16 / Elem<IN>::B; }
 
-struct AccF {
-  using T = float;
-  static constexpr int DT = FJAGG_F32;
-  static __device__ __forceinline__ T mul(T x, T w) { return __fmul_rn(x, w); }
-  static __device__ __forceinline__ T add(T a, T b) { return __fadd_rn(a, b); }
-};
-struct AccI {  // XLA int32 arithmetic wraps
-  using T = int;
-  static constexpr int DT = FJAGG_I32;
-  static __device__ __forceinline__ T mul(T x, T w) { return (int)((unsigned)x * (unsigned)w); }
-  static __device__ __forceinline__ T add(T a, T b) { return (int)((unsigned)a + (unsigned)b); }
-};
-
 __device__ __forceinline__ float bf16_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 __device__ __forceinline__ unsigned f32_to_bf16(float f) {  // RNE, NaN stays NaN
@@ -92,6 +79,42 @@ __device__ __forceinline__ unsigned f32_to_bf16(float f) {  // RNE, NaN stays Na
   u += 0x7fffu + ((u >> 16) & 1u);
   return u >> 16;
 }
+
+// Fold arithmetic policies: T is the fold state, weight() maps a weight as stored in
+// w_dev (and the final scale) to the value the fold multiplies by.
+struct AccF {
+  using T = float;
+  static constexpr int DT = FJAGG_F32;
+  static __device__ __forceinline__ T weight(T w) { return w; }
+  static __device__ __forceinline__ T mul(T x, T w) { return __fmul_rn(x, w); }
+  static __device__ __forceinline__ T add(T a, T b) { return __fadd_rn(a, b); }
+};
+struct AccI {  // XLA int32 arithmetic wraps
+  using T = int;
+  static constexpr int DT = FJAGG_I32;
+  static __device__ __forceinline__ T weight(T w) { return w; }
+  static __device__ __forceinline__ T mul(T x, T w) { return (int)((unsigned)x * (unsigned)w); }
+  static __device__ __forceinline__ T add(T a, T b) { return (int)((unsigned)a + (unsigned)b); }
+};
+// The reference's bfloat16 arithmetic (jnp on bf16 leaves, tree_util.py:32,50,60, weights
+// weakly typed): the weight and the scale become bf16, every product and every sum is
+// rounded to bf16. Each op runs in f32 and is rounded once to bf16 (RNE): the product of
+// two bf16 values is exact in f32, and for sums f32's 24 bits >= 2*8 + 2 make the double
+// rounding innocuous (Figueroa), so every op is the correctly rounded bf16 op. Values
+// stay bf16-representable floats; NaNs that reach rnd() come from bf16 data or from the
+// hardware's default NaN (low 16 bits zero), so the NaN-preserving branch is not needed
+// there — weight() keeps it for caller-supplied weights.
+struct AccB {
+  using T = float;
+  static constexpr int DT = FJAGG_BF16;
+  static __device__ __forceinline__ T rnd(T f) {
+    const unsigned u = __float_as_uint(f);
+    return __uint_as_float((u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u);
+  }
+  static __device__ __forceinline__ T weight(T w) { return __uint_as_float(f32_to_bf16(w) << 16); }
+  static __device__ __forceinline__ T mul(T x, T w) { return rnd(__fmul_rn(x, w)); }
+  static __device__ __forceinline__ T add(T a, T b) { return rnd(__fadd_rn(a, b)); }
+};
 
 // A "unit" is what one lane loads per client: 16 bytes (V = vec_width) or one
 // element (V = 1).
@@ -172,6 +195,8 @@ __device__ __forceinline__ unsigned finish(typename ACC::T s, bool do_scale, flo
     float f = do_scale ? __fmul_rn(s, scale) : s;
     if constexpr (OUT == FJAGG_BF16) return f32_to_bf16(f);
     else return __float_as_uint(f);
+  } else if constexpr (ACC::DT == FJAGG_BF16) {  // out is bf16: fl_bf16(s * bf16(scale))
+    return f32_to_bf16(do_scale ? ACC::mul(s, ACC::weight(scale)) : s);
   } else {
     if constexpr (OUT == FJAGG_I32) return (unsigned)s;  // scale rejected on the host
     else return __float_as_uint(do_scale ? __fmul_rn((float)s, scale) : (float)s);
@@ -181,7 +206,7 @@ __device__ __forceinline__ unsigned finish(typename ACC::T s, bool do_scale, flo
 // output element bits -> fold state (FJAGG_ACCUMULATE)
 template <int OUT, class ACC>
 __device__ __forceinline__ typename ACC::T init_from(unsigned bits) {
-  if constexpr (ACC::DT == FJAGG_F32) {
+  if constexpr (ACC::DT != FJAGG_I32) {
     if constexpr (OUT == FJAGG_BF16) return __uint_as_float(bits << 16);
     else return __uint_as_float(bits);
   } else {
@@ -324,7 +349,7 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
     Raw v[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) v[j] = load_unit<IN, V, NT>(r, off[j]);
-    const T w0 = w[0];
+    const T w0 = ACC::weight(w[0]);
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       T t[V];
@@ -372,7 +397,7 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
     if constexpr (BURST) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const T wk = w[k + u];
+      const T wk = ACC::weight(w[k + u]);
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         T t[V];
@@ -386,7 +411,7 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
   }
   for (; k < K; ++k) {
     const auto r = row_rsrc(row(k), row_bytes);
-    const T wk = w[k];
+    const T wk = ACC::weight(w[k]);
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       T t[V];
@@ -823,7 +848,7 @@ __device__ __forceinline__ void narrow_fold(Rows rows, int64_t K, int64_t ncols,
     }
     if (threadIdx.x < kNarrowTile) {
       const int64_t k = k0 + threadIdx.x;
-      wr = w[k < K ? k : K - 1];
+      wr = ACC::weight(w[k < K ? k : K - 1]);
     }
   };
   auto store = [&](int64_t t) {  // registers -> LDS buffer t & 1
@@ -1061,7 +1086,8 @@ bool combo_ok(int in, int acc, int out) {
   static const Combo ok[] = {{FJAGG_F32, FJAGG_F32, FJAGG_F32},  {FJAGG_F32, FJAGG_F32, FJAGG_BF16},
                              {FJAGG_BF16, FJAGG_F32, FJAGG_BF16},
                              {FJAGG_BF16, FJAGG_F32, FJAGG_F32}, {FJAGG_I32, FJAGG_F32, FJAGG_F32},
-                             {FJAGG_I32, FJAGG_I32, FJAGG_I32},  {FJAGG_I32, FJAGG_I32, FJAGG_F32}};
+                             {FJAGG_I32, FJAGG_I32, FJAGG_I32},  {FJAGG_I32, FJAGG_I32, FJAGG_F32},
+                             {FJAGG_BF16, FJAGG_BF16, FJAGG_BF16}};
   for (const Combo& c : ok)
     if (c.in == in && c.acc == acc && c.out == out) return true;
   return false;
@@ -1175,6 +1201,22 @@ int launch_dense_v(int variant, const DenseArgs& a, int64_t gy, hipStream_t s) {
   if constexpr (V == 1) {  // element-granular path (tails, unaligned rows): one shape
     launch_dense_t<IN, ACC, OUT, 1, 1, 8, NT, 0>(a, gy, s);
     return check_launch("k_dense");
+  } else if constexpr (ACC::DT == FJAGG_BF16) {  // the shapes pick_variant chooses
+    switch (variant) {
+      case 2: launch_dense_t<IN, ACC, OUT, V, 1, 8, NT, 0>(a, gy, s); break;
+      case 5: launch_dense_t<IN, ACC, OUT, V, 4, 4, NT, 0>(a, gy, s); break;
+      case 12: {
+        const int64_t ntiles = (a.nunits + (int64_t)kThreads * 8 - 1) / ((int64_t)kThreads * 8);
+        const int cus = residency(reinterpret_cast<const void*>(k_dense<IN, ACC, OUT, V, 8, 4, NT, 0>)).cus;
+        if (!a.balanced || ntiles * gy >= 2 * (int64_t)cus)
+          launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0>(a, gy, s);
+        else
+          launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0, true>(a, gy, s);
+        break;
+      }
+      default: return fail(FJAGG_EUNSUPPORTED, "variant %d is not built for the bf16 reference fold", variant);
+    }
+    return check_launch("k_dense");
   } else {
     switch (variant) {
       case 1: launch_dense_t<IN, ACC, OUT, V, 2, 8, NT, 0>(a, gy, s); break;
@@ -1234,6 +1276,7 @@ int launch_dense_dispatch(int in, int acc, int out, bool vec, bool nt, int varia
   FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
   FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
   FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
+  FJ_CASE(FJAGG_BF16, FJAGG_BF16, FJAGG_BF16, AccB)
 #undef FJ_CASE
   return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination (%d,%d,%d)", in, acc, out);
 }
@@ -1256,7 +1299,8 @@ int validate_common(int in, int acc, int out, int64_t K, int flags, float scale)
   if (acc == FJAGG_I32 && out == FJAGG_I32 && (flags & FJAGG_SCALE))
     return fail(FJAGG_EINVAL, "FJAGG_SCALE needs a float output");
   if ((flags & FJAGG_ACCUMULATE) && !((acc == FJAGG_F32 && out != FJAGG_I32) ||
-                                      (acc == FJAGG_I32 && out == FJAGG_I32)))
+                                      (acc == FJAGG_I32 && out == FJAGG_I32) ||
+                                      (acc == FJAGG_BF16 && out == FJAGG_BF16)))
     return fail(FJAGG_EINVAL, "FJAGG_ACCUMULATE needs the output in the fold's type");
   (void)scale;
   return FJAGG_OK;
@@ -1297,6 +1341,7 @@ int launch_narrow(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, 
   FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
   FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
   FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
+  FJ_CASE(FJAGG_BF16, FJAGG_BF16, FJAGG_BF16, AccB)
 #undef FJ_CASE
   return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination (%d,%d,%d)", in, acc, out);
 }
@@ -1514,6 +1559,8 @@ int fjagg_wsum_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_d
     return dense_exact_chunked(in_dtype, acc_dtype, out_dtype, x, ld * ib, K, P, w_dev, scale, y,
                                flags, s, K, 1, 0);
   if (mode != FJAGG_MODE_SPLIT) return fail(FJAGG_EINVAL, "unknown mode %d", mode);
+  if (acc_dtype == FJAGG_BF16)
+    return fail(FJAGG_EUNSUPPORTED, "split mode reorders the fold; the bf16 reference fold runs in exact mode");
   const int64_t S = split_count(K, P);
   if (S <= 1)  // nothing to split: the exact path already fills the chip
     return dense_exact_chunked(in_dtype, acc_dtype, out_dtype, x, ld * ib, K, P, w_dev, scale, y,
@@ -1652,6 +1699,7 @@ int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* im
     FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
     FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
     FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
+    FJ_CASE(FJAGG_BF16, FJAGG_BF16, FJAGG_BF16, AccB)
 #undef FJ_CASE
     return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination");
   }
@@ -1664,6 +1712,7 @@ int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* im
   FJ_CASE(FJAGG_I32, FJAGG_F32, FJAGG_F32, AccF)
   FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_I32, AccI)
   FJ_CASE(FJAGG_I32, FJAGG_I32, FJAGG_F32, AccI)
+  FJ_CASE(FJAGG_BF16, FJAGG_BF16, FJAGG_BF16, AccB)
 #undef FJ_CASE
   return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination");
 }

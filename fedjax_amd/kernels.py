@@ -75,13 +75,16 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
                        out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None,
                        accumulate: bool = False, mode: str = "exact",
                        workspace: Optional[torch.Tensor] = None, nontemporal: bool = False,
-                       variant: int = 0, balanced: bool = True) -> torch.Tensor:
+                       variant: int = 0, balanced: bool = True, reference_bf16: bool = False) -> torch.Tensor:
     """Fold a client-major slab ``x[K, P]`` (row stride ``x.stride(0)``, unit column
     stride) with per-client weights ``w[K]`` into ``out[P]``.
 
     ``w`` is float32 (float fold) or int32 (integer fold; int32 ``x`` only).
     ``scale`` multiplies the fold at the end (tree_mean's f32(1/W)).
     ``accumulate`` starts the fold from ``out``'s current contents.
+    ``reference_bf16`` (bfloat16 ``x`` and ``out``, float32 ``w``): the reference's
+    bfloat16 arithmetic — weights and scale rounded to bf16, every product and sum
+    rounded to bf16 (acc dtype FJAGG_BF16) — instead of a float32 fold.
     """
     if x.dim() != 2 or x.stride(1) != 1:
         raise ValueError("x must be a [K, P] tensor with unit column stride")
@@ -91,9 +94,15 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
     acc = _lib.I32 if w.dtype == torch.int32 else _lib.F32
     if w.dtype not in (torch.float32, torch.int32) or not w.is_contiguous():
         raise TypeError("w must be a contiguous float32 or int32 tensor")
+    if reference_bf16:
+        if x.dtype != torch.bfloat16 or w.dtype != torch.float32:
+            raise TypeError("reference_bf16 folds bfloat16 deltas with float32 weights")
+        acc = _lib.BF16
     if out is None:
         if out_dtype is None:
-            if acc == _lib.F32:  # int32 leaves * float weights promote to float32
+            if acc == _lib.BF16:
+                out_dtype = torch.bfloat16
+            elif acc == _lib.F32:  # int32 leaves * float weights promote to float32
                 out_dtype = torch.float32 if x.dtype == torch.int32 else x.dtype
             else:
                 out_dtype = torch.float32 if scale is not None else torch.int32

@@ -83,13 +83,19 @@ class ClientDeltaSlab:
 
     def weighted_sum_flat(self, w_dev: torch.Tensor, *, scale=None, out: Optional[torch.Tensor] = None,
                           accumulate: bool = False, mode: str = "exact",
-                          nontemporal: Optional[bool] = None, variant: int = 0) -> torch.Tensor:
-        """Flat P-element fold of the slab with device weights (one launch)."""
+                          nontemporal: Optional[bool] = None, variant: int = 0,
+                          reference_bf16: Optional[bool] = None) -> torch.Tensor:
+        """Flat P-element fold of the slab with device weights (one launch). A bfloat16
+        slab folds with the reference's bf16 arithmetic when ``reference_bf16`` (default:
+        ``tree_util.set_bf16_semantics("reference")`` is in force and mode is exact)."""
         nbytes = self.rows.numel() * self.rows.element_size()
         nt = nbytes >= tree_util.NONTEMPORAL_MIN_BYTES if nontemporal is None else nontemporal
+        if reference_bf16 is None:
+            reference_bf16 = (self.dtype == torch.bfloat16 and mode == "exact"
+                              and tree_util.bf16_semantics() == "reference")
         return kernels.weighted_sum_dense(
             self.rows, w_dev, scale=None if scale is None else float(np.float32(scale)), out=out,
-            accumulate=accumulate, mode=mode, nontemporal=nt, variant=variant)
+            accumulate=accumulate, mode=mode, nontemporal=nt, variant=variant, reference_bf16=reference_bf16)
 
     def mean(self, weights: Sequence, *, out: Optional[torch.Tensor] = None, mode: str = "exact",
              with_norms: bool = False):
@@ -103,6 +109,12 @@ class ClientDeltaSlab:
         for x in weights:
             W += tree_util._host_weight(x)
         scale = tree_util._inverse(W)
+        if with_norms and self.dtype == torch.bfloat16 and tree_util.bf16_semantics() == "reference":
+            # no fused-norm kernel for the bf16 reference fold: the mean, then the norms
+            if mode != "exact":
+                raise ValueError("fused norms run in exact mode")
+            flat = self.weighted_sum_flat(self.weight_vector(weights), scale=scale, out=out)
+            return self.unflatten(flat), self.l2_norms()
         if with_norms:
             if mode != "exact":
                 raise ValueError("fused norms run in exact mode")

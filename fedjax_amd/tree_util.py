@@ -18,8 +18,9 @@ Semantics follow the reference under JAX's defaults (x64 disabled):
 * Python numbers are weakly typed (take the leaf's dtype), int64/float64 leaves
   canonicalise to int32/float32, int32 leaves with Python-int weights fold in
   wrapping int32 and become float32 only at the final ``1/W`` scale;
-* bfloat16 leaves are folded in float32 and rounded once (the reference rounds
-  every op to bfloat16; DESIGN.md §4 states the bound against an f64 oracle).
+* bfloat16 leaves are folded in float32 and rounded once (DESIGN.md §4 states the
+  bound against an f64 oracle); ``set_bf16_semantics("reference")`` instead rounds
+  every product and sum to bfloat16 as the reference's jnp ops do, bit for bit.
 """
 
 from __future__ import annotations
@@ -40,6 +41,7 @@ __all__ = [
     "tree_weight", "tree_inverse_weight", "tree_zeros_like", "tree_add", "tree_sum",
     "tree_mean", "tree_size", "tree_l2_squared", "tree_l2_norm", "tree_clip_by_global_norm",
     "tree_l2_norms", "tree_mean_with_l2_norms", "WeightedTree", "PendingSum", "set_deferred_sums",
+    "set_bf16_semantics", "bf16_semantics",
 ]
 
 # Non-temporal loads pay off once the deltas cannot stay in the 256 MiB Infinity
@@ -160,13 +162,39 @@ def _inverse(W):
 
 
 # ----------------------------------------------------------------------- fold engine
+_BF16 = {"mode": "f32"}
+
+
+def set_bf16_semantics(mode: str) -> None:
+    """How folds over bfloat16 leaves round (tree_mean, tree_sum, tree_add, tree_weight,
+    tree_inverse_weight, RunningMean, ClientDeltaSlab.mean).
+
+    ``"f32"`` (default): accumulate in float32 and round once to bfloat16 — far more
+    accurate than the reference, within the bound of DESIGN.md §4 of the exact value.
+    ``"reference"``: the reference's arithmetic bit for bit — jnp on bf16 leaves with
+    weakly typed weights (tree_util.py:32,50,60): each weight and ``1/W`` become bf16 and
+    every product and every sum is rounded to bf16 (fjagg acc dtype FJAGG_BF16).
+    A strongly typed float32 weight promotes the fold to float32 in both modes, as in
+    the reference."""
+    if mode not in ("f32", "reference"):
+        raise ValueError(f"bf16 semantics must be 'f32' or 'reference', got {mode!r}")
+    _BF16["mode"] = mode
+
+
+def bf16_semantics() -> str:
+    """The current :func:`set_bf16_semantics` mode."""
+    return _BF16["mode"]
+
+
 def _leaf_rule(dt: torch.dtype, kinds: Sequence[int], scaled_kind: Optional[int]):
     """(in_code, acc_code, out_dtype) of one leaf position under JAX promotion."""
     strong_float = any(k == _STRONG_FLOAT for k in kinds) or scaled_kind == _STRONG_FLOAT
     if dt == torch.float32:
         return _lib.F32, _lib.F32, torch.float32
     if dt == torch.bfloat16:
-        return _lib.BF16, _lib.F32, (torch.float32 if strong_float else torch.bfloat16)
+        if strong_float:
+            return _lib.BF16, _lib.F32, torch.float32
+        return _lib.BF16, (_lib.BF16 if _BF16["mode"] == "reference" else _lib.F32), torch.bfloat16
     # int32 leaves: int * int folds in int32; int * float promotes to float32
     if all(k in (_WEAK_INT, _STRONG_INT) for k in kinds):
         return _lib.I32, _lib.I32, (torch.int32 if scaled_kind is None else torch.float32)
@@ -226,6 +254,7 @@ def _fold(rows, weights, *, scale=None,
 
     if l2sq is not None:
         if len(groups) != 1 or next(iter(groups))[1] != _lib.F32 or next(iter(groups))[0] == _lib.I32:
+            # (a bf16 reference fold has no fused-norm kernel: callers take two passes)
             raise TypeError("fused l2 norms need float leaves of one dtype and a float fold")
         if l2sq.dtype != torch.float32 or l2sq.numel() != K or l2sq.device != device:
             raise ValueError(f"l2sq must be a float32 [{K}] tensor on {device}")
@@ -248,8 +277,8 @@ def _fold(rows, weights, *, scale=None,
         else:
             blocks, unaligned = _leaf_plan(in_c, leaf_n, in_ptrs, out_ptrs, device)
         if packed is not None:
-            w_host = packed.f32 if acc_c == _lib.F32 else packed.i32
-        elif acc_c == _lib.F32:
+            w_host = packed.i32 if acc_c == _lib.I32 else packed.f32
+        elif acc_c != _lib.I32:  # F32, or BF16 (the kernel rounds each f32 weight to bf16)
             w_host = np.array([np.float32(w) for w in weights], dtype=np.float32)
         else:
             w_host = np.array([np.int64(w) for w in weights], dtype=np.int64).astype(np.int32)
@@ -1030,6 +1059,9 @@ def tree_mean_with_l2_norms(pytrees_and_weights: Iterable[Tuple[PyTree, float]])
     if not rows[0]:
         return pytree.unflatten(td, []), torch.zeros(len(trees), dtype=torch.float32, device=_default_device())
     float_one = len({x.dtype for x in rows[0]}) == 1 and rows[0][0].dtype in (torch.float32, torch.bfloat16)
+    if float_one and rows[0][0].dtype == torch.bfloat16:
+        kinds = weights.kinds if isinstance(weights, _Weights) else [_weight_kind(w) for w in weights]
+        float_one = _leaf_rule(torch.bfloat16, kinds, _WEAK_FLOAT)[1] == _lib.F32
     if len(trees) > _L2_MAX_CLIENTS or not float_one:
         # the fused pass keeps K partial norms per workgroup in LDS (K <= 4096) and sums one
         # float dtype: otherwise the mean and the norms take one pass each

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define FJAGG_ABI_VERSION 1
+#define FJAGG_ABI_VERSION 2
 
 /* element types */
 enum fjagg_dtype {
@@ -91,12 +91,16 @@ int fjagg_abi_version(void);
 
 /*
  * Dense client-major slab: client k's delta is x_dev + k*ld elements, P
- * contiguous elements each. acc_dtype is FJAGG_F32 (w_dev is float[K]) or
- * FJAGG_I32 (integer fold, w_dev is int32[K]). Supported (in, acc, out):
+ * contiguous elements each. acc_dtype is FJAGG_F32 (w_dev is float[K]),
+ * FJAGG_I32 (integer fold, w_dev is int32[K]) or FJAGG_BF16 (the reference's bfloat16
+ * arithmetic, w_dev is float[K]: each weight and the scale are rounded to bf16, every
+ * product and sum is rounded to bf16 — jnp on bf16 leaves with weakly typed weights,
+ * tree_util.py:32,50,60). Supported (in, acc, out):
  *   (F32,F32,F32) (F32,F32,BF16) (BF16,F32,BF16) (BF16,F32,F32) (I32,F32,F32) (I32,I32,I32)
- *   (I32,I32,F32); the pytree path supports the same set except (F32,F32,BF16).
+ *   (I32,I32,F32) (BF16,BF16,BF16); the pytree path supports the same set except
+ *   (F32,F32,BF16).
  * mode FJAGG_MODE_SPLIT needs ws_dev of fjagg_split_workspace_bytes(K, P) bytes
- * (ws may be NULL in exact mode).
+ * (ws may be NULL in exact mode); acc FJAGG_BF16 runs in exact mode only.
  * Replaces: the per-client loop of tree_mean, fedjax/core/tree_util.py:85-96.
  */
 int fjagg_wsum_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_dev,

@@ -173,6 +173,27 @@ def _place(c, dev):
     return out
 
 
+def _rnd_bf16(a):
+    return _bf16_f32(_bf16_bits(a))
+
+
+def _bf16_ref_fold(np_trees, ws, scale, zero_init=False):
+    """The reference's bf16 sequence: t_k = bf16(x_k * bf16(f32(w_k))), s_0 = t_0 (or
+    bf16(0 + t_0) for the running sum from tree_zeros_like), s_k = bf16(s + t_k),
+    y = bf16(s * bf16(f32(scale))); bfloat16 bits out."""
+    per = [ref.flatten(t)[0] for t in np_trees]
+    out = []
+    for l in range(len(per[0])):
+        s = np.zeros(per[0][l].shape, np.float32) if zero_init else None
+        for k, w in enumerate(ws):
+            t = _rnd_bf16(per[k][l].astype(np.float32) * _rnd_bf16(np.float32(w)))
+            s = t if s is None else _rnd_bf16(s + t)
+        if scale is not None:
+            s = _rnd_bf16(s * _rnd_bf16(np.float32(scale)))
+        out.append(_bf16_bits(s))
+    return ref.unflatten(ref.flatten(np_trees[0])[1], out)
+
+
 def _np_leaves(t):
     def host(x):
         if isinstance(x, torch.Tensor):
@@ -223,11 +244,11 @@ def test_random_case_matches_oracle(cuda, seed, monkeypatch):
     np_trees = [_realize(c["struct"], leaves) for leaves in c["host"]]
     ws, K = c["ws"], c["K"]
     bf16 = c["dtype"] == "bf16"
+    strong = any(isinstance(w, np.generic) for w in ws)
     if bf16:
         W = 0.0
         for w in ws:
             W += w  # tree_util.py:95
-        strong = any(isinstance(w, np.generic) for w in ws)
         want = _bf16_fold(np_trees, ws, (1.0 / W) if W > 0.0 else 0.0, out_bf16=not strong)
         want_sum = _bf16_fold(np_trees, [1] * K, None, out_bf16=True)
     else:
@@ -242,6 +263,21 @@ def test_random_case_matches_oracle(cuda, seed, monkeypatch):
     got, _ = agg.apply(((f"c{k}", t, w) for k, (t, w) in enumerate(zip(trees, ws))), agg.init())
     _same(got, want, "mean_aggregator().apply")
     _same(tu.tree_sum(trees), want_sum, "tree_sum")
+    if bf16 and not strong:
+        # the reference's own bf16 arithmetic (set_bf16_semantics("reference")): every weight,
+        # 1/W, product and sum rounded to bf16 (tests/test_gpu_bf16_reference.py restates it)
+        tu.set_bf16_semantics("reference")
+        try:
+            _same(tu.tree_mean(list(zip(trees, ws))),
+                  _bf16_ref_fold(np_trees, ws, (1.0 / W) if W > 0.0 else 0.0), "tree_mean (bf16 reference)")
+            _same(tu.tree_sum(trees), _bf16_ref_fold(np_trees, [1] * K, None), "tree_sum (bf16 reference)")
+            s = tu.tree_zeros_like(trees[0])
+            for t, w in zip(trees, ws):
+                s = tu.tree_add(s, tu.tree_weight(t, w))
+            _same(tu.tree_inverse_weight(s, W), _bf16_ref_fold(np_trees, ws, (1.0 / W) if W > 0.0 else 0.0,
+                                                                zero_init=True), "library loop (bf16 reference)")
+        finally:
+            tu.set_bf16_semantics("f32")
     if c["dtype"] != np.int32 and c["placement"] != "host" and any(int(np.prod(s)) for s in c["shapes"]):
         # one pass: the mean and every client's l2 norm
         mean, norms = tu.tree_mean_with_l2_norms(list(zip(trees, ws)))

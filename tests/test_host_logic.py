@@ -172,3 +172,23 @@ def test_server_descriptor_constants_follow_jax_weak_typing():
     s = server.sgd(0.1, momentum=0.9, nesterov=True)
     assert s.kind == _lib.OPT_MOMENTUM and s.descriptor(1).nesterov == 1
     assert server.sgd(1.0).kind == _lib.OPT_SGD
+
+
+def test_bf16_semantics_switch_and_leaf_rule():
+    """set_bf16_semantics("reference") selects the bf16 fold (acc FJAGG_BF16) for bf16
+    leaves with weakly typed weights only; strongly typed float32 weights promote to f32."""
+    from fedjax_amd import tree_util as tu
+    assert tu.bf16_semantics() == "f32"
+    W, S = tu._WEAK_INT, tu._STRONG_FLOAT
+    assert tu._leaf_rule(torch.bfloat16, [W], None) == (_lib.BF16, _lib.F32, torch.bfloat16)
+    tu.set_bf16_semantics("reference")
+    try:
+        assert tu._leaf_rule(torch.bfloat16, [W, tu._WEAK_FLOAT], tu._WEAK_FLOAT) == (_lib.BF16, _lib.BF16,
+                                                                                       torch.bfloat16)
+        assert tu._leaf_rule(torch.bfloat16, [S], None) == (_lib.BF16, _lib.F32, torch.float32)
+        assert tu._leaf_rule(torch.float32, [W], None) == (_lib.F32, _lib.F32, torch.float32)
+        assert tu._leaf_rule(torch.int32, [W], None) == (_lib.I32, _lib.I32, torch.int32)
+    finally:
+        tu.set_bf16_semantics("f32")
+    with pytest.raises(ValueError):
+        tu.set_bf16_semantics("bf16")
