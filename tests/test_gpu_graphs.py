@@ -1,0 +1,75 @@
+"""HIP graph capture of the launches whose arguments live on the device or in the kernel
+arguments (no allocation or synchronisation inside the library).
+
+A server that runs the same round shape every round can capture the aggregation once
+and replay it (torch.cuda.CUDAGraph = hipGraph on ROCm): the dense slab fold (weights on
+the device) and the per-call tree ops (fjtree: the leaf table is in the kernel arguments)
+are capturable. The pytree fold of tree_mean uploads a fresh plan image from pinned host
+memory per call, so it is not (replaying it would read a freed staging buffer).
+Replays must give the eager launch's bits on the new contents of the same buffers.
+"""
+import numpy as np
+import pytest
+import torch
+
+from fedjax_amd import kernels, pytree, tree_util as tu
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dense_fold_replays_bitwise(cuda):
+    K, P = 64, 100_003
+    x = torch.empty(K, P + 1, device=cuda)[:, :P]
+    w = torch.tensor(np.float32(np.random.RandomState(0).randint(1, 501, size=K)), device=cuda)
+    out = torch.empty(P, device=cuda)
+    scale = float(np.float32(1.0 / float(w.double().sum())))
+    kernels.fill_synth(x, seed=1)
+    kernels.weighted_sum_dense(x, w, scale=scale, out=out)  # warm-up outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            kernels.weighted_sum_dense(x, w, scale=scale, out=out)
+    for seed in (2, 3):
+        kernels.fill_synth(x, seed=seed)
+        g.replay()
+        torch.cuda.synchronize()
+        want = kernels.weighted_sum_dense(x, w, scale=scale)
+        assert torch.equal(out.view(torch.int32), want.view(torch.int32))
+
+
+def test_per_call_tree_ops_replay_bitwise(cuda):
+    """tree_add(a, tree_weight(b, 3)) and tree_l2_norm(b) in eager mode (one fjtree launch
+    each) captured once, replayed on new contents of a and b."""
+    tu.set_deferred_sums(False)
+    try:
+        g0 = torch.Generator(device=cuda).manual_seed(0)
+        a = {"u": torch.rand(5000, device=cuda, generator=g0), "v": torch.rand(33, 9, device=cuda, generator=g0)}
+        b = {"u": torch.rand(5000, device=cuda, generator=g0), "v": torch.rand(33, 9, device=cuda, generator=g0)}
+        tu.tree_add(a, tu.tree_weight(b, 3))  # warm-up: workspaces, plans
+        tu.tree_l2_norm(b)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            tu.tree_add(a, tu.tree_weight(b, 3))  # this stream's norm workspace exists before capture
+            tu.tree_l2_norm(b)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=st):
+                out = tu.tree_add(a, tu.tree_weight(b, 3))
+                nrm = tu.tree_l2_norm(b)
+        for k in range(2):
+            with torch.no_grad():
+                for t in (a, b):
+                    for leaf in pytree.leaves_of(t):
+                        leaf.copy_(torch.rand(leaf.shape, device=cuda, generator=g0))
+            g.replay()
+            torch.cuda.synchronize()
+            want = tu.tree_add(a, tu.tree_weight(b, 3))
+            want_n = tu.tree_l2_norm(b)
+            for x, y in zip(pytree.leaves_of(out), pytree.leaves_of(want)):
+                assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+            assert torch.equal(nrm.view(torch.int32), want_n.view(torch.int32))
+    finally:
+        tu.set_deferred_sums(True)
