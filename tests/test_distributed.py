@@ -144,3 +144,31 @@ def test_sharded_tree_mean_without_clients_world3_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == {0: True, 1: True, 2: True}
+
+
+@pytest.mark.parametrize("world", [1, 4, 8])
+def test_sharded_mean_1_to_8_ranks_gloo(world, coracle):
+    """The analogue of for_each_client_test.py:388-438 (the pmap backend on 1..8 simulated
+    devices against the single-device result): 1, 4 and 8 gloo ranks on the CPU. One rank
+    is bitwise the single fold; G ranks stay within the G-partial bound of DESIGN.md §4."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, True, 2, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (y, W2)) for r, y, W2 in (q.get(timeout=180) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
+    x = ref.synth(K, P, seed=9)
+    r = ref.mean_scale(weights)
+    want = ref.wsum_dense(x, np.float32(weights), scale=r)
+    if world == 1:
+        assert np.array_equal(res[0][0].view(np.uint32), want.astype(np.float32).view(np.uint32))
+    bound = coracle.bound_f32(x, np.float32(weights), r, want) * (K + world + 2) / (K + 2)
+    for rank in range(world):  # all_ranks: every rank holds the mean, the same bits on each
+        assert np.all(np.abs(res[rank][0].astype(np.float64) - want) <= bound), rank
+        assert np.array_equal(res[rank][0], res[0][0])
+        assert res[rank][1] == float(sum(weights))
