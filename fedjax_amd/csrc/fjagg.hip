@@ -789,15 +789,17 @@ struct SlabRows {
   __device__ __forceinline__ const uint8_t* row(int, int64_t k, int64_t) const { return base + k * ld_bytes; }
 };
 
-// Client rows of the pytree plan: pointers from the K x L table, staged through LDS one
-// tile ahead of the data loads that use them (a per-row scalar load from the table would
-// put one more memory round trip in front of every tile's loads).
+// Client rows of the pytree plan: pointers from the K x L table, staged through LDS
+// (kRowSlots tiles of pointers; a per-row scalar load from the table would put one more
+// memory round trip in front of every tile's loads). fetch() reads one tile's pointers
+// into a register three tiles ahead of their use, commit() writes them to their slot.
+constexpr int kRowSlots = 4;
 template <int TILE>
 struct TableRows {
   const int64_t* in_ptrs;
   int L, leaf;
   int64_t eoff;           // the stripe's first element, in bytes
-  unsigned long long* lds;  // [2][TILE] row pointers
+  unsigned long long* lds;  // [kRowSlots][TILE] row pointers
   unsigned long long pr;    // this thread's fetched pointer (threads < TILE)
   __device__ __forceinline__ void fetch(int64_t k0, int64_t K) {
     if (threadIdx.x < TILE) {
@@ -814,6 +816,10 @@ struct TableRows {
   }
 };
 
+// Pipeline per workgroup (t = tile of kNarrowTile clients): while wave 0 folds tile t from
+// LDS buffer t&1, the loads of tile t+1 (register set A) and tile t+2 (set B) are in
+// flight; then tile t+1 goes to LDS buffer (t+1)&1. Two tiles in flight per workgroup:
+// with one, each step waited out a full memory round trip for ~32 KiB (profiles/r02i_*).
 template <int IN, class ACC, int OUT, bool NT, int kNarrowTile, class Rows>
 __device__ __forceinline__ void narrow_fold(Rows rows, int64_t K, int64_t ncols,
                                             const typename ACC::T* __restrict__ w, float scale, int do_scale,
@@ -829,15 +835,15 @@ __device__ __forceinline__ void narrow_fold(Rows rows, int64_t K, int64_t ncols,
   const bool active = lane < ncols;
   const uint32_t coff = (uint32_t)((active ? lane : ncols - 1) * IB);
   const int64_t ntiles = (K + kNarrowTile - 1) / kNarrowTile;
-  unsigned r[PER];
-  T wr = T(0);
-  auto load = [&](int64_t t) {  // this wave's rows of tile t -> registers (+ the tile's weights)
+  unsigned ra[PER], rb[PER];
+  T wa = T(0), wb = T(0);
+  auto load = [&](int64_t t, unsigned(&r)[PER], T& wr) {  // this wave's rows of tile t -> registers
     const int64_t k0 = t * kNarrowTile;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int64_t k = k0 + wave + (int64_t)(kThreads / 64) * i;
       k = k < K ? k : K - 1;
-      const uint8_t* p = rows.row((int)(t & 1), k, k0) + coff;
+      const uint8_t* p = rows.row((int)(t % kRowSlots), k, k0) + coff;
       if constexpr (IB == 4) {
         r[i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p))
                   : *reinterpret_cast<const unsigned*>(p);
@@ -851,69 +857,76 @@ __device__ __forceinline__ void narrow_fold(Rows rows, int64_t K, int64_t ncols,
       wr = ACC::weight(w[k < K ? k : K - 1]);
     }
   };
-  auto store = [&](int64_t t) {  // registers -> LDS buffer t & 1
+  auto store = [&](int64_t t, const unsigned(&r)[PER], T wr) {  // registers -> LDS buffer t & 1
     unsigned(*b)[kNarrowCols] = tile[t & 1];
 #pragma unroll
     for (int i = 0; i < PER; ++i) b[wave + (kThreads / 64) * i][lane] = r[i];
     if (threadIdx.x < kNarrowTile) wt[t & 1][threadIdx.x] = wr;
   };
-  rows.fetch(0, K);
-  rows.commit(0);
-  if (ntiles > 1) {
-    rows.fetch(kNarrowTile, K);
-    rows.commit(1);
-  }
-  __syncthreads();
-  load(0);
-  store(0);
-  __syncthreads();
   T acc = T(0);
-  for (int64_t t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) load(t + 1);  // in flight while wave 0 folds tile t
-    if (t + 2 < ntiles) rows.fetch((t + 2) * kNarrowTile, K);  // row pointers, one tile further
-    if (wave == 0) {
-      const unsigned(*b)[kNarrowCols] = tile[t & 1];
-      const T* wk = wt[t & 1];
-      const int64_t k0 = t * kNarrowTile;
-      const int n = (int)(K - k0 < kNarrowTile ? K - k0 : kNarrowTile);
-      int j = 0;
-      if (t == 0) {  // client 0: s_0 = t_0, or out + t_0 (running sum)
-        T v[1];
-        decode<IN, ACC, 1>(b[0][lane], v);
-        acc = ACC::mul(v[0], wk[0]);
-        if (accumulate && active) {
-          unsigned ob[1];
-          load_out_unit<OUT, 1>(out + lane * OB, ob);
-          acc = ACC::add(init_from<OUT, ACC>(ob[0]), acc);
-        }
-        j = 1;
+  auto fold_tile = [&](int64_t t) {  // wave 0: clients of tile t, in order, from LDS
+    const unsigned(*b)[kNarrowCols] = tile[t & 1];
+    const T* wk = wt[t & 1];
+    const int64_t k0 = t * kNarrowTile;
+    const int n = (int)(K - k0 < kNarrowTile ? K - k0 : kNarrowTile);
+    int j = 0;
+    if (t == 0) {  // client 0: s_0 = t_0, or out + t_0 (running sum)
+      T v[1];
+      decode<IN, ACC, 1>(b[0][lane], v);
+      acc = ACC::mul(v[0], wk[0]);
+      if (accumulate && active) {
+        unsigned ob[1];
+        load_out_unit<OUT, 1>(out + lane * OB, ob);
+        acc = ACC::add(init_from<OUT, ACC>(ob[0]), acc);
       }
-      // 8 clients' LDS reads in flight before their folds: the chain of adds is serial,
-      // the reads are not (a read-fold-read loop waits out the LDS latency per client)
-      for (; j + 8 <= n; j += 8) {
-        unsigned raw[8];
-        T wv[8];
+      j = 1;
+    }
+    // 8 clients' LDS reads in flight before their folds: the chain of adds is serial,
+    // the reads are not (a read-fold-read loop waits out the LDS latency per client)
+    for (; j + 8 <= n; j += 8) {
+      unsigned raw[8];
+      T wv[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          raw[u] = b[j + u][lane];
-          wv[u] = wk[j + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          T v[1];
-          decode<IN, ACC, 1>(raw[u], v);
-          acc = ACC::add(acc, ACC::mul(v[0], wv[u]));
-        }
+      for (int u = 0; u < 8; ++u) {
+        raw[u] = b[j + u][lane];
+        wv[u] = wk[j + u];
       }
-      for (; j < n; ++j) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
         T v[1];
-        decode<IN, ACC, 1>(b[j][lane], v);
-        acc = ACC::add(acc, ACC::mul(v[0], wk[j]));
+        decode<IN, ACC, 1>(raw[u], v);
+        acc = ACC::add(acc, ACC::mul(v[0], wv[u]));
       }
     }
-    if (t + 1 < ntiles) store(t + 1);  // buffer (t+1)&1 was last read in iteration t-1
-    if (t + 2 < ntiles) rows.commit((int)(t & 1));  // tile t's pointers were used at iteration t-1
+    for (; j < n; ++j) {
+      T v[1];
+      decode<IN, ACC, 1>(b[j][lane], v);
+      acc = ACC::add(acc, ACC::mul(v[0], wk[j]));
+    }
+  };
+  // one step of the pipeline: `cur` holds tile t+1's loads, `nxt` receives tile t+2's
+  auto step = [&](int64_t t, unsigned(&cur)[PER], T& curw, unsigned(&nxt)[PER], T& nxtw) {
+    if (t + 2 < ntiles) load(t + 2, nxt, nxtw);
+    if (wave == 0) fold_tile(t);
+    if (t + 1 < ntiles) store(t + 1, cur, curw);  // buffer (t+1)&1 was last read at step t-1
+    if (t + 3 < ntiles) rows.commit((int)((t + 3) % kRowSlots));  // slot of tile t-1: done
+    if (t + 4 < ntiles) rows.fetch((t + 4) * kNarrowTile, K);
     __syncthreads();
+  };
+  for (int64_t t = 0; t < 3 && t < ntiles; ++t) {  // row pointers of tiles 0..2
+    rows.fetch(t * kNarrowTile, K);
+    rows.commit((int)t);
+  }
+  __syncthreads();
+  load(0, ra, wa);
+  store(0, ra, wa);
+  if (ntiles > 3) rows.fetch(3 * (int64_t)kNarrowTile, K);
+  __syncthreads();
+  if (ntiles > 1) load(1, ra, wa);
+  for (int64_t t = 0; t < ntiles; t += 2) {
+    step(t, ra, wa, rb, wb);
+    if (t + 1 >= ntiles) break;
+    step(t + 1, rb, wb, ra, wa);
   }
   if (wave == 0 && active) {
     const unsigned b[1] = {finish<OUT, ACC>(acc, do_scale != 0, scale)};
@@ -941,7 +954,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs_narrow(const int64_t* __restr
                                                           const typename ACC::T* __restrict__ w, float scale,
                                                           int do_scale, int accumulate) {
   constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
-  __shared__ unsigned long long rowp[2 * kNarrowTile];
+  __shared__ unsigned long long rowp[kRowSlots * kNarrowTile];
   const int64_t* in_ptrs = img;
   const int64_t* out_ptrs = img + K * L;
   const int64_t* leaf_n = out_ptrs + L;
