@@ -13,7 +13,7 @@ export TMPDIR=/tmp
 step() {  # name limit allow_rc1 cmd...
   local name=$1 lim=$2 allow1=$3; shift 3
   timeout -k 10 "$lim" "$@"; local rc=$?
-  echo "[$name] rc=$rc"
+  echo "[$name] rc=$rc" >&2
   if [ $rc -eq 0 ] || { [ "$allow1" = 1 ] && [ $rc -eq 1 ]; }; then return 0; fi
   exit $rc
 }
