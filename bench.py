@@ -201,6 +201,9 @@ def main():
     ap.add_argument("--reference-bf16", action="store_true",
                     help="bf16 workloads: the reference's bf16 arithmetic (every product and sum rounded to bf16, "
                          "tree_util.set_bf16_semantics('reference')) instead of the f32 fold")
+    ap.add_argument("--device-weights", action="store_true",
+                    help="upload the weights each step (pinned H2D in front of the fold) instead of passing "
+                         "them in the kernel arguments (A/B of FJAGG_HOST_TABLES)")
     args = ap.parse_args()
     if args.single_process:
         return single_process(args)
@@ -315,7 +318,12 @@ def main():
     collective = "all_reduce" if args.all_ranks else "reduce"  # the exchange of the partials
 
     def step(events=None):
-        wd = torch.from_numpy(np.float32(w_local)).pin_memory().to(dev, non_blocking=True)
+        # the round's weights: host float32, carried in the fold's kernel arguments
+        # (FJAGG_HOST_TABLES) when the launch allows it; uploaded (pinned H2D on the stream)
+        # for the fused-norm / server-step kernels and with --device-weights
+        wd = np.float32(w_local)
+        if args.device_weights or args.server != "none" or args.with_norms:
+            wd = torch.from_numpy(wd).pin_memory().to(dev, non_blocking=True)
         if args.server != "none":
             desc = sopt.descriptor(1)  # copied by value into the kernel arguments at launch
             if events is not None:
@@ -451,6 +459,7 @@ def main():
                        "exchange_engine": engine if sharded else None,
                        "exchange_collective": collective if sharded else None,
                        "exchange_autotune_ms": {k: round(t, 4) for k, t in tune.items()} or None,
+                       "weights_path": {k: v for k, v in kernels.HOST_WEIGHT_PATHS.items() if v} or "device tensor",
                        "nontemporal": nt,
                        "variant": args.variant, "fused_l2_norms": bool(args.with_norms),
                        "bf16_arithmetic": ("reference (every op rounded to bf16)" if args.reference_bf16 else
@@ -507,7 +516,7 @@ def single_process(args):
         x = torch.empty(k1 - k0, (P + vw - 1) // vw * vw, dtype=dtype, device=dev)[:, :P]
         kernels.fill_synth(x, seed=0, k0=k0)
         xs.append(x)
-        ws.append(torch.tensor(np.float32(weights[k0:k1]), device=dev))
+        ws.append(weights[k0:k1])
     comm = fd.MultiDeviceCommunicator(devs)
     outs = [torch.empty(P, dtype=torch.float32, device=dev) for dev in devs]
     buckets = (tuple(float(v) for v in args.buckets.split(":")) if ":" in args.buckets
@@ -517,8 +526,8 @@ def single_process(args):
         for dev in devs:
             torch.cuda.synchronize(dev)
 
-    def step():
-        fd.multi_device_weighted_mean(xs, ws, W, comm=comm, buckets=buckets, outs=outs,
+    def step():  # the round's weights on the host, per device (kernel arguments of the folds)
+        fd.multi_device_weighted_mean(xs, [np.float32(w) for w in ws], W, comm=comm, buckets=buckets, outs=outs,
                                       all_devices=args.all_ranks)
 
     for _ in range(args.warmup):

@@ -28,10 +28,11 @@ LIB_PATH = os.environ.get("FJAGG_LIB", os.path.join(_HERE, "_build", "libfjagg.s
 # enum fjagg_dtype
 F32, BF16, I32 = 0, 1, 2
 # enum fjagg_flags
-SCALE, ACCUMULATE, NONTEMPORAL, UNALIGNED, UNBALANCED, NARROW = 1, 2, 4, 8, 16, 32
+SCALE, ACCUMULATE, NONTEMPORAL, UNALIGNED, UNBALANCED, NARROW, HOST_TABLES = 1, 2, 4, 8, 16, 32, 64
+KARG_MAX_WEIGHTS, KARG_MAX_WORDS = 1024, 3584
 # enum fjagg_mode
 MODE_EXACT, MODE_SPLIT = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 COMP_ABI_VERSION = 1
 COMM_ABI_VERSION = 1
 COMM_ID_BYTES = 128
@@ -56,6 +57,7 @@ _SIGNATURES = {
     "fjagg_ptrs_plan": (_i64, [_i32, _i32, _vp, _i32, _vp, _i64]),
     "fjagg_ptrs_plan_leaves": (_i64, [_i32, _i32, _vp, _vp, _i32, _vp, _i64]),
     "fjagg_wsum_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _i32, _vp]),
+    "fjagg_karg_image_words": (_i64, [_i64, _i32, _i64]),
     "fjagg_wsum_l2_ptrs_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_wsum_l2_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _vp, _i32, _vp, _i64, _vp]),
     "fjagg_server_update_dense": (_i32, [_i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),

@@ -22,7 +22,10 @@
 //     (k_dense_l2), and the server optimizer step consuming the mean in registers
 //     (k_dense_opt);
 //   * FJAGG_MODE_SPLIT splits the client axis over blockIdx.y for shapes whose
-//     parameter axis cannot fill 256 CUs, and combines the range sums in order.
+//     parameter axis cannot fill 256 CUs, and combines the range sums in order;
+//   * FJAGG_HOST_TABLES: the weights (dense) or the whole plan image + weights
+//     (pytree) travel in the kernel arguments instead of a pinned upload in front of
+//     the fold on the stream (a blit kernel and its dependency, ~5-10 us per call).
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
@@ -30,6 +33,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <cstring>
 #include <mutex>
 #include <type_traits>
 #include <unordered_map>
@@ -62,6 +66,16 @@ int check_launch(const char* what) {
 constexpr int kThreads = 256;   // 4 waves of 64
 constexpr int kSplitMax = 64;   // max client ranges in FJAGG_MODE_SPLIT
 constexpr int64_t kSplitHeader = 256;  // bytes of ones at the head of the split workspace
+
+// FJAGG_HOST_TABLES: tables passed BY VALUE in the kernel arguments. An aggregate
+// kernel argument lives in the kernarg segment, and the kernels read it in place
+// through a pointer (scalar loads, no private copy: these kernels have no scratch).
+// The launch copies the struct, so the caller's host tables are free on return.
+// Kernels built without the feature take a 4-byte placeholder (N = 1).
+template <int N> struct KargWords { int64_t w[N]; };
+template <int N> struct KargF32 { float w[N]; };
+constexpr int kKargWeights = FJAGG_KARG_MAX_WEIGHTS;  // dense: f32 / i32 weights
+constexpr int kKargWords = FJAGG_KARG_MAX_WORDS;      // pytree: image + packed f32 weights
 
 // ---------------------------------------------------------------- element types
 template <int DT> struct Elem;
@@ -448,17 +462,19 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
 // blockIdx.y selects a client range [y*kchunk, min(K, (y+1)*kchunk)) and writes to
 // out + y*out_ystride_bytes (FJAGG_MODE_SPLIT); exact mode has gridDim.y == 1.
 // MINW > 0 asks for MINW waves per SIMD (caps VGPRs: 8 -> 64 registers).
-template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW, bool BURST = false>
+// WK > 0: the weights are kw.w (FJAGG_HOST_TABLES), not w.
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW, bool BURST = false, int WK = 0>
 __global__ __launch_bounds__(kThreads, MINW) void k_dense(
     const uint8_t* __restrict__ x, int64_t ld_bytes, int64_t K, int64_t nunits, int tail_n,
     const typename ACC::T* __restrict__ w, float scale, int do_scale, int accumulate,
-    uint8_t* __restrict__ out, int64_t kchunk, int64_t out_ystride_bytes, int64_t S) {
+    uint8_t* __restrict__ out, int64_t kchunk, int64_t out_ystride_bytes, int64_t S,
+    const KargF32<(WK > 0 ? WK : 1)> kw) {
   constexpr int IB = Elem<IN>::B, OB = Elem<OUT>::B;
   const int tid = threadIdx.x;
   const int64_t k0 = (int64_t)blockIdx.y * kchunk;
   const int64_t kn = (K - k0 < kchunk) ? (K - k0) : kchunk;
   const uint8_t* xb = x + k0 * ld_bytes;
-  const typename ACC::T* wb = w + k0;
+  const typename ACC::T* wb = (WK > 0 ? reinterpret_cast<const typename ACC::T*>(kw.w) : w) + k0;
   uint8_t* ob = out + (int64_t)blockIdx.y * out_ystride_bytes;
   auto row = [=](int64_t k) { return xb + k * ld_bytes; };
   const uint32_t row_bytes = (uint32_t)((nunits * V + tail_n) * IB);
@@ -660,14 +676,20 @@ __device__ __forceinline__ void walk_units(RowFn row, uint32_t row_bytes, int64_
 // element flag is set: a leaf whose client or output pointers are not 16-byte
 // aligned (fjagg_ptrs_plan_leaves) takes element units without pulling the other
 // leaves of the launch off the 16-byte path.
-template <int IN, class ACC, int OUT, int V, bool NT, bool L2 = false, bool BURST = true>
-__global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ img, int L,
+// IW > 0 (FJAGG_HOST_TABLES): the image is ki.w and the K f32 weights follow its
+// blocks (word K*L + 2L + 2*nblk, nblk = gridDim.x); img_p and w_p are unused.
+template <int IN, class ACC, int OUT, int V, bool NT, bool L2 = false, bool BURST = true, int IW = 0>
+__global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ img_p, int L,
                                                    int64_t K,
-                                                   const typename ACC::T* __restrict__ w,
+                                                   const typename ACC::T* __restrict__ w_p,
                                                    float scale, int do_scale, int accumulate,
-                                                   float* __restrict__ ws) {
+                                                   float* __restrict__ ws,
+                                                   const KargWords<(IW > 0 ? IW : 1)> ki) {
   constexpr int IB = Elem<IN>::B;
   const int tid = threadIdx.x;
+  const int64_t* img = IW > 0 ? ki.w : img_p;
+  const typename ACC::T* w =
+      IW > 0 ? reinterpret_cast<const typename ACC::T*>(ki.w + K * L + 2 * L + 2 * (int64_t)gridDim.x) : w_p;
   const int64_t* in_ptrs = img;
   const int64_t* out_ptrs = img + K * L;
   const int64_t* leaf_n = out_ptrs + L;
@@ -1120,6 +1142,7 @@ struct DenseArgs {
   uint8_t* out;
   int64_t kchunk, out_ystride;
   bool balanced;
+  bool host_w;  // FJAGG_HOST_TABLES: w is host memory (K <= kKargWeights)
 };
 
 // (CUs, workgroups of `kern` per CU at once), cached per kernel and device. Used
@@ -1165,9 +1188,9 @@ void balanced_grid(const Residency& r, int64_t nunits, int64_t tile, int64_t gy,
   *nblk_out = (nunits + S - 1) / S;
 }
 
-template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW, bool BURST = false>
+template <int IN, class ACC, int OUT, int V, int E, int U, bool NT, int MINW, bool BURST = false, int WK = 0>
 void launch_dense_t(const DenseArgs& a, int64_t gy, hipStream_t s) {
-  auto kern = k_dense<IN, ACC, OUT, V, E, U, NT, MINW, BURST>;
+  auto kern = k_dense<IN, ACC, OUT, V, E, U, NT, MINW, BURST, WK>;
   const int64_t tile = (int64_t)kThreads * E;
   const int64_t ntiles = (a.nunits + tile - 1) / tile;
   int64_t nblk = ntiles, S = tile;
@@ -1178,9 +1201,14 @@ void launch_dense_t(const DenseArgs& a, int64_t gy, hipStream_t s) {
     balanced_grid(residency(reinterpret_cast<const void*>(kern)), a.nunits, tile, gy, &S, &nblk);
   }
   dim3 grid((unsigned)(nblk + (a.tail_n > 0 ? 1 : 0)), (unsigned)gy);
+  KargF32<(WK > 0 ? WK : 1)> kw;  // host weights copied into the kernel arguments
+  if constexpr (WK > 0)
+    std::memcpy(kw.w, a.w, sizeof(float) * (size_t)a.K);
+  else
+    kw.w[0] = 0.f;
   hipLaunchKernelGGL(kern, grid, dim3(kThreads), 0, s, a.x, a.ld_bytes, a.K, a.nunits, a.tail_n,
-                     reinterpret_cast<const typename ACC::T*>(a.w), a.scale, a.do_scale,
-                     a.accumulate, a.out, a.kchunk, a.out_ystride, S);
+                     WK > 0 ? nullptr : reinterpret_cast<const typename ACC::T*>(a.w), a.scale, a.do_scale,
+                     a.accumulate, a.out, a.kchunk, a.out_ystride, S, kw);
 }
 
 struct VariantShape {
@@ -1209,8 +1237,45 @@ int pick_variant(int64_t nunits, int64_t K) {
   return 12;                       // E=8 x U=4
 }
 
+// (in, acc, out) combinations built with FJAGG_HOST_TABLES weights (fjagg.h)
+template <int IN, class ACC, int OUT>
+constexpr bool kHostWeights = std::is_same<ACC, AccF>::value &&
+                              ((IN == FJAGG_F32 && OUT == FJAGG_F32) || IN == FJAGG_BF16);
+
+// The shapes pick_variant and launch_dense_v's variant 12 choose, with the weights in
+// the kernel arguments (FJAGG_HOST_TABLES); other variants are not built that way.
+template <int IN, class ACC, int OUT, int V, bool NT>
+int launch_dense_hostw(int variant, const DenseArgs& a, int64_t gy, hipStream_t s) {
+  if constexpr (!kHostWeights<IN, ACC, OUT>) {
+    return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: dtype combination not built with kernel-argument weights");
+  } else if constexpr (V == 1) {
+    launch_dense_t<IN, ACC, OUT, 1, 1, 8, NT, 0, false, kKargWeights>(a, gy, s);
+  } else {
+    switch (variant) {
+      case 2: launch_dense_t<IN, ACC, OUT, V, 1, 8, NT, 0, false, kKargWeights>(a, gy, s); break;
+      case 5: launch_dense_t<IN, ACC, OUT, V, 4, 4, NT, 0, false, kKargWeights>(a, gy, s); break;
+      case 12: {
+        const int64_t ntiles = (a.nunits + (int64_t)kThreads * 8 - 1) / ((int64_t)kThreads * 8);
+        const int cus = residency(reinterpret_cast<const void*>(k_dense<IN, ACC, OUT, V, 8, 4, NT, 0>)).cus;
+        if (!a.balanced || ntiles * gy >= 2 * (int64_t)cus)
+          launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0, false, kKargWeights>(a, gy, s);
+        else
+          launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0, true, kKargWeights>(a, gy, s);
+        break;
+      }
+      case 16: launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0, true, kKargWeights>(a, gy, s); break;
+      case 17: launch_dense_t<IN, ACC, OUT, V, 8, 4, NT, 0, false, kKargWeights>(a, gy, s); break;
+      default:
+        return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: variant %d is not built with kernel-argument weights",
+                    variant);
+    }
+  }
+  return check_launch("k_dense");
+}
+
 template <int IN, class ACC, int OUT, int V, bool NT>
 int launch_dense_v(int variant, const DenseArgs& a, int64_t gy, hipStream_t s) {
+  if (a.host_w) return launch_dense_hostw<IN, ACC, OUT, V, NT>(variant, a, gy, s);
   if constexpr (V == 1) {  // element-granular path (tails, unaligned rows): one shape
     launch_dense_t<IN, ACC, OUT, 1, 1, 8, NT, 0>(a, gy, s);
     return check_launch("k_dense");
@@ -1372,6 +1437,8 @@ int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, in
   // from 256 Ki f32 up the 16-byte kernels keep enough loads in flight (profiles/r02i_*)
   if (variant == 0 && gy == 1 && K >= 16 && P * ib <= (512 << 10)) variant = kNarrowVariant;
   if (variant == 0) variant = pick_variant(P / V, K);
+  if (variant == kNarrowVariant && (flags & FJAGG_HOST_TABLES))  // (fjagg_wsum_dense checks this first)
+    return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: the narrow kernel takes device weights");
   if (variant == kNarrowVariant && gy == 1) return launch_narrow(in, acc, out, x, ld_bytes, K, P, w, scale, y, flags, s);
   DenseArgs a;
   a.x = x;
@@ -1387,6 +1454,7 @@ int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, in
   a.kchunk = kchunk;
   a.out_ystride = y_ystride;
   a.balanced = !(flags & FJAGG_UNBALANCED);
+  a.host_w = (flags & FJAGG_HOST_TABLES) != 0;
   (void)ob;
   (void)ib;
   return launch_dense_dispatch(in, acc, out, vec, (flags & FJAGG_NONTEMPORAL) != 0, variant, a,
@@ -1419,10 +1487,10 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
       const size_t smem = (size_t)(kThreads / 64) * K * sizeof(float);
       if (nt)
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true>), dim3((unsigned)nblk), dim3(kThreads), smem, s,
-                           img, L, K, wt, scale, do_scale, accumulate, ws);
+                           img, L, K, wt, scale, do_scale, accumulate, ws, KargWords<1>{});
       else
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true>), dim3((unsigned)nblk), dim3(kThreads), smem,
-                           s, img, L, K, wt, scale, do_scale, accumulate, ws);
+                           s, img, L, K, wt, scale, do_scale, accumulate, ws, KargWords<1>{});
       if (int rc = check_launch("k_ptrs (l2)")) return rc;
       hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s,
                          ws, nblk, K, l2);
@@ -1434,16 +1502,16 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
   const bool burst = nblk < 2 * (int64_t)residency(reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true>)).cus;
   if (nt && burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, KargWords<1>{});
   else if (nt)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, KargWords<1>{});
   else if (burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, KargWords<1>{});
   else
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr);
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, KargWords<1>{});
   return check_launch("k_ptrs");
 }
 
@@ -1541,6 +1609,25 @@ constexpr int64_t kL2MaxClients = 4096;  // (kThreads/64) x K floats of LDS <= 6
 
 }  // namespace
 
+// Whether an exact-mode dense fold of K x P (one launch per <= 1 GiB column chunk) can
+// take FJAGG_HOST_TABLES weights: FJAGG_OK or FJAGG_EUNSUPPORTED (message set). Callers
+// that launch several folds (fjcomm's buckets) check every one before the first launch.
+__attribute__((visibility("hidden"))) int fjagg_host_weights_check(int in_dtype, int acc_dtype, int out_dtype,
+                                                                   int64_t K, int64_t P, int flags) {
+  const int variant = (flags >> 8) & 0xff;
+  const int64_t ib = elem_bytes(in_dtype), chunk = kMaxRowBytes / ib;
+  const int64_t last = P > 0 ? P - (P - 1) / chunk * chunk : 0;
+  if (K > kKargWeights)
+    return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: K = %lld > %d weights", (long long)K, kKargWeights);
+  if (acc_dtype != FJAGG_F32 || !((in_dtype == FJAGG_F32 && out_dtype == FJAGG_F32) || in_dtype == FJAGG_BF16))
+    return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: dtype combination not built with kernel-argument weights");
+  if (!(variant == 0 || variant == 2 || variant == 5 || variant == 12 || variant == 16 || variant == 17))
+    return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: variant %d takes device weights", variant);
+  if (variant == 0 && K >= 16 && last * ib <= (512 << 10))  // dense_exact's narrow rule (last chunk)
+    return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: the narrow kernel takes device weights");
+  return FJAGG_OK;
+}
+
 // ====================================================================== C ABI
 extern "C" {
 
@@ -1568,6 +1655,10 @@ int fjagg_wsum_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_d
   const uint8_t* x = reinterpret_cast<const uint8_t*>(x_dev);
   uint8_t* y = reinterpret_cast<uint8_t*>(out_dev);
   const int64_t ib = elem_bytes(in_dtype);
+  if (flags & FJAGG_HOST_TABLES) {  // checked up front: nothing may launch before a refusal
+    if (mode != FJAGG_MODE_EXACT) return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: exact mode only");
+    if (int rc = fjagg_host_weights_check(in_dtype, acc_dtype, out_dtype, K, P, flags)) return rc;
+  }
   if (mode == FJAGG_MODE_EXACT)
     return dense_exact_chunked(in_dtype, acc_dtype, out_dtype, x, ld * ib, K, P, w_dev, scale, y,
                                flags, s, K, 1, 0);
@@ -1694,6 +1785,48 @@ int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, c
 }
 
 namespace {
+// FJAGG_HOST_TABLES on the pytree path: the host image and the K f32 weights are copied
+// into ONE kernel-argument struct (k_ptrs<..., kKargWords>), float32 leaves, 16-byte units.
+int launch_ptrs_karg(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w, float scale,
+                     int ds, int ac, float* ws, float* l2, hipStream_t s) {
+  constexpr int IN = FJAGG_F32, OUT = FJAGG_F32, V = 4;
+  using ACC = AccF;
+  KargWords<kKargWords> ki;
+  const int64_t nimg = K * L + 2 * (int64_t)L + 2 * nblk;
+  std::memcpy(ki.w, img, sizeof(int64_t) * (size_t)nimg);
+  ki.w[nimg + (K + 1) / 2 - 1] = 0;  // the odd weight slot, if any
+  std::memcpy(ki.w + nimg, w, sizeof(float) * (size_t)K);
+  const dim3 grid((unsigned)nblk), block(kThreads);
+  if (ws) {
+    const size_t smem = (size_t)(kThreads / 64) * K * sizeof(float);
+    if (nt)
+      hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true, true, kKargWords>), grid, block, smem, s, nullptr, L,
+                         K, nullptr, scale, ds, ac, ws, ki);
+    else
+      hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true, true, kKargWords>), grid, block, smem, s, nullptr, L,
+                         K, nullptr, scale, ds, ac, ws, ki);
+    if (int rc = check_launch("k_ptrs (l2, kernel-argument image)")) return rc;
+    hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s, ws, nblk, K,
+                       l2);
+    return check_launch("k_l2_combine");
+  }
+  // the schedule rule of launch_ptrs_t
+  const bool burst = nblk < 2 * (int64_t)residency(reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true>)).cus;
+  if (nt && burst)
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, true, kKargWords>), grid, block, 0, s, nullptr, L, K,
+                       nullptr, scale, ds, ac, nullptr, ki);
+  else if (nt)
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, false, kKargWords>), grid, block, 0, s, nullptr, L, K,
+                       nullptr, scale, ds, ac, nullptr, ki);
+  else if (burst)
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, true, kKargWords>), grid, block, 0, s, nullptr, L, K,
+                       nullptr, scale, ds, ac, nullptr, ki);
+  else
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, false, kKargWords>), grid, block, 0, s, nullptr, L, K,
+                       nullptr, scale, ds, ac, nullptr, ki);
+  return check_launch("k_ptrs (kernel-argument image)");
+}
+
 int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,
                    int64_t K, int64_t nblk, const void* w_dev, float scale, int flags, float* ws,
                    float* l2, void* stream) {
@@ -1701,6 +1834,16 @@ int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* im
   const bool vec = !(flags & FJAGG_UNALIGNED);
   const bool nt = (flags & FJAGG_NONTEMPORAL) != 0;
   const int ds = (flags & FJAGG_SCALE) ? 1 : 0, ac = (flags & FJAGG_ACCUMULATE) ? 1 : 0;
+  if (flags & FJAGG_HOST_TABLES) {
+    if (in_dtype != FJAGG_F32 || acc_dtype != FJAGG_F32 || out_dtype != FJAGG_F32)
+      return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: float32 leaves and fold only");
+    if (flags & (FJAGG_UNALIGNED | FJAGG_NARROW))
+      return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: 16-byte unit plans only (no UNALIGNED / NARROW)");
+    const int64_t words = fjagg_karg_image_words(K, L, nblk);
+    if (words > kKargWords)
+      return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: %lld words > %d", (long long)words, kKargWords);
+    return launch_ptrs_karg(nt, image_dev, L, K, nblk, w_dev, scale, ds, ac, ws, l2, s);
+  }
   if (flags & FJAGG_NARROW) {
     if (ws) return fail(FJAGG_EINVAL, "FJAGG_NARROW plans fold only (no fused norms)");
 #define FJ_CASE(I, A, O, ACCT)                                                                          \
@@ -1730,6 +1873,11 @@ int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* im
   return fail(FJAGG_EUNSUPPORTED, "unsupported dtype combination");
 }
 }  // namespace
+
+int64_t fjagg_karg_image_words(int64_t K, int L, int64_t nblk) {
+  if (K < 0 || L < 0 || nblk < 0) return -1;
+  return K * L + 2 * (int64_t)L + 2 * nblk + (K + 1) / 2;
+}
 
 int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,
                     int64_t K, int64_t nblk, const void* w_dev, float scale, int flags,

@@ -17,6 +17,8 @@
 #include "fjcomm.h"
 
 extern thread_local char fjagg_g_err[512];
+// fjagg.hip (same library): whether a dense fold can take FJAGG_HOST_TABLES weights
+int fjagg_host_weights_check(int in_dtype, int acc_dtype, int out_dtype, int64_t K, int64_t P, int flags);
 
 namespace {
 
@@ -234,11 +236,15 @@ int fjcomm_sharded_wsum_dense_edges(void* comm, int in_dtype, const void* x_dev,
   if (P == 0) return FJAGG_OK;
   if (int rc = check_edges(edges, nbuckets, P)) return rc;
   if (!out_dev || (K > 0 && (!x_dev || !w_dev))) return fail(FJAGG_EINVAL, "null pointer argument");
-  if (flags & ~(FJAGG_NONTEMPORAL | FJAGG_VARIANT(0xff)))
-    return fail(FJAGG_EINVAL, "flags may hold FJAGG_NONTEMPORAL and FJAGG_VARIANT bits only");
+  if (flags & ~(FJAGG_NONTEMPORAL | FJAGG_HOST_TABLES | FJAGG_VARIANT(0xff)))
+    return fail(FJAGG_EINVAL, "flags may hold FJAGG_NONTEMPORAL, FJAGG_HOST_TABLES and FJAGG_VARIANT bits only");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t esz = in_dtype == FJAGG_BF16 ? 2 : 4;
   const int nb = nbuckets;
+  if ((flags & FJAGG_HOST_TABLES) && K > 0)  // every bucket's fold must take them: refuse before any launch
+    for (int b = 0; b < nb; ++b)
+      if (int rc = fjagg_host_weights_check(in_dtype, FJAGG_F32, FJAGG_F32, K, edges[b + 1] - edges[b], flags))
+        return rc;
   for (int b = 0; b < nb; ++b) {
     const int64_t p0 = edges[b];
     const int64_t n = edges[b + 1] - p0;
@@ -330,8 +336,8 @@ int fjcomm_multi_wsum_dense(void* const* comms, int ndev, int in_dtype, const vo
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16) return fail(FJAGG_EINVAL, "in_dtype must be F32 or BF16");
   if (P < 0) return fail(FJAGG_EINVAL, "P < 0");
   if (root >= ndev) return fail(FJAGG_EINVAL, "root %d >= ndev %d", root, ndev);
-  if (flags & ~(FJAGG_NONTEMPORAL | FJAGG_VARIANT(0xff)))
-    return fail(FJAGG_EINVAL, "flags may hold FJAGG_NONTEMPORAL and FJAGG_VARIANT bits only");
+  if (flags & ~(FJAGG_NONTEMPORAL | FJAGG_HOST_TABLES | FJAGG_VARIANT(0xff)))
+    return fail(FJAGG_EINVAL, "flags may hold FJAGG_NONTEMPORAL, FJAGG_HOST_TABLES and FJAGG_VARIANT bits only");
   Comm* cs[FJCOMM_MAX_DEVICES];
   for (int d = 0; d < ndev; ++d) {
     cs[d] = reinterpret_cast<Comm*>(comms[d]);
@@ -347,6 +353,11 @@ int fjcomm_multi_wsum_dense(void* const* comms, int ndev, int in_dtype, const vo
   DeviceGuard guard;
   const int64_t esz = in_dtype == FJAGG_BF16 ? 2 : 4;
   const int nb = nbuckets;
+  if (flags & FJAGG_HOST_TABLES)  // every device's every bucket must take them: refuse before any launch
+    for (int d = 0; d < ndev; ++d)
+      for (int b = 0; K[d] > 0 && b < nb; ++b)
+        if (int rc = fjagg_host_weights_check(in_dtype, FJAGG_F32, FJAGG_F32, K[d], edges[b + 1] - edges[b], flags))
+          return rc;
   for (int b = 0; b < nb; ++b) {
     const int64_t p0 = edges[b], n = edges[b + 1] - p0;
     // every device folds its clients' share of bucket b on its own stream, then signals

@@ -71,6 +71,9 @@ namespace {
 enum { kTChecks, kTOutputs, kTPlan, kTImage, kTUpload, kTLaunch, kTWrap, kTPhases };
 double g_timers[kTPhases] = {};
 long long g_timer_calls = 0;
+// how fold_table's plan images reached the kernel: in the kernel arguments, or through a
+// pinned staging buffer + upload (image too large, or a plan the kernarg kernels lack)
+long long g_image_karg = 0, g_image_upload = 0;
 struct Stamp {
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   void lap(int phase) {
@@ -384,35 +387,56 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     // plan image (fjagg.h): in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk] | f32 weights
     const int64_t nw = (K + 1) / 2, n = K * L + 2 * L + 2 * nblk + nw;
     st.lap(kTPlan);
-    at::Tensor img = at::empty({n}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
-    int64_t* p = img.data_ptr<int64_t>();
-    std::memcpy(p, in, sizeof(int64_t) * K * L);
-    for (Py_ssize_t l = 0; l < L; ++l) {
-      p[K * L + l] = reinterpret_cast<int64_t>(outs[l].data_ptr());
-      p[K * L + L + l] = leaf_n[l];
-    }
-    if (plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) Py_RETURN_NONE;
-    p[n - 1] = 0;
-    std::memcpy(p + n - nw, bw.buf, 4 * K);
-    st.lap(kTImage);
-    at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);
-    st.lap(kTUpload);
+    auto fill = [&](int64_t* p) {
+      std::memcpy(p, in, sizeof(int64_t) * K * L);
+      for (Py_ssize_t l = 0; l < L; ++l) {
+        p[K * L + l] = reinterpret_cast<int64_t>(outs[l].data_ptr());
+        p[K * L + L + l] = leaf_n[l];
+      }
+      if (plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) return false;
+      p[n - 1] = 0;
+      std::memcpy(p + n - nw, bw.buf, 4 * K);
+      return true;
+    };
     const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
     const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0) |
                       (narrow ? FJAGG_NARROW : 0);
-    const int64_t* dp = dimg.data_ptr<int64_t>();
-    int rc;
-    if (with_l2) {  // fused per-client squared l2 norms (fjagg_wsum_l2_ptrs), workspace from torch's allocator
-      const at::Tensor& q = THPVariable_Unpack(l2sq);
+    at::Tensor ws;  // fused l2 norms: per-workgroup partials, from torch's allocator (stream-ordered)
+    float* l2p = nullptr;
+    if (with_l2) {
       const int64_t need = reinterpret_cast<L2WsFn>(l2ws_addr)(K, nblk);
       if (need < 0) Py_RETURN_NONE;
-      at::Tensor ws = at::empty({need > 4 ? need : 4}, dimg.options().dtype(at::kByte));
-      rc = reinterpret_cast<WsumL2Fn>(l2_addr)(kF32, kF32, kF32, dp, static_cast<int>(L), K, nblk, dp + (n - nw),
-                                               static_cast<float>(scale), q.data_ptr<float>(), flags,
-                                               ws.data_ptr(), ws.numel(), reinterpret_cast<void*>(stream));
-    } else {
-      rc = reinterpret_cast<WsumFn>(wsum_addr)(kF32, kF32, kF32, dp, static_cast<int>(L), K, nblk, dp + (n - nw),
-                                               static_cast<float>(scale), flags, reinterpret_cast<void*>(stream));
+      ws = at::empty({need > 4 ? need : 4}, outs[0].options().dtype(at::kByte));
+      l2p = THPVariable_Unpack(l2sq).data_ptr<float>();
+    }
+    auto launch = [&](const int64_t* image, const int64_t* w, int fl) {
+      if (with_l2)
+        return reinterpret_cast<WsumL2Fn>(l2_addr)(kF32, kF32, kF32, image, static_cast<int>(L), K, nblk, w,
+                                                   static_cast<float>(scale), l2p, fl, ws.data_ptr(), ws.numel(),
+                                                   reinterpret_cast<void*>(stream));
+      return reinterpret_cast<WsumFn>(wsum_addr)(kF32, kF32, kF32, image, static_cast<int>(L), K, nblk, w,
+                                                 static_cast<float>(scale), fl, reinterpret_cast<void*>(stream));
+    };
+    int rc = FJAGG_EUNSUPPORTED;
+    if (!narrow && n <= FJAGG_KARG_MAX_WORDS) {
+      // the image and weights travel in the kernel arguments (FJAGG_HOST_TABLES): no pinned
+      // staging buffer and no upload on the stream in front of the fold
+      thread_local std::vector<int64_t> host_img;
+      host_img.resize(static_cast<size_t>(n));
+      if (!fill(host_img.data())) Py_RETURN_NONE;
+      st.lap(kTImage);
+      rc = launch(host_img.data(), host_img.data() + (n - nw), flags | FJAGG_HOST_TABLES);
+      if (rc != FJAGG_EUNSUPPORTED) ++g_image_karg;
+    }
+    if (rc == FJAGG_EUNSUPPORTED) {  // too large for the kernel arguments: pinned image + stream-ordered upload
+      at::Tensor img = at::empty({n}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+      if (!fill(img.data_ptr<int64_t>())) Py_RETURN_NONE;
+      st.lap(kTImage);
+      at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);
+      st.lap(kTUpload);
+      const int64_t* dp = dimg.data_ptr<int64_t>();
+      rc = launch(dp, dp + (n - nw), flags);
+      ++g_image_upload;
     }
     st.lap(kTLaunch);
     PyObject* list = PyList_New(L);
@@ -895,6 +919,10 @@ PyObject* leaf_fold(PyObject*, PyObject* args) {
   }
 }
 
+PyObject* image_paths(PyObject*, PyObject*) {
+  return Py_BuildValue("{s:L,s:L}", "kernel_args", g_image_karg, "uploaded", g_image_upload);
+}
+
 PyObject* host_timers(PyObject*, PyObject*) {
   static const char* names[kTPhases] = {"checks", "outputs", "plan", "image", "upload", "launch", "wrap"};
   PyObject* d = PyDict_New();
@@ -914,6 +942,7 @@ PyObject* host_timers(PyObject*, PyObject*) {
 
 PyMethodDef kMethods[] = {
     {"host_timers", host_timers, METH_NOARGS, "mean per-call microseconds of fold_table's phases (resets)"},
+    {"image_paths", image_paths, METH_NOARGS, "fold_table launches with the image in kernel arguments / uploaded"},
     {"gather_rows", gather_rows, METH_VARARGS, "pointer table of K client pytrees (see fjhost.cpp)"},
     {"leaf_versions", leaf_versions, METH_VARARGS, "torch in-place version counters of K pytrees' leaves"},
     {"fold_weights", fold_weights, METH_VARARGS, "f32/i32 weights and W of Python-number weights"},

@@ -144,6 +144,8 @@ def _native_sharded(comm: RcclCommunicator, x_local: torch.Tensor, w_local: torc
         raise ValueError("client rows need unit column stride")
     if out.dtype != torch.float32 or out.numel() != P or not out.is_contiguous():
         raise ValueError("out must be a contiguous float32 [P] tensor")
+    if isinstance(w_local, np.ndarray):
+        w_local = torch.from_numpy(w_local)
     if w_local.dtype != torch.float32 or w_local.numel() != K:
         raise ValueError("w_local must be float32 [K_g]")
     nbytes = K * P * x_local.element_size()
@@ -159,11 +161,24 @@ def _native_sharded(comm: RcclCommunicator, x_local: torch.Tensor, w_local: torc
         if len(fold_events) < 2 * len(spans):
             raise ValueError(f"fold_events needs 2 events per bucket ({2 * len(spans)})")
         ev = (ctypes.c_void_p * len(fold_events))(*[e.handle for e in fold_events])
+    flags = _lib.NONTEMPORAL if nt else 0
+    stream = torch.cuda.current_stream(out.device).cuda_stream
+    if not w_local.is_cuda:  # host weights: in the bucket folds' kernel arguments when those launches allow it
+        w_local = w_local.contiguous()
+        rc = _lib.load().fjcomm_sharded_wsum_dense_edges(
+            comm.handle, kernels.dtype_code(x_local.dtype), x_local.data_ptr() if K else None,
+            x_local.stride(0) if K else P, K, P, w_local.data_ptr() if K else None, float(np.float32(scale)),
+            out.data_ptr(), edges.ctypes.data, len(spans), int(root), flags | _lib.HOST_TABLES, stream, ev)
+        if rc != kernels._EUNSUPPORTED:
+            _lib.check(rc, "fjcomm_sharded_wsum_dense_edges")
+            kernels.HOST_WEIGHT_PATHS["kernel_args"] += 1
+            return
+        w_local = w_local.pin_memory().to(out.device, non_blocking=True)
+        kernels.HOST_WEIGHT_PATHS["uploaded"] += 1
     _lib.call("fjcomm_sharded_wsum_dense_edges", comm.handle, kernels.dtype_code(x_local.dtype),
               x_local.data_ptr() if K else None, x_local.stride(0) if K else P, K, P,
               w_local.data_ptr() if K else None, float(np.float32(scale)), out.data_ptr(), edges.ctypes.data,
-              len(spans), int(root), _lib.NONTEMPORAL if nt else 0, torch.cuda.current_stream(out.device).cuda_stream,
-              ev)
+              len(spans), int(root), flags, stream, ev)
 
 
 def sharded_weighted_mean(x_local: torch.Tensor, w_local: torch.Tensor, W_total, *, group=None,
@@ -177,8 +192,10 @@ def sharded_weighted_mean(x_local: torch.Tensor, w_local: torch.Tensor, W_total,
     """Weighted mean over all ranks' client rows.
 
     x_local: this rank's client deltas [K_g, P] (unit column stride, may be K_g = 0
-    only if partial_fn handles it); w_local: their float32 weights [K_g] on the same
-    device; W_total: sum of ALL clients' weights (reference semantics, host scalar).
+    only if partial_fn handles it); w_local: their float32 weights [K_g], on the same
+    device or on the host (a numpy array / CPU tensor: then carried in the folds' kernel
+    arguments, FJAGG_HOST_TABLES, when the launches allow it — no upload in front of the
+    step); W_total: sum of ALL clients' weights (reference semantics, host scalar).
     Returns the float32 mean [P] — valid on ``dst`` (every rank with ``all_ranks``).
     partial_fn(x, w, scale, out) computes ``out = fl(sum_k x_k w_k) * scale`` for one
     bucket; the default is the HIP kernel (tests inject the oracle to run on gloo).
@@ -335,7 +352,8 @@ def multi_device_weighted_mean(xs: Sequence[torch.Tensor], ws: Sequence[torch.Te
     """Weighted mean over clients spread across the GPUs of this process.
 
     xs[d]: the client slab [K_d, P] (unit column stride, float32 or bfloat16) on
-    ``comm.devices[d]``; ws[d]: its float32 weights [K_d] there; W_total: the sum of ALL
+    ``comm.devices[d]``; ws[d]: its float32 weights [K_d] there, or every ws[d] on the
+    host (carried in the folds' kernel arguments when they allow it); W_total: the sum of ALL
     clients' weights (tree_util.py:86,95, host value). Each device folds its clients into
     a float32 partial already scaled by f32(1/W); the partials are summed by one grouped
     RCCL reduce per bucket (all-reduce with ``all_devices``). Returns the per-device
@@ -346,6 +364,8 @@ def multi_device_weighted_mean(xs: Sequence[torch.Tensor], ws: Sequence[torch.Te
     n = len(comm)
     if len(xs) != n or len(ws) != n:
         raise ValueError(f"need one slab and one weight vector per device ({n})")
+    ws = [torch.from_numpy(w) if isinstance(w, np.ndarray) else w for w in ws]
+    host_w = all(not w.is_cuda for w in ws)  # host weights: kernel arguments of the folds (FJAGG_HOST_TABLES)
     P = xs[0].shape[1]
     dt = xs[0].dtype
     for d, (x, w, dev) in enumerate(zip(xs, ws, comm.devices)):
@@ -353,8 +373,8 @@ def multi_device_weighted_mean(xs: Sequence[torch.Tensor], ws: Sequence[torch.Te
             raise ValueError(f"device {d}: slabs must be [K_d, {P}] of one float dtype")
         if x.shape[0] and x.stride(1) != 1:
             raise ValueError(f"device {d}: client rows need unit column stride")
-        if x.device != dev or w.device != dev:
-            raise ValueError(f"device {d}: slab and weights must be on {dev}")
+        if x.device != dev or (w.device != dev and not host_w):
+            raise ValueError(f"device {d}: slab and weights must be on {dev} (or every weight vector on the host)")
         if w.dtype != torch.float32 or w.numel() != x.shape[0]:
             raise ValueError(f"device {d}: weights must be float32 [K_d]")
     if outs is None:
@@ -373,10 +393,24 @@ def multi_device_weighted_mean(xs: Sequence[torch.Tensor], ws: Sequence[torch.Te
     scale = float(np.float32(tree_util._inverse(W_total)))
     vp = ctypes.c_void_p * n
     i64 = ctypes.c_int64 * n
-    _lib.call("fjcomm_multi_wsum_dense", comm.handles, n, kernels.dtype_code(dt),
-              vp(*[x.data_ptr() if x.shape[0] else None for x in xs]),
-              i64(*[x.stride(0) if x.shape[0] > 1 else P for x in xs]), i64(*[x.shape[0] for x in xs]), P,
-              vp(*[w.data_ptr() if w.numel() else None for w in ws]), scale, vp(*[o.data_ptr() for o in outs]),
-              edges.ctypes.data, len(spans), -1 if all_devices else int(root), _lib.NONTEMPORAL if nt else 0,
-              vp(*[torch.cuda.current_stream(dev).cuda_stream for dev in comm.devices]))
+    flags = _lib.NONTEMPORAL if nt else 0
+
+    def issue(wv, fl):
+        return _lib.load().fjcomm_multi_wsum_dense(
+            comm.handles, n, kernels.dtype_code(dt), vp(*[x.data_ptr() if x.shape[0] else None for x in xs]),
+            i64(*[x.stride(0) if x.shape[0] > 1 else P for x in xs]), i64(*[x.shape[0] for x in xs]), P,
+            vp(*[w.data_ptr() if w.numel() else None for w in wv]), scale, vp(*[o.data_ptr() for o in outs]),
+            edges.ctypes.data, len(spans), -1 if all_devices else int(root), fl,
+            vp(*[torch.cuda.current_stream(dev).cuda_stream for dev in comm.devices]))
+
+    if host_w:
+        ws = [w.contiguous() for w in ws]
+        rc = issue(ws, flags | _lib.HOST_TABLES)
+        if rc != kernels._EUNSUPPORTED:
+            _lib.check(rc, "fjcomm_multi_wsum_dense")
+            kernels.HOST_WEIGHT_PATHS["kernel_args"] += 1
+            return list(outs)
+        ws = [w.pin_memory().to(dev, non_blocking=True) for w, dev in zip(ws, comm.devices)]
+        kernels.HOST_WEIGHT_PATHS["uploaded"] += 1
+    _lib.check(issue(ws, flags), "fjcomm_multi_wsum_dense")
     return list(outs)

@@ -1,9 +1,10 @@
 """Tensor-level wrappers over the C ABI (include/fjagg.h).
 
-Every function here takes device-resident ``torch`` tensors, launches on torch's
-current HIP stream and returns without synchronising (like a JAX dispatch).
-They are the only route from Python to the kernels; there is no CPU or PyTorch
-fallback: a host tensor, an unsupported dtype or a missing library raises.
+Every function here takes device-resident ``torch`` tensors (only the weights of
+:func:`weighted_sum_dense` may be host arrays), launches on torch's current HIP
+stream and returns without synchronising (like a JAX dispatch). They are the only
+route from Python to the kernels; there is no CPU or PyTorch fallback: host client
+deltas, an unsupported dtype or a missing library raise.
 """
 
 from __future__ import annotations
@@ -15,6 +16,10 @@ import torch
 
 from fedjax_amd import _lib
 
+_EUNSUPPORTED = -3  # FJAGG_EUNSUPPORTED: the launch was refused, nothing was issued
+# how host weights reached the dense folds: in the kernel arguments, or uploaded because
+# the launch was not built that way (tests and bench.py read these)
+HOST_WEIGHT_PATHS = {"kernel_args": 0, "uploaded": 0}
 _CODES = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.int32: _lib.I32}
 
 
@@ -79,7 +84,10 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
     """Fold a client-major slab ``x[K, P]`` (row stride ``x.stride(0)``, unit column
     stride) with per-client weights ``w[K]`` into ``out[P]``.
 
-    ``w`` is float32 (float fold) or int32 (integer fold; int32 ``x`` only).
+    ``w`` is float32 (float fold) or int32 (integer fold; int32 ``x`` only): a device
+    tensor, or host weights (a numpy array or CPU tensor), which then travel in the
+    kernel arguments (``FJAGG_HOST_TABLES``: no upload in front of the fold on the
+    stream) when the library builds that launch, and are uploaded otherwise.
     ``scale`` multiplies the fold at the end (tree_mean's f32(1/W)).
     ``accumulate`` starts the fold from ``out``'s current contents.
     ``reference_bf16`` (bfloat16 ``x`` and ``out``, float32 ``w``): the reference's
@@ -89,7 +97,9 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
     if x.dim() != 2 or x.stride(1) != 1:
         raise ValueError("x must be a [K, P] tensor with unit column stride")
     K, P = x.shape
-    if w.shape != (K,):
+    if isinstance(w, np.ndarray):
+        w = torch.from_numpy(w)
+    if tuple(w.shape) != (K,):
         raise ValueError(f"w must have shape ({K},), got {tuple(w.shape)}")
     acc = _lib.I32 if w.dtype == torch.int32 else _lib.F32
     if w.dtype not in (torch.float32, torch.int32) or not w.is_contiguous():
@@ -109,11 +119,25 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
         out = torch.empty(P, dtype=out_dtype, device=x.device)
     if out.numel() != P or not out.is_contiguous():
         raise ValueError("out must be a contiguous tensor of P elements")
-    dev = _require_device(x, w, out)
+    dev = _require_device(x, out) if not w.is_cuda else _require_device(x, w, out)
     flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
     flags |= (_lib.NONTEMPORAL if nontemporal else 0) | ((variant & 0xFF) << 8)
     flags |= 0 if balanced else _lib.UNBALANCED
     m = {"exact": _lib.MODE_EXACT, "split": _lib.MODE_SPLIT}[mode]
+    ld = x.stride(0) if K > 1 else P
+    sc = float(scale if scale is not None else 1.0)
+    if not w.is_cuda:
+        w = w.contiguous()
+        if m == _lib.MODE_EXACT:
+            rc = _lib.load().fjagg_wsum_dense(dtype_code(x.dtype), acc, dtype_code(out.dtype), x.data_ptr(), ld, K, P,
+                                              w.data_ptr(), sc, out.data_ptr(), flags | _lib.HOST_TABLES, m, None, 0,
+                                              _stream_handle(dev))
+            if rc != _EUNSUPPORTED:
+                _lib.check(rc, "fjagg_wsum_dense")
+                HOST_WEIGHT_PATHS["kernel_args"] += 1
+                return out
+        w = w.pin_memory().to(dev, non_blocking=True)  # not built with kernel-argument weights
+        HOST_WEIGHT_PATHS["uploaded"] += 1
     ws_ptr, ws_bytes = None, 0
     if m == _lib.MODE_SPLIT:
         need = split_workspace_bytes(K, P)
@@ -121,10 +145,8 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
             if workspace is None:
                 workspace = torch.empty(need, dtype=torch.uint8, device=dev)
             ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
-    ld = x.stride(0) if K > 1 else P
     _lib.call("fjagg_wsum_dense", dtype_code(x.dtype), acc, dtype_code(out.dtype), x.data_ptr(), ld,
-              K, P, w.data_ptr(), float(scale if scale is not None else 1.0), out.data_ptr(), flags,
-              m, ws_ptr, ws_bytes, _stream_handle(dev))
+              K, P, w.data_ptr(), sc, out.data_ptr(), flags, m, ws_ptr, ws_bytes, _stream_handle(dev))
     return out
 
 

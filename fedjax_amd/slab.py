@@ -74,18 +74,23 @@ class ClientDeltaSlab:
         return self
 
     # ------------------------------------------------------------- aggregation
-    def weight_vector(self, weights: Sequence) -> torch.Tensor:
-        """float32 weights f32(w_k) on the device (pinned H2D, stream-ordered)."""
+    def host_weights(self, weights: Sequence) -> np.ndarray:
+        """float32 weights f32(w_k) on the host."""
         if len(weights) != self.num_clients:
             raise ValueError(f"need {self.num_clients} weights, got {len(weights)}")
-        w = np.array([np.float32(tree_util._host_weight(x)) for x in weights], dtype=np.float32)
-        return torch.from_numpy(w).pin_memory().to(self.device, non_blocking=True)
+        return np.array([np.float32(tree_util._host_weight(x)) for x in weights], dtype=np.float32)
+
+    def weight_vector(self, weights: Sequence) -> torch.Tensor:
+        """float32 weights f32(w_k) on the device (pinned H2D, stream-ordered)."""
+        return torch.from_numpy(self.host_weights(weights)).pin_memory().to(self.device, non_blocking=True)
 
     def weighted_sum_flat(self, w_dev: torch.Tensor, *, scale=None, out: Optional[torch.Tensor] = None,
                           accumulate: bool = False, mode: str = "exact",
                           nontemporal: Optional[bool] = None, variant: int = 0,
                           reference_bf16: Optional[bool] = None) -> torch.Tensor:
-        """Flat P-element fold of the slab with device weights (one launch). A bfloat16
+        """Flat P-element fold of the slab (one launch). ``w_dev``: device weights, or host
+        float32 weights (carried in the kernel arguments when the launch allows it, see
+        :func:`kernels.weighted_sum_dense`). A bfloat16
         slab folds with the reference's bf16 arithmetic when ``reference_bf16`` (default:
         ``tree_util.set_bf16_semantics("reference")`` is in force and mode is exact)."""
         nbytes = self.rows.numel() * self.rows.element_size()
@@ -113,7 +118,7 @@ class ClientDeltaSlab:
             # no fused-norm kernel for the bf16 reference fold: the mean, then the norms
             if mode != "exact":
                 raise ValueError("fused norms run in exact mode")
-            flat = self.weighted_sum_flat(self.weight_vector(weights), scale=scale, out=out)
+            flat = self.weighted_sum_flat(self.host_weights(weights), scale=scale, out=out)
             return self.unflatten(flat), self.l2_norms()
         if with_norms:
             if mode != "exact":
@@ -123,7 +128,7 @@ class ClientDeltaSlab:
                 self.rows, self.weight_vector(weights), scale=float(np.float32(scale)), out=out,
                 nontemporal=nbytes >= tree_util.NONTEMPORAL_MIN_BYTES)
             return self.unflatten(flat), torch.sqrt(l2sq)
-        flat = self.weighted_sum_flat(self.weight_vector(weights), scale=scale, out=out, mode=mode)
+        flat = self.weighted_sum_flat(self.host_weights(weights), scale=scale, out=out, mode=mode)
         return self.unflatten(flat)
 
     def l2_norms(self) -> torch.Tensor:

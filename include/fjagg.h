@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define FJAGG_ABI_VERSION 2
+#define FJAGG_ABI_VERSION 3
 
 /* element types */
 enum fjagg_dtype {
@@ -68,7 +68,20 @@ enum fjagg_flags {
   FJAGG_NARROW = 1 << 5,      /* pytree path, plan AND launch: 64-element stripes per workgroup,
                                  client rows staged through LDS (k_ptrs_narrow) — for small
                                  leaves and many clients; fold only (no fused norms) */
+  FJAGG_HOST_TABLES = 1 << 6, /* the weights (and on the pytree path the plan image) are HOST
+                                 pointers: the launch copies them into the kernel arguments, so
+                                 no upload or staging copy runs on the stream before the fold and
+                                 the caller's buffers are free again when the call returns.
+                                 Dense: K <= FJAGG_KARG_MAX_WEIGHTS, (in, acc, out) one of
+                                 (F32,F32,F32) (BF16,F32,BF16) (BF16,F32,F32), not FJAGG_NARROW
+                                 shapes. Pytree: (F32,F32,F32), 16-byte units (no FJAGG_UNALIGNED,
+                                 no FJAGG_NARROW), fjagg_karg_image_words(K, L, nblk) <=
+                                 FJAGG_KARG_MAX_WORDS. Anything else returns FJAGG_EUNSUPPORTED
+                                 (nothing launched): upload the tables and call without the flag. */
 };
+/* kernel-argument capacity of FJAGG_HOST_TABLES launches */
+#define FJAGG_KARG_MAX_WEIGHTS 1024 /* dense path: 4 KiB of weights */
+#define FJAGG_KARG_MAX_WORDS 3584   /* pytree path: 28 KiB = image words + ceil(K/2) weight words */
 /* bits 8..15 of flags select a kernel shape of the dense path: 0 = automatic,
  * 1..11 = fixed (units per lane, clients in flight, waves/SIMD) for tuning; see fjagg.hip */
 #define FJAGG_VARIANT(v) (((v)&0xff) << 8)
@@ -143,6 +156,10 @@ int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, c
 int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev,
                     int L, int64_t K, int64_t nblk, const void* w_dev, float scale,
                     int flags, void* stream);
+/* int64 words a FJAGG_HOST_TABLES pytree launch carries in its kernel arguments: the
+ * image (K*L + 2*L + 2*nblk words; image_dev and w_dev are then host pointers) and the
+ * K f32 weights packed two per word. Compare with FJAGG_KARG_MAX_WORDS. */
+int64_t fjagg_karg_image_words(int64_t K, int L, int64_t nblk);
 
 /*
  * fjagg_wsum_ptrs fused with every client's squared L2 norm over ALL L leaves, in the

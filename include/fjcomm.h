@@ -58,8 +58,10 @@ int fjcomm_destroy(void* comm);
  * it afterwards sees the reduced result (valid on root, or everywhere with root < 0).
  * fold_events: NULL, or 2*nbuckets events made by fjagg_event_create; the fold of
  * bucket b is bracketed by fold_events[2b], fold_events[2b+1] on `stream`.
- * K may be 0 (the rank contributes zeros). flags: FJAGG_NONTEMPORAL and the
- * FJAGG_VARIANT bits of fjagg_wsum_dense.
+ * K may be 0 (the rank contributes zeros). flags: FJAGG_NONTEMPORAL, the
+ * FJAGG_VARIANT bits of fjagg_wsum_dense, and FJAGG_HOST_TABLES (w_dev is then a HOST
+ * float[K] carried in each bucket fold's kernel arguments; every bucket is checked
+ * before the first launch and FJAGG_EUNSUPPORTED means nothing was issued).
  * Replaces: the gather-to-devices[0] + tree_mean of for_each_client.py:351-353 and
  * tree_util.py:85-96 for one round.
  */
@@ -98,7 +100,8 @@ int fjcomm_sharded_wsum_dense_edges(void* comm, int in_dtype, const void* x_dev,
  * when root < 0), bucket by bucket over `edges` as in fjcomm_sharded_wsum_dense_edges.
  * The collectives of one bucket are one ncclGroupStart/End group (required when one
  * thread drives several ranks). streams[d] waits for the last collective of device d.
- * K[d] may be 0 (device d contributes zeros).
+ * K[d] may be 0 (device d contributes zeros). flags as fjcomm_sharded_wsum_dense
+ * (with FJAGG_HOST_TABLES, w_dev[d] are host arrays).
  */
 #define FJCOMM_MAX_DEVICES 16
 int fjcomm_init_all(void** comms, int ndev, const int* devs);

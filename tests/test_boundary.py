@@ -67,6 +67,37 @@ def test_host_side_validation_without_gpu():
         _lib.call("fjagg_wsum_ptrs", _lib.F32, _lib.F32, _lib.F32, None, 1, 1, 5, None, 1.0, 0, None)
 
 
+def test_host_tables_refused_before_any_launch():
+    """FJAGG_HOST_TABLES launches the library does not build are refused on the host with
+    FJAGG_EUNSUPPORTED (the callers then upload the tables); no GPU call happens first."""
+    lib = _lib.load()
+    w = np.ones(2000, np.float32)
+    dense = [  # (in, acc, out, K, P, mode, flags)
+        (_lib.F32, _lib.F32, _lib.F32, 2000, 200_000, 0, 0),           # K > FJAGG_KARG_MAX_WEIGHTS
+        (_lib.F32, _lib.F32, _lib.F32, 64, 20_000, 0, 0),              # the narrow kernel's shape
+        (_lib.F32, _lib.F32, _lib.F32, 64, 200_000, 1, 0),             # split mode
+        (_lib.F32, _lib.F32, _lib.F32, 64, 200_000, 0, 1 << 8),        # a tuning variant
+        (_lib.I32, _lib.I32, _lib.I32, 64, 200_000, 0, 0),             # integer fold
+        (_lib.BF16, _lib.BF16, _lib.BF16, 64, 200_000, 0, 0),          # bf16 reference fold
+        (_lib.F32, _lib.F32, _lib.BF16, 64, 200_000, 0, 0),
+    ]
+    for in_c, acc, out_c, K, P, mode, fl in dense:
+        rc = lib.fjagg_wsum_dense(in_c, acc, out_c, 16, P, K, P, w.ctypes.data, 1.0, 16, fl | _lib.HOST_TABLES, mode,
+                                  None, 0, None)
+        assert rc == -3 and b"HOST_TABLES" in lib.fjagg_last_error(), (in_c, acc, out_c, K, P, mode, fl)
+    img = np.zeros(64, np.int64)
+    for in_c, out_c, fl in ((_lib.BF16, _lib.BF16, 0), (_lib.F32, _lib.F32, _lib.NARROW),
+                            (_lib.F32, _lib.F32, _lib.UNALIGNED)):
+        rc = lib.fjagg_wsum_ptrs(in_c, _lib.F32, out_c, img.ctypes.data, 2, 4, 3, w.ctypes.data, 1.0,
+                                 fl | _lib.HOST_TABLES, None)
+        assert rc == -3, (in_c, fl)
+    assert lib.fjagg_karg_image_words(128, 8, 256) == 128 * 8 + 16 + 512 + 64
+    assert lib.fjagg_karg_image_words(4000, 1, 10) > _lib.KARG_MAX_WORDS
+    rc = lib.fjagg_wsum_ptrs(_lib.F32, _lib.F32, _lib.F32, img.ctypes.data, 1, 4000, 10, w.ctypes.data, 1.0,
+                             _lib.HOST_TABLES, None)
+    assert rc == -3 and b"words" in lib.fjagg_last_error()
+
+
 def test_split_workspace_sizing():
     assert kernels.split_workspace_bytes(1024, 4 * 1024 * 1024) == 0  # exact path fills the chip
     ws = kernels.split_workspace_bytes(1024, 16384)

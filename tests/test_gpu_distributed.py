@@ -16,6 +16,7 @@ from oracle import tree_util_ref as ref
 
 pytestmark = pytest.mark.gpu
 K, P = 48, 70001
+P2 = (1 << 20) + 3  # host-weight runs: buckets too wide for the narrow kernel (which takes device weights)
 
 
 def _port():
@@ -114,6 +115,20 @@ def _native_worker(port, q):
             torch.cuda.synchronize()
             ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(0, 2 * nb, 2)]
             res[(buckets, all_ranks)] = (y.cpu().numpy(), ms)
+        # host weights (FJAGG_HOST_TABLES): the bucket folds carry them in their kernel arguments
+        x2 = torch.empty(K, P2 + 1, dtype=torch.float32, device=dev)[:, :P2]
+        kernels.fill_synth(x2, seed=11)
+        before = dict(kernels.HOST_WEIGHT_PATHS)
+        for buckets, all_ranks in ((1, False), ((4, 2, 1), True)):
+            y = fd.sharded_weighted_mean(x2, np.float32(weights), W, buckets=buckets, all_ranks=all_ranks, comm=comm)
+            torch.cuda.synchronize()
+            res[("host", buckets, all_ranks)] = (y.cpu().numpy(), [1.0])
+        # narrow buckets refuse kernel-argument weights: uploaded instead, same bits
+        y = fd.sharded_weighted_mean(x, np.float32(weights), W, buckets=3, comm=comm)
+        torch.cuda.synchronize()
+        res[("host-narrow", 3, False)] = (y.cpu().numpy(), [1.0])
+        res["host_paths"] = {k: v - before[k] for k, v in kernels.HOST_WEIGHT_PATHS.items()}
+        del x2
         xb = torch.empty(K, P, dtype=torch.bfloat16, device=dev)
         kernels.fill_synth(xb, seed=9)
         yb = fd.sharded_weighted_mean(xb, wl, W, buckets=2, comm=comm)
@@ -148,6 +163,11 @@ def test_native_rccl_pipeline_world1(cuda, coracle):
     x = coracle.synth_f32(K, P, seed=9)
     r = ref.mean_scale(weights)
     want = coracle.wsum_f32(x, np.float32(weights), scale=r)
+    assert res.pop("host_paths") == {"kernel_args": 2, "uploaded": 1}
+    want2 = coracle.wsum_f32(coracle.synth_f32(K, P2, seed=11), np.float32(weights), scale=r)
+    for key in [k for k in res if k[0] == "host"]:
+        y, _ = res.pop(key)
+        assert np.array_equal(y.view(np.uint32), want2.astype(np.float32).view(np.uint32)), key
     for key, (y, ms) in res.items():
         # one rank: the partial is the exact fold (per-element, so bucketing is invisible)
         assert np.array_equal(y.view(np.uint32), want.astype(np.float32).view(np.uint32)), key
@@ -178,6 +198,15 @@ def _multi_device_worker(q):
         outs = fd.multi_device_weighted_mean([x], [wl], W, comm=comm, buckets=buckets, all_devices=alld)
         torch.cuda.synchronize()
         res[(fd.bucket_name(buckets), alld)] = outs[0].cpu().numpy()
+    x2 = torch.empty(K, P2 + 1, dtype=torch.float32, device=dev)[:, :P2]
+    kernels.fill_synth(x2, seed=11)
+    before = dict(kernels.HOST_WEIGHT_PATHS)
+    for buckets in (1, (4, 2, 1)):  # host weights: kernel arguments of every device's folds
+        outs = fd.multi_device_weighted_mean([x2], [np.float32(weights)], W, comm=comm, buckets=buckets)
+        torch.cuda.synchronize()
+        res[("host", fd.bucket_name(buckets))] = outs[0].cpu().numpy()
+    res["host_paths"] = {k: v - before[k] for k, v in kernels.HOST_WEIGHT_PATHS.items()}
+    del x2
     z = fd.multi_device_weighted_mean([x[:0]], [wl[:0]], W, comm=comm)[0]  # a device without clients
     torch.cuda.synchronize()
     errs = []
@@ -207,6 +236,11 @@ def test_single_process_multi_device_ndev1(cuda, coracle):
     weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
     x = coracle.synth_f32(K, P, seed=9)
     want = coracle.wsum_f32(x, np.float32(weights), scale=ref.mean_scale(weights))
+    assert res.pop("host_paths") == {"kernel_args": 2, "uploaded": 0}
+    want2 = coracle.wsum_f32(coracle.synth_f32(K, P2, seed=11), np.float32(weights), scale=ref.mean_scale(weights))
+    for key in [k for k in res if k[0] == "host"]:
+        y = res.pop(key)
+        assert np.array_equal(y.view(np.uint32), want2.astype(np.float32).view(np.uint32)), key
     for key, y in res.items():
         assert np.array_equal(y.view(np.uint32), want.astype(np.float32).view(np.uint32)), key
     assert np.all(z == 0)

@@ -11,6 +11,9 @@
 #   narrow_tree   k_ptrs_narrow vs k_ptrs on small models (FJAGG_NARROW_MAX_BYTES A/B, profiles/r02k_*)
 #   ptrs_u        k_ptrs at configs[1] with 4 / 8 / 16 clients in flight (FJAGG_PTRS_U, an experiment build
 #                 of k_ptrs not kept in the tree; profiles/r02n_ptrs_u)
+#   karg          FJAGG_HOST_TABLES: parity tests, tree_mean wall at configs[1], bench c2 / c3 / N=8 shard
+#                 rehearsal with kernel-argument weights vs uploaded weights, kernel trace of the
+#                 tree_mean loop                                       (profiles/r02r_*)
 # Every GPU step runs under its own time limit; the script stops at the first failure.
 set -u
 STUDY=${1:?study name}
@@ -80,6 +83,26 @@ case "$STUDY" in
     done
     python tools/pmc_table.py k_ptrs $O/table.json $O/u4_views $O/u4_clones $O/u8_views $O/u8_clones \
       $O/u16_views $O/u16_clones | grep -E '"u|duration'
+    ;;
+  karg)
+    timeout -k 10 600 $PT tests/test_gpu_host_tables.py tests/test_gpu_distributed.py tests/test_boundary.py \
+      > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python tools/time_pytree.py > $O/time_pytree.jsonl 2> $O/time_pytree.err || die time_pytree
+    cat $O/time_pytree.jsonl
+    for wl in c2 c3; do
+      for dw in "" "--device-weights"; do
+        timeout -k 10 300 python bench.py --workload $wl --steps 50 --warmup 10 --no-cpu-baseline $dw \
+          > $O/bench_${wl}${dw:+_dw}.json 2> $O/bench_${wl}${dw:+_dw}.err || die "bench $wl $dw"
+      done
+    done
+    for dw in "" "--device-weights"; do
+      timeout -k 10 300 python bench.py --rehearse-shard 8 --steps 50 --warmup 10 --buckets 1 $dw \
+        > $O/shard8${dw:+_dw}.json 2> $O/shard8${dw:+_dw}.err || die "shard8 $dw"
+    done
+    grep -h -o '"ms_per_step": [0-9.]*\|"workload": "[^"]*"\|"weights_path": [^}]*}\|"mean_launch_ms": [0-9.]*' \
+      $O/bench_*.json $O/shard8*.json
+    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $O/trace -o run --output-format csv -- \
+      python tools/time_pytree.py > $O/trace.log 2>&1 || die trace
     ;;
   *) echo "unknown study $STUDY"; exit 2 ;;
 esac
