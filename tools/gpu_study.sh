@@ -33,7 +33,7 @@ case "$STUDY" in
     rm -f $O/prof/run_kernel_trace.csv
     ;;
   placement)
-    for m in views clones rows2m bigseg; do
+    for m in ${MODES:-views clones rows2m bigseg expseg}; do
       timeout -s KILL 90 rocprofv3 --kernel-trace -d $O/$m/trace -o run --output-format csv -- \
         python tools/probe_ptrs_pmc.py $m 20 > $O/$m.log 2>&1 || die "trace $m"
       timeout -s KILL 90 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
@@ -45,7 +45,7 @@ case "$STUDY" in
       timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_RDREQ TCC_TAG_STALL_sum TCC_EA0_RDREQ_DRAM_sum \
         -d $O/$m/pmcC -o run --output-format csv -- python tools/probe_ptrs_pmc.py $m 10 >> $O/$m.log 2>&1 || die "pmcC $m"
     done
-    python tools/pmc_table.py k_ptrs $O/table.json $O/views $O/clones $O/rows2m $O/bigseg
+    python tools/pmc_table.py k_ptrs $O/table.json $(for m in ${MODES:-views clones rows2m bigseg expseg}; do echo $O/$m; done)
     ;;
   quant)
     B="python tools/bench_compression.py --only uniform,terngrad --rounds 3 --warmup 1 --cpu-sample 0"

@@ -6,7 +6,11 @@ next #5): the same 128 x EMNIST-CNN deltas folded by tree_mean with the clients'
   rows2m  - one allocation, every client's leaves packed at its own 2 MiB-aligned offset
             (the clones' alignment inside a single allocation);
   bigseg  - one allocation per client, each made 32 MiB (above the caching allocator's
-            20 MiB segments, so each is its own hipMalloc).
+            20 MiB segments, so each is its own hipMalloc);
+  expseg  - one allocation per (client, leaf) like clones, under torch's expandable-segments
+            allocator (PYTORCH_HIP_ALLOC_CONF=expandable_segments:True, set before torch loads):
+            the caller's allocation pattern unchanged, the leaves mapped into one growing
+            virtual range in 2 MiB pages.
 
 usage: python tools/probe_ptrs_pmc.py MODE [calls]   (run under rocprofv3 --kernel-trace or
 --pmc; every k_ptrs dispatch of the run is of MODE's placement)
@@ -14,6 +18,9 @@ usage: python tools/probe_ptrs_pmc.py MODE [calls]   (run under rocprofv3 --kern
 import os
 import sys
 
+if len(sys.argv) > 1 and sys.argv[1] == "expseg":
+    os.environ["PYTORCH_HIP_ALLOC_CONF"] = "expandable_segments:True"
+    os.environ["PYTORCH_CUDA_ALLOC_CONF"] = "expandable_segments:True"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import torch
@@ -49,7 +56,7 @@ def main(mode, calls=20, K=128):
     per = (P + 4 * 8 + 3) // 4 * 4
     if mode == "views":
         clients = [slab.client(k) for k in range(K)]
-    elif mode == "clones":
+    elif mode in ("clones", "expseg"):
         clients = [tmap(lambda v: v.clone(), slab.client(k)) for k in range(K)]
     elif mode == "rows2m":
         stride = -(-per * 4 // (2 << 20)) * (2 << 20) // 4
