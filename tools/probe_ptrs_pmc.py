@@ -10,7 +10,8 @@ next #5): the same 128 x EMNIST-CNN deltas folded by tree_mean with the clients'
   expseg  - one allocation per (client, leaf) like clones, under torch's expandable-segments
             allocator (PYTORCH_HIP_ALLOC_CONF=expandable_segments:True, set before torch loads):
             the caller's allocation pattern unchanged, the leaves mapped into one growing
-            virtual range in 2 MiB pages.
+            virtual range. This torch build refuses it on ROCm (a warning; the run is then
+            the clones case, profiles/r02s_placement/).
 
 usage: python tools/probe_ptrs_pmc.py MODE [calls]   (run under rocprofv3 --kernel-trace or
 --pmc; every k_ptrs dispatch of the run is of MODE's placement)
