@@ -13,8 +13,9 @@
 //                                  pass: a lane owns the element PAIR (i, i + h) that one
 //                                  threefry2x32 call produces (JAX's counter layout), walks
 //                                  the clients in order and keeps the running sum in a
-//                                  register. Threefry costs ~40 VALU ops per element, so
-//                                  this kernel is VALU-bound, not HBM-bound;
+//                                  register. Threefry costs ~31 VALU ops per element (of
+//                                  ~58), so this kernel is VALU-bound, not HBM-bound
+//                                  (DESIGN.md §3c);
 //   k_rademacher                   the rotation signs, one bit per element, packed with
 //                                  wave ballots; computed once per key and read by both the
 //                                  forward and the inverse rotation;
@@ -79,9 +80,8 @@ __host__ __device__ inline uint32_t rotl32(uint32_t x, int r) { return (x << r) 
 #define FJ_TF_ROT0 FJ_TF_ROUND(13) FJ_TF_ROUND(15) FJ_TF_ROUND(26) FJ_TF_ROUND(6)
 #define FJ_TF_ROT1 FJ_TF_ROUND(17) FJ_TF_ROUND(29) FJ_TF_ROUND(16) FJ_TF_ROUND(24)
 
-// Threefry-2x32 with 20 rounds and JAX's key schedule (jax/_src/prng.py).
-__host__ __device__ inline void threefry(uint32_t k0, uint32_t k1, uint32_t& x0, uint32_t& x1) {
-  const uint32_t k2 = k0 ^ k1 ^ 0x1BD11BDAu;
+// Threefry-2x32 with 20 rounds and JAX's key schedule (jax/_src/prng.py); k2 = k0 ^ k1 ^ C.
+__host__ __device__ inline void threefry_k(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t& x0, uint32_t& x1) {
   x0 += k0;
   x1 += k1;
   FJ_TF_ROT0 x0 += k1; x1 += k2 + 1u;
@@ -90,9 +90,15 @@ __host__ __device__ inline void threefry(uint32_t k0, uint32_t k1, uint32_t& x0,
   FJ_TF_ROT1 x0 += k1; x1 += k2 + 4u;
   FJ_TF_ROT0 x0 += k2; x1 += k0 + 5u;
 }
+__host__ __device__ inline void threefry(uint32_t k0, uint32_t k1, uint32_t& x0, uint32_t& x1) {
+  threefry_k(k0, k1, k0 ^ k1 ^ 0x1BD11BDAu, x0, x1);
+}
 
 // jax.random.uniform's bits -> [0, 1): bitcast((b >> 9) | 1.0f) - 1
-__device__ inline float bits_to_unit(uint32_t b) { return __uint_as_float((b >> 9) | 0x3f800000u) - 1.0f; }
+// ((b >> 9) | 0x3f800000) is one v_alignbit: the low word of (0x7f : b) >> 9.
+__device__ inline float bits_to_unit(uint32_t b) {
+  return __uint_as_float(__builtin_amdgcn_alignbit(0x7fu, b, 9u)) - 1.0f;
+}
 
 // ------------------------------------------------------------------ f32 helpers
 // Branch-free (the branchy forms compiled to exec-mask regions inside the per-element loop).
@@ -100,7 +106,10 @@ __device__ inline float bits_to_unit(uint32_t b) { return __uint_as_float((b >> 
 __device__ inline float nan_to_num(float x) { return x != x ? 0.0f : __builtin_amdgcn_fmed3f(x, -FLT_MAX, FLT_MAX); }
 // numpy's maximum(0, minimum(nan_to_num(a), 1)) (first argument wins ties, so -0 -> +0):
 // NaN and everything <= 0 give +0, +inf gives 1.
-__device__ inline float clamp01_nan(float a) { return a > 0.0f ? fminf(a, 1.0f) : 0.0f; }
+// maxnum(NaN, 0) = 0, so NaN -> +0 as well; -0 may stay -0, which no caller can tell from
+// +0 (every use compares u > a or scales a by a positive constant and takes floor/ceil of
+// a value that then indexes level 0).
+__device__ inline float clamp01_nan(float a) { return fminf(fmaxf(a, 0.0f), 1.0f); }
 __device__ inline float xla_sign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x); }
 // correctly rounded a / b given r = RN_f64(1 / b) (see the header comment)
 __device__ inline float div_by(float a, double r) { return (float)((double)a * r); }
@@ -331,6 +340,7 @@ struct UniformQ {
   float lm1;
   double rcp_lm1;
   static constexpr bool kTable = false;
+  static constexpr bool kPair = false;
   // uniform_stochastic_quantize (compression.py:84-97); *level = chosen level index
   __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float* level) const {
     const float a = clamp01_nan(div_by(v - p.vmin, p.rcp_range));
@@ -353,43 +363,77 @@ struct UniformQ {
 // 2^-55 in magnitude unless fl = 0, where num = a >= 0 and any threshold below 2^-23
 // compares like 0 against u (u is 0 or >= 2^-23). When ce == fl both branches pick the
 // same level, so thr (and the unused rd[lm1] = 0) does not matter; no nan_to_num needed.
+// One 16-byte entry per level, {lev[j], lev[j+1], rd[j]} (lev[lm1+1] := lev[lm1]), so a
+// lane reads everything its element needs with one ds_read_b128 at j << 4.
 constexpr int kLevelTable = 4096;
+typedef float f2 __attribute__((ext_vector_type(2)));
 struct UniformTQ {
   float lm1;
   int num_levels;
   double rcp_lm1;
-  const float* lev;   // LDS, lm1 + 1 entries (lm1 + 2 with a trailing copy)
-  const double* rd;   // LDS, lm1 + 1 entries
+  const uint4* tab;  // LDS, num_levels entries
   static constexpr bool kTable = true;
-  static size_t lds_bytes(int num_levels) { return (size_t)(num_levels + 1) * (sizeof(double) + sizeof(float)) + 16; }
+  static size_t lds_bytes(int num_levels) { return (size_t)num_levels * sizeof(uint4) + 16; }
   __device__ inline void build(void* smem) {
-    double* r = reinterpret_cast<double*>(smem);
-    float* lv = reinterpret_cast<float*>(r + num_levels + 1);
+    uint4* e = reinterpret_cast<uint4*>(smem);
     const int top = num_levels - 1;  // == lm1
-    for (int j = threadIdx.x; j <= top + 1; j += blockDim.x) lv[j] = div_by((float)(j <= top ? j : top), rcp_lm1);
+    for (int j = threadIdx.x; j <= top; j += blockDim.x) e[j].x = __float_as_uint(div_by((float)j, rcp_lm1));
     __syncthreads();
-    for (int j = threadIdx.x; j <= top; j += blockDim.x) r[j] = j < top ? 1.0 / (double)(lv[j + 1] - lv[j]) : 0.0;
+    for (int j = threadIdx.x; j <= top; j += blockDim.x) {
+      const float lv = __uint_as_float(e[j].x), nx = j < top ? __uint_as_float(e[j + 1].x) : lv;
+      const double r = j < top ? 1.0 / (double)(nx - lv) : 0.0;
+      const uint64_t rb = (uint64_t)__double_as_longlong(r);
+      e[j].y = __float_as_uint(nx);
+      e[j].z = (uint32_t)rb;
+      e[j].w = (uint32_t)(rb >> 32);
+    }
     __syncthreads();
-    lev = lv;
-    rd = r;
+    tab = e;
   }
   __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float* level) const {
     const float a = clamp01_nan(div_by(v - p.vmin, p.rcp_range));
     const float s = a * lm1;
     const float fl = floorf(s), ce = ceilf(s);
-    const int j = (int)fl;
-    const float v_floor = lev[j], v_next = lev[j + 1];  // lev has a trailing entry
+    const uint4 t = tab[(int)fl];
+    const float v_floor = __uint_as_float(t.x), v_next = __uint_as_float(t.y);
+    const double rd = __longlong_as_double((long long)(((uint64_t)t.w << 32) | t.z));
     const float v_ceil = ce != fl ? v_next : v_floor;
-    const float thr = (float)((double)(a - v_floor) * rd[j]);
+    const float thr = (float)((double)(a - v_floor) * rd);
     const bool down = u > thr;
     *level = down ? fl : ce;
     const float q = down ? v_floor : v_ceil;
+    return p.vmin + q * p.range;
+  }
+  // The same for a lane's element pair: the ops that take both elements through the same
+  // constant (v - vmin, a * lm1, a - v_floor, vmin + q * range) are packed f32 ops.
+  static constexpr bool kPair = true;
+  __device__ inline f2 pair(f2 v, f2 u, const fjcomp_qparams& p, float* l0, float* l1) const {
+    const f2 d = v - p.vmin;
+    const f2 a = {clamp01_nan(div_by(d.x, p.rcp_range)), clamp01_nan(div_by(d.y, p.rcp_range))};
+    const f2 s = a * lm1;
+    const f2 fl = {floorf(s.x), floorf(s.y)}, ce = {ceilf(s.x), ceilf(s.y)};
+    const uint4 t0 = tab[(int)fl.x], t1 = tab[(int)fl.y];
+    const f2 v_floor = {__uint_as_float(t0.x), __uint_as_float(t1.x)};
+    const f2 v_ceil = {ce.x != fl.x ? __uint_as_float(t0.y) : v_floor.x, ce.y != fl.y ? __uint_as_float(t1.y) : v_floor.y};
+    const double rd0 = __longlong_as_double((long long)(((uint64_t)t0.w << 32) | t0.z));
+    const double rd1 = __longlong_as_double((long long)(((uint64_t)t1.w << 32) | t1.z));
+    const f2 num = a - v_floor;
+    const bool down0 = u.x > (float)((double)num.x * rd0), down1 = u.y > (float)((double)num.y * rd1);
+    *l0 = down0 ? fl.x : ce.x;
+    *l1 = down1 ? fl.y : ce.y;
+    const f2 q = {down0 ? v_floor.x : v_ceil.x, down1 ? v_floor.y : v_ceil.y};
     return p.vmin + q * p.range;
   }
 };
 
 struct BinaryQ {
   static constexpr bool kTable = false;
+  static constexpr bool kPair = true;
+  template <class Self>
+  __device__ static inline f2 pair_of(const Self& q, f2 v, f2 u, const fjcomp_qparams& p) {
+    return f2{q(v.x, u.x, p, nullptr), q(v.y, u.y, p, nullptr)};
+  }
+  __device__ inline f2 pair(f2 v, f2 u, const fjcomp_qparams& p, float*, float*) const { return pair_of(*this, v, u, p); }
   // binary_stochastic_quantize (compression.py:58-63)
   __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float*) const {
     const float a = clamp01_nan(div_by(v - p.vmin, p.rcp_range));
@@ -399,6 +443,12 @@ struct BinaryQ {
 
 struct TernQ {
   static constexpr bool kTable = false;
+  static constexpr bool kPair = true;
+  template <class Self>
+  __device__ static inline f2 pair_of(const Self& q, f2 v, f2 u, const fjcomp_qparams& p) {
+    return f2{q(v.x, u.x, p, nullptr), q(v.y, u.y, p, nullptr)};
+  }
+  __device__ inline f2 pair(f2 v, f2 u, const fjcomp_qparams& p, float*, float*) const { return pair_of(*this, v, u, p); }
   // terngrad_quantize (compression.py:323-336) with binary_stochastic_quantize(|v|, 0, vmax)
   __device__ inline float operator()(float v, float u, const fjcomp_qparams& p, float*) const {
     const float vc = (fabsf(v) > p.thr) ? p.thr * xla_sign(v) : v;
@@ -425,16 +475,16 @@ __global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* 
     quant.build(qtab);
   }
   const int64_t n = leaf_n[l], h = (n + 1) >> 1;
-  const int64_t i = (b - prefix[l]) * kQThreads + threadIdx.x;
+  const int64_t i0 = (b - prefix[l]) * kQThreads, i = i0 + threadIdx.x;
   const bool valid = i < h, second = i + h < n;
-  // Offsets every lane loads unconditionally (masked lanes re-read an element of the
-  // leaf): no branch around the loads, so waiting for one group's deltas never waits
-  // for the next group's as well.
-  const int64_t ia = valid ? i : 0, ib = second ? i + h : ia;
-  // Pointers read from the tables are generic: cast to the global address space, so
-  // that loads are global_load. A FLAT load may also touch LDS, so while one is pending
-  // the compiler waits with vmcnt(0) and that would drain the next group's loads too.
-  typedef __attribute__((address_space(1))) const float GFloat;
+  // Deltas are read with buffer loads: per client, two descriptors (this block's first
+  // element, and the element h further) built on the scalar unit from the row pointer,
+  // and one loop-invariant lane offset, so a load costs no address VALU. Every lane loads
+  // unconditionally (no branch around the loads, so waiting for one group's deltas never
+  // waits for the next group's as well); lanes past the leaf read zeros (range check).
+  const uint32_t lane_off = threadIdx.x * 4u;
+  const int lim_a = (int)((n - i0) * 4 < 0x7fffffffll ? (n - i0) * 4 : 0x7fffffffll);
+  const int lim_b = (int)((n - i0 - h) * 4 < 0x7fffffffll ? (n - i0 - h) * 4 : 0x7fffffffll);
   typedef __attribute__((address_space(1))) float GFloatOut;
   GFloatOut* out = (GFloatOut*)out_ptrs[l];
   const bool accumulate = flags & FJAGG_ACCUMULATE;
@@ -445,35 +495,62 @@ __global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* 
   }
   __shared__ int32_t sh[HIST ? kHistLdsBins : 1];
   const bool lds_hist = HIST && nbins <= kHistLdsBins;
-  // A lane walks all K clients, so one dependent HBM round trip per client would bound
-  // the kernel. The deltas of the next kQGroup clients are loaded before this group's
-  // threefry draws and quantizers run, which hide their latency. Fold order unchanged.
+  // Per-client constants of this leaf (row pointer, key, weight, quantizer constants) are
+  // staged in LDS, kQThreads clients at a time, by one coalesced pass of the block: read
+  // straight from the (client, leaf) tables with scalar loads, every client cost a
+  // scalar-cache miss and a wait in every wave (the rows of one leaf are L entries apart).
+  struct QClient {
+    uint64_t ptr;
+    uint32_t k0, k1, k2, wbits;
+    fjcomp_qparams p;
+  };
+  __shared__ QClient qc[kQThreads];
   constexpr int G = kQGroup;
-  auto fetch = [&](int64_t kg, float (&a)[G], float (&c)[G]) {
+  // A lane walks all K clients, so one dependent HBM round trip per client would bound
+  // the kernel. The deltas of the next G clients are loaded before this group's threefry
+  // draws and quantizers run, which hide their latency. Fold order unchanged.
+  auto fetch = [&](int64_t j, int64_t jn, float (&a)[G], float (&c)[G]) {
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-      const int64_t k = kg + u < K ? kg + u : K - 1;
-      const GFloat* x = (const GFloat*)in_ptrs[k * L + l];
-      a[u] = x[ia];
-      c[u] = x[ib];
+      const uint64_t pv = qc[j + u < jn ? j + u : jn - 1].ptr;
+      const uint64_t pb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pv >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pv);
+      float* x = reinterpret_cast<float*>(pb) + i0;
+      a[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          __builtin_amdgcn_make_buffer_rsrc(x, (short)0, lim_a, 0x00020000), lane_off, 0, 0));
+      c[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          __builtin_amdgcn_make_buffer_rsrc(x + h, (short)0, lim_b, 0x00020000), lane_off, 0, 0));
     }
   };
-  // fold clients kg .. kg+G-1 (those < K) from their loaded deltas a / c
-  auto fold_group = [&](int64_t kg, const float (&a)[G], const float (&c)[G]) {
+  // fold chunk clients j .. j+G-1 (those < jn; global index kc + j) from their deltas a / c
+  auto fold_group = [&](int64_t kc, int64_t j, int64_t jn, const float (&a)[G], const float (&c)[G]) {
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-      const int64_t k = kg + u;
-      if (k >= K) break;  // wave-uniform
-      const int64_t row = k * L + l;
-      const uint32_t k0 = keys[2 * row], k1 = keys[2 * row + 1];
-      const fjcomp_qparams p = qps[row];
-      const float wk = w[k];
+      if (j + u >= jn) break;  // wave-uniform
+      const int64_t k = kc + j + u;
+      const QClient& e = qc[j + u];
+      const uint32_t k0 = e.k0, k1 = e.k1, k2 = e.k2;
+      const fjcomp_qparams p = e.p;
+      const float wk = __uint_as_float(e.wbits);
       float lv0 = -1.0f, lv1 = -1.0f;
-      if (valid) {
+      if constexpr (Q::kPair) {
+        // Both elements, on every lane: lanes past the leaf (they read zeros) and lanes
+        // without a second element fold junk that is never stored. No branch, so the
+        // compiler can interleave the independent threefry chains of the group's clients.
+        uint32_t c0 = (uint32_t)i, c1 = (uint32_t)(second ? i + h : 0);
+        threefry_k(k0, k1, k2, c0, c1);
+        const f2 uu = {__uint_as_float(__builtin_amdgcn_alignbit(0x7fu, c0, 9u)),
+                       __uint_as_float(__builtin_amdgcn_alignbit(0x7fu, c1, 9u))};
+        const f2 t = quant.pair(f2{a[u], c[u]}, uu - 1.0f, p, &lv0, &lv1) * wk;
+        f2 sv = {s0, s1};
+        sv = (k == 0 && !accumulate) ? t : sv + t;
+        s0 = sv.x;
+        s1 = sv.y;
+      } else if (valid) {
         const float v0 = a[u];
         const float v1 = c[u];  // used only when `second`
         uint32_t c0 = (uint32_t)i, c1 = (uint32_t)(second ? i + h : 0);
-        threefry(k0, k1, c0, c1);
+        threefry_k(k0, k1, k2, c0, c1);
         const float q0 = quant(v0, bits_to_unit(c0), p, &lv0);
         const float t0 = q0 * wk;
         s0 = (k == 0 && !accumulate) ? t0 : s0 + t0;
@@ -484,19 +561,19 @@ __global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* 
         }
       }
       if constexpr (HIST) {
-        int32_t* __restrict__ hrow = hist + row * nbins;
+        int32_t* __restrict__ hrow = hist + (k * L + l) * nbins;
         const int top = nbins - 1;
         auto bin = [&](float lv) { return (lv >= 0.0f && lv < (float)top) ? (int)lv : top; };
         if (lds_hist) {
-          for (int e = threadIdx.x; e < nbins; e += kQThreads) sh[e] = 0;
+          for (int e2 = threadIdx.x; e2 < nbins; e2 += kQThreads) sh[e2] = 0;
           __syncthreads();
           if (valid) {
             atomicAdd(&sh[bin(lv0)], 1);
             if (second) atomicAdd(&sh[bin(lv1)], 1);
           }
           __syncthreads();
-          for (int e = threadIdx.x; e < nbins; e += kQThreads)
-            if (sh[e]) atomicAdd(&hrow[e], sh[e]);
+          for (int e2 = threadIdx.x; e2 < nbins; e2 += kQThreads)
+            if (sh[e2]) atomicAdd(&hrow[e2], sh[e2]);
           __syncthreads();
         } else if (valid) {
           atomicAdd(&hrow[bin(lv0)], 1);
@@ -505,16 +582,32 @@ __global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* 
       }
     }
   };
-  // Two register sets in turn (no copies between them, which would wait for the loads):
-  // while one group is folded, the next group's loads are in flight.
-  float xa[G], xb[G], ya[G], yb[G];
-  fetch(0, xa, xb);
-  for (int64_t kg = 0; kg < K; kg += 2 * G) {
-    fetch(kg + G, ya, yb);
-    fold_group(kg, xa, xb);
-    if (kg + G >= K) break;  // wave-uniform
-    fetch(kg + 2 * G, xa, xb);
-    fold_group(kg + G, ya, yb);
+  for (int64_t kc = 0; kc < K; kc += kQThreads) {
+    const int64_t jn = K - kc < kQThreads ? K - kc : kQThreads;
+    if (kc) __syncthreads();  // every wave is done with the previous chunk's entries
+    if (threadIdx.x < jn) {
+      const int64_t k = kc + threadIdx.x, row = k * L + l;
+      QClient e;
+      e.ptr = (uint64_t)in_ptrs[row];
+      e.k0 = keys[2 * row];
+      e.k1 = keys[2 * row + 1];
+      e.k2 = e.k0 ^ e.k1 ^ 0x1BD11BDAu;
+      e.wbits = __float_as_uint(w[k]);
+      e.p = qps[row];
+      qc[threadIdx.x] = e;
+    }
+    __syncthreads();
+    // Two register sets in turn (no copies between them, which would wait for the loads):
+    // while one group is folded, the next group's loads are in flight.
+    float xa[G], xb[G], ya[G], yb[G];
+    fetch(0, jn, xa, xb);
+    for (int64_t j = 0; j < jn; j += 2 * G) {
+      fetch(j + G, jn, ya, yb);
+      fold_group(kc, j, jn, xa, xb);
+      if (j + G >= jn) break;  // wave-uniform
+      fetch(j + 2 * G, jn, xa, xb);
+      fold_group(kc, j + G, jn, ya, yb);
+    }
   }
   if (!valid) return;
   if (flags & FJAGG_SCALE) {
