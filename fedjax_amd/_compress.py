@@ -43,7 +43,7 @@ WHT_BITS = 13       # butterfly bits of pass 0
 WHT_HIGH_BITS = 8   # butterfly bits of each later pass
 WHT_MAX_LOG2 = 34
 QBLOCK = 256  # k_quant_fold threads (element pairs) per workgroup
-SIGN_BLOCK = 256
+SIGN_BLOCK = 8192  # FJCOMP_SIGN_BLOCK_PAIRS (include/fjcomp.h)
 DEFAULT_WORKSPACE_BYTES = 4 << 30
 
 

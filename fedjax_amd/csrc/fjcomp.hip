@@ -90,6 +90,23 @@ __host__ __device__ inline void threefry_k(uint32_t k0, uint32_t k1, uint32_t k2
   FJ_TF_ROT1 x0 += k1; x1 += k2 + 4u;
   FJ_TF_ROT0 x0 += k2; x1 += k0 + 5u;
 }
+// Two independent blocks through the same key, round by round (instruction-level parallelism).
+#define FJ_TF_ROUND2(r) \
+  a0 += a1; b0 += b1;   \
+  a1 = rotl32(a1, r);   \
+  b1 = rotl32(b1, r);   \
+  a1 ^= a0; b1 ^= b0;
+#define FJ_TF_ROT0_2 FJ_TF_ROUND2(13) FJ_TF_ROUND2(15) FJ_TF_ROUND2(26) FJ_TF_ROUND2(6)
+#define FJ_TF_ROT1_2 FJ_TF_ROUND2(17) FJ_TF_ROUND2(29) FJ_TF_ROUND2(16) FJ_TF_ROUND2(24)
+__device__ inline void threefry2_k(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t& a0, uint32_t& a1, uint32_t& b0,
+                                   uint32_t& b1) {
+  a0 += k0; a1 += k1; b0 += k0; b1 += k1;
+  FJ_TF_ROT0_2 a0 += k1; a1 += k2 + 1u; b0 += k1; b1 += k2 + 1u;
+  FJ_TF_ROT1_2 a0 += k2; a1 += k0 + 2u; b0 += k2; b1 += k0 + 2u;
+  FJ_TF_ROT0_2 a0 += k0; a1 += k1 + 3u; b0 += k0; b1 += k1 + 3u;
+  FJ_TF_ROT1_2 a0 += k1; a1 += k2 + 4u; b0 += k1; b1 += k2 + 4u;
+  FJ_TF_ROT0_2 a0 += k2; a1 += k0 + 5u; b0 += k2; b1 += k0 + 5u;
+}
 __host__ __device__ inline void threefry(uint32_t k0, uint32_t k1, uint32_t& x0, uint32_t& x1) {
   threefry_k(k0, k1, k0 ^ k1 ^ 0x1BD11BDAu, x0, x1);
 }
@@ -156,32 +173,80 @@ __global__ __launch_bounds__(256) void k_random_bits(uint32_t k0, uint32_t k1, i
 
 // ------------------------------------------------------------------ rademacher signs
 // Sign of element g is bit 31 of its uniform draw's bits (uniform < 0.5 <=> +1).
+// A workgroup owns FJCOMP_SIGN_BLOCK_PAIRS consecutive pairs of one job and each wave a
+// run of kSignRounds x 64 of them: the segment search, the job record and the key schedule
+// are paid once per 8 threefry calls of a lane, and the wave's 2 x 16 sign words are
+// stored once, coalesced, instead of 4 single-lane stores per 64 pairs.
+constexpr int kSignRounds = FJCOMP_SIGN_BLOCK_PAIRS / 256;
+static_assert(kSignRounds % 2 == 0 && 2 * kSignRounds <= 64, "a wave's sign words fit its lanes");
 __global__ __launch_bounds__(256) void k_rademacher(const fjcomp_sign_job* __restrict__ jobs,
                                                      const int64_t* __restrict__ prefix, int64_t J) {
   const int64_t b = blockIdx.x;
   const int64_t j = find_segment(prefix, J, b);
   const fjcomp_sign_job jb = jobs[j];
   const int64_t d = jb.d, h = (d + 1) >> 1;
-  const int64_t i = (b - prefix[j]) * 256 + threadIdx.x;
-  uint32_t x0 = (uint32_t)i, x1 = (uint32_t)(i + h < d ? i + h : 0);
-  const bool valid = i < h, second = i + h < d;
-  if (valid) threefry(jb.key[0], jb.key[1], x0, x1);
-  const uint64_t m0 = __ballot(valid && (x0 >> 31));
-  const uint64_t m1 = __ballot(valid && second && (x1 >> 31));
+  const uint32_t k0 = jb.key[0], k1 = jb.key[1], k2 = k0 ^ k1 ^ 0x1BD11BDAu;
   const int lane = threadIdx.x & 63;
   if (d < 64) {  // one word, written by the first lane of the job's first wave
-    if (b == prefix[j] && threadIdx.x == 0) {
+    if (b != prefix[j] || threadIdx.x >= 64) return;
+    uint32_t x0 = (uint32_t)lane, x1 = (uint32_t)(lane + h < d ? lane + h : 0);
+    threefry_k(k0, k1, k2, x0, x1);
+    const uint64_t m0 = __ballot(lane < h && (x0 >> 31));
+    const uint64_t m1 = __ballot(lane < h && lane + h < d && (x1 >> 31));
+    if (lane == 0) {
       const uint64_t lo = m0 & ((1ull << h) - 1), hi = m1 & ((1ull << (d - h)) - 1);
       jb.words[0] = (uint32_t)(lo | (hi << h));
     }
     return;
   }
-  const int64_t i0 = i - lane;  // wave's first pair; h and i0 are multiples of 32
-  if (i0 >= h) return;
-  if (lane == 0) jb.words[i0 >> 5] = (uint32_t)m0;
-  if (lane == 1 && i0 + 32 < h) jb.words[(i0 >> 5) + 1] = (uint32_t)(m0 >> 32);
-  if (lane == 2) jb.words[(i0 + h) >> 5] = (uint32_t)m1;
-  if (lane == 3 && i0 + 32 < h) jb.words[((i0 + h) >> 5) + 1] = (uint32_t)(m1 >> 32);
+  // d >= 64: h is a multiple of 32, so words never straddle the two halves. Lane 0 parks
+  // each round's two 64-bit ballots in LDS; at the end lane t of the wave stores word t of
+  // both runs (one coalesced store each instead of single-lane stores per round).
+  __shared__ uint64_t masks[4][2][kSignRounds];
+  const int w = threadIdx.x >> 6;
+  const int64_t p0 = (b - prefix[j]) * FJCOMP_SIGN_BLOCK_PAIRS + (int64_t)w * 64 * kSignRounds;
+  const bool lead = lane == 0;
+  if (p0 < h) {  // wave-uniform
+    if (!(d & 1) && p0 + 64 * kSignRounds <= h && h + (int64_t)h <= 0xffffffffll) {
+      // common case (every DRIVE / rotation job: d even, so i + h < d <=> i < h; the whole
+      // run is inside the job; 32-bit counters): no masks, 32-bit index arithmetic
+      const uint32_t hh = (uint32_t)h;
+      uint32_t ctr = (uint32_t)p0 + (uint32_t)lane;
+#pragma unroll 1
+      for (int r = 0; r < kSignRounds; ++r, ctr += 64u) {
+        uint32_t a0 = ctr, a1 = ctr + hh;
+        // opaque to the optimizer: otherwise loop strength reduction rewrites the first
+        // rounds as sums of induction variables (7 extra adds per pair, measured in the ISA)
+        asm("" : "+v"(a0), "+v"(a1));
+        threefry_k(k0, k1, k2, a0, a1);
+        const uint64_t m0 = __ballot((int)a0 < 0), m1 = __ballot((int)a1 < 0);
+        if (lead) {
+          masks[w][0][r] = m0;
+          masks[w][1][r] = m1;
+        }
+      }
+    } else {  // pairs past h are masked out of the ballots; their words are not stored
+#pragma unroll 1
+      for (int r = 0; r < kSignRounds; ++r) {
+        if (p0 + r * 64 >= h) break;  // wave-uniform
+        const int64_t i = p0 + r * 64 + lane;
+        uint32_t a0 = (uint32_t)i, a1 = (uint32_t)(i + h < d ? i + h : 0);
+        threefry_k(k0, k1, k2, a0, a1);
+        const uint64_t m0 = __ballot(i < h && (a0 >> 31)), m1 = __ballot(i < h && i + h < d && (a1 >> 31));
+        if (lead) {
+          masks[w][0][r] = m0;
+          masks[w][1][r] = m1;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (p0 < h && lane < 2 * kSignRounds && p0 + 32 * lane < h) {
+    const uint32_t* m = reinterpret_cast<const uint32_t*>(masks[w][0]);
+    const uint32_t* n = reinterpret_cast<const uint32_t*>(masks[w][1]);
+    jb.words[(p0 >> 5) + lane] = m[lane];
+    jb.words[((p0 + h) >> 5) + lane] = n[lane];
+  }
 }
 
 // ------------------------------------------------------------------ row statistics

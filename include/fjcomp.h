@@ -109,7 +109,9 @@ int fjcomp_random_bits(uint32_t k0, uint32_t k1, int64_t n, uint32_t* out, void*
 int fjcomp_uniform(uint32_t k0, uint32_t k1, int64_t n, float* out, void* stream);
 
 /* Bit-packed jax.random.rademacher(key, (d,)) for J jobs. block_prefix[J+1]
- * (device) is the running sum of ceil(ceil(d/2) / 256) over jobs; nblocks its last entry. */
+ * (device) is the running sum of ceil(ceil(d/2) / FJCOMP_SIGN_BLOCK_PAIRS) over jobs;
+ * nblocks its last entry. */
+#define FJCOMP_SIGN_BLOCK_PAIRS 8192
 int fjcomp_rademacher(const fjcomp_sign_job* jobs, const int64_t* block_prefix, int64_t J,
                       int64_t nblocks, void* stream);
 

@@ -187,3 +187,12 @@ def test_multi_device_entry_points_validate_without_gpu():
     rc = lib.fjcomm_multi_wsum_dense(h, 0, _lib.F32, vp(16), i64(4), i64(1), 4, vp(16), 1.0, vp(16),
                                      None, 1, 0, 0, vp(0))
     assert rc == -1 and b"ndev" in lib.fjagg_last_error()
+
+
+def test_host_constants_match_headers():
+    """Constants the Python host shares with the C ABI are the headers' values."""
+    from fedjax_amd import _compress as C
+
+    text = open(os.path.join(ROOT, "include", "fjcomp.h")).read()
+    defines = dict(re.findall(r"#define (FJCOMP_\w+) (\d+)", text))
+    assert int(defines["FJCOMP_SIGN_BLOCK_PAIRS"]) == C.SIGN_BLOCK
