@@ -43,7 +43,8 @@ WHT_BITS = 13       # butterfly bits of pass 0
 WHT_HIGH_BITS = 8   # butterfly bits of each later pass
 WHT_MAX_LOG2 = 34
 QBLOCK = 256  # k_quant_fold threads (element pairs) per workgroup
-SIGN_BLOCK = 8192  # FJCOMP_SIGN_BLOCK_PAIRS (include/fjcomp.h)
+SIGN_BLOCK = 8192  # FJCOMP_SIGN_BLOCK_PAIRS (include/fjcomp.h): the largest share
+SIGN_MIN_BLOCKS = 2048  # k_rademacher workgroups wanted before the share grows (8 per CU)
 DEFAULT_WORKSPACE_BYTES = 4 << 30
 
 
@@ -192,12 +193,18 @@ def rademacher_words(keys: np.ndarray, ds: Sequence[int], device: torch.device) 
     keys = np.asarray(keys, dtype=np.uint32).reshape(J, 2)
     jobs["k0"], jobs["k1"], jobs["d"] = keys[:, 0], keys[:, 1], ds
     jobs["words"] = words.data_ptr() + 4 * woff[:-1]
-    blocks = ((ds + 1) // 2 + SIGN_BLOCK - 1) // SIGN_BLOCK
+    # the largest workgroup share (power of two pairs, 256 .. SIGN_BLOCK) that still gives
+    # every CU a few workgroups
+    pairs = int(((ds + 1) // 2).sum())
+    bp = SIGN_BLOCK
+    while bp > 256 and pairs < bp * SIGN_MIN_BLOCKS:
+        bp //= 2
+    blocks = ((ds + 1) // 2 + bp - 1) // bp
     prefix = np.concatenate([[0], np.cumsum(blocks)]).astype(np.int64)
     up = Upload()
     o_jobs, o_pre = up.add(jobs), up.add(prefix)
     base = up.commit(device)
-    _lib.call("fjcomp_rademacher", base + o_jobs, base + o_pre, J, int(prefix[-1]), _stream(device))
+    _lib.call("fjcomp_rademacher", base + o_jobs, base + o_pre, J, int(prefix[-1]), bp, _stream(device))
     return words, woff
 
 

@@ -76,7 +76,7 @@ _SIGNATURES = {
     "fjcomp_prng_sequence": (_i32, [_vp, _i64, _vp]),
     "fjcomp_random_bits": (_i32, [_u32, _u32, _i64, _vp, _vp]),
     "fjcomp_uniform": (_i32, [_u32, _u32, _i64, _vp, _vp]),
-    "fjcomp_rademacher": (_i32, [_vp, _vp, _i64, _i64, _vp]),
+    "fjcomp_rademacher": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp]),
     "fjcomp_row_stats_workspace_bytes": (_i64, [_i64]),
     "fjcomp_row_stats": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _vp]),
     "fjcomp_quant_fold": (_i32, [_i32, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i64, _i32, _f32, _i32, _vp,

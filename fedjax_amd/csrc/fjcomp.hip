@@ -173,14 +173,14 @@ __global__ __launch_bounds__(256) void k_random_bits(uint32_t k0, uint32_t k1, i
 
 // ------------------------------------------------------------------ rademacher signs
 // Sign of element g is bit 31 of its uniform draw's bits (uniform < 0.5 <=> +1).
-// A workgroup owns FJCOMP_SIGN_BLOCK_PAIRS consecutive pairs of one job and each wave a
-// run of kSignRounds x 64 of them: the segment search, the job record and the key schedule
+// A workgroup owns `block_pairs` (256 x rounds, at most FJCOMP_SIGN_BLOCK_PAIRS) consecutive
+// pairs of one job and each wave a run of rounds x 64 of them: the segment search, the job record and the key schedule
 // are paid once per 8 threefry calls of a lane, and the wave's 2 x 16 sign words are
 // stored once, coalesced, instead of 4 single-lane stores per 64 pairs.
 constexpr int kSignRounds = FJCOMP_SIGN_BLOCK_PAIRS / 256;
 static_assert(kSignRounds % 2 == 0 && 2 * kSignRounds <= 64, "a wave's sign words fit its lanes");
 __global__ __launch_bounds__(256) void k_rademacher(const fjcomp_sign_job* __restrict__ jobs,
-                                                     const int64_t* __restrict__ prefix, int64_t J) {
+                                                     const int64_t* __restrict__ prefix, int64_t J, int rounds) {
   const int64_t b = blockIdx.x;
   const int64_t j = find_segment(prefix, J, b);
   const fjcomp_sign_job jb = jobs[j];
@@ -204,16 +204,16 @@ __global__ __launch_bounds__(256) void k_rademacher(const fjcomp_sign_job* __res
   // both runs (one coalesced store each instead of single-lane stores per round).
   __shared__ uint64_t masks[4][2][kSignRounds];
   const int w = threadIdx.x >> 6;
-  const int64_t p0 = (b - prefix[j]) * FJCOMP_SIGN_BLOCK_PAIRS + (int64_t)w * 64 * kSignRounds;
+  const int64_t p0 = (b - prefix[j]) * (256 * rounds) + (int64_t)w * 64 * rounds;
   const bool lead = lane == 0;
   if (p0 < h) {  // wave-uniform
-    if (!(d & 1) && p0 + 64 * kSignRounds <= h && h + (int64_t)h <= 0xffffffffll) {
+    if (!(d & 1) && p0 + 64 * rounds <= h && h + (int64_t)h <= 0xffffffffll) {
       // common case (every DRIVE / rotation job: d even, so i + h < d <=> i < h; the whole
       // run is inside the job; 32-bit counters): no masks, 32-bit index arithmetic
       const uint32_t hh = (uint32_t)h;
       uint32_t ctr = (uint32_t)p0 + (uint32_t)lane;
 #pragma unroll 1
-      for (int r = 0; r < kSignRounds; ++r, ctr += 64u) {
+      for (int r = 0; r < rounds; ++r, ctr += 64u) {
         uint32_t a0 = ctr, a1 = ctr + hh;
         // opaque to the optimizer: otherwise loop strength reduction rewrites the first
         // rounds as sums of induction variables (7 extra adds per pair, measured in the ISA)
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void k_rademacher(const fjcomp_sign_job* __res
       }
     } else {  // pairs past h are masked out of the ballots; their words are not stored
 #pragma unroll 1
-      for (int r = 0; r < kSignRounds; ++r) {
+      for (int r = 0; r < rounds; ++r) {
         if (p0 + r * 64 >= h) break;  // wave-uniform
         const int64_t i = p0 + r * 64 + lane;
         uint32_t a0 = (uint32_t)i, a1 = (uint32_t)(i + h < d ? i + h : 0);
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void k_rademacher(const fjcomp_sign_job* __res
     }
   }
   __syncthreads();
-  if (p0 < h && lane < 2 * kSignRounds && p0 + 32 * lane < h) {
+  if (p0 < h && lane < 2 * rounds && p0 + 32 * lane < h) {
     const uint32_t* m = reinterpret_cast<const uint32_t*>(masks[w][0]);
     const uint32_t* n = reinterpret_cast<const uint32_t*>(masks[w][1]);
     jb.words[(p0 >> 5) + lane] = m[lane];
@@ -944,12 +944,16 @@ int fjcomp_uniform(uint32_t k0, uint32_t k1, int64_t n, float* out, void* stream
 }
 
 int fjcomp_rademacher(const fjcomp_sign_job* jobs, const int64_t* block_prefix, int64_t J, int64_t nblocks,
-                      void* stream) {
+                      int block_pairs, void* stream) {
   fjagg_g_err[0] = 0;
   if (J < 0 || nblocks < 0 || (J && (!jobs || !block_prefix)) || nblocks > INT32_MAX)
     return fail(FJAGG_EINVAL, "rademacher: bad arguments");
+  if (block_pairs < 256 || block_pairs > FJCOMP_SIGN_BLOCK_PAIRS || block_pairs % 256)
+    return fail(FJAGG_EINVAL, "rademacher: block_pairs=%d (a multiple of 256, at most %d)", block_pairs,
+                FJCOMP_SIGN_BLOCK_PAIRS);
   if (!J || !nblocks) return FJAGG_OK;
-  hipLaunchKernelGGL(k_rademacher, dim3((unsigned)nblocks), dim3(256), 0, as_stream(stream), jobs, block_prefix, J);
+  hipLaunchKernelGGL(k_rademacher, dim3((unsigned)nblocks), dim3(256), 0, as_stream(stream), jobs, block_prefix, J,
+                     block_pairs / 256);
   return check_launch("k_rademacher");
 }
 

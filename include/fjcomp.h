@@ -108,12 +108,14 @@ int fjcomp_prng_sequence(uint32_t key[2], int64_t n, uint32_t* subkeys);
 int fjcomp_random_bits(uint32_t k0, uint32_t k1, int64_t n, uint32_t* out, void* stream);
 int fjcomp_uniform(uint32_t k0, uint32_t k1, int64_t n, float* out, void* stream);
 
-/* Bit-packed jax.random.rademacher(key, (d,)) for J jobs. block_prefix[J+1]
- * (device) is the running sum of ceil(ceil(d/2) / FJCOMP_SIGN_BLOCK_PAIRS) over jobs;
- * nblocks its last entry. */
+/* Bit-packed jax.random.rademacher(key, (d,)) for J jobs. A workgroup takes block_pairs
+ * (a multiple of 256, at most FJCOMP_SIGN_BLOCK_PAIRS) consecutive element pairs of one job:
+ * block_prefix[J+1] (device) is the running sum of ceil(ceil(d/2) / block_pairs) over jobs,
+ * nblocks its last entry. Large blocks amortise the per-workgroup setup; small ones fill the
+ * chip when there are few pairs in total. */
 #define FJCOMP_SIGN_BLOCK_PAIRS 8192
 int fjcomp_rademacher(const fjcomp_sign_job* jobs, const int64_t* block_prefix, int64_t J,
-                      int64_t nblocks, void* stream);
+                      int64_t nblocks, int block_pairs, void* stream);
 
 /* Statistics of R rows (f32). chunk_prefix[R+1] (device): running sum of
  * max(1, ceil(n / FJCOMP_STATS_CHUNK)); nchunks its last entry. Writes stats[R] and, when
