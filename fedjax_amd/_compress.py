@@ -182,8 +182,10 @@ def quant_fold(method: int, in_ptrs: np.ndarray, keys: np.ndarray, qparams_ptr: 
     return up
 
 
-def rademacher_words(keys: np.ndarray, ds: Sequence[int], device: torch.device) -> Tuple[torch.Tensor, np.ndarray]:
-    """Sign bits for jobs (keys [J, 2], lengths ds): one word buffer, per-job word offsets."""
+def rademacher_words(keys: np.ndarray, ds: Sequence[int], device: torch.device,
+                     block_pairs: int = 0) -> Tuple[torch.Tensor, np.ndarray]:
+    """Sign bits for jobs (keys [J, 2], lengths ds): one word buffer, per-job word offsets.
+    ``block_pairs`` (tests) forces the kernel's workgroup share instead of the sized one."""
     J = len(ds)
     ds = np.asarray(ds, dtype=np.int64)
     nwords = (ds + 31) // 32
@@ -199,6 +201,7 @@ def rademacher_words(keys: np.ndarray, ds: Sequence[int], device: torch.device) 
     bp = SIGN_BLOCK
     while bp > 256 and pairs < bp * SIGN_MIN_BLOCKS:
         bp //= 2
+    bp = block_pairs or bp
     blocks = ((ds + 1) // 2 + bp - 1) // bp
     prefix = np.concatenate([[0], np.cumsum(blocks)]).astype(np.int64)
     up = Upload()

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void k_rademacher(const fjcomp_sign_job* __res
   const int64_t d = jb.d, h = (d + 1) >> 1;
   const uint32_t k0 = jb.key[0], k1 = jb.key[1], k2 = k0 ^ k1 ^ 0x1BD11BDAu;
   const int lane = threadIdx.x & 63;
-  if (d < 64) {  // one word, written by the first lane of the job's first wave
+  if (d < 64) {  // one or two words, written by the first lane of the job's first wave
     if (b != prefix[j] || threadIdx.x >= 64) return;
     uint32_t x0 = (uint32_t)lane, x1 = (uint32_t)(lane + h < d ? lane + h : 0);
     threefry_k(k0, k1, k2, x0, x1);
@@ -195,15 +195,36 @@ __global__ __launch_bounds__(256) void k_rademacher(const fjcomp_sign_job* __res
     const uint64_t m1 = __ballot(lane < h && lane + h < d && (x1 >> 31));
     if (lane == 0) {
       const uint64_t lo = m0 & ((1ull << h) - 1), hi = m1 & ((1ull << (d - h)) - 1);
-      jb.words[0] = (uint32_t)(lo | (hi << h));
+      const uint64_t all = lo | (hi << h);  // d <= 63 bits
+      jb.words[0] = (uint32_t)all;
+      if (d > 32) jb.words[1] = (uint32_t)(all >> 32);
     }
     return;
   }
-  // d >= 64: h is a multiple of 32, so words never straddle the two halves. Lane 0 parks
+  const int w = threadIdx.x >> 6;
+  if (h & 31) {
+    // halves that are not whole words (lengths other than a multiple of 64, none of them from
+    // the aggregators, which pad to powers of two): element-major, a lane per element, so a
+    // ballot is two whole words. Twice the threefry calls; the block covers 2 x its pairs.
+    const int64_t e0 = (b - prefix[j]) * (512 * (int64_t)rounds) + (int64_t)w * 128 * rounds;
+    for (int r = 0; r < 2 * rounds; ++r) {
+      const int64_t g0 = e0 + 64 * r;
+      if (g0 >= d) return;  // wave-uniform
+      const int64_t g = g0 + lane, i = g < h ? g : g - h;
+      uint32_t x0 = (uint32_t)i, x1 = (uint32_t)(i + h < d ? i + h : 0);
+      threefry_k(k0, k1, k2, x0, x1);
+      const uint64_t m = __ballot(g < d && ((g < h ? x0 : x1) >> 31));
+      if (lane == 0) {
+        jb.words[g0 >> 5] = (uint32_t)m;
+        if (g0 + 32 < d) jb.words[(g0 >> 5) + 1] = (uint32_t)(m >> 32);
+      }
+    }
+    return;
+  }
+  // h is a multiple of 32, so words never straddle the two halves. Lane 0 parks
   // each round's two 64-bit ballots in LDS; at the end lane t of the wave stores word t of
   // both runs (one coalesced store each instead of single-lane stores per round).
   __shared__ uint64_t masks[4][2][kSignRounds];
-  const int w = threadIdx.x >> 6;
   const int64_t p0 = (b - prefix[j]) * (256 * rounds) + (int64_t)w * 64 * rounds;
   const bool lead = lane == 0;
   if (p0 < h) {  // wave-uniform

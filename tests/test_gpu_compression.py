@@ -103,6 +103,28 @@ def test_sign_words(d, cuda):
         npt.assert_array_equal(got == 1, jr.rademacher(keys[j], (d,)) == -1)
 
 
+@pytest.mark.parametrize("block_pairs", [256, 512, 2048, 8192])
+def test_sign_words_every_workgroup_share(block_pairs, cuda):
+    """k_rademacher's fast path (even d, the wave's run inside the job) and general path
+    (odd d, runs that cross the job end, jobs shorter than a wave) at every workgroup share,
+    jobs of mixed lengths in one launch."""
+    ds = [1, 63, 64, 96, 1000, 4095, 4096, 8193, 65536, 100001, 1 << 18, (1 << 18) + 3]
+    keys = jr.split(jr.prng_key(block_pairs), len(ds))
+    words, woff = C.rademacher_words(keys, ds, cuda, block_pairs=block_pairs)
+    w = host(words).view(np.uint32)
+    for j, d in enumerate(ds):
+        g = np.arange(d)
+        got = (w[woff[j] + (g >> 5)] >> (g & 31)) & 1
+        npt.assert_array_equal(got == 1, jr.rademacher(keys[j], (d,)) == -1, err_msg=f"job {j}, d={d}")
+
+
+def test_sign_words_bad_share(cuda):
+    from fedjax_amd._lib import FjaggError
+
+    with pytest.raises(FjaggError, match="block_pairs"):
+        C.rademacher_words(jr.split(jr.prng_key(0), 1), [64], cuda, block_pairs=300)
+
+
 # ------------------------------------------------------------------ Walsh-Hadamard
 @pytest.mark.parametrize("m", [0, 1, 2, 5, 12, 13, 14, 17, 21, 26, 27])
 def test_wht_bitwise(m, cuda):
