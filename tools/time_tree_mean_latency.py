@@ -1,0 +1,54 @@
+"""Single-call latency of tree_mean at configs[1] (128 clients x EMNIST-CNN, one allocation
+per client leaf): the device is idle before each call and the call is waited for, as a
+server that aggregates once per round sees it. Also the pipelined rate (calls back to back)
+for comparison. Prints one JSON line (microseconds, medians)."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from fedjax_amd import tree_util as tu
+
+SHAPES = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "conv2_d_1": {"b": (64,), "w": (3, 3, 32, 64)},
+          "linear": {"b": (128,), "w": (9216, 128)}, "linear_1": {"b": (62,), "w": (128, 62)}}
+
+
+def tmap(f, t):
+    return {k: tmap(f, v) for k, v in t.items()} if isinstance(t, dict) else f(t)
+
+
+def main(K=128, reps=100):
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    clients = [tmap(lambda s: torch.rand(s, device=dev, generator=g), SHAPES) for _ in range(K)]
+    pairs = list(zip(clients, np.random.RandomState(1).randint(1, 501, size=K).tolist()))
+    pc = time.perf_counter
+    single, issue = [], []
+    for i in range(reps + 10):
+        torch.cuda.synchronize()
+        t0 = pc()
+        out = tu.tree_mean(pairs)
+        t1 = pc()
+        torch.cuda.synchronize()
+        t2 = pc()
+        if i >= 10:
+            issue.append((t1 - t0) * 1e6)
+            single.append((t2 - t0) * 1e6)
+        del out
+    torch.cuda.synchronize()
+    t0 = pc()
+    for _ in range(reps):
+        tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    piped = (pc() - t0) / reps * 1e6
+    print(json.dumps({"K": K, "single_call_us": round(float(np.median(single)), 1),
+                      "single_call_host_issue_us": round(float(np.median(issue)), 1),
+                      "pipelined_us_per_call": round(piped, 1)}))
+
+
+if __name__ == "__main__":
+    main()
