@@ -147,6 +147,25 @@ def row_stats_table(ptrs, ns, method: int, device: torch.device,
     return stats, qp
 
 
+def stats_from_partials(ptrs, ns, part_prefix: np.ndarray, part: torch.Tensor, method: int,
+                        device: torch.device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Min / max stats and qparams of rows whose per-tile partials a ROTATE WHT wrote into
+    ``part`` (row r: partials part_prefix[r] .. part_prefix[r+1]-1)."""
+    ns = np.asarray(ns, dtype=np.int64).reshape(-1)
+    R = ns.size
+    tab = np.empty(R, dtype=ROW)
+    tab["ptr"] = np.asarray(ptrs, dtype=np.uint64).reshape(-1)
+    tab["n"] = ns
+    up = Upload()
+    o_rows, o_pre = up.add(tab), up.add(np.ascontiguousarray(part_prefix, dtype=np.int64))
+    base = up.commit(device)
+    stats = torch.empty(R * STATS.itemsize, dtype=torch.uint8, device=device)
+    qp = torch.empty(R * QPARAMS.itemsize, dtype=torch.uint8, device=device)
+    _lib.call("fjcomp_stats_combine", base + o_rows, base + o_pre, R, method, part.data_ptr(), stats.data_ptr(),
+              qp.data_ptr(), _stream(device))
+    return stats, qp, up
+
+
 def qparams_host(vmin: float, vmax: float) -> np.ndarray:
     """Quantizer parameters for explicitly given v_min / v_max (compression.py:58-61)."""
     q = np.zeros(1, dtype=QPARAMS)
@@ -316,15 +335,25 @@ def rotated_quantized_mean(rows: List[List[torch.Tensor]], rot_keys: np.ndarray,
     loff = 4 * offs[:-1].astype(np.uint64)
     sptr = np.asarray(sptr, dtype=np.uint64)
     src_all = tree_util._ptr_table(rows, np.uint64)
+    # the rotation's last pass writes every tile's min / max (fjcomp_wht ROTATE partials), so
+    # the quantizer constants need no separate pass over the rotated deltas
+    last_tiles = np.array([wht_tiles(int(d).bit_length() - 1, wht_passes(int(d).bit_length() - 1) - 1)
+                           for d in leaf_d], dtype=np.int64)
+    part_slot = int(_lib.load().fjcomp_row_stats_workspace_bytes(1))
+    part = torch.empty(max(B * int(last_tiles.sum()) * part_slot, 16), dtype=torch.uint8, device=device)
     keep = []
     for k0 in range(0, K, B):
         kb = min(B, K - k0)
         ybase = np.uint64(Y.data_ptr()) + np.uint64(4 * D) * np.arange(kb, dtype=np.uint64)[:, None]
         ydst = ybase + loff[None, :]  # [kb, L]
+        pre = np.zeros(kb * L + 1, dtype=np.int64)
+        np.cumsum(np.tile(last_tiles, kb), out=pre[1:])
+        pptr = (np.uint64(part.data_ptr()) + np.uint64(part_slot) * pre[:-1].astype(np.uint64)).reshape(kb, L)
         keep.append(run_wht(wht_jobs(src_all[k0:k0 + kb], ydst, ydst, leaf_d[None, :], kind=_lib.WHT_ROTATE,
-                                     n_in=leaf_n[None, :], signs=sptr[None, :]), device))
-        _, qp = row_stats_table(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1),
-                                _lib.COMP_UNIFORM, device)
+                                     n_in=leaf_n[None, :], signs=sptr[None, :], stats=pptr), device))
+        _, qp, up = stats_from_partials(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1), pre, part,
+                                        _lib.COMP_UNIFORM, device)
+        keep.append(up)
         out_ptrs = np.uint64(acc.data_ptr()) + loff
         last = k0 + kb == K
         keep.append(quant_fold(_lib.COMP_UNIFORM, ydst, client_keys[k0:k0 + kb], qp.data_ptr(), w[k0:k0 + kb],

@@ -79,6 +79,7 @@ _SIGNATURES = {
     "fjcomp_rademacher": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp]),
     "fjcomp_row_stats_workspace_bytes": (_i64, [_i64]),
     "fjcomp_row_stats": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _vp]),
+    "fjcomp_stats_combine": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp]),
     "fjcomp_quant_fold": (_i32, [_i32, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i64, _i32, _f32, _i32, _vp,
                                  _vp, _vp]),
     "fjcomp_wht_tiles": (_i64, [_i32, _i32]),

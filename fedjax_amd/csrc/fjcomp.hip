@@ -322,6 +322,35 @@ struct LaneStats {
   }
 };
 
+// Min / max / |max| of a workgroup's values (the order-independent part of LaneStats),
+// stored as a Partial with zero sums by thread 0 after a wave butterfly and an LDS combine.
+// Every thread of the workgroup must call store().
+struct MinMax {
+  float mn = INFINITY, mx = -INFINITY, amx = -INFINITY;
+  bool nan = false;
+  __device__ inline void add(float x) {
+    nan |= x != x;
+    mn = fminf(mn, x);
+    mx = fmaxf(mx, x);
+    amx = fmaxf(amx, fabsf(x));
+  }
+  __device__ inline void store(Partial* out) const {
+    const double qn = __longlong_as_double(0x7ff8000000000000ll);
+    Partial p{nan ? qn : (double)mn, nan ? qn : (double)mx, nan ? qn : (double)amx, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) merge(p, shfl_xor(p, m));
+    __shared__ Partial sp[16];  // waves of the widest caller (k_wht: 512 threads)
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sp[threadIdx.x >> 6] = p;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      Partial t = sp[0];
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) merge(t, sp[w]);
+      *out = t;
+    }
+  }
+};
+
 // One workgroup per 16 Ki-element chunk of a row: a scalar head up to the first 16-byte
 // boundary, float4 loads eight deep per lane, a scalar tail; then the fixed-order wave
 // butterfly and a per-workgroup combine in wave order (deterministic).
@@ -844,6 +873,10 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
     __syncthreads();
   }
   float* __restrict__ dptr = last ? jb.dst : jb.mid;
+  // ROTATE with a partials pointer: this tile's min / max / |max| of the rotated values
+  // (order-independent, so the row's combine equals k_row_stats' exactly; sums stay 0)
+  const bool tile_stats = last && kind == FJCOMP_WHT_ROTATE && jb.stats;
+  MinMax mm;
   if (quads && ((uintptr_t)dptr & 15) == 0) {
     for (int e = 4 * threadIdx.x; e < t.tile; e += 4 * kWhtThreads) {
       const int64_t g = base + ((int64_t)(e >> t.lc) << t.lo) + (e & (t.c - 1));
@@ -856,6 +889,11 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
         if (kind == FJCOMP_WHT_ROTATE) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) v[u] = div_by(v[u], rcp_sqrt_d);
+          if (tile_stats) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (g + u < jb.n_out) mm.add(v[u]);
+          }
         } else if (kind != FJCOMP_WHT_PLAIN) {
           const uint32_t sw = jb.signs[g >> 5] >> (g & 31);
 #pragma unroll
@@ -870,6 +908,7 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
       }
       *reinterpret_cast<float4*>(dptr + g) = make_float4(v[0], v[1], v[2], v[3]);
     }
+    if (tile_stats) mm.store(reinterpret_cast<Partial*>(const_cast<fjcomp_stats*>(jb.stats)) + tix);
     return;
   }
   for (int e = threadIdx.x; e < t.tile; e += kWhtThreads) {
@@ -882,11 +921,13 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
     if (g >= jb.n_out) continue;
     if (kind == FJCOMP_WHT_ROTATE) {
       v = div_by(v, rcp_sqrt_d);
+      if (tile_stats) mm.add(v);
     } else if (kind != FJCOMP_WHT_PLAIN) {
       v = div_by(v * sign_of(jb.signs, g), rcp_sqrt_d);
     }
     jb.dst[g] = v;
   }
+  if (tile_stats) mm.store(reinterpret_cast<Partial*>(const_cast<fjcomp_stats*>(jb.stats)) + tix);
 }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -997,6 +1038,20 @@ int fjcomp_row_stats(const fjcomp_row* rows, const int64_t* chunk_prefix, int64_
   if (int rc = check_launch("k_row_stats")) return rc;
   hipLaunchKernelGGL(k_stats_combine, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, s, rows, chunk_prefix, R, part,
                      method, stats, qparams);
+  return check_launch("k_stats_combine");
+}
+
+int fjcomp_stats_combine(const fjcomp_row* rows, const int64_t* part_prefix, int64_t R, int method,
+                         const void* part, fjcomp_stats* stats, fjcomp_qparams* qparams, void* stream) {
+  fjagg_g_err[0] = 0;
+  if (R < 0 || (R && (!rows || !part_prefix || !part || !stats)))
+    return fail(FJAGG_EINVAL, "stats_combine: bad arguments (R=%lld)", (long long)R);
+  if (qparams && method != FJCOMP_UNIFORM && method != FJCOMP_BINARY)
+    return fail(FJAGG_EINVAL, "stats_combine: min/max partials give qparams for UNIFORM or BINARY only, got %d",
+                method);
+  if (!R) return FJAGG_OK;
+  hipLaunchKernelGGL(k_stats_combine, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), rows,
+                     part_prefix, R, static_cast<const Partial*>(part), method, stats, qparams);
   return check_launch("k_stats_combine");
 }
 

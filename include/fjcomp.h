@@ -83,7 +83,9 @@ typedef struct fjcomp_wht_job {
   float* mid;                 /* intermediate of a multi-pass job (d floats; may alias src) */
   float* dst;                 /* last-pass output, n_out floats */
   const uint32_t* signs;      /* ROTATE / UNROTATE*: d sign bits (fjcomp_rademacher) */
-  const fjcomp_stats* stats;  /* UNROTATE_DRIVE: sumsq / sumabs of src */
+  const fjcomp_stats* stats;  /* UNROTATE_DRIVE: sumsq / sumabs of src. ROTATE: optional (may be NULL) per-tile
+                                 partials of dst for fjcomp_stats_combine, one slot of
+                                 fjcomp_row_stats_workspace_bytes(1) B per last-pass tile */
   int64_t n_in;               /* valid src elements (ROTATE zero-pads to d) */
   int64_t n_out;              /* elements written to dst (<= d) */
   int32_t log2d;
@@ -123,6 +125,11 @@ int fjcomp_rademacher(const fjcomp_sign_job* jobs, const int64_t* block_prefix, 
  * Workspace: fjcomp_row_stats_workspace_bytes(nchunks). */
 #define FJCOMP_STATS_CHUNK 16384
 int64_t fjcomp_row_stats_workspace_bytes(int64_t nchunks);
+/* min / max statistics (sums zero) and UNIFORM / BINARY qparams of R rows from per-tile
+ * partials written by fjcomp_wht (ROTATE jobs with a stats pointer): row r owns partials
+ * part_prefix[r] .. part_prefix[r+1]-1 (device). Equal to fjcomp_row_stats' min / max. */
+int fjcomp_stats_combine(const fjcomp_row* rows, const int64_t* part_prefix, int64_t R, int method,
+                         const void* part, fjcomp_stats* stats, fjcomp_qparams* qparams, void* stream);
 int fjcomp_row_stats(const fjcomp_row* rows, const int64_t* chunk_prefix, int64_t R, int64_t nchunks,
                      int method, fjcomp_stats* stats, fjcomp_qparams* qparams, void* ws,
                      int64_t ws_bytes, void* stream);

@@ -125,6 +125,42 @@ def test_sign_words_bad_share(cuda):
         C.rademacher_words(jr.split(jr.prng_key(0), 1), [64], cuda, block_pairs=300)
 
 
+@pytest.mark.parametrize("nan", [False, True])
+def test_rotate_tile_partials_equal_row_stats(nan, cuda):
+    """The ROTATE pass's per-tile min / max partials (fjcomp_stats_combine) give the same
+    stats min / max and the same UNIFORM qparams bytes as a k_row_stats pass over the rotated
+    rows (one- and two-pass lengths, NaN propagation)."""
+    rs = np.random.RandomState(5)
+    ns = [1, 5, 64, 300, 8192, 8193, 100000, 1 << 18]
+    ds = [C.padded_size(n) for n in ns]
+    srcs = [rs.standard_normal(n).astype(F32) for n in ns]
+    if nan:
+        srcs[3][7] = np.nan
+        srcs[6][99] = np.nan
+    xs = [dev(x, cuda) for x in srcs]
+    keys = jr.split(jr.prng_key(11), len(ns))
+    signs, woff = C.rademacher_words(keys, ds, cuda)
+    ys = [torch.empty(d, dtype=torch.float32, device=cuda) for d in ds]
+    last = np.array([C.wht_tiles(d.bit_length() - 1, C.wht_passes(d.bit_length() - 1) - 1) for d in ds])
+    pre = np.concatenate([[0], np.cumsum(last)]).astype(np.int64)
+    slot = int(fedjax_amd._lib.load().fjcomp_row_stats_workspace_bytes(1))
+    part = torch.empty(int(pre[-1]) * slot, dtype=torch.uint8, device=cuda)
+    yp = np.array([y.data_ptr() for y in ys], dtype=np.uint64)
+    sp = np.uint64(signs.data_ptr()) + np.uint64(4) * woff[:-1].astype(np.uint64)
+    keep = C.run_wht(C.wht_jobs([x.data_ptr() for x in xs], yp, yp, ds, kind=fedjax_amd._lib.WHT_ROTATE,
+                                n_in=ns, signs=sp,
+                                stats=np.uint64(part.data_ptr()) + np.uint64(slot) * pre[:-1].astype(np.uint64)),
+                     cuda)
+    st_a, qp_a, up = C.stats_from_partials(yp, ds, pre, part, fedjax_amd._lib.COMP_UNIFORM, cuda)
+    st_b, qp_b = C.row_stats_table(yp, ds, fedjax_amd._lib.COMP_UNIFORM, cuda)
+    torch.cuda.synchronize()
+    del keep, up
+    a, b = host(st_a).view(C.STATS), host(st_b).view(C.STATS)
+    for f in ("min", "max", "absmax"):
+        npt.assert_array_equal(a[f].view(np.uint64), b[f].view(np.uint64), err_msg=f)
+    npt.assert_array_equal(host(qp_a), host(qp_b))
+
+
 # ------------------------------------------------------------------ Walsh-Hadamard
 @pytest.mark.parametrize("m", [0, 1, 2, 5, 12, 13, 14, 17, 21, 26, 27])
 def test_wht_bitwise(m, cuda):
