@@ -335,18 +335,36 @@ struct MinMax {
     amx = fmaxf(amx, fabsf(x));
   }
   __device__ inline void store(Partial* out) const {
-    const double qn = __longlong_as_double(0x7ff8000000000000ll);
-    Partial p{nan ? qn : (double)mn, nan ? qn : (double)mx, nan ? qn : (double)amx, 0.0, 0.0, 0.0};
+    // f32 wave reduction (min / max are exact in any order; NaN as one wave vote), then
+    // the waves through LDS: a few dozen cross-lane ops per tile instead of six f64 lanes
+    float a = mn, b = mx, c = amx;
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) merge(p, shfl_xor(p, m));
-    __shared__ Partial sp[16];  // waves of the widest caller (k_wht: 512 threads)
+    for (int m = 32; m >= 1; m >>= 1) {
+      a = fminf(a, __shfl_xor(a, m));
+      b = fmaxf(b, __shfl_xor(b, m));
+      c = fmaxf(c, __shfl_xor(c, m));
+    }
+    const bool any_nan = __any(nan);
+    __shared__ float sp[16][4];  // waves of the widest caller (k_wht: 512 threads)
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) sp[threadIdx.x >> 6] = p;
+    if ((threadIdx.x & 63) == 0) {
+      sp[threadIdx.x >> 6][0] = a;
+      sp[threadIdx.x >> 6][1] = b;
+      sp[threadIdx.x >> 6][2] = c;
+      sp[threadIdx.x >> 6][3] = any_nan ? 1.0f : 0.0f;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-      Partial t = sp[0];
-      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) merge(t, sp[w]);
-      *out = t;
+      float n = sp[0][3];
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+        a = fminf(a, sp[w][0]);
+        b = fmaxf(b, sp[w][1]);
+        c = fmaxf(c, sp[w][2]);
+        n = fmaxf(n, sp[w][3]);
+      }
+      const double qn = __longlong_as_double(0x7ff8000000000000ll);
+      *out = Partial{n != 0.0f ? qn : (double)a, n != 0.0f ? qn : (double)b, n != 0.0f ? qn : (double)c, 0.0, 0.0,
+                     0.0};
     }
   }
 };
