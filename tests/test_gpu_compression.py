@@ -365,6 +365,32 @@ def test_uniform_quantizer_bitwise(levels, enc, cuda):
         npt.assert_array_equal(st.rng, rst.rng)
 
 
+SMALL = {"b": (17,), "w": (3001,)}
+
+
+@pytest.mark.parametrize("K", [257, 300, 513])
+@pytest.mark.parametrize("kind", ["uniform16", "arithmetic", "terngrad"])
+def test_quantizers_many_clients_bitwise(K, kind, cuda):
+    """More clients than k_quant_fold stages in LDS at once (256): the per-client constants
+    are restaged per chunk and the delta look-ahead restarts at each chunk boundary."""
+    rs = np.random.RandomState(K)
+    trees = [_tree(rs, shapes=SMALL) for _ in range(K)]
+    w = [int(v) for v in rs.randint(1, 500, K)]
+    clients = [(f"c{k}", _to_dev(t, cuda), w[k]) for k, t in enumerate(trees)]
+    ref_clients = [(f"c{k}", t, w[k]) for k, t in enumerate(trees)]
+    if kind == "terngrad":
+        q, (init, apply) = comp.terngrad_quantizer(random.PRNGKey(6)), cref.terngrad_quantizer(jr.prng_key(6))
+    else:
+        enc = "arithmetic" if kind == "arithmetic" else None
+        q = comp.uniform_stochastic_quantizer(16, random.PRNGKey(6), enc)
+        init, apply = cref.uniform_stochastic_quantizer(16, jr.prng_key(6), enc)
+    p, st = q.apply(clients, q.init())
+    rp, rst = apply(ref_clients, init())
+    for a, b in zip(_leaves(p), _leaves(rp)):
+        same(host(a), b)
+    assert st.num_bits == rst.num_bits
+
+
 def test_terngrad_quantizer_bitwise(cuda):
     clients, ref_clients = _fleet(cuda, seed=1)
     q = comp.terngrad_quantizer(random.PRNGKey(2))
