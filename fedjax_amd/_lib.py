@@ -113,10 +113,12 @@ class ServerOpt(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int), ("nesterov", ctypes.c_int), ("neg_lr", ctypes.c_float),
                 ("decay", ctypes.c_float), ("one_minus_b1", ctypes.c_float), ("b1", ctypes.c_float),
                 ("one_minus_b2", ctypes.c_float), ("b2", ctypes.c_float), ("bc1", ctypes.c_float),
-                ("bc2", ctypes.c_float), ("eps", ctypes.c_float), ("eps_root", ctypes.c_float)]
+                ("bc2", ctypes.c_float), ("eps", ctypes.c_float), ("eps_root", ctypes.c_float),
+                ("flags", ctypes.c_int)]
 
 
-OPT_SGD, OPT_MOMENTUM, OPT_ADAM = 1, 2, 3
+OPT_SGD, OPT_MOMENTUM, OPT_ADAM, OPT_ADAGRAD, OPT_RMSPROP, OPT_YOGI = 1, 2, 3, 4, 5, 6
+OPT_F_MOMENTUM = 1
 
 
 class TreeLeaves(ctypes.Structure):

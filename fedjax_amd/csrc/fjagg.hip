@@ -308,6 +308,11 @@ struct LdsNorm {
 // 227-250) and only the updated params and optimizer state are written.
 __device__ __forceinline__ float div_rn(float a, float b) { return (float)((double)a / (double)b); }
 __device__ __forceinline__ float sqrt_rn(float a) { return (float)__dsqrt_rn((double)a); }
+// jax.lax.rsqrt restated as 1 / sqrt evaluated in f64 (each op correctly rounded) and
+// rounded once to f32 (XLA's own rsqrt is not pinned by any reference test)
+__device__ __forceinline__ float rsqrt_rn(float a) { return (float)__ddiv_rn(1.0, __dsqrt_rn((double)a)); }
+// jnp.sign: -1 / 0 / +1, NaN stays NaN
+__device__ __forceinline__ float xla_sign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x); }
 
 struct PlainEpi {};
 struct OptEpi {
@@ -325,7 +330,7 @@ struct OptEpi {
       const float t = __fadd_rn(g, __fmul_rn(o.decay, m[e]));
       m[e] = t;
       u = o.nesterov ? __fadd_rn(g, __fmul_rn(o.decay, t)) : t;
-    } else {  // optax.scale_by_adam
+    } else if (o.kind == FJAGG_OPT_ADAM) {  // optax.scale_by_adam
       const float mu = __fadd_rn(__fmul_rn(o.one_minus_b1, g), __fmul_rn(o.b1, m[e]));
       const float nu = __fadd_rn(__fmul_rn(o.one_minus_b2, __fmul_rn(g, g)), __fmul_rn(o.b2, v[e]));
       m[e] = mu;
@@ -334,6 +339,26 @@ struct OptEpi {
       // 2*24 + 2, double rounding is innocuous), as IEEE binary32 div/sqrt must be.
       const float mh = div_rn(mu, o.bc1), nh = div_rn(nu, o.bc2);
       u = div_rn(mh, __fadd_rn(sqrt_rn(__fadd_rn(nh, o.eps_root)), o.eps));
+    } else if (o.kind == FJAGG_OPT_ADAGRAD) {  // optax.scale_by_rss
+      const float ss = __fadd_rn(__fmul_rn(g, g), v[e]);
+      v[e] = ss;
+      u = __fmul_rn(ss > 0.0f ? rsqrt_rn(__fadd_rn(ss, o.eps)) : 0.0f, g);
+    } else if (o.kind == FJAGG_OPT_RMSPROP) {  // optax.scale_by_rms [+ optax.trace]
+      const float nu = __fadd_rn(__fmul_rn(o.one_minus_b2, __fmul_rn(g, g)), __fmul_rn(o.b2, v[e]));
+      v[e] = nu;
+      u = __fmul_rn(g, rsqrt_rn(__fadd_rn(nu, o.eps)));
+      if (o.flags & FJAGG_OPT_F_MOMENTUM) {
+        const float t = __fadd_rn(u, __fmul_rn(o.decay, m[e]));
+        m[e] = t;
+        u = o.nesterov ? __fadd_rn(u, __fmul_rn(o.decay, t)) : t;
+      }
+    } else {  // optax.scale_by_yogi: nu - (1 - b2) * sign(nu - g^2) * g^2, no bias correction
+      const float mu = __fadd_rn(__fmul_rn(o.one_minus_b1, g), __fmul_rn(o.b1, m[e]));
+      const float g2 = __fmul_rn(g, g), nv = v[e];
+      const float nu = __fsub_rn(nv, __fmul_rn(__fmul_rn(o.one_minus_b2, xla_sign(__fsub_rn(nv, g2))), g2));
+      m[e] = mu;
+      v[e] = nu;
+      u = div_rn(mu, __fadd_rn(sqrt_rn(__fadd_rn(nu, o.eps_root)), o.eps));
     }
     params[e] = __fadd_rn(p, __fmul_rn(o.neg_lr, u));  // scale_by_learning_rate, apply_updates
   }
@@ -1892,13 +1917,23 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
                         nullptr, nullptr, stream);
 }
 
+}  // extern "C"
+namespace {
+bool opt_needs_m(const fjagg_server_opt& o) {
+  return o.kind == FJAGG_OPT_MOMENTUM || o.kind == FJAGG_OPT_ADAM || o.kind == FJAGG_OPT_YOGI ||
+         (o.kind == FJAGG_OPT_RMSPROP && (o.flags & FJAGG_OPT_F_MOMENTUM));
+}
+bool opt_needs_v(const fjagg_server_opt& o) { return o.kind >= FJAGG_OPT_ADAM; }
+}  // namespace
+extern "C" {
+
 int fjagg_server_update_ptrs(int in_dtype, const int64_t* image_dev, int L, int64_t K, int64_t nblk,
                              const float* w_dev, float scale, const fjagg_server_opt* opt,
                              const int64_t* state_dev, int flags, void* stream) {
   g_err[0] = 0;
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16)
     return fail(FJAGG_EUNSUPPORTED, "server update: f32 or bf16 deltas");
-  if (!opt || opt->kind < FJAGG_OPT_SGD || opt->kind > FJAGG_OPT_ADAM)
+  if (!opt || opt->kind < FJAGG_OPT_SGD || opt->kind > FJAGG_OPT_YOGI || (opt->flags & ~FJAGG_OPT_F_MOMENTUM))
     return fail(FJAGG_EINVAL, "server update: bad optimizer descriptor");
   if (K < 1) return fail(FJAGG_EINVAL, "need K >= 1");
   if (nblk == 0) return FJAGG_OK;
@@ -1958,13 +1993,13 @@ int fjagg_server_update_dense(int in_dtype, const void* x_dev, int64_t ld, int64
   g_err[0] = 0;
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16)
     return fail(FJAGG_EUNSUPPORTED, "server update: f32 or bf16 deltas");
-  if (!opt || opt->kind < FJAGG_OPT_SGD || opt->kind > FJAGG_OPT_ADAM)
+  if (!opt || opt->kind < FJAGG_OPT_SGD || opt->kind > FJAGG_OPT_YOGI || (opt->flags & ~FJAGG_OPT_F_MOMENTUM))
     return fail(FJAGG_EINVAL, "server update: bad optimizer descriptor");
   if (K < 1 || P < 1 || ld < P) return fail(FJAGG_EINVAL, "bad shape (K=%lld, P=%lld)", (long long)K, (long long)P);
   if (P * elem_bytes(in_dtype) > kMaxRowBytes) return fail(FJAGG_EUNSUPPORTED, "rows > 1 GiB");
   if (!x_dev || !w_dev || !params_dev) return fail(FJAGG_EINVAL, "null pointer argument");
-  if (opt->kind != FJAGG_OPT_SGD && !m_dev) return fail(FJAGG_EINVAL, "optimizer state m is null");
-  if (opt->kind == FJAGG_OPT_ADAM && !v_dev) return fail(FJAGG_EINVAL, "optimizer state v is null");
+  if (opt_needs_m(*opt) && !m_dev) return fail(FJAGG_EINVAL, "optimizer state m is null");
+  if (opt_needs_v(*opt) && !v_dev) return fail(FJAGG_EINVAL, "optimizer state v is null");
   const int ib = elem_bytes(in_dtype), vw = vwidth(in_dtype);
   const uint8_t* x = reinterpret_cast<const uint8_t*>(x_dev);
   const bool vec = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && ((ld * ib) % 16 == 0) && P >= vw;

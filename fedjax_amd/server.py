@@ -3,7 +3,8 @@
 The step after the mean in every FedJAX algorithm is the server update
 (examples/fed_avg.py:97-101, fedjax/algorithms/fed_avg.py:150-154):
 ``opt_state, params = server_optimizer.apply(mean_delta, opt_state, params)``
-with ``fedjax.optimizers.sgd`` or ``adam`` (fedjax/core/optimizers.py:148-250, optax).
+with any of ``fedjax.optimizers.sgd``, ``adam``, ``adagrad``, ``rmsprop`` (not centered)
+or ``yogi`` (fedjax/core/optimizers.py:117-281, optax).
 :func:`fused_mean_update` folds the round's client deltas and applies that update
 in the same kernel (``fjagg_server_update_dense``): the mean stays in registers,
 params / momentum / second moments are read and written once.
@@ -30,7 +31,10 @@ from fedjax_amd.slab import ClientDeltaSlab
 
 @dataclasses.dataclass(frozen=True)
 class ServerOptimizer:
-    """Hyperparameters of fedjax.optimizers.sgd / adam (optimizers.py:148-250)."""
+    """Hyperparameters of fedjax.optimizers.sgd / adam / adagrad / rmsprop / yogi
+    (optimizers.py:117-281). ``b2`` is rmsprop's ``decay``; ``momentum`` its trace decay;
+    ``init_m`` / ``init_v`` the initial values of the state (adagrad's
+    initial_accumulator_value, rmsprop's initial_scale, yogi's 1e-6)."""
     kind: int
     learning_rate: float
     momentum: Optional[float] = None
@@ -39,16 +43,32 @@ class ServerOptimizer:
     b2: float = 0.999
     eps: float = 1e-8
     eps_root: float = 0.0
+    init_m: float = 0.0
+    init_v: float = 0.0
+
+    def needs_m(self) -> bool:
+        return self.kind in (_lib.OPT_MOMENTUM, _lib.OPT_ADAM, _lib.OPT_YOGI) or (
+            self.kind == _lib.OPT_RMSPROP and self.momentum is not None)
+
+    def needs_v(self) -> bool:
+        return self.kind >= _lib.OPT_ADAM
 
     def init(self, params) -> dict:
-        """Optimizer state (optax init: zeros, count 0) for flat float32 device params or
-        a pytree of them (then m / v are pytrees of the same structure)."""
-        zeros = torch.zeros_like if isinstance(params, torch.Tensor) else tree_util.tree_zeros_like
+        """Optimizer state (optax init, count 0) for flat float32 device params or a pytree
+        of them (then m / v are pytrees of the same structure)."""
+        def full(value):
+            if isinstance(params, torch.Tensor):
+                return torch.full_like(params, float(np.float32(value)))
+            z = tree_util.tree_zeros_like(params)
+            if value != 0.0:
+                for x in pytree.flatten(z)[0]:
+                    x.fill_(float(np.float32(value)))
+            return z
         st = {"count": 0}
-        if self.kind in (_lib.OPT_MOMENTUM, _lib.OPT_ADAM):
-            st["m"] = zeros(params)
-        if self.kind == _lib.OPT_ADAM:
-            st["v"] = zeros(params)
+        if self.needs_m():
+            st["m"] = full(self.init_m)
+        if self.needs_v():
+            st["v"] = full(self.init_v)
         return st
 
     def descriptor(self, count: int) -> _lib.ServerOpt:
@@ -65,6 +85,7 @@ class ServerOptimizer:
         d.bc1 = f32(1) - np.power(f32(self.b1), f32(count))
         d.bc2 = f32(1) - np.power(f32(self.b2), f32(count))
         d.eps, d.eps_root = f32(self.eps), f32(self.eps_root)
+        d.flags = _lib.OPT_F_MOMENTUM if (self.kind == _lib.OPT_RMSPROP and self.momentum is not None) else 0
         return d
 
 
@@ -78,6 +99,26 @@ def adam(learning_rate: float, b1: float = 0.9, b2: float = 0.999, eps: float = 
          eps_root: float = 0.0) -> ServerOptimizer:
     """fedjax.optimizers.adam (optimizers.py:148-178)."""
     return ServerOptimizer(_lib.OPT_ADAM, learning_rate, b1=b1, b2=b2, eps=eps, eps_root=eps_root)
+
+
+def adagrad(learning_rate: float, initial_accumulator_value: float = 0.1, eps: float = 1e-6) -> ServerOptimizer:
+    """fedjax.optimizers.adagrad (optimizers.py:117-145): optax.scale_by_rss, then -lr."""
+    return ServerOptimizer(_lib.OPT_ADAGRAD, learning_rate, eps=eps, init_v=initial_accumulator_value)
+
+
+def rmsprop(learning_rate: float, decay: float = 0.9, eps: float = 1e-8, initial_scale: float = 0.,
+            centered: bool = False, momentum: Optional[float] = None, nesterov: bool = False) -> ServerOptimizer:
+    """fedjax.optimizers.rmsprop (optimizers.py:181-224): optax.scale_by_rms [+ trace]."""
+    if centered:
+        raise NotImplementedError("centered rmsprop (optax.scale_by_stddev) has no fused server step")
+    return ServerOptimizer(_lib.OPT_RMSPROP, learning_rate, momentum=momentum, nesterov=nesterov, b2=decay,
+                           eps=eps, init_v=initial_scale)
+
+
+def yogi(learning_rate: float, b1: float = 0.9, b2: float = 0.999, eps: float = 1e-3) -> ServerOptimizer:
+    """fedjax.optimizers.yogi (optimizers.py:253-281): optax.scale_by_yogi (eps_root 0,
+    initial_accumulator_value 1e-6 for both moments), then -lr."""
+    return ServerOptimizer(_lib.OPT_YOGI, learning_rate, b1=b1, b2=b2, eps=eps, init_m=1e-6, init_v=1e-6)
 
 
 def fused_mean_update(slab: ClientDeltaSlab, weights: Sequence, opt: ServerOptimizer,
@@ -179,4 +220,5 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
     return new
 
 
-__all__ = ["ServerOptimizer", "adam", "fused_mean_update", "fused_tree_mean_update", "sgd"]
+__all__ = ["ServerOptimizer", "adagrad", "adam", "fused_mean_update", "fused_tree_mean_update", "rmsprop", "sgd",
+           "yogi"]

@@ -207,7 +207,17 @@ int fjagg_wsum_l2_dense(int in_dtype, int acc_dtype, int out_dtype, const void* 
  * mean_dev (optional) also receives g. Only the params/state are written: the
  * mean never round-trips through HBM.
  */
-enum fjagg_opt_kind { FJAGG_OPT_SGD = 1, FJAGG_OPT_MOMENTUM = 2, FJAGG_OPT_ADAM = 3 };
+enum fjagg_opt_kind {
+  FJAGG_OPT_SGD = 1,      /* optimizers.py:227-250 (momentum None)                          */
+  FJAGG_OPT_MOMENTUM = 2, /* optimizers.py:227-250, optax.trace (m)                          */
+  FJAGG_OPT_ADAM = 3,     /* optimizers.py:148-178, optax.scale_by_adam (m, v)               */
+  FJAGG_OPT_ADAGRAD = 4,  /* optimizers.py:117-145, optax.scale_by_rss (v = sum of squares)  */
+  FJAGG_OPT_RMSPROP = 5,  /* optimizers.py:181-224, optax.scale_by_rms (v) [+ trace (m)]     */
+  FJAGG_OPT_YOGI = 6      /* optimizers.py:253-281, optax.scale_by_yogi (m, v)               */
+};
+/* RMSPROP: b2 / one_minus_b2 = decay / 1 - decay; flags & FJAGG_OPT_F_MOMENTUM adds
+ * optax.trace(decay = this struct's `decay`, nesterov) after the rescale. */
+#define FJAGG_OPT_F_MOMENTUM 1
 typedef struct fjagg_server_opt {
   int kind;
   int nesterov;
@@ -216,6 +226,7 @@ typedef struct fjagg_server_opt {
   float one_minus_b1, b1, one_minus_b2, b2;
   float bc1, bc2;
   float eps, eps_root;
+  int flags;
 } fjagg_server_opt;
 int fjagg_server_update_dense(int in_dtype, const void* x_dev, int64_t ld, int64_t K, int64_t P,
                               const float* w_dev, float scale, const fjagg_server_opt* opt,

@@ -273,8 +273,12 @@ def uniform_stochastic_quantizer(num_levels: int, rng, encode_algorithm=None):
             qs.append((q, w))
         agg = tu.tree_mean(qs)
         if encode_algorithm == "arithmetic":
-            new_bits = F32(F32(np.sum(np.array(total_bits, np.float32), dtype=np.float32)) / F32(len(total_bits))) \
-                if total_bits else 0.0
+            # compression.py:211: sum(total_bits) / len(total_bits) -- Python's sequential sum of
+            # float32 scalars (np.sum would add pairwise and differ from K = 9 clients on)
+            total = 0
+            for b in total_bits:
+                total = total + b
+            new_bits = F32(F32(total) / F32(len(total_bits))) if total_bits else 0.0
         else:
             new_bits = _bits_per_param(math.log2(num_levels), agg)
         return agg, CompressionState(_accumulate_bits(state.num_bits, new_bits), rng2)

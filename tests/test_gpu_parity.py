@@ -623,21 +623,46 @@ def _np_server_step(opt, d, g, p, m, v):
     """numpy restatement of optax's op order (sgd / trace / scale_by_adam, then
     scale_by_learning_rate and apply_updates) with the descriptor's f32 constants."""
     f = np.float32
+
+    def rsqrt(x):  # jax.lax.rsqrt restated: 1 / sqrt in f64, rounded once (DESIGN.md §4)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            return (1.0 / np.sqrt(x.astype(np.float64))).astype(f)
+
     if opt.kind == 1:
         u = g
     elif opt.kind == 2:
         m = g + f(d.decay) * m
         u = g + f(d.decay) * m if opt.nesterov else m
-    else:
+    elif opt.kind == 3:
         m = f(d.one_minus_b1) * g + f(d.b1) * m
         v = f(d.one_minus_b2) * (g * g) + f(d.b2) * v
         u = (m / f(d.bc1)) / (np.sqrt(v / f(d.bc2) + f(d.eps_root)) + f(d.eps))
+    elif opt.kind == 4:  # optax.scale_by_rss
+        v = g * g + v
+        u = np.where(v > 0, rsqrt(v + f(d.eps)), f(0)) * g
+    elif opt.kind == 5:  # optax.scale_by_rms [+ trace]
+        v = f(d.one_minus_b2) * (g * g) + f(d.b2) * v
+        u = g * rsqrt(v + f(d.eps))
+        if opt.momentum is not None:
+            m = u + f(d.decay) * m
+            u = u + f(d.decay) * m if opt.nesterov else m
+    else:  # optax.scale_by_yogi
+        m = f(d.one_minus_b1) * g + f(d.b1) * m
+        v = v - (f(d.one_minus_b2) * np.sign(v - g * g)).astype(f) * (g * g)
+        u = m / (np.sqrt(v + f(d.eps_root)) + f(d.eps))
     return p + f(d.neg_lr) * u, m, v
 
 
-@pytest.mark.parametrize("make", [lambda s: s.sgd(0.5), lambda s: s.sgd(0.1, momentum=0.9),
-                                  lambda s: s.sgd(0.1, momentum=0.9, nesterov=True),
-                                  lambda s: s.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)])
+OPTIMIZERS = [lambda s: s.sgd(0.5), lambda s: s.sgd(0.1, momentum=0.9),
+              lambda s: s.sgd(0.1, momentum=0.9, nesterov=True),
+              lambda s: s.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4),
+              lambda s: s.adagrad(0.1), lambda s: s.adagrad(0.3, initial_accumulator_value=0.0, eps=1e-7),
+              lambda s: s.rmsprop(0.01), lambda s: s.rmsprop(0.01, decay=0.8, initial_scale=1.0, momentum=0.5),
+              lambda s: s.rmsprop(0.01, momentum=0.9, nesterov=True),
+              lambda s: s.yogi(0.01), lambda s: s.yogi(0.05, b1=0.5, b2=0.99, eps=1e-4)]
+
+
+@pytest.mark.parametrize("make", OPTIMIZERS)
 def test_fused_server_update_matches_restated_optax(make, cuda, coracle):
     from fedjax_amd import server
     opt = make(server)
@@ -647,8 +672,8 @@ def test_fused_server_update_matches_restated_optax(make, cuda, coracle):
     params = torch.from_numpy(coracle.synth_f32(1, P, seed=61)[0].copy()).to(cuda)
     state = opt.init(params)
     p_np = host(params).copy()
-    m_np = np.zeros(P, np.float32)
-    v_np = np.zeros(P, np.float32)
+    m_np = np.full(P, opt.init_m, np.float32)
+    v_np = np.full(P, opt.init_v, np.float32)
     for rnd in range(3):
         slab.fill_synthetic(seed=62 + rnd)
         xh = coracle.synth_f32(K, P, seed=62 + rnd)
@@ -745,9 +770,7 @@ def test_tree_mean_with_l2_norms_edges(cuda):
     npt.assert_allclose(host(nm), [np.sqrt(60.0)], rtol=1e-6)
 
 
-@pytest.mark.parametrize("make", [lambda s: s.sgd(0.5), lambda s: s.sgd(0.1, momentum=0.9),
-                                  lambda s: s.sgd(0.1, momentum=0.9, nesterov=True),
-                                  lambda s: s.adam(10 ** -2.5, b1=0.9, b2=0.999, eps=1e-4)])
+@pytest.mark.parametrize("make", OPTIMIZERS)
 @pytest.mark.parametrize("offset", [0, 1])
 def test_fused_tree_server_update_matches_restated_optax(make, offset, cuda, coracle):
     """Pytree path (fjagg_server_update_ptrs): tree_mean of separate client pytrees + the
@@ -769,8 +792,8 @@ def test_fused_tree_server_update_matches_restated_optax(make, offset, cuda, cor
     params = tree_of(base[offset:].clone())
     state = opt.init(params)
     p_np = {k: host(v).copy() for k, v in params.items()}
-    m_np = {k: np.zeros_like(v) for k, v in p_np.items()}
-    v_np = {k: np.zeros_like(v) for k, v in p_np.items()}
+    m_np = {k: np.full_like(v, opt.init_m) for k, v in p_np.items()}
+    v_np = {k: np.full_like(v, opt.init_v) for k, v in p_np.items()}
     for rnd in range(3):
         ld = (P + offset + 3) // 4 * 4
         x = torch.zeros(K, ld, device=cuda)
