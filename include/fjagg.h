@@ -201,6 +201,12 @@ int fjagg_wsum_l2_dense(int in_dtype, int acc_dtype, int out_dtype, const void* 
  *   MOMENTUM  t = g + decay*t; u = nesterov ? g + decay*t : t; p += neg_lr * u
  *   ADAM      mu = (1-b1) g + b1 mu; nu = (1-b2) g*g + b2 nu;
  *             u = (mu/bc1) / (sqrt(nu/bc2 + eps_root) + eps); p += neg_lr * u
+ *   ADAGRAD   v = g*g + v; u = (v > 0 ? rsqrt(v + eps) : 0) * g; p += neg_lr * u
+ *   RMSPROP   v = (1-b2) g*g + b2 v; u = g * rsqrt(v + eps);
+ *             [F_MOMENTUM: t = u + decay*m; u = nesterov ? u + decay*t : t]; p += neg_lr * u
+ *   YOGI      mu = (1-b1) g + b1 mu; nu = nu - ((1-b2) sign(nu - g*g)) g*g;
+ *             u = mu / (sqrt(nu + eps_root) + eps); p += neg_lr * u
+ * (rsqrt = 1/sqrt evaluated in f64, rounded once; div / sqrt correctly rounded)
  * with every constant pre-rounded to f32 on the host as JAX's weak typing does
  * (bc1 = f32(1 - b1^t), bc2 = f32(1 - b2^t) for the step count t after the
  * increment). params, m (mu / trace) and v (nu) are float32[P], updated in place;
