@@ -21,6 +21,7 @@ to a workspace budget so HBM holds K rotated deltas only when it fits.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -32,7 +33,9 @@ ROW = np.dtype([("ptr", "<u8"), ("n", "<i8")])
 SIGN_JOB = np.dtype([("k0", "<u4"), ("k1", "<u4"), ("d", "<i8"), ("words", "<u8")])
 WHT_JOB = np.dtype([("src", "<u8"), ("mid", "<u8"), ("dst", "<u8"), ("signs", "<u8"), ("stats", "<u8"),
                     ("n_in", "<i8"), ("n_out", "<i8"), ("log2d", "<i4"), ("kind", "<i4"),
-                    ("sqrt_d", "<f4"), ("reserved", "<f4")])
+                    ("sqrt_d", "<f4"), ("flags", "<i4")])
+WHT_F_SUMS = 1  # FJCOMP_WHT_F_SUMS (include/fjcomp.h)
+_AB_ROW_STATS = os.environ.get("FJCOMP_DRIVE_ROW_STATS") == "1"  # A/B switch (tools only)
 QPARAMS = np.dtype([("vmin", "<f4"), ("vmax", "<f4"), ("range", "<f4"), ("thr", "<f4"), ("rcp_range", "<f8")])
 STATS = np.dtype([("min", "<f8"), ("max", "<f8"), ("absmax", "<f8"), ("sum", "<f8"), ("sumsq", "<f8"),
                   ("sumabs", "<f8")])
@@ -148,7 +151,7 @@ def row_stats_table(ptrs, ns, method: int, device: torch.device,
 
 
 def stats_from_partials(ptrs, ns, part_prefix: np.ndarray, part: torch.Tensor, method: int,
-                        device: torch.device) -> Tuple[torch.Tensor, torch.Tensor]:
+                        device: torch.device, want_qparams: bool = True):
     """Min / max stats and qparams of rows whose per-tile partials a ROTATE WHT wrote into
     ``part`` (row r: partials part_prefix[r] .. part_prefix[r+1]-1)."""
     ns = np.asarray(ns, dtype=np.int64).reshape(-1)
@@ -160,10 +163,16 @@ def stats_from_partials(ptrs, ns, part_prefix: np.ndarray, part: torch.Tensor, m
     o_rows, o_pre = up.add(tab), up.add(np.ascontiguousarray(part_prefix, dtype=np.int64))
     base = up.commit(device)
     stats = torch.empty(R * STATS.itemsize, dtype=torch.uint8, device=device)
-    qp = torch.empty(R * QPARAMS.itemsize, dtype=torch.uint8, device=device)
+    qp = torch.empty(R * QPARAMS.itemsize, dtype=torch.uint8, device=device) if want_qparams else None
     _lib.call("fjcomp_stats_combine", base + o_rows, base + o_pre, R, method, part.data_ptr(), stats.data_ptr(),
-              qp.data_ptr(), _stream(device))
+              None if qp is None else qp.data_ptr(), _stream(device))
     return stats, qp, up
+
+
+def _last_pass_tiles(leaf_d: np.ndarray) -> np.ndarray:
+    """Tiles of each power-of-two job's last WHT pass (its partials slots)."""
+    return np.array([wht_tiles(int(d).bit_length() - 1, wht_passes(int(d).bit_length() - 1) - 1) for d in leaf_d],
+                    dtype=np.int64)
 
 
 def qparams_host(vmin: float, vmax: float) -> np.ndarray:
@@ -258,7 +267,7 @@ def run_wht(jobs: np.ndarray, device: torch.device) -> Upload:
     return up
 
 
-def wht_jobs(src, mid, dst, d, *, kind: int, n_in=None, n_out=None, signs=0, stats=0) -> np.ndarray:
+def wht_jobs(src, mid, dst, d, *, kind: int, n_in=None, n_out=None, signs=0, stats=0, flags: int = 0) -> np.ndarray:
     """WHT_JOB table; every argument is a scalar or an array broadcast to the job count.
     d are the (power-of-two) transform lengths; n_in / n_out default to d."""
     cols = np.broadcast_arrays(*(np.asarray(a, dtype=np.uint64 if i < 3 or i > 5 else np.int64)
@@ -272,7 +281,7 @@ def wht_jobs(src, mid, dst, d, *, kind: int, n_in=None, n_out=None, signs=0, sta
     j = np.zeros(d.size, dtype=WHT_JOB)
     j["src"], j["mid"], j["dst"], j["signs"], j["stats"] = src, mid, dst, signs, stats
     j["n_in"], j["n_out"] = n_in, n_out
-    j["log2d"], j["kind"] = log2, kind
+    j["log2d"], j["kind"], j["flags"] = log2, kind, flags
     j["sqrt_d"] = np.sqrt(d.astype(np.float32))  # jnp.sqrt(d): correctly rounded f32
     return j
 
@@ -337,8 +346,7 @@ def rotated_quantized_mean(rows: List[List[torch.Tensor]], rot_keys: np.ndarray,
     src_all = tree_util._ptr_table(rows, np.uint64)
     # the rotation's last pass writes every tile's min / max (fjcomp_wht ROTATE partials), so
     # the quantizer constants need no separate pass over the rotated deltas
-    last_tiles = np.array([wht_tiles(int(d).bit_length() - 1, wht_passes(int(d).bit_length() - 1) - 1)
-                           for d in leaf_d], dtype=np.int64)
+    last_tiles = _last_pass_tiles(leaf_d)
     part_slot = int(_lib.load().fjcomp_row_stats_workspace_bytes(1))
     part = torch.empty(max(B * int(last_tiles.sum()) * part_slot, 16), dtype=torch.uint8, device=device)
     keep = []
@@ -391,6 +399,11 @@ def drive_mean(rows: List[List[torch.Tensor]], client_keys: np.ndarray, w: np.nd
     yoff = 4 * offs[:-1].astype(np.uint64)
     zoff = 4 * loff[:-1].astype(np.uint64)
     src_all = tree_util._ptr_table(rows, np.uint64)
+    # the rotation's last pass writes every tile's sumsq / sumabs (f64) partials, so DRIVE's
+    # scale needs no separate pass over the rotated deltas
+    last_tiles = _last_pass_tiles(leaf_d)
+    part_slot = int(_lib.load().fjcomp_row_stats_workspace_bytes(1))
+    part = torch.empty(max(B * int(last_tiles.sum()) * part_slot, 16), dtype=torch.uint8, device=device)
     for k0 in range(0, K, B):
         kb = min(B, K - k0)
         signs, woff = rademacher_words(client_keys[k0:k0 + kb].reshape(-1, 2), ds * kb, device)
@@ -398,17 +411,27 @@ def drive_mean(rows: List[List[torch.Tensor]], client_keys: np.ndarray, w: np.nd
         bidx = np.arange(kb, dtype=np.uint64)[:, None]
         ydst = np.uint64(Y.data_ptr()) + np.uint64(4 * D) * bidx + yoff[None, :]
         zdst = np.uint64(Z.data_ptr()) + np.uint64(4 * Pp) * bidx + zoff[None, :]
-        t1 = run_wht(wht_jobs(src_all[k0:k0 + kb], ydst, ydst, leaf_d[None, :], kind=_lib.WHT_ROTATE,
-                              n_in=leaf_n[None, :], signs=sptr), device)
-        stats, _ = row_stats_table(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1), 0, device,
-                                   want_qparams=False)
+        pre = np.zeros(kb * L + 1, dtype=np.int64)
+        np.cumsum(np.tile(last_tiles, kb), out=pre[1:])
+        pptr = (np.uint64(part.data_ptr()) + np.uint64(part_slot) * pre[:-1].astype(np.uint64)).reshape(kb, L)
+        if _AB_ROW_STATS:  # A/B: the separate k_row_stats pass
+            t1 = run_wht(wht_jobs(src_all[k0:k0 + kb], ydst, ydst, leaf_d[None, :], kind=_lib.WHT_ROTATE,
+                                  n_in=leaf_n[None, :], signs=sptr), device)
+            stats, _ = row_stats_table(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1), 0, device,
+                                       want_qparams=False)
+            t0 = None
+        else:
+            t1 = run_wht(wht_jobs(src_all[k0:k0 + kb], ydst, ydst, leaf_d[None, :], kind=_lib.WHT_ROTATE,
+                                  n_in=leaf_n[None, :], signs=sptr, stats=pptr, flags=WHT_F_SUMS), device)
+            stats, _, t0 = stats_from_partials(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1), pre,
+                                               part, 0, device, want_qparams=False)
         sts = np.uint64(stats.data_ptr()) + np.uint64(STATS.itemsize) * np.arange(kb * L, dtype=np.uint64)
         t2 = run_wht(wht_jobs(ydst, ydst, zdst, leaf_d[None, :], kind=_lib.WHT_UNROTATE_DRIVE,
                               n_out=leaf_n[None, :], signs=sptr, stats=sts.reshape(kb, L)), device)
         last = k0 + kb == K
         kernels.weighted_sum_dense(Z[:kb, :P], w_dev[k0:k0 + kb], scale=scale if last else None, out=out_flat,
                                    accumulate=k0 > 0)
-        del t1, t2, signs, stats
+        del t0, t1, t2, signs, stats
 
 
 # ----------------------------------------------------------------------------- bits

@@ -322,36 +322,55 @@ struct LaneStats {
   }
 };
 
-// Min / max / |max| of a workgroup's values (the order-independent part of LaneStats),
-// stored as a Partial with zero sums by thread 0 after a wave butterfly and an LDS combine.
-// Every thread of the workgroup must call store().
+// Min / max / |max| of a workgroup's values (the order-independent part of LaneStats) and,
+// with `sums`, the f64 sums of squares and of magnitudes (DRIVE's sumsq / sumabs), stored
+// as a Partial (sum 0) by thread 0 after wave butterflies and an LDS combine. Every
+// thread of the workgroup must call store().
 struct MinMax {
   float mn = INFINITY, mx = -INFINITY, amx = -INFINITY;
+  double s2 = 0.0, sa = 0.0;
   bool nan = false;
-  __device__ inline void add(float x) {
+  __device__ inline void add(float x, bool sums) {
     nan |= x != x;
     mn = fminf(mn, x);
     mx = fmaxf(mx, x);
     amx = fmaxf(amx, fabsf(x));
+    if (sums) {
+      const double v = (double)x;
+      s2 = __fma_rn(v, v, s2);
+      sa += fabs(v);
+    }
   }
-  __device__ inline void store(Partial* out) const {
+  __device__ inline void store(Partial* out, bool sums) const {
     // f32 wave reduction (min / max are exact in any order; NaN as one wave vote), then
-    // the waves through LDS: a few dozen cross-lane ops per tile instead of six f64 lanes
+    // the waves through LDS: a few dozen cross-lane ops per tile
     float a = mn, b = mx, c = amx;
+    double q = s2, r = sa;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
       a = fminf(a, __shfl_xor(a, m));
       b = fmaxf(b, __shfl_xor(b, m));
       c = fmaxf(c, __shfl_xor(c, m));
     }
+    if (sums) {
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        q += __shfl_xor(q, m);
+        r += __shfl_xor(r, m);
+      }
+    }
     const bool any_nan = __any(nan);
     __shared__ float sp[16][4];  // waves of the widest caller (k_wht: 512 threads)
+    __shared__ double sq[16][2];
     __syncthreads();
     if ((threadIdx.x & 63) == 0) {
-      sp[threadIdx.x >> 6][0] = a;
-      sp[threadIdx.x >> 6][1] = b;
-      sp[threadIdx.x >> 6][2] = c;
-      sp[threadIdx.x >> 6][3] = any_nan ? 1.0f : 0.0f;
+      const int w = threadIdx.x >> 6;
+      sp[w][0] = a;
+      sp[w][1] = b;
+      sp[w][2] = c;
+      sp[w][3] = any_nan ? 1.0f : 0.0f;
+      sq[w][0] = q;
+      sq[w][1] = r;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -361,10 +380,12 @@ struct MinMax {
         b = fmaxf(b, sp[w][1]);
         c = fmaxf(c, sp[w][2]);
         n = fmaxf(n, sp[w][3]);
+        q += sq[w][0];
+        r += sq[w][1];
       }
       const double qn = __longlong_as_double(0x7ff8000000000000ll);
-      *out = Partial{n != 0.0f ? qn : (double)a, n != 0.0f ? qn : (double)b, n != 0.0f ? qn : (double)c, 0.0, 0.0,
-                     0.0};
+      *out = Partial{n != 0.0f ? qn : (double)a, n != 0.0f ? qn : (double)b, n != 0.0f ? qn : (double)c, 0.0,
+                     sums ? q : 0.0, sums ? r : 0.0};
     }
   }
 };
@@ -894,6 +915,7 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
   // ROTATE with a partials pointer: this tile's min / max / |max| of the rotated values
   // (order-independent, so the row's combine equals k_row_stats' exactly; sums stay 0)
   const bool tile_stats = last && kind == FJCOMP_WHT_ROTATE && jb.stats;
+  const bool tile_sums = tile_stats && (jb.flags & FJCOMP_WHT_F_SUMS);
   MinMax mm;
   if (quads && ((uintptr_t)dptr & 15) == 0) {
     for (int e = 4 * threadIdx.x; e < t.tile; e += 4 * kWhtThreads) {
@@ -910,7 +932,7 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
           if (tile_stats) {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              if (g + u < jb.n_out) mm.add(v[u]);
+              if (g + u < jb.n_out) mm.add(v[u], tile_sums);
           }
         } else if (kind != FJCOMP_WHT_PLAIN) {
           const uint32_t sw = jb.signs[g >> 5] >> (g & 31);
@@ -926,7 +948,7 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
       }
       *reinterpret_cast<float4*>(dptr + g) = make_float4(v[0], v[1], v[2], v[3]);
     }
-    if (tile_stats) mm.store(reinterpret_cast<Partial*>(const_cast<fjcomp_stats*>(jb.stats)) + tix);
+    if (tile_stats) mm.store(reinterpret_cast<Partial*>(const_cast<fjcomp_stats*>(jb.stats)) + tix, tile_sums);
     return;
   }
   for (int e = threadIdx.x; e < t.tile; e += kWhtThreads) {
@@ -939,13 +961,13 @@ __global__ __launch_bounds__(kWhtThreads) void k_wht(const fjcomp_wht_job* __res
     if (g >= jb.n_out) continue;
     if (kind == FJCOMP_WHT_ROTATE) {
       v = div_by(v, rcp_sqrt_d);
-      if (tile_stats) mm.add(v);
+      if (tile_stats) mm.add(v, tile_sums);
     } else if (kind != FJCOMP_WHT_PLAIN) {
       v = div_by(v * sign_of(jb.signs, g), rcp_sqrt_d);
     }
     jb.dst[g] = v;
   }
-  if (tile_stats) mm.store(reinterpret_cast<Partial*>(const_cast<fjcomp_stats*>(jb.stats)) + tix);
+  if (tile_stats) mm.store(reinterpret_cast<Partial*>(const_cast<fjcomp_stats*>(jb.stats)) + tix, tile_sums);
 }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

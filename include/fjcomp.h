@@ -84,15 +84,17 @@ typedef struct fjcomp_wht_job {
   float* dst;                 /* last-pass output, n_out floats */
   const uint32_t* signs;      /* ROTATE / UNROTATE*: d sign bits (fjcomp_rademacher) */
   const fjcomp_stats* stats;  /* UNROTATE_DRIVE: sumsq / sumabs of src. ROTATE: optional (may be NULL) per-tile
-                                 partials of dst for fjcomp_stats_combine, one slot of
+                                 partials of dst for fjcomp_stats_combine (min / max / |max|, and with
+                                 FJCOMP_WHT_F_SUMS sumsq / sumabs in f64), one slot of
                                  fjcomp_row_stats_workspace_bytes(1) B per last-pass tile */
   int64_t n_in;               /* valid src elements (ROTATE zero-pads to d) */
   int64_t n_out;              /* elements written to dst (<= d) */
   int32_t log2d;
   int32_t kind;
   float sqrt_d;               /* f32(sqrt(d)), correctly rounded */
-  float reserved;
+  int32_t flags;              /* ROTATE with stats: FJCOMP_WHT_F_SUMS also accumulates sumsq / sumabs */
 } fjcomp_wht_job;
+#define FJCOMP_WHT_F_SUMS 1
 
 int fjcomp_abi_version(void);
 
@@ -125,9 +127,10 @@ int fjcomp_rademacher(const fjcomp_sign_job* jobs, const int64_t* block_prefix, 
  * Workspace: fjcomp_row_stats_workspace_bytes(nchunks). */
 #define FJCOMP_STATS_CHUNK 16384
 int64_t fjcomp_row_stats_workspace_bytes(int64_t nchunks);
-/* min / max statistics (sums zero) and UNIFORM / BINARY qparams of R rows from per-tile
+/* Statistics and (qparams != NULL) UNIFORM / BINARY qparams of R rows from per-tile
  * partials written by fjcomp_wht (ROTATE jobs with a stats pointer): row r owns partials
- * part_prefix[r] .. part_prefix[r+1]-1 (device). Equal to fjcomp_row_stats' min / max. */
+ * part_prefix[r] .. part_prefix[r+1]-1 (device). min / max / |max| equal fjcomp_row_stats';
+ * sumsq / sumabs (FJCOMP_WHT_F_SUMS) are f64 sums in tile order, sum is 0. */
 int fjcomp_stats_combine(const fjcomp_row* rows, const int64_t* part_prefix, int64_t R, int method,
                          const void* part, fjcomp_stats* stats, fjcomp_qparams* qparams, void* stream);
 int fjcomp_row_stats(const fjcomp_row* rows, const int64_t* chunk_prefix, int64_t R, int64_t nchunks,

@@ -125,8 +125,9 @@ def test_sign_words_bad_share(cuda):
         C.rademacher_words(jr.split(jr.prng_key(0), 1), [64], cuda, block_pairs=300)
 
 
+@pytest.mark.parametrize("sums", [False, True])
 @pytest.mark.parametrize("nan", [False, True])
-def test_rotate_tile_partials_equal_row_stats(nan, cuda):
+def test_rotate_tile_partials_equal_row_stats(nan, sums, cuda):
     """The ROTATE pass's per-tile min / max partials (fjcomp_stats_combine) give the same
     stats min / max and the same UNIFORM qparams bytes as a k_row_stats pass over the rotated
     rows (one- and two-pass lengths, NaN propagation)."""
@@ -149,7 +150,8 @@ def test_rotate_tile_partials_equal_row_stats(nan, cuda):
     sp = np.uint64(signs.data_ptr()) + np.uint64(4) * woff[:-1].astype(np.uint64)
     keep = C.run_wht(C.wht_jobs([x.data_ptr() for x in xs], yp, yp, ds, kind=fedjax_amd._lib.WHT_ROTATE,
                                 n_in=ns, signs=sp,
-                                stats=np.uint64(part.data_ptr()) + np.uint64(slot) * pre[:-1].astype(np.uint64)),
+                                stats=np.uint64(part.data_ptr()) + np.uint64(slot) * pre[:-1].astype(np.uint64),
+                                flags=C.WHT_F_SUMS if sums else 0),
                      cuda)
     st_a, qp_a, up = C.stats_from_partials(yp, ds, pre, part, fedjax_amd._lib.COMP_UNIFORM, cuda)
     st_b, qp_b = C.row_stats_table(yp, ds, fedjax_amd._lib.COMP_UNIFORM, cuda)
@@ -159,6 +161,11 @@ def test_rotate_tile_partials_equal_row_stats(nan, cuda):
     for f in ("min", "max", "absmax"):
         npt.assert_array_equal(a[f].view(np.uint64), b[f].view(np.uint64), err_msg=f)
     npt.assert_array_equal(host(qp_a), host(qp_b))
+    for f in ("sumsq", "sumabs"):  # f64 sums in tile order vs chunk order: equal to ~1e-15
+        if sums:
+            npt.assert_allclose(a[f], b[f], rtol=1e-13, err_msg=f)
+        else:
+            assert not a[f].any()
 
 
 # ------------------------------------------------------------------ Walsh-Hadamard
