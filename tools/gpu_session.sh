@@ -4,6 +4,8 @@
 # Every GPU step has its own time limit; the session ends at the first step that fails
 # with anything but ordinary test failures (faults, aborts, time limits end it).
 # usage (on the box, from the repo root): bash tools/gpu_session.sh TAG [pytest -k expr]
+# (tools/gpu_full.sh TAG adds the FETCH_SIZE / WRITE_SIZE PMC passes behind profiles/traffic_c3.json;
+#  tools/gpu_study.sh STUDY runs the studies behind DESIGN.md's other numbers)
 set -u
 TAG=${1:-r02}
 KEXPR=${2:-}
