@@ -393,7 +393,9 @@ def drive_mean(rows: List[List[torch.Tensor]], client_keys: np.ndarray, w: np.nd
     B = _batch_size(K, 4 * (D + Pp), workspace_bytes)
     Y = torch.empty((B, D), dtype=torch.float32, device=device)
     Z = torch.empty((B, Pp), dtype=torch.float32, device=device)
-    w_dev = torch.from_numpy(np.ascontiguousarray(w, dtype=np.float32)).to(device)
+    # pinned + non_blocking: a pageable copy would make the host wait for the previous
+    # round to drain and then leave the GPU idle while this round's tables are built
+    w_dev = torch.from_numpy(np.ascontiguousarray(w, dtype=np.float32)).pin_memory().to(device, non_blocking=True)
     leaf_n = np.asarray(leaf_n, dtype=np.int64)
     leaf_d = np.asarray(ds, dtype=np.int64)
     yoff = 4 * offs[:-1].astype(np.uint64)
