@@ -21,7 +21,6 @@ to a workspace budget so HBM holds K rotated deltas only when it fits.
 from __future__ import annotations
 
 import math
-import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -35,7 +34,6 @@ WHT_JOB = np.dtype([("src", "<u8"), ("mid", "<u8"), ("dst", "<u8"), ("signs", "<
                     ("n_in", "<i8"), ("n_out", "<i8"), ("log2d", "<i4"), ("kind", "<i4"),
                     ("sqrt_d", "<f4"), ("flags", "<i4")])
 WHT_F_SUMS = 1  # FJCOMP_WHT_F_SUMS (include/fjcomp.h)
-_AB_ROW_STATS = os.environ.get("FJCOMP_DRIVE_ROW_STATS") == "1"  # A/B switch (tools only)
 QPARAMS = np.dtype([("vmin", "<f4"), ("vmax", "<f4"), ("range", "<f4"), ("thr", "<f4"), ("rcp_range", "<f8")])
 STATS = np.dtype([("min", "<f8"), ("max", "<f8"), ("absmax", "<f8"), ("sum", "<f8"), ("sumsq", "<f8"),
                   ("sumabs", "<f8")])
@@ -416,17 +414,10 @@ def drive_mean(rows: List[List[torch.Tensor]], client_keys: np.ndarray, w: np.nd
         pre = np.zeros(kb * L + 1, dtype=np.int64)
         np.cumsum(np.tile(last_tiles, kb), out=pre[1:])
         pptr = (np.uint64(part.data_ptr()) + np.uint64(part_slot) * pre[:-1].astype(np.uint64)).reshape(kb, L)
-        if _AB_ROW_STATS:  # A/B: the separate k_row_stats pass
-            t1 = run_wht(wht_jobs(src_all[k0:k0 + kb], ydst, ydst, leaf_d[None, :], kind=_lib.WHT_ROTATE,
-                                  n_in=leaf_n[None, :], signs=sptr), device)
-            stats, _ = row_stats_table(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1), 0, device,
-                                       want_qparams=False)
-            t0 = None
-        else:
-            t1 = run_wht(wht_jobs(src_all[k0:k0 + kb], ydst, ydst, leaf_d[None, :], kind=_lib.WHT_ROTATE,
-                                  n_in=leaf_n[None, :], signs=sptr, stats=pptr, flags=WHT_F_SUMS), device)
-            stats, _, t0 = stats_from_partials(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1), pre,
-                                               part, 0, device, want_qparams=False)
+        t1 = run_wht(wht_jobs(src_all[k0:k0 + kb], ydst, ydst, leaf_d[None, :], kind=_lib.WHT_ROTATE,
+                              n_in=leaf_n[None, :], signs=sptr, stats=pptr, flags=WHT_F_SUMS), device)
+        stats, _, t0 = stats_from_partials(ydst.reshape(-1), np.broadcast_to(leaf_d, (kb, L)).reshape(-1), pre,
+                                           part, 0, device, want_qparams=False)
         sts = np.uint64(stats.data_ptr()) + np.uint64(STATS.itemsize) * np.arange(kb * L, dtype=np.uint64)
         t2 = run_wht(wht_jobs(ydst, ydst, zdst, leaf_d[None, :], kind=_lib.WHT_UNROTATE_DRIVE,
                               n_out=leaf_n[None, :], signs=sptr, stats=sts.reshape(kb, L)), device)
