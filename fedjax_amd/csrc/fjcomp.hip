@@ -649,6 +649,8 @@ __global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* 
   }
   __shared__ int32_t sh[HIST ? kHistLdsBins : 1];
   const bool lds_hist = HIST && nbins <= kHistLdsBins;
+  const int hist_group = lds_hist ? kHistLdsBins / nbins : 1;  // clients per LDS histogram cycle
+  int hslot = 0;
   // Per-client constants of this leaf (row pointer, key, weight, quantizer constants) are
   // staged in LDS, kQThreads clients at a time, by one coalesced pass of the block: read
   // straight from the (client, leaf) tables with scalar loads, every client cost a
@@ -719,16 +721,31 @@ __global__ __launch_bounds__(kQThreads) void k_quant_fold(Q quant, const float* 
         const int top = nbins - 1;
         auto bin = [&](float lv) { return (lv >= 0.0f && lv < (float)top) ? (int)lv : top; };
         if (lds_hist) {
-          for (int e2 = threadIdx.x; e2 < nbins; e2 += kQThreads) sh[e2] = 0;
-          __syncthreads();
-          if (valid) {
-            atomicAdd(&sh[bin(lv0)], 1);
-            if (second) atomicAdd(&sh[bin(lv1)], 1);
+          // hist_group consecutive clients share one zero / count / flush cycle: client
+          // j counts into LDS slot j % hist_group, the slots go out together (2 barriers
+          // per group instead of 3 per client)
+          // (hslot: this client's slot, counted per chunk; wave-uniform)
+          if (hslot == 0) {  // first client of a group
+            for (int e2 = threadIdx.x; e2 < hist_group * nbins; e2 += kQThreads) sh[e2] = 0;
+            __syncthreads();
           }
-          __syncthreads();
-          for (int e2 = threadIdx.x; e2 < nbins; e2 += kQThreads)
-            if (sh[e2]) atomicAdd(&hrow[e2], sh[e2]);
-          __syncthreads();
+          int32_t* hs = sh + hslot * nbins;
+          if (valid) {
+            atomicAdd(&hs[bin(lv0)], 1);
+            if (second) atomicAdd(&hs[bin(lv1)], 1);
+          }
+          if (hslot == hist_group - 1 || j + u == jn - 1) {  // last client of a group
+            __syncthreads();
+            const int64_t g0 = k - hslot;  // the group's first client
+            for (int e2 = threadIdx.x; e2 < (hslot + 1) * nbins; e2 += kQThreads) {
+              const int c = e2 / nbins;  // 32-bit: at most kHistLdsBins entries
+              if (sh[e2]) atomicAdd(&hist[((g0 + c) * L + l) * nbins + (e2 - c * nbins)], sh[e2]);
+            }
+            __syncthreads();
+            hslot = 0;
+          } else {
+            ++hslot;
+          }
         } else if (valid) {
           atomicAdd(&hrow[bin(lv0)], 1);
           if (second) atomicAdd(&hrow[bin(lv1)], 1);
