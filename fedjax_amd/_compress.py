@@ -472,20 +472,28 @@ def arithmetic_bits_host(H: np.ndarray, Q: np.ndarray, K: int, leaf_n: Sequence[
     with np.errstate(all="ignore"):
         qv = (np.arange(num_levels, dtype=f32) / lm1).astype(f32)
         vals = (Q["vmin"][:, None] + (qv[None, :] * Q["range"][:, None]).astype(f32)).astype(f32)
-    vals = np.concatenate([vals, np.zeros((R, 1), f32)], axis=1)  # the NaN bin: nan_to_num(NaN) = 0
-    vals = np.nan_to_num(vals, nan=0.0, posinf=fmax, neginf=-fmax).astype(f32)
-    # distinct values of the occupied bins, ascending (np.unique order), counts merged
-    big = np.where(H > 0, vals, np.inf)
-    order = np.argsort(big, axis=1, kind="stable")
-    sv = np.take_along_axis(big, order, axis=1)
-    sc = np.take_along_axis(H, order, axis=1)
-    occupied = sc > 0
-    new = occupied.copy()
-    new[:, 1:] &= sv[:, 1:] != sv[:, :-1]
-    grp = np.cumsum(new, axis=1) - 1  # group index of each occupied sorted bin
-    u = new.sum(axis=1)  # distinct values per row
-    flat = (np.arange(R)[:, None] * nb + grp)[occupied]
-    merged = np.bincount(flat, weights=sc[occupied], minlength=R * nb).astype(np.int64).reshape(R, nb)
+    if not H[:, -1].any() and np.isfinite(vals).all() and (vals[:, 1:] > vals[:, :-1]).all():
+        # common case: no NaN-bin counts and strictly increasing finite levels, so the
+        # occupied bins ARE the distinct values in ascending (np.unique) order
+        occupied = H[:, :num_levels] > 0
+        u = occupied.sum(axis=1)
+        merged = np.zeros((R, nb), dtype=np.int64)
+        merged[np.arange(nb)[None, :] < u[:, None]] = H[:, :num_levels][occupied]
+    else:
+        vals = np.concatenate([vals, np.zeros((R, 1), f32)], axis=1)  # the NaN bin: nan_to_num(NaN) = 0
+        vals = np.nan_to_num(vals, nan=0.0, posinf=fmax, neginf=-fmax).astype(f32)
+        # distinct values of the occupied bins, ascending (np.unique order), counts merged
+        big = np.where(H > 0, vals, np.inf)
+        order = np.argsort(big, axis=1, kind="stable")
+        sv = np.take_along_axis(big, order, axis=1)
+        sc = np.take_along_axis(H, order, axis=1)
+        occupied = sc > 0
+        new = occupied.copy()
+        new[:, 1:] &= sv[:, 1:] != sv[:, :-1]
+        grp = np.cumsum(new, axis=1) - 1  # group index of each occupied sorted bin
+        u = new.sum(axis=1)  # distinct values per row
+        flat = (np.arange(R)[:, None] * nb + grp)[occupied]
+        merged = np.bincount(flat, weights=sc[occupied], minlength=R * nb).astype(np.int64).reshape(R, nb)
     d = np.asarray(leaf_n, dtype=np.int64)[np.arange(R) % L]
     e = f32(np.exp(f32(1)))
     per_row = np.zeros(R, dtype=f32)

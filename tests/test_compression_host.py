@@ -168,6 +168,25 @@ def test_arithmetic_bits_vectorised_matches_rowwise(num_levels):
     assert np.array_equal(np.array(got, np.float32).view(np.uint32), np.array(want, np.float32).view(np.uint32))
 
 
+@pytest.mark.parametrize("num_levels", [2, 16])
+def test_arithmetic_bits_fast_path_matches_rowwise(num_levels):
+    """No NaN-bin counts and strictly increasing levels: the compaction fast path."""
+    rs = np.random.RandomState(100 + num_levels)
+    K, leaf_n = 29, [32, 288, 64, 18432, 128, 1179648, 62, 7936]
+    R = K * len(leaf_n)
+    Q = np.zeros(R, dtype=C.QPARAMS)
+    Q["vmin"] = rs.standard_normal(R).astype(np.float32)
+    Q["range"] = (np.abs(rs.standard_normal(R)) + 0.1).astype(np.float32)
+    H = rs.randint(0, 50, size=(R, num_levels + 1)).astype(np.int64)
+    H[rs.rand(R, num_levels + 1) < 0.3] = 0
+    H[:, -1] = 0
+    H[::5, :] = 0
+    H[::5, 0] = 9
+    got = C.arithmetic_bits_host(H, Q, K, leaf_n, num_levels)
+    want = _arith_bits_rowwise(H, Q, K, leaf_n, num_levels)
+    assert np.array_equal(np.array(got, np.float32).view(np.uint32), np.array(want, np.float32).view(np.uint32))
+
+
 def test_wht_jobs_vectorised_matches_single():
     d = np.array([32, 512, 2 ** 21], dtype=np.int64)
     j = C.wht_jobs(np.array([[1, 2, 3]], np.uint64) * 16, 64, [5 * 16, 6 * 16, 7 * 16], d[None, :],
