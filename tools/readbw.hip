@@ -21,6 +21,7 @@ __global__ __launch_bounds__(256) void k_stream(const u32x4* __restrict__ x, int
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+template <int AUX>
 __global__ __launch_bounds__(256) void k_rows(const uint8_t* __restrict__ x, int64_t ld, int64_t K,
                                                int64_t nunits, int64_t S, unsigned* sink) {
   unsigned acc = 0;
@@ -39,7 +40,7 @@ __global__ __launch_bounds__(256) void k_rows(const uint8_t* __restrict__ x, int
       for (int r = 0; r < 4; ++r) {
         auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + (k + r) * ld), (short)0, (int)(nunits * 16), 0x00020000);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[r][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[j], 0, 2);
+        for (int j = 0; j < 8; ++j) v[r][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[j], 0, AUX);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -60,8 +61,26 @@ extern "C" int readbw(int mode, const void* x, int64_t ld_bytes, int64_t K, int6
     const int64_t nunits = row_bytes / 16;
     const int64_t S = ((nunits + grid - 1) / grid + 63) / 64 * 64;
     const int64_t nblk = (nunits + S - 1) / S;
-    hipLaunchKernelGGL(k_rows, dim3((unsigned)nblk), dim3(256), 0, s, (const uint8_t*)x, ld_bytes,
+    hipLaunchKernelGGL(k_rows<2>, dim3((unsigned)nblk), dim3(256), 0, s, (const uint8_t*)x, ld_bytes,
                        K, nunits, S, sink);
   }
+  return (int)hipGetLastError();
+}
+
+// The row walk with another cache policy on the loads (aux of buffer_load on gfx950:
+// bit 0 sc0, bit 1 nt, bit 4 sc1); 2 (nt) is what the fold uses.
+extern "C" int readbw_policy(int aux, const void* x, int64_t ld_bytes, int64_t K, int64_t row_bytes,
+                             int64_t grid, unsigned* sink, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nunits = row_bytes / 16;
+  const int64_t S = ((nunits + grid - 1) / grid + 63) / 64 * 64;
+  const dim3 g((unsigned)((nunits + S - 1) / S));
+  const uint8_t* p = (const uint8_t*)x;
+#define FJ_AUX(A) case A: hipLaunchKernelGGL(k_rows<A>, g, dim3(256), 0, s, p, ld_bytes, K, nunits, S, sink); break;
+  switch (aux) {
+    FJ_AUX(0) FJ_AUX(1) FJ_AUX(2) FJ_AUX(3) FJ_AUX(16) FJ_AUX(17) FJ_AUX(18) FJ_AUX(19)
+    default: return -1;
+  }
+#undef FJ_AUX
   return (int)hipGetLastError();
 }
