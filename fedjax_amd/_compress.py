@@ -497,7 +497,21 @@ def arithmetic_bits_host(H: np.ndarray, Q: np.ndarray, K: int, leaf_n: Sequence[
     d = np.asarray(leaf_n, dtype=np.int64)[np.arange(R) % L]
     e = f32(np.exp(f32(1)))
     per_row = np.zeros(R, dtype=f32)
-    for k in np.unique(u):
+    # rows with 1..7 distinct values at once: numpy sums fewer than 8 terms left to right,
+    # so zero terms appended to a row leave its entropy sum's bits unchanged
+    small = np.nonzero((u >= 1) & (u < 8))[0]
+    if small.size:
+        kk = u[small]
+        hist = np.ascontiguousarray(merged[small, :7])
+        with np.errstate(divide="ignore", invalid="ignore"):
+            p = (hist.astype(f32) / hist.sum(axis=1).astype(f32)[:, None]).astype(f32)
+            term = np.where(hist > 0, (p * _log2_f32(p)).astype(f32), f32(0))
+            ent = (-np.sum(term, axis=1, dtype=f32)).astype(f32)
+            dk, kf = d[small], kk.astype(f32)
+            hist_bits = (kf * _log2_f32(((e * (dk + kk).astype(f32)).astype(f32) / kf).astype(f32))).astype(f32)
+            per_row[small] = (((hist_bits + (dk.astype(f32) * ent).astype(f32)).astype(f32) + f32(64)).astype(f32)
+                              + f32(2)).astype(f32)
+    for k in np.unique(u[(u < 1) | (u >= 8)]):
         sel = np.nonzero(u == k)[0]
         hist = np.ascontiguousarray(merged[sel, :k])
         with np.errstate(divide="ignore", invalid="ignore"):
