@@ -65,10 +65,12 @@ class RunningMean:
         self.buffer_clients = max(1, int(buffer_clients))
         self._trees: List[PyTree] = []
         self._weights: List[Any] = []
-        self._versions: List[Any] = []
         self.copy_on_add = bool(copy_on_add)
         self._spec = pytree.native_spec(self.treedef)
         self._nleaves = len(self._sum)
+        # versions recorded at add(): row k belongs to self._trees[k] (grown by doubling)
+        self._vrows = np.empty((min(self.buffer_clients, 64), self._nleaves), dtype=np.int64)
+        self._host = None
 
     def _leaf_versions(self, trees: List[PyTree]):
         """int64 [len(trees), L] in-place version counters of every tensor leaf (-1 for
@@ -84,6 +86,21 @@ class RunningMean:
                     for x in pytree.flatten_as(self.treedef, t)]
         return v
 
+    def _record_versions(self, delta: PyTree) -> None:
+        """_leaf_versions([delta]) into row len(self._trees) of self._vrows; the native
+        walk writes the row in place (no per-client array: add() is on the client loop)."""
+        i = len(self._trees)
+        if i >= self._vrows.shape[0]:
+            self._vrows = np.concatenate([self._vrows, np.empty_like(self._vrows)])
+        row = self._vrows[i]
+        if self._spec is not None:
+            if self._host is None:
+                from fedjax_amd import _lib
+                self._host = _lib.host()
+            if self._host.leaf_versions([delta], self._spec, self._nleaves, row) == 0:
+                return
+        row[:] = self._leaf_versions([delta])[0]
+
     def add(self, delta: PyTree, weight) -> None:
         """tree_add(sum, tree_weight(delta, weight)); fed_avg.py:137-139. The delta is
         buffered by reference (a clone with ``copy_on_add``); its leaves are read when
@@ -93,7 +110,7 @@ class RunningMean:
             delta = pytree.unflatten(self.treedef, [
                 x.clone() if isinstance(x, torch.Tensor) else x for x in pytree.flatten_as(self.treedef, delta)])
         else:
-            self._versions.append(self._leaf_versions([delta])[0])
+            self._record_versions(delta)
         self._trees.append(delta)
         self._weights.append(w)
         self.total_weight += w
@@ -109,11 +126,11 @@ class RunningMean:
         flattened against the template and copied to the device first."""
         if not self._trees:
             return
-        trees, weights, versions = self._trees, self._weights, self._versions
-        self._trees, self._weights, self._versions = [], [], []
+        trees, weights = self._trees, self._weights
+        self._trees, self._weights = [], []
         if not self._sum:  # dtype rules checked by _fold (the sum has the template's dtypes)
             return
-        if versions and not np.array_equal(self._leaf_versions(trees), np.stack(versions)):
+        if not self.copy_on_add and not np.array_equal(self._leaf_versions(trees), self._vrows[:len(trees)]):
             raise RuntimeError("a buffered client delta was modified in place after RunningMean.add(); "
                                "the reference would have summed its value at add() time. Add a copy, "
                                "or construct RunningMean(..., copy_on_add=True)")
