@@ -52,9 +52,7 @@ class RunningMean:
                  device: Optional[torch.device] = None, copy_on_add: bool = False):
         leaves, self.treedef = pytree.flatten(template)
         self.device = device or tree_util._find_device(leaves)
-        zeros = tree_util.tree_zeros_like(pytree.unflatten(self.treedef, [
-            tree_util._device_leaf(x, self.device) for x in leaves]))
-        self._sum: List[torch.Tensor] = pytree.leaves_of(zeros)  # fed_avg.py:132
+        self._sum: List[torch.Tensor] = self._zero_sum(leaves)  # fed_avg.py:132
         self.total_weight: Any = 0.0  # fed_avg.py:133 (num_examples_sum = 0.)
         self.num_clients = 0
         if buffer_clients is None:
@@ -71,6 +69,21 @@ class RunningMean:
         # versions recorded at add(): row k belongs to self._trees[k] (grown by doubling)
         self._vrows = np.empty((min(self.buffer_clients, 64), self._nleaves), dtype=np.int64)
         self._host = None
+
+    def _zero_sum(self, leaves) -> List[torch.Tensor]:
+        """tree_zeros_like(template) on the device, as leaves. An all-float32 template gets
+        one zeroed allocation carved into 256-byte-aligned contiguous leaf views (one
+        allocation and one memset per round instead of one per leaf)."""
+        shapes = [tuple(x.shape) for x in leaves]
+        if leaves and all(isinstance(x, torch.Tensor) and x.dtype == torch.float32 or
+                          isinstance(x, np.ndarray) and x.dtype == np.float32 for x in leaves):
+            sizes = [int(np.prod(s, dtype=np.int64)) for s in shapes]
+            offs = np.concatenate([[0], np.cumsum([(n + 63) // 64 * 64 for n in sizes])])
+            flat = torch.zeros(int(offs[-1]), dtype=torch.float32, device=self.device)
+            return [flat[int(o):int(o) + n].view(s) for o, n, s in zip(offs, sizes, shapes)]
+        zeros = tree_util.tree_zeros_like(pytree.unflatten(self.treedef, [
+            tree_util._device_leaf(x, self.device) for x in leaves]))
+        return pytree.leaves_of(zeros)
 
     def _leaf_versions(self, trees: List[PyTree]):
         """int64 [len(trees), L] in-place version counters of every tensor leaf (-1 for
