@@ -478,6 +478,33 @@ def test_running_mean_detects_in_place_reuse(cuda):
     assert torch.equal(ru.result()["d"].view(torch.int32), want.view(torch.int32))
 
 
+def test_running_mean_carved_sum_and_version_growth(cuda):
+    """The zero sum of an all-float32 template is one allocation carved into leaf views
+    (0-d, odd and 64-multiple sizes here); the add()-time version rows grow past their
+    first 64 (150 buffered clients). Bitwise the eager loop, sum() mid-stream included."""
+    K = 150
+    shapes = {"s": (), "a": (3,), "b": (5, 7), "c": (64,), "d": (129,)}
+    g = torch.Generator(device="cpu").manual_seed(13)
+    trees = [{k: torch.randn(s, generator=g).to(cuda) for k, s in shapes.items()} for _ in range(K)]
+    w = [int(v) for v in torch.randint(1, 500, (K,), generator=g)]
+    rm = fedjax_amd.aggregators.RunningMean(trees[0], buffer_clients=200, device=cuda)
+    s = {k: torch.zeros(sh, device=cuda) for k, sh in shapes.items()}
+    for k in range(K):
+        rm.add(trees[k], w[k])
+        s = {n: s[n] + trees[k][n] * float(np.float32(w[k])) for n in shapes}
+        if k == 99:
+            mid = rm.sum()
+            for n in shapes:
+                assert mid[n].shape == shapes[n] and mid[n].is_contiguous()
+                assert mid[n].data_ptr() % 256 == 0
+                assert torch.equal(mid[n].view(torch.int32), s[n].view(torch.int32))
+    W = float(sum(w))
+    got = rm.result()
+    for n in shapes:
+        want = s[n] * float(np.float32(1.0 / W))
+        assert torch.equal(got[n].view(torch.int32), want.view(torch.int32))
+
+
 # ------------------------------------------------------------ fused fold + l2 norms
 @pytest.mark.parametrize("K,P,dt", [(1, 7, "f32"), (37, 10007, "f32"), (128, 1206590, "f32"),
                                     (300, 65536 + 5, "f32"), (64, 20000, "bf16"), (5, 3, "f32")])
