@@ -146,7 +146,16 @@ def spawn_ranks(nproc: int, argv, script: str = None, timeout: float = None) -> 
     except subprocess.TimeoutExpired:
         log(f"spawned ranks did not finish within {timeout} s")
         return 124
-    lines = [ln for ln in proc.stdout.decode(errors="replace").splitlines() if ln.startswith("{")]
+    lines = []
+    for ln in proc.stdout.decode(errors="replace").splitlines():
+        # the ranks share one pipe: another rank's unterminated banner can precede the JSON
+        i = ln.find('{"')
+        if i >= 0:
+            try:
+                json.loads(ln[i:])
+                lines.append(ln[i:])
+            except ValueError:
+                pass
     if proc.returncode != 0:
         log(f"rank launcher exited with status {proc.returncode}")
         return proc.returncode
