@@ -44,8 +44,10 @@ class RunningMean:
     (reusing one buffer for every client, as torch loops often do) would change the
     sum here but not there. Each tensor leaf's in-place version counter is recorded
     at ``add()`` and checked before the buffer is read: a changed leaf raises
-    ``RuntimeError``. ``copy_on_add=True`` clones every delta at ``add()`` instead
-    (one extra device copy per client; safe for any reuse).
+    ``RuntimeError``. The guard watches the tensors, not the containers: putting a
+    different tensor into a buffered dict or list after ``add()`` is not detected.
+    ``copy_on_add=True`` clones every delta (into a fresh container) at ``add()``
+    instead (one extra device copy per client; safe for any reuse).
     """
 
     def __init__(self, template: PyTree, *, buffer_clients: Optional[int] = None,
