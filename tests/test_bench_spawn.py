@@ -49,6 +49,18 @@ def test_spawn_forwards_rank0_json(rank_script, capfd, n):
     assert d["launcher"].startswith("bench.py")
 
 
+def test_spawn_finds_json_after_unterminated_banner(tmp_path, capfd):
+    """The ranks share one stdout pipe: a banner written without a newline can precede
+    rank 0's JSON on the same line; the launcher still forwards exactly the JSON."""
+    p = tmp_path / "rank.py"
+    p.write_text("import json, sys\nsys.stdout.write('banner without newline ')\n"
+                 "print(json.dumps({'n_gpus': 1}))\n")
+    rc = bench.spawn_ranks(1, [], script=str(p), timeout=120)
+    out = capfd.readouterr().out
+    assert rc == 0
+    assert out.strip() == '{"n_gpus": 1}'
+
+
 def test_spawn_propagates_rank_failure(rank_script, capfd):
     rc = bench.spawn_ranks(2, ["1"], script=rank_script, timeout=180)
     assert rc != 0
