@@ -82,7 +82,9 @@ def cpu_baseline(K, seconds=6.0):
     """Reference op sequence (per client: fresh w*x buffer, in-place add; final
     scale) on the host, bounded sample, timed at 1 thread, at the cgroup's CPU
     share and at every core this process may run on (os.sched_getaffinity, SURVEY
-    §8(d)). ``value`` / ``cores`` are the all-cores run; ``sweep`` holds the others."""
+    §8(d)). ``value`` / ``cores`` are the fastest of those runs (on a box whose cgroup
+    quota is below its visible cores, the quota's thread count beats all cores);
+    ``sweep`` holds every run."""
     from tests import coracle as co
 
     lib_path = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
@@ -105,14 +107,105 @@ def cpu_baseline(K, seconds=6.0):
             t += time.perf_counter() - t0
             reps += 1
         res[nt] = K * Ps * 4 * reps / t / 1e9
-    return {"value": round(res[cores], 2), "unit": "GB/s", "cores": cores, "kind": "port",
+    best = max(res, key=res.get)
+    return {"value": round(res[best], 2), "unit": "GB/s", "cores": best, "kind": "port",
             "single_thread_value": round(res[1], 2),
+            "all_cores_value": round(res[cores], 2), "visible_cores": cores,
             "sweep": {str(n): round(v, 2) for n, v in sorted(res.items())},
             "cgroup_cpu_share": share,
             "sample": f"{K} clients x {Ps} params fp32 ({K * Ps * 4 / 2**30:.2f} GiB), reference op "
                       f"sequence (tree_util.py:85-96) restated in C, oracle/fold_ref.c; "
-                      f"{os.uname().machine} host, {cores} threads = every core in sched_getaffinity"
+                      f"{os.uname().machine} host; fastest of 1 thread / the cgroup quota / all "
+                      f"{cores} cores in sched_getaffinity: {best} threads"
                       + (f" (cgroup quota: {share} CPUs)" if share else "")}
+
+
+def dropin_surface(dev, calls=20):
+    """The drop-in surface itself, timed in the same run as the headline but outside its
+    timed region: what examples/fed_avg.py:82 (tree_mean) and
+    fedjax/aggregators/aggregator.py:73 (mean_aggregator().apply) call, over caller-held
+    pytrees rather than the bench's slab.
+
+    * configs[2] as 1024 separately allocated 4 Mi float32 tensors through
+      ``mean_aggregator().apply`` (calls back to back);
+    * configs[1] as 128 EMNIST-CNN pytrees, every (client, leaf) its own allocation,
+      through ``tree_mean``: calls back to back, and one synchronous call on an idle GPU
+      (the latency a server aggregating once per round sees).
+
+    GB/s = the K*P*4 algorithmic bytes of client deltas / the time per call."""
+    import fedjax_amd
+    from fedjax_amd import kernels, tree_util as tu
+
+    res = {}
+    pc = time.perf_counter
+    # configs[2]: 1024 x 4 Mi as separate tensors through the Aggregator surface
+    K, P = 1024, 4 * 1024 * 1024
+    clients = []
+    for k in range(K):
+        t = torch.empty(P, dtype=torch.float32, device=dev)
+        kernels.fill_synth(t.view(1, P), seed=0, k0=k)
+        clients.append(t)
+    triples = [(f"c{k}", t, w) for k, (t, w) in enumerate(zip(clients, fedavg_weights(K)))]
+    agg = fedjax_amd.aggregators.mean_aggregator()
+    state = agg.init()
+    for _ in range(3):
+        agg.apply(triples, state)
+    torch.cuda.synchronize()
+    t0 = pc()
+    for _ in range(calls):
+        out, state = agg.apply(triples, state)
+    torch.cuda.synchronize()
+    ms = (pc() - t0) / calls * 1e3
+    res["c2_mean_aggregator_apply_ms"] = round(ms, 4)
+    res["c2_mean_aggregator_apply_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+    del clients, triples, out
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    # configs[1]: 128 EMNIST-CNN pytrees, one allocation per (client, leaf)
+    shapes = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "conv2_d_1": {"b": (64,), "w": (3, 3, 32, 64)},
+              "linear": {"b": (128,), "w": (9216, 128)}, "linear_1": {"b": (62,), "w": (128, 62)}}
+    K, P = 128, 1206590
+
+    def tree(k):
+        out, seed = {}, 1
+        for mod, leaves in shapes.items():
+            out[mod] = {}
+            for name, shp in leaves.items():
+                n = int(np.prod(shp))
+                x = torch.empty(1, n, dtype=torch.float32, device=dev)
+                kernels.fill_synth(x, seed=seed, k0=k)
+                out[mod][name] = x.view(shp)
+                seed += 1
+        return out
+
+    pairs = list(zip([tree(k) for k in range(K)], fedavg_weights(K)))
+    for _ in range(5):
+        tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    n = 5 * calls
+    t0 = pc()
+    for _ in range(n):
+        tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    ms = (pc() - t0) / n * 1e3
+    res["c1_tree_mean_back_to_back_ms"] = round(ms, 4)
+    res["c1_tree_mean_back_to_back_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+    single = []
+    for _ in range(n):
+        torch.cuda.synchronize()
+        t0 = pc()
+        tu.tree_mean(pairs)
+        torch.cuda.synchronize()
+        single.append(pc() - t0)
+    ms = float(np.median(single)) * 1e3
+    res["c1_tree_mean_sync_call_ms"] = round(ms, 4)
+    res["c1_tree_mean_sync_call_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+    res["note"] = ("caller-held pytrees, separate allocations; timed after the headline, outside its "
+                   "timed region; GB/s = K*P*4 client-delta bytes per call")
+    del pairs
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
 
 def _free_port() -> int:
@@ -133,38 +226,62 @@ def spawn_ranks(nproc: int, argv, script: str = None, timeout: float = None) -> 
     (``python -m torch.distributed.run``, rendezvous on 127.0.0.1): nothing is exec'd.
     Every rank's stderr passes through; stdout is collected and only the JSON line
     (rank 0's) is printed. Returns the launcher's exit status, non-zero if any rank
-    failed or no JSON line came back."""
+    failed or no JSON line came back. Rank 0 writes its line to the file named in
+    FJ_BENCH_JSON (emit_json); the shared stdout pipe is the fallback for scripts that
+    do not."""
     import subprocess
+    import tempfile
 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script or os.path.abspath(__file__),
            *argv]
-    env = dict(os.environ, FJ_BENCH_LAUNCHER="bench.py -> torch.distributed.run child")
+    fd, json_path = tempfile.mkstemp(prefix="fj_bench_", suffix=".json")
+    os.close(fd)
+    env = dict(os.environ, FJ_BENCH_LAUNCHER="bench.py -> torch.distributed.run child", FJ_BENCH_JSON=json_path)
     log("+", " ".join(cmd))
     try:
-        proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, timeout=timeout)
-    except subprocess.TimeoutExpired:
-        log(f"spawned ranks did not finish within {timeout} s")
-        return 124
-    lines = []
-    for ln in proc.stdout.decode(errors="replace").splitlines():
-        # the ranks share one pipe: another rank's unterminated banner can precede the JSON
-        i = ln.find('{"')
-        if i >= 0:
-            try:
-                json.loads(ln[i:])
-                lines.append(ln[i:])
-            except ValueError:
-                pass
+        try:
+            proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, timeout=timeout)
+        except subprocess.TimeoutExpired:
+            log(f"spawned ranks did not finish within {timeout} s")
+            return 124
+        with open(json_path) as f:
+            filed = f.read().strip()
+    finally:
+        os.unlink(json_path)
     if proc.returncode != 0:
         log(f"rank launcher exited with status {proc.returncode}")
         return proc.returncode
+    if filed:  # rank 0's line from its own file: nothing else can be interleaved into it
+        lines = [filed]
+    else:  # a script that does not write FJ_BENCH_JSON: rank 0's JSON object on the shared pipe
+        lines = []
+        for ln in proc.stdout.decode(errors="replace").splitlines():
+            i = ln.find('{"')  # another rank's unterminated banner can precede the JSON
+            if i >= 0:
+                try:
+                    json.loads(ln[i:])
+                    lines.append(ln[i:])
+                except ValueError:
+                    pass
     if len(lines) != 1:
         log(f"expected one JSON line from rank 0, got {len(lines)}")
         return 1
     sys.stdout.write(lines[0] + "\n")
     sys.stdout.flush()
     return 0
+
+
+def emit_json(json_fd, res):
+    """Rank 0's result line: to the saved stdout, and to the file a spawning parent named in
+    FJ_BENCH_JSON (ranks share one stdout pipe, where a line longer than PIPE_BUF could be
+    interleaved with another rank's output)."""
+    line = json.dumps(res) + "\n"
+    path = os.environ.get("FJ_BENCH_JSON")
+    if path:
+        with open(path, "w") as f:
+            f.write(line)
+    os.write(json_fd, line.encode())
 
 
 def load_traffic(workload):
@@ -188,6 +305,9 @@ def main():
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=-1, help="-1 auto, 0 off, 1 on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in surface sub-record (mean_aggregator().apply / tree_mean over "
+                         "caller-held pytrees, timed after the headline)")
     ap.add_argument("--e2e", action="store_true", help="also time host-resident deltas (H2D + fold + D2H)")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--all-ranks", action="store_true",
@@ -219,11 +339,9 @@ def main():
     if args.reference_bf16 and (WORKLOADS[args.workload][2] != torch.bfloat16 or args.gpus > 1 or args.with_norms):
         raise SystemExit("--reference-bf16 runs a bf16 workload (c5s) at N=1 without fused norms")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # bare `python bench.py --gpus N`: one rank per GPU as child processes (no GPU
-        # call has happened in this process, and nothing is exec'd)
-        if args.backend == "nccl" and torch.cuda.device_count() < args.gpus:
-            raise SystemExit(f"--gpus {args.gpus} needs {args.gpus} visible GPUs for RCCL "
-                             f"(found {torch.cuda.device_count()}); --backend gloo rehearses on fewer")
+        # bare `python bench.py --gpus N`: one rank per GPU as child processes (nothing in
+        # this process touches the GPU runtime, not even a device count — the ranks check
+        # that there are enough GPUs — and nothing is exec'd)
         raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:]))
     # stdout carries exactly one line, rank 0's JSON: native libraries write banners to fd 1
     # (RCCL's version block, gloo's connection notes), so fd 1 is pointed at stderr for the
@@ -238,7 +356,11 @@ def main():
     if args.gpus != world:
         if world == 1 and args.gpus > 1:
             raise SystemExit("launch N>1 with torch.distributed.run (one rank per GPU)")
-    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    ngpu = torch.cuda.device_count()
+    if world > 1 and args.backend == "nccl" and ngpu < world:
+        raise SystemExit(f"--gpus {world} needs {world} visible GPUs for RCCL (found {ngpu}); "
+                         f"--backend gloo rehearses on fewer")
+    dev = torch.device("cuda", local_rank % max(1, ngpu))
     torch.cuda.set_device(dev)
     nshard = world
     if args.rehearse_shard > 1:
@@ -487,9 +609,12 @@ def main():
             res["e2e_host_resident_GBs"] = round(e2e, 2)
         if nshard != world:
             res["rehearsal_projected_whole_job_GBs"] = round(value * nshard, 2)
+        if (not sharded and not args.no_dropin and args.workload == "c3" and not args.clients
+                and args.server == "none" and not args.with_norms):
+            res["drop_in"] = dropin_surface(dev)
         if not sharded and not args.no_cpu_baseline and dtype == torch.float32:
             res["cpu_baseline"] = cpu_baseline(K)
-        os.write(json_fd, (json.dumps(res) + "\n").encode())
+        emit_json(json_fd, res)
     if comm is not None:
         torch.cuda.synchronize()
         comm.close()
@@ -558,7 +683,7 @@ def single_process(args):
                       "parallelism": f"client-sharded x{N}, one process, grouped RCCL "
                                      f"{'all_reduce' if args.all_ranks else 'reduce'}",
                       "buckets": fd.bucket_name(buckets)}}
-    os.write(json_fd, (json.dumps(res) + "\n").encode())
+    emit_json(json_fd, res)
 
 
 if __name__ == "__main__":

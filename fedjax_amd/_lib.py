@@ -41,6 +41,7 @@ COMM_MAX_DEVICES = 16
 TREE_ABI_VERSION = 1
 TREE_MAX_LEAVES, TREE_MAX_OPERANDS = 64, 2
 TREE_NORM, TREE_NO_OUT = 1 << 8, 1 << 9
+TREE_ORDERED = 1 << 10  # FJTREE_ORDERED: norm combine by release/acquire atomics (fjtree.h)
 # include/fjcomp.h
 COMP_UNIFORM, COMP_TERNGRAD, COMP_BINARY = 1, 2, 3
 WHT_PLAIN, WHT_ROTATE, WHT_UNROTATE, WHT_UNROTATE_DRIVE = 0, 1, 2, 3

@@ -2,10 +2,10 @@
 
 Mirror of google/fedjax 0.0.17 ``fedjax/aggregators/aggregator.py``:
 
-* :class:`Aggregator` — frozen pytree dataclass of ``init`` / ``apply`` (:53-80);
-* :class:`MeanAggregatorState` — empty state (:83-85);
+* :class:`Aggregator` — frozen pytree dataclass of ``init`` / ``apply`` (:26-53);
+* :class:`MeanAggregatorState` — empty state (:56-58);
 * :func:`mean_aggregator` — ``apply`` lazily drops client ids and calls
-  :func:`fedjax_amd.tree_util.tree_mean` (:88-102), which folds all K clients on
+  :func:`fedjax_amd.tree_util.tree_mean` (:61-75; the call at :73), which folds all K clients on
   the GPU in one kernel launch per leaf-dtype group.
 """
 
@@ -21,7 +21,7 @@ AggregatorState = PyTree
 
 @dataclasses.dataclass
 class Aggregator:
-    """Interface for algorithms to aggregate (aggregator.py:53-80).
+    """Interface for algorithms to aggregate (aggregator.py:26-53).
 
     Usage, as in the reference::
 

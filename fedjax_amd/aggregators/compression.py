@@ -180,7 +180,7 @@ def _bits_per_param(per_param: float, P: int, L: int) -> np.float32:
 
 def _consume(clients: Iterable) -> Tuple[list, list]:
     trees, weights = [], []
-    for _, params, weight in clients:  # client ids are ignored (aggregator.py:96)
+    for _, params, weight in clients:  # client ids are ignored (aggregator.py:69)
         trees.append(params)
         weights.append(weight)
     return trees, weights

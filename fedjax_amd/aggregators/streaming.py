@@ -31,6 +31,17 @@ from fedjax_amd import pytree, tree_util
 from fedjax_amd.typing import PyTree
 
 
+_NO_VERSION = -2  # fjhost.cpp kNoVersion: an inference tensor (no in-place version counter)
+
+
+def _version_of(x) -> int:
+    """In-place version counter of a tensor leaf; -1 for host arrays and scalars, and
+    _NO_VERSION for inference tensors (``torch.inference_mode``), whose ``_version`` raises."""
+    if not isinstance(x, torch.Tensor):
+        return -1
+    return _NO_VERSION if x.is_inference() else int(x._version)
+
+
 class RunningMean:
     """Running weighted sum of client deltas with the structure of ``template``.
 
@@ -47,7 +58,9 @@ class RunningMean:
     ``RuntimeError``. The guard watches the tensors, not the containers: putting a
     different tensor into a buffered dict or list after ``add()`` is not detected.
     ``copy_on_add=True`` clones every delta (into a fresh container) at ``add()``
-    instead (one extra device copy per client; safe for any reuse).
+    instead (one extra device copy per client; safe for any reuse). Inference tensors
+    (``torch.inference_mode``) have no version counter, so their leaves are always
+    cloned at ``add()``.
     """
 
     def __init__(self, template: PyTree, *, buffer_clients: Optional[int] = None,
@@ -97,8 +110,7 @@ class RunningMean:
             if _lib.host().leaf_versions(trees, self._spec, L, v) == 0:
                 return v
         for k, t in enumerate(trees):  # other leaf types or node kinds; raises on mismatch
-            v[k] = [x._version if isinstance(x, torch.Tensor) else -1
-                    for x in pytree.flatten_as(self.treedef, t)]
+            v[k] = [_version_of(x) for x in pytree.flatten_as(self.treedef, t)]
         return v
 
     def _record_versions(self, delta: PyTree) -> None:
@@ -126,6 +138,14 @@ class RunningMean:
                 x.clone() if isinstance(x, torch.Tensor) else x for x in pytree.flatten_as(self.treedef, delta)])
         else:
             self._record_versions(delta)
+            if (self._vrows[len(self._trees)] == _NO_VERSION).any():
+                # inference tensors carry no version counter to guard the reference with:
+                # buffer a snapshot of those leaves instead (their values at add(), as the
+                # reference reads them)
+                delta = pytree.unflatten(self.treedef, [
+                    x.clone() if isinstance(x, torch.Tensor) and x.is_inference() else x
+                    for x in pytree.flatten_as(self.treedef, delta)])
+                self._vrows[len(self._trees)] = self._leaf_versions([delta])[0]
         self._trees.append(delta)
         self._weights.append(w)
         self.total_weight += w

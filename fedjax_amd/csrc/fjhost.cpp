@@ -1,7 +1,7 @@
 // fjhost.cpp — native host side of the pytree aggregation path (CPython extension).
 //
 // tree_mean over separate client pytrees (fedjax/core/tree_util.py:76-96, called from
-// examples/fed_avg.py:82 and aggregator.py:100) spends its host time walking K pytrees
+// examples/fed_avg.py:82 and aggregator.py:73) spends its host time walking K pytrees
 // and reading, per (client, leaf), the tensor's type / dtype / device / contiguity /
 // shape and device pointer. In Python that is five attribute calls per leaf; here it
 // is a handful of loads from the TensorImpl. The GPU arithmetic stays in libfjagg.so
@@ -83,6 +83,14 @@ struct Stamp {
   }
 };
 
+// torch's in-place version counter of t. Inference tensors (torch.inference_mode) carry
+// none (_version() throws): kNoVersion, and the callers that need a guard (capture,
+// append_check, RunningMean) treat such a leaf as "cannot be deferred by reference".
+constexpr int64_t kNoVersion = -2;
+inline int64_t version_of(const at::Tensor& t) {
+  return t.is_inference() ? kNoVersion : static_cast<int64_t>(t._version());
+}
+
 struct Walk {
   const std::vector<at::ScalarType>* dtypes;  // nullptr: record versions only (leaf_versions)
   const std::vector<c10::IntArrayRef>* sizes;
@@ -98,7 +106,7 @@ enum { kLeaf = 0, kNone = 1, kDict = 2, kList = 3, kTuple = 4 };
 int leaf(PyObject* x, Walk& w) {
   if (w.dtypes == nullptr) {  // leaf_versions: any tensor, its in-place modification counter
     if (!THPVariable_Check(x) || w.leaf >= w.cap) return 1;
-    w.out[w.leaf++] = static_cast<int64_t>(THPVariable_Unpack(x)._version());
+    w.out[w.leaf++] = version_of(THPVariable_Unpack(x));
     return 0;
   }
   if (Py_TYPE(x) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) return 1;
@@ -584,16 +592,22 @@ bool f32_weight(PyObject* w, float* out) {
 }
 
 // Leaves of operand k: float32, strided, contiguous, on cuda:dev, leaf l shaped like
-// operand 0's. Fills the version sum. false: not the fast case.
-bool check_leaves(const PWalk& w, int k, c10::DeviceIndex dev, int64_t* vsum) {
+// operand 0's. Fills the version sum; *unversioned (optional) is set when some leaf is an
+// inference tensor (no version counter). false: not the fast case.
+bool check_leaves(const PWalk& w, int k, c10::DeviceIndex dev, int64_t* vsum, bool* unversioned = nullptr) {
   int64_t vs = 0;
+  if (unversioned) *unversioned = false;
   for (size_t l = 0; l < w.leaves[k].size(); ++l) {
     const at::Tensor& t = THPVariable_Unpack(w.leaves[k][l]);
     if (t.layout() != c10::kStrided || t.scalar_type() != at::kFloat || !t.is_cuda() || t.get_device() != dev ||
         !t.is_contiguous())
       return false;
     if (k > 0 && t.sizes() != THPVariable_Unpack(w.leaves[0][l]).sizes()) return false;
-    vs += static_cast<int64_t>(t._version());
+    if (t.is_inference()) {
+      if (unversioned) *unversioned = true;
+    } else {
+      vs += static_cast<int64_t>(t._version());
+    }
   }
   *vsum = vs;
   return true;
@@ -637,7 +651,9 @@ PyObject* capture(PyObject*, PyObject* args) {
       if (!t0.is_cuda()) Py_RETURN_NONE;
       dev = t0.get_device();
     }
-    if (!check_leaves(w, 0, static_cast<c10::DeviceIndex>(dev), &vs)) Py_RETURN_NONE;
+    bool unv = false;
+    // an inference tensor has no version counter to guard a lazy capture with: not deferred
+    if (!check_leaves(w, 0, static_cast<c10::DeviceIndex>(dev), &vs, &unv) || unv) Py_RETURN_NONE;
     const Py_ssize_t L = static_cast<Py_ssize_t>(w.leaves[0].size());
     PyObject* tup = PyTuple_New(L);
     if (!tup) return nullptr;
@@ -668,7 +684,7 @@ PyObject* matches(PyObject*, PyObject* args) {
     int64_t vs = 0;
     for (size_t l = 0; l < w.leaves[0].size(); ++l) {
       if (w.leaves[0][l] != PyTuple_GET_ITEM(tup, l)) Py_RETURN_FALSE;
-      vs += static_cast<int64_t>(THPVariable_Unpack(w.leaves[0][l])._version());
+      vs += version_of(THPVariable_Unpack(w.leaves[0][l]));
     }
     if (vs != vsum) Py_RETURN_FALSE;
     Py_RETURN_TRUE;
@@ -721,7 +737,9 @@ PyObject* append_check(PyObject*, PyObject* args) {
     const at::Tensor& t0 = THPVariable_Unpack(w.leaves[0][0]);
     if (!t0.is_cuda()) Py_RETURN_NONE;
     int64_t vs0, vs;
-    if (!check_leaves(w, 0, t0.get_device(), &vs0) || !check_leaves(w, 1, t0.get_device(), &vs)) Py_RETURN_NONE;
+    bool unv = false;
+    if (!check_leaves(w, 0, t0.get_device(), &vs0) || !check_leaves(w, 1, t0.get_device(), &vs, &unv) || unv)
+      Py_RETURN_NONE;  // (an inference-tensor item cannot be held by reference: eager tree_add)
     const Py_ssize_t L = static_cast<Py_ssize_t>(w.leaves[1].size());
     if (cap != Py_None) {
       if (!PyTuple_Check(cap) || PyTuple_GET_SIZE(cap) < 2) Py_RETURN_NONE;
@@ -795,7 +813,7 @@ PyObject* table_from_caps(PyObject*, PyObject* args) {
       int64_t vs = 0;
       for (Py_ssize_t l = 0; l < L; ++l) {
         const at::Tensor& t = THPVariable_Unpack(PyTuple_GET_ITEM(tup, l));
-        vs += static_cast<int64_t>(t._version());
+        vs += version_of(t);
         out[k * L + l] = reinterpret_cast<int64_t>(t.data_ptr());
       }
       if (vs != PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1))) return PyLong_FromSsize_t(k);

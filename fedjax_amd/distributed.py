@@ -241,39 +241,51 @@ def sharded_tree_mean(local_pytrees_and_weights, *, W_total=None, group=None, ds
     size): it contributes a zero partial, so every rank reaches the same collectives.
     One small all_gather of (local W, partial size) runs first; it gives every rank
     W (when ``W_total`` is None) and lets all ranks agree on the partial's size — or
-    raise together when the ranks' trees disagree. A rank that must return the mean
+    raise together when the ranks' trees disagree, or when one rank's own clients fail
+    validation (that rank raises its own error, the others a ValueError naming it: no rank is left waiting in a collective). A rank that must return the mean
     but has no clients needs ``template`` (any pytree with the clients' structure and
     leaf shapes, e.g. the server params) for the structure of the result. Returns
     ``None`` on every rank when no rank has a client.
     """
     pairs = list(local_pytrees_and_weights)
     trees = [t for t, _ in pairs]
-    weights = [tree_util._host_weight(w) for _, w in pairs]
-    W_local = 0.0
-    for w in weights:
-        W_local += w  # tree_util.py:95 on this rank's share
     nccl = dist.get_backend(group) == "nccl"
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
-    td, views, sizes = None, None, None
-    if trees:
-        td, rows = tree_util._client_table(trees)
-        row0 = rows[0]
-        if any(x.dtype != torch.float32 for x in row0):
-            raise TypeError("sharded_tree_mean needs float32 leaves")
-        sizes = [x.numel() for x in row0]
-        shapes = [x.shape for x in row0]
-        dev = row0[0].device if row0 else dev
-    elif template is not None:
-        leaves, td = pytree.flatten(template)
-        shapes = [tuple(tree_util._to_tensor(x).shape) for x in leaves]
-        sizes = [int(np.prod(s, dtype=np.int64)) for s in shapes]
+    td, views, sizes, weights, W_local = None, None, None, [], 0.0
+    # Local validation runs BEFORE the header exchange, but a failure does not raise here
+    # alone (the other ranks would block in the all_gather): it is flagged in the header,
+    # and every rank raises after the exchange.
+    local_error = None
+    try:
+        weights = [tree_util._host_weight(w) for _, w in pairs]
+        for w in weights:
+            W_local += w  # tree_util.py:95 on this rank's share
+        if trees:
+            td, rows = tree_util._client_table(trees)
+            row0 = rows[0]
+            if any(x.dtype != torch.float32 for x in row0):
+                raise TypeError("sharded_tree_mean needs float32 leaves")
+            sizes = [x.numel() for x in row0]
+            shapes = [x.shape for x in row0]
+            dev = row0[0].device if row0 else dev
+        elif template is not None:
+            leaves, td = pytree.flatten(template)
+            shapes = [tuple(tree_util._to_tensor(x).shape) for x in leaves]
+            sizes = [int(np.prod(s, dtype=np.int64)) for s in shapes]
+    except Exception as e:  # noqa: BLE001 - re-raised below, after the other ranks are told
+        local_error, sizes, W_local = e, None, 0.0
     P = sum(sizes) if sizes is not None else -1
-    hdr = torch.tensor([float(W_local), float(P), float(len(trees))], dtype=torch.float64,
-                       device=dev if nccl else None)
+    hdr = torch.tensor([float(W_local), float(P), float(len(trees)), 1.0 if local_error else 0.0],
+                       dtype=torch.float64, device=dev if nccl else None)
     world = dist.get_world_size(group)
     got = [torch.empty_like(hdr) for _ in range(world)]
     dist.all_gather(got, hdr, group=group)
     got = [t.cpu().numpy() for t in got]
+    failed = [r for r, g in enumerate(got) if g[3] != 0]
+    if local_error is not None:
+        raise local_error
+    if failed:
+        raise ValueError(f"sharded_tree_mean: rank(s) {failed} rejected their local clients (see their error)")
     if W_total is None:
         W_total = 0.0
         for g in got:

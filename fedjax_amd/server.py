@@ -11,6 +11,11 @@ params / momentum / second moments are read and written once.
 
 Arithmetic restates optax's op order with IEEE single-precision ops; constants are
 rounded to float32 on the host the way JAX's weak typing rounds Python floats.
+``learning_rate`` is a float or a schedule (``ScalarOrSchedule``, optimizers.py:114):
+a schedule is evaluated on the host once per round, at optax's pre-increment step count
+(``optax.scale_by_schedule``), into the kernel's descriptor. :func:`ignore_grads_haiku`
+(optimizers.py:69-109) freezes haiku parameters: their leaves are left out of the fused
+launch, so params and optimizer state pass through untouched.
 Bitwise parity holds against the numpy restatement in tests/test_gpu_parity.py;
 against XLA it is unpinned (XLA:CPU may contract mul+add, and evaluates
 ``b1 ** count`` with its own pow).
@@ -20,7 +25,7 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
-from typing import Optional, Sequence
+from typing import Callable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -34,9 +39,11 @@ class ServerOptimizer:
     """Hyperparameters of fedjax.optimizers.sgd / adam / adagrad / rmsprop / yogi
     (optimizers.py:117-281). ``b2`` is rmsprop's ``decay``; ``momentum`` its trace decay;
     ``init_m`` / ``init_v`` the initial values of the state (adagrad's
-    initial_accumulator_value, rmsprop's initial_scale, yogi's 1e-6)."""
+    initial_accumulator_value, rmsprop's initial_scale, yogi's 1e-6). ``learning_rate`` is
+    a float or a schedule ``count -> float`` (ScalarOrSchedule, optimizers.py:114);
+    ``frozen`` holds the haiku ``(module_name, name)`` pairs of ignore_grads_haiku."""
     kind: int
-    learning_rate: float
+    learning_rate: Union[float, Callable[[int], float]]
     momentum: Optional[float] = None
     nesterov: bool = False
     b1: float = 0.9
@@ -45,6 +52,15 @@ class ServerOptimizer:
     eps_root: float = 0.0
     init_m: float = 0.0
     init_v: float = 0.0
+    frozen: Tuple[Tuple[str, str], ...] = ()
+
+    def lr(self, count: int) -> float:
+        """The learning rate of the step whose INCREMENTED count is ``count``: a schedule is
+        evaluated at the count before the step (optax.scale_by_schedule reads state.count,
+        then increments it)."""
+        if callable(self.learning_rate):
+            return float(np.asarray(self.learning_rate(count - 1), dtype=np.float64))
+        return float(self.learning_rate)
 
     def needs_m(self) -> bool:
         return self.kind in (_lib.OPT_MOMENTUM, _lib.OPT_ADAM, _lib.OPT_YOGI) or (
@@ -77,7 +93,7 @@ class ServerOptimizer:
         d = _lib.ServerOpt()
         d.kind = self.kind
         d.nesterov = int(self.nesterov)
-        d.neg_lr = f32(-self.learning_rate)  # scale_by_learning_rate: scale(-lr)
+        d.neg_lr = f32(-self.lr(count))  # scale_by_learning_rate: scale(-lr) / scale_by_schedule(-lr(t))
         d.decay = f32(self.momentum or 0.0)
         d.one_minus_b1, d.b1 = f32(1 - self.b1), f32(self.b1)
         d.one_minus_b2, d.b2 = f32(1 - self.b2), f32(self.b2)
@@ -121,6 +137,31 @@ def yogi(learning_rate: float, b1: float = 0.9, b2: float = 0.999, eps: float = 
     return ServerOptimizer(_lib.OPT_YOGI, learning_rate, b1=b1, b2=b2, eps=eps, init_m=1e-6, init_v=1e-6)
 
 
+def ignore_grads_haiku(optimizer: ServerOptimizer, non_trainable_names: List[Tuple[str, str]]) -> ServerOptimizer:
+    """fedjax.optimizers.ignore_grads_haiku (optimizers.py:69-109): ``optimizer`` with the
+    haiku parameters ``params[module_name][name]`` for every pair in ``non_trainable_names``
+    frozen. The reference maps them to ``None`` for the update and puts the old values
+    back; here their leaves are left out of the fused launch (no fold, no update), so the
+    params and the optimizer state of those leaves pass through untouched. The step count
+    still advances, as optax's does."""
+    return dataclasses.replace(optimizer, frozen=tuple((str(m), str(n)) for m, n in non_trainable_names))
+
+
+def _frozen_leaves(opt: ServerOptimizer, params, treedef) -> np.ndarray:
+    """bool [L]: leaf l (flatten order of ``treedef``) is one of opt.frozen. ``params`` is
+    a haiku-style ``{module_name: {name: leaf}}`` mapping, as the reference requires."""
+    L = treedef.num_leaves
+    if not opt.frozen:
+        return np.zeros(L, dtype=bool)
+    for m, n in opt.frozen:  # optimizers.py:103 indexes params[module_name][name]
+        params[m][n]  # noqa: B018 - KeyError for a name the params do not have
+    marks = {m: ({n: (m, n) in opt.frozen for n in sub} if isinstance(sub, dict) else False)
+             for m, sub in params.items()}
+    mask = np.array(pytree.flatten_as(treedef, marks), dtype=bool)
+    assert mask.size == L
+    return mask
+
+
 def fused_mean_update(slab: ClientDeltaSlab, weights: Sequence, opt: ServerOptimizer,
                       params: torch.Tensor, state: dict, *, mean_out: Optional[torch.Tensor] = None,
                       nontemporal: Optional[bool] = None) -> dict:
@@ -146,11 +187,30 @@ def fused_mean_update(slab: ClientDeltaSlab, weights: Sequence, opt: ServerOptim
     nt = nbytes >= tree_util.NONTEMPORAL_MIN_BYTES if nontemporal is None else nontemporal
     w_dev = slab.weight_vector(weights)
     ld = rows.stride(0) if rows.shape[0] > 1 else rows.shape[1]
-    ptr = lambda t: None if t is None else t.data_ptr()
-    _lib.call("fjagg_server_update_dense", kernels.dtype_code(rows.dtype), rows.data_ptr(), ld,
-              rows.shape[0], rows.shape[1], w_dev.data_ptr(), float(scale), ctypes.byref(desc),
-              params.data_ptr(), ptr(m), ptr(v), ptr(mean_out), _lib.NONTEMPORAL if nt else 0,
-              torch.cuda.current_stream(params.device).cuda_stream)
+    # ignore_grads_haiku: frozen leaves are column ranges of the slab; the fused step runs
+    # over each maximal run of trainable leaves (one launch without frozen leaves)
+    frozen = _frozen_leaves(opt, slab.unflatten(params), slab.treedef)
+    runs, l0 = [], 0
+    for l in range(len(frozen) + 1):
+        if l == len(frozen) or frozen[l]:
+            if l > l0:
+                runs.append((int(slab.offsets[l0]), int(slab.offsets[l])))
+            l0 = l + 1
+    esz = rows.element_size()
+    ptr = lambda t, o: None if t is None else t.data_ptr() + 4 * o
+    for c0, c1 in runs:
+        if c1 == c0:
+            continue
+        _lib.call("fjagg_server_update_dense", kernels.dtype_code(rows.dtype), rows.data_ptr() + esz * c0, ld,
+                  rows.shape[0], c1 - c0, w_dev.data_ptr(), float(scale), ctypes.byref(desc),
+                  params.data_ptr() + 4 * c0, ptr(m, c0), ptr(v, c0), ptr(mean_out, c0), _lib.NONTEMPORAL if nt else 0,
+                  torch.cuda.current_stream(params.device).cuda_stream)
+    if mean_out is not None:  # the mean of frozen leaves too (no update consumes it)
+        for l in np.flatnonzero(frozen):
+            c0, c1 = int(slab.offsets[l]), int(slab.offsets[l + 1])
+            if c1 > c0:
+                kernels.weighted_sum_dense(rows[:, c0:c1], w_dev, scale=float(scale), out=mean_out[c0:c1],
+                                           nontemporal=nt)
     new = dict(state)
     new["count"] = count
     return new
@@ -192,7 +252,10 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
     count = state["count"] + 1  # optax safe_int32_increment
     desc = opt.descriptor(count)
     in_c = kernels.dtype_code(dt)
-    leaf_n = np.array([x.numel() for x in row0], dtype=np.int64)
+    # ignore_grads_haiku: a frozen leaf gets no workgroups (leaf_n 0 in the plan), so its
+    # params and state are never read or written
+    frozen = _frozen_leaves(opt, params, td)
+    leaf_n = np.array([0 if f else x.numel() for x, f in zip(row0, frozen)], dtype=np.int64)
     in_ptrs = tree_util._ptr_table(rows)
     out_ptrs = np.array([x.data_ptr() for x in p], dtype=np.int64)
     st = np.zeros(3 * L, dtype=np.int64)
@@ -212,13 +275,21 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
     nbytes = int(leaf_n.sum()) * K * row0[0].element_size()
     nt = nbytes >= tree_util.NONTEMPORAL_MIN_BYTES if nontemporal is None else nontemporal
     flags = (_lib.NONTEMPORAL if nt else 0) | (_lib.UNALIGNED if unaligned else 0)
-    _lib.call("fjagg_server_update_ptrs", in_c, base, L, K, blocks.size // 2, w_ptr,
-              float(np.float32(tree_util._inverse(W))), ctypes.byref(desc), st_ptr, flags,
-              torch.cuda.current_stream(device).cuda_stream)
+    if blocks.size:
+        _lib.call("fjagg_server_update_ptrs", in_c, base, L, K, blocks.size // 2, w_ptr,
+                  float(np.float32(tree_util._inverse(W))), ctypes.byref(desc), st_ptr, flags,
+                  torch.cuda.current_stream(device).cuda_stream)
+    if mo is not None and frozen.any():  # the mean of frozen leaves too (no update consumes it)
+        idx = np.flatnonzero(frozen)
+        if isinstance(rows, tree_util._Table):  # every leaf is already the caller's device tensor
+            sub = [[pytree.flatten_as(td, t)[i] for i in idx] for t in trees]
+        else:
+            sub = [[r[i] for i in idx] for r in rows]
+        tree_util._fold(sub, weights, scale=tree_util._inverse(W), out=[mo[i] for i in idx])
     new = dict(state)
     new["count"] = count
     return new
 
 
-__all__ = ["ServerOptimizer", "adagrad", "adam", "fused_mean_update", "fused_tree_mean_update", "rmsprop", "sgd",
-           "yogi"]
+__all__ = ["ServerOptimizer", "adagrad", "adam", "fused_mean_update", "fused_tree_mean_update", "ignore_grads_haiku",
+           "rmsprop", "sgd", "yogi"]

@@ -519,12 +519,29 @@ def _tree_addrs():
     return _TREE_ADDRS
 
 
+# How the per-call norm's workgroup partials are ordered before the last workgroup reads
+# them (include/fjtree.h): "handoff" = write-through partials drained before
+# a relaxed counter add (gfx950's hand-off form, the default); "ordered" = an acquire-release
+# counter add (HIP memory model; a whole-L2 write-back per workgroup). Same bits either way.
+_NORM_COMBINE = os.environ.get("FJTREE_NORM_COMBINE", "handoff")
+
+
+def set_norm_combine(mode: str) -> None:
+    """Select the cross-workgroup ordering of the per-call fused norm: ``"handoff"``
+    (default) or ``"ordered"`` (release/acquire atomics, FJTREE_ORDERED)."""
+    global _NORM_COMBINE
+    if mode not in ("handoff", "ordered"):
+        raise ValueError("norm combine is 'handoff' or 'ordered'")
+    _NORM_COMBINE = mode
+
+
 def _leaf_fold(trees, weights, caps, scale=None, norm_operand=-1, no_out=False):
     """fjhost.leaf_fold: (out_tree, l2sq, l2) from one fjtree launch; None when the call
     is not the fast case (nothing launched). Raises when a captured operand is stale."""
     fold, ws = _TREE_ADDRS or _tree_addrs()
     flags = ((_lib.SCALE if scale is not None else 0) | (_lib.TREE_NORM if norm_operand >= 0 else 0)
-             | (_lib.TREE_NO_OUT if no_out else 0))
+             | (_lib.TREE_NO_OUT if no_out else 0)
+             | (_lib.TREE_ORDERED if norm_operand >= 0 and _NORM_COMBINE == "ordered" else 0))
     got = _lib.host().leaf_fold(trees, weights, caps, 1.0 if scale is None else float(scale), flags,
                                 max(norm_operand, 0), -1, 0, fold, ws)
     if got is None:
@@ -548,6 +565,10 @@ class WeightedTree:
     ``materialize()`` returns it. The input's leaf objects and their in-place versions are
     captured at ``tree_weight``: if a leaf is replaced or modified before the weighted
     value is used, using it raises RuntimeError (the reference's arrays are immutable).
+    The guard is torch's in-place version counter: writes that bypass it (through
+    ``tensor.data``, or by native code writing the tensor's memory) are not seen, and the
+    deferred multiply then reads the new values. Inference tensors, which have no version
+    counter, are weighted eagerly.
     ``isinstance(w, dict)`` is False: call ``materialize()`` where the concrete container
     type matters.
     """
@@ -591,7 +612,10 @@ pytree.register_lazy_type(WeightedTree, WeightedTree.materialize)
 _F32_EXACT_INT = 1 << 53
 
 # Deferred running sums (PendingSum): on by default; see set_deferred_sums.
-_DEFER = {"enabled": True, "budget_bytes": 4 << 30, "max_clients": 4095}
+# budget_bytes None = automatic: min(4 GiB, 1/8 of the device's free memory when the
+# process first defers a sum on it), see _defer_budget
+_DEFER = {"enabled": True, "budget_bytes": None, "max_clients": 4095}
+_AUTO_BUDGET = {}  # device index -> automatic budget in bytes
 
 
 def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = None,
@@ -603,12 +627,38 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
     ``max_clients`` (<= 4095) clients per launch (an older part of the chain is folded
     first when a limit would be passed, so memory stays bounded). Disabled: every call is
     one fused launch (fjtree_fold_leaves), which also suits loops that update delta
-    tensors in place between clients. Both give the reference's bits."""
+    tensors in place between clients. Both give the reference's bits.
+
+    Memory: a deferred chain keeps its clients' deltas alive until its fold, where the
+    reference's loop frees each delta after its ``tree_add`` (tree_util.py:85-96). The
+    default budget is therefore min(4 GiB, 1/8 of the device memory free when the process
+    first defers a sum there), per chain; a loop that keeps several running sums at once
+    holds up to that much per sum — pass a smaller ``budget_bytes`` (or disable deferral)
+    on a device close to full. ``budget_bytes=0`` restores the automatic value.
+
+    Semantics: deferral holds each delta by reference, guarded by torch's in-place
+    version counter (a modified delta makes the fold raise). Writes that bypass that
+    counter — ``tensor.data`` writes, native code or kernels writing the memory — are not
+    detected, and the deferred fold reads the new values: loops that write deltas that
+    way must disable deferral."""
     _DEFER["enabled"] = bool(enabled)
     if budget_bytes is not None:
-        _DEFER["budget_bytes"] = int(budget_bytes)
+        _DEFER["budget_bytes"] = int(budget_bytes) if int(budget_bytes) > 0 else None
     if max_clients is not None:
         _DEFER["max_clients"] = min(4095, max(1, int(max_clients)))
+
+
+def _defer_budget(device: torch.device) -> int:
+    """Bytes of deltas one deferred chain may hold on ``device`` (see set_deferred_sums)."""
+    b = _DEFER["budget_bytes"]
+    if b is not None:
+        return b
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    got = _AUTO_BUDGET.get(idx)
+    if got is None:
+        free, _ = torch.cuda.mem_get_info(idx)
+        got = _AUTO_BUDGET[idx] = int(min(4 << 30, max(64 << 20, free // 8)))
+    return got
 
 
 class _Chain:
@@ -684,7 +734,11 @@ class PendingSum:
     The deltas stay referenced until the fold (bounded by :func:`set_deferred_sums`). A
     delta modified in place after it was added makes the fold raise RuntimeError (the
     reference's arrays are immutable); loops that reuse delta buffers should call
-    ``set_deferred_sums(False)``. ``isinstance(s, dict)`` is False: call
+    ``set_deferred_sums(False)``. The check is torch's in-place version counter, so a
+    write that bypasses it — through ``tensor.data``, or by native code / a kernel writing
+    the tensor's memory — is NOT detected: the fold then sums the new values where the
+    reference summed the old ones. Such loops must use ``set_deferred_sums(False)`` (or add
+    copies). Inference tensors have no version counter and are never deferred. ``isinstance(s, dict)`` is False: call
     ``materialize()`` where the concrete container type matters.
     """
 
@@ -827,7 +881,8 @@ def _defer(sum_side, item, item_weight, item_cap):
                            "place) before its weighted value was used; the reference computes "
                            "tree_weight eagerly")
     if parent is not None and parent._value is None and (
-            parent._n + 1 > _DEFER["max_clients"] or parent._bytes + cap[2] > _DEFER["budget_bytes"]):
+            parent._n + 1 > _DEFER["max_clients"] or
+            parent._bytes + cap[2] > _defer_budget(cap[0][0].device)):
         parent.materialize()  # bound the chain: fold what is pending, continue from it
     bcap = None
     if parent is None or parent._value is not None:  # this link starts a run: capture its base

@@ -14,7 +14,7 @@ Restates google/fedjax 0.0.17 ``fedjax/core/tree_util.py`` op for op:
 * ``tree_mean``              tree_util.py:76-96   weighted fold, W summed in Python
 * ``tree_size``              tree_util.py:99-102
 * ``tree_l2_squared/norm``   tree_util.py:105-114
-* ``mean_aggregator``        fedjax/aggregators/aggregator.py:88-102
+* ``mean_aggregator``        fedjax/aggregators/aggregator.py:61-75
 
 and the JAX dtype rules those lines run under (x64 disabled, the jax default):
 Python ints/floats are *weakly typed* (they take the leaf's dtype), int64/float64
@@ -224,7 +224,7 @@ def tree_l2_norm(pytree) -> np.float32:
 
 
 # ----------------------------------------------------------------------------
-# Aggregator (fedjax/aggregators/aggregator.py:53-102)
+# Aggregator (fedjax/aggregators/aggregator.py:26-75)
 # ----------------------------------------------------------------------------
 
 Aggregator = collections.namedtuple("Aggregator", ["init", "apply"])

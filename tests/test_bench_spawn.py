@@ -67,8 +67,31 @@ def test_spawn_propagates_rank_failure(rank_script, capfd):
     assert capfd.readouterr().out.strip() == ""
 
 
+def test_spawn_takes_rank0_line_from_its_file(tmp_path, capfd):
+    """Rank 0 writes its line to FJ_BENCH_JSON (bench.emit_json): a line longer than
+    PIPE_BUF comes back whole while every rank writes to the shared stdout."""
+    p = tmp_path / "rank.py"
+    p.write_text(textwrap.dedent("""
+        import json, os, sys
+        sys.path.insert(0, %r)
+        import bench
+        r = int(os.environ["RANK"])
+        for _ in range(200):
+            sys.stdout.write(f"rank {r} noise " * 20 + "\\n")
+        if r == 0:
+            bench.emit_json(os.dup(1), {"n_gpus": 2, "blob": "x" * 20000})
+        sys.stdout.flush()
+    """ % bench.ROOT))
+    rc = bench.spawn_ranks(2, [], script=str(p), timeout=180)
+    out = capfd.readouterr().out
+    assert rc == 0
+    d = json.loads(out)
+    assert d["n_gpus"] == 2 and d["blob"] == "x" * 20000
+
+
 def test_bare_bench_refuses_nccl_without_gpus():
-    """--gpus 2 on a box without 2 GPUs and the RCCL backend: a clear error, no spawn."""
+    """--gpus 2 on a box without 2 GPUs and the RCCL backend: the ranks (not the parent,
+    which never touches the GPU runtime) stop with a clear error."""
     import subprocess
     import sys
 

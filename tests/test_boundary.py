@@ -123,7 +123,7 @@ def test_reference_api_surface():
     for name in ["tree_weight", "tree_inverse_weight", "tree_zeros_like", "tree_add", "tree_sum",
                  "tree_mean", "tree_size", "tree_l2_squared", "tree_l2_norm", "tree_clip_by_global_norm"]:
         assert callable(getattr(fedjax_amd.tree_util, name)), name
-    # fedjax/aggregators/aggregator.py:53-102
+    # fedjax/aggregators/aggregator.py:26-75
     for name in ["Aggregator", "MeanAggregatorState", "mean_aggregator"]:
         assert hasattr(fedjax_amd.aggregators, name), name
     assert callable(fedjax_amd.dataclass)

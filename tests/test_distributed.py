@@ -146,6 +146,42 @@ def test_sharded_tree_mean_without_clients_world3_gloo():
     assert res == {0: True, 1: True, 2: True}
 
 
+def _worker_bad(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fedjax_amd import distributed as fd
+        tmpl = {"w": torch.zeros(3, 2), "b": torch.zeros(2)}
+        # rank 1's own clients fail its local checks (here: no GPU for the fold's pointer
+        # table); rank 0 has none. Both must raise — neither may wait in the all_gather.
+        clients = [(tmpl, 1), ({"w": torch.zeros(3, 2), "c": torch.zeros(2)}, 2)] if rank == 1 else []
+        try:
+            fd.sharded_tree_mean(clients, template=tmpl)
+            q.put((rank, "returned"))
+        except Exception as e:  # noqa: BLE001
+            q.put((rank, type(e).__name__ + ": " + str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_tree_mean_local_failure_raises_on_every_rank_gloo():
+    """a rank whose local validation fails flags it in the header exchange, so
+    every rank raises (that rank its own error, the others a ValueError naming it)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_bad, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0].startswith("ValueError") and "rank(s) [1]" in res[0], res
+    assert not res[1].startswith(("returned", "ValueError: sharded_tree_mean: rank")), res
+
+
 @pytest.mark.parametrize("world", [1, 4, 8])
 def test_sharded_mean_1_to_8_ranks_gloo(world, coracle):
     """The analogue of for_each_client_test.py:388-438 (the pmap backend on 1..8 simulated

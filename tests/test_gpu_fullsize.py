@@ -178,6 +178,86 @@ def _bf16_f32(u16):
     return (np.asarray(u16, np.uint32) << 16).view(np.float32)
 
 
+def _configs4_rank0_worker(port, q):
+    """configs[4], rank 0 of 8: the step bench.py --workload c5 times per rank (bench.py
+    step(): sharded_weighted_mean -> f32 partial, then the bf16 cast of the mean)."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from fedjax_amd import distributed as fd
+        K, P, N = 8192, 125_000_000, 8
+        weights = [int(v) for v in ref.fedavg_weights(K, seed=19)]
+        W = 0.0
+        for w in weights:
+            W += w  # every rank sums all 8192 clients' weights (tree_util.py:95)
+        k0, k1 = fd.shard_range(K, 0, N)
+        free, _ = torch.cuda.mem_get_info()
+        need = (k1 - k0) * P * 2 + P * 6
+        if free < need + (1 << 30):
+            q.put(("skip", f"needs {need / 2**30:.0f} GiB free, have {free / 2**30:.0f}"))
+            return
+        x = torch.empty(k1 - k0, P, dtype=torch.bfloat16, device=dev)
+        kernels.fill_synth(x, seed=20, k0=k0)
+        wl = torch.tensor(np.float32(weights[k0:k1]), device=dev)
+        ones = torch.ones(1, dtype=torch.float32, device=dev)
+        comm = fd.RcclCommunicator(device=dev)
+        cols = sample_cols(P, n=2000)
+        ct = torch.from_numpy(cols).to(dev)
+        outs = {}
+        for buckets in (1, (4, 2, 1, 1), 8):
+            part = fd.sharded_weighted_mean(x, wl, W, buckets=buckets, comm=comm, nontemporal=True)
+            final = kernels.weighted_sum_dense(part.view(1, P), ones, out=torch.empty(P, dtype=torch.bfloat16,
+                                                                                       device=dev))
+            torch.cuda.synchronize()
+            outs[fd.bucket_name(buckets)] = (part.index_select(0, ct).cpu().numpy(),
+                                             final.index_select(0, ct).view(torch.int16).cpu().numpy().view(np.uint16))
+            del part, final
+        comm.close()
+        q.put(("ok", (k0, k1, W, cols, outs)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_configs4_rank0_share_native_pipeline(cuda):
+    """configs[4], rank 0 of 8: 1024 of the 8192 clients x 125 M bf16
+    (256 GB) through fjcomm_sharded_wsum_dense_edges on a world-1 RCCL communicator (equal,
+    8-way and 4:2:1:1 tapered buckets), then the bf16 cast of bench.py's step. The f32
+    partial is bitwise the oracle's f32 fold of the bf16 inputs scaled by f32(1/W) over all
+    8192 weights; the bf16 mean is its RNE rounding and within DESIGN.md §4's bound of the
+    f64 oracle."""
+    import torch.multiprocessing as mp
+    _free()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_configs4_rank0_worker, args=(_port(), q))
+    p.start()
+    status, payload = q.get(timeout=600)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    if status == "skip":
+        pytest.skip(payload)
+    k0, k1, W, cols, outs = payload
+    assert (k0, k1) == (0, 1024)
+    weights = [int(v) for v in ref.fedavg_weights(8192, seed=19)]
+    r = np.float32(tu._inverse(W))
+    assert r == ref.mean_scale(weights)
+    xb = _bf16_f32(_bf16_round(synth_cols(range(k0, k1), cols, 20)))
+    wsh = np.float32(weights[k0:k1])
+    want = ref.wsum_dense(xb, wsh, scale=r)
+    # f64 oracle of the shard's partial and DESIGN §4's bound for the bf16 mean
+    xf = xb.astype(np.float64)
+    y64 = (xf * wsh.astype(np.float64)[:, None]).sum(0) * float(r)
+    fbound = (1024 + 3) * U * float(r) * np.abs(xf * wsh.astype(np.float64)[:, None]).sum(0) + U * np.abs(y64)
+    for name, (part, final) in outs.items():
+        assert np.array_equal(bits(part), bits(want)), name
+        assert np.array_equal(final, _bf16_round(want)), name
+        assert np.all(np.abs(_bf16_f32(final) - y64) <= 2.0 ** -8 * np.abs(y64) + fbound), name
+
+
 def test_configs4_shard_bf16_1024x125M(cuda):
     """configs[4], one GPU's share: 1024 clients x 125,000,000 bf16 deltas (256 GB
     resident). Sampled columns: the synthetic fill equals the oracle's bf16 rounding,

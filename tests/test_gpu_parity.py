@@ -198,6 +198,103 @@ def test_narrow_fold_bitwise_every_dtype_and_alignment(K, P, dt, offset, cuda, c
         assert np.array_equal(bits(host(y18)), bits(want))
 
 
+STRIPE_CASES = [  # (K, P, dtype): tiles of 192 / 384 / 768 clients, stripes of 64 / 32 / 16 columns
+    (16384, 4096, "f32"), (4096, 16384, "f32"), (1000, 4101, "f32"), (193, 70, "f32"), (16, 33, "f32"),
+    (769, 2048 + 8, "bf16"), (385, 300, "bf16"), (300, 1000, "i32"), (2000, 9000, "f32")]
+
+
+@pytest.mark.parametrize("K,P,dt", STRIPE_CASES)
+def test_stripe_fold_bitwise(K, P, dt, cuda, coracle):
+    """k_dense_stripe (variants 19-22: auto, 64, 32, 16 columns; fjstripe.hip): tiles not
+    full (K not a multiple of 192 / 384 / 768, K below one tile), stripes not full, rows
+    padded to 16 bytes, accumulate mode, bf16 in / out, the bf16 reference fold, wrapping
+    int32 and int32 -> f32 — bitwise the E1U8 fold (variant 2) and, for f32, the oracle."""
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "i32": torch.int32}[dt]
+    es = torch.empty((), dtype=tdt).element_size()
+    ld = (P + 16 // es - 1) // (16 // es) * (16 // es) + 16 // es  # a padded, 16-byte multiple row
+    base = torch.empty(K, ld, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(base, seed=K + 3 * P)
+    if dt == "i32":
+        x = (base * 1e6).to(torch.int32)[:, :P]
+        wsets = [torch.tensor([int(v) for v in ref.fedavg_weights(K, seed=5)], dtype=torch.int32, device=cuda),
+                 torch.tensor(np.float32(ref.fedavg_weights(K, seed=6)), device=cuda)]
+    else:
+        x = base.to(tdt)[:, :P]
+        wsets = [torch.tensor(np.float32(ref.fedavg_weights(K, seed=5)), device=cuda)]
+    assert x.stride(0) * es % 16 == 0 and x.data_ptr() % 16 == 0
+    for w in wsets:
+        scale = None if w.dtype == torch.int32 else 0.125
+        modes = [dict()]
+        if dt == "bf16":
+            modes += [dict(reference_bf16=True), dict(out_dtype=torch.float32)]
+        if dt == "f32":
+            modes += [dict(out_dtype=torch.bfloat16)]
+        for kw in modes:
+            for acc in (False, True):
+                outs = []
+                for variant in (2, 19, 20, 21, 22):
+                    o = None
+                    if acc:
+                        probe = kernels.weighted_sum_dense(x[:1], w[:1], scale=scale, **kw)
+                        o = torch.full((P,), 3, dtype=probe.dtype, device=cuda)
+                    for nt in (False, True):
+                        oo = None if o is None else o.clone()
+                        outs.append((variant, nt, kernels.weighted_sum_dense(
+                            x, w, scale=scale, variant=variant, out=oo, accumulate=acc, nontemporal=nt, **kw)))
+                ref_out = outs[0][2].view(torch.uint8)
+                for variant, nt, y in outs[1:]:
+                    assert torch.equal(y.view(torch.uint8), ref_out), (dt, kw, acc, variant, nt, w.dtype)
+    if dt == "f32":  # and against the oracle
+        w = wsets[0]
+        want = coracle.wsum_f32(np.ascontiguousarray(host(x)), host(w), scale=np.float32(0.125))
+        y = kernels.weighted_sum_dense(x, w, scale=0.125, variant=19)
+        assert np.array_equal(bits(host(y)), bits(want))
+
+
+def test_stripe_fold_special_values(cuda, coracle):
+    """-0 / NaN / Inf / subnormal deltas and weights through k_dense_stripe: the -0.0 start
+    and padding of the stripe pipeline keep every bit of the reference sequence."""
+    K, P = 800, 256
+    x = torch.empty(K, P, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(x, seed=9)
+    x[0, :8] = torch.tensor([-0.0, 0.0, float("nan"), float("inf"), -float("inf"), 1e-45, -1e-45, -0.0])
+    x[:, 8] = -0.0  # a column that stays -0 throughout: s_0 = -0*w... = -0, sums of -0 stay -0
+    x[5, 9] = float("nan")
+    w = torch.tensor(np.float32(ref.fedavg_weights(K, seed=8)), device=cuda)
+    w[3] = -0.0
+    w[4] = 1e-40
+    want = coracle.wsum_f32(np.ascontiguousarray(host(x)), host(w), scale=np.float32(0.5))
+    for variant in (19, 20, 21, 22):
+        y = kernels.weighted_sum_dense(x, w, scale=0.5, variant=variant)
+        assert np.array_equal(bits(host(y)), bits(want)), variant
+
+
+@pytest.mark.parametrize("variant", [0, 2, 5, 12, 16, 17])
+def test_f32_in_bf16_out_units(variant, cuda, coracle):
+    """(F32, F32, BF16): a float32 16-byte unit holds 4 elements, i.e. 8 bytes of bf16
+    output. Round 2's store wrote 16 bytes per unit (4 of them the next unit's), so the
+    bf16 cast of the configs[4] step raced; now bitwise the RNE rounding of the f32 fold,
+    in plain and accumulate mode."""
+    K, P = 9, 4 * 4099
+    x = torch.empty(K, P, dtype=torch.float32, device=cuda)
+    kernels.fill_synth(x, seed=77)
+    xh = coracle.synth_f32(K, P, seed=77)
+    w = np.float32(ref.fedavg_weights(K, seed=78))
+    want = coracle.wsum_f32(xh, w, scale=np.float32(0.25))
+    u = want.view(np.uint32).astype(np.uint64)
+    want16 = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    y = kernels.weighted_sum_dense(x, torch.from_numpy(w).to(cuda), scale=0.25, out_dtype=torch.bfloat16,
+                                   variant=variant)
+    assert np.array_equal(host(y.view(torch.int16)).view(np.uint16), want16)
+    init16 = (np.arange(P) % 7).astype(np.float32)
+    o = torch.from_numpy(init16).to(cuda).to(torch.bfloat16)
+    kernels.weighted_sum_dense(x, torch.from_numpy(w).to(cuda), out=o, accumulate=True, variant=variant)
+    want_acc = coracle.wsum_f32(xh, w, init=init16)
+    ua = want_acc.view(np.uint32).astype(np.uint64)
+    assert np.array_equal(host(o.view(torch.int16)).view(np.uint16),
+                          ((ua + 0x7FFF + ((ua >> 16) & 1)) >> 16).astype(np.uint16))
+
+
 def test_dense_accumulate_and_strided_rows(cuda, coracle):
     K, P, ld = 17, 3001, 3072
     base = torch.empty(K, ld, dtype=torch.float32, device=cuda)

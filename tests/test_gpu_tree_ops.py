@@ -331,3 +331,82 @@ def test_lazy_norms_of_a_deferred_sum(cuda, sum_mode):
     s = tu.tree_add(tu.tree_zeros_like(xs[0]), tu.tree_weight(xs[0], 1))
     s = tu.tree_add(s, tu.tree_weight(xs[1], 1))
     assert type(tu.tree_l2_norm(xs[0])) is not tu._NormView
+
+
+def test_norm_combine_orders_give_the_same_bits(cuda):
+    """The per-call fused norm with its workgroup partials handed off by the gfx950
+    write-through + drain form (default) and by release/acquire atomics (FJTREE_ORDERED,
+    tree_util.set_norm_combine('ordered')): the same bits, many workgroups, repeated."""
+    g = torch.Generator().manual_seed(31)
+    d = to_dev(rand_tree({"a": (3_000_001,), "b": (513, 7), "c": (64,)}, g), cuda)
+    s = to_dev(rand_tree({"a": (3_000_001,), "b": (513, 7), "c": (64,)}, g), cuda)
+    got = {}
+    try:
+        for mode in ("handoff", "ordered"):
+            tu.set_norm_combine(mode)
+            outs = []
+            for _ in range(20):
+                alone = tu._leaf_fold([d], [1], [None], norm_operand=0, no_out=True)[2]
+                fused = tu._leaf_fold([s, d], [1, 5], [None, None], norm_operand=1)[2]
+                outs.append((alone.view(torch.int32).item(), fused.view(torch.int32).item()))
+            assert len(set(outs)) == 1, (mode, outs[:3])
+            got[mode] = outs[0]
+    finally:
+        tu.set_norm_combine("handoff")
+    assert got["handoff"] == got["ordered"]
+    assert got["handoff"][0] == got["handoff"][1]  # fused and standalone norms of d: one order
+    x64 = np.concatenate([x.astype(np.float64) for x in leaves_np(d)])
+    np.testing.assert_allclose(np.int32(got["handoff"][0]).view(np.float32), np.sqrt((x64 * x64).sum()), rtol=2e-6)
+
+
+def test_data_writes_bypass_the_deferred_guard_as_documented(cuda, sum_mode):
+    """the deferred sum's staleness guard is torch's in-place version counter.
+    A write through ``tensor.data`` does not bump it (its own counter), so — as
+    set_deferred_sums / PendingSum document — a deferred fold reads the NEW values, while
+    the eager path (set_deferred_sums(False)) has already summed the old ones, as the
+    reference does. An ordinary in-place write is caught in deferred mode."""
+    g = torch.Generator().manual_seed(41)
+    h0, h1 = rand_tree({"a": (500,)}, g), rand_tree({"a": (500,)}, g)
+    d = to_dev(h0, cuda)
+    s = tu.tree_add(tu.tree_zeros_like(d), tu.tree_weight(d, 3))
+    d["a"].data.copy_(h1["a"].to(cuda))  # bypasses d["a"]._version
+    got = tu.tree_inverse_weight(s, 3.)["a"].cpu().numpy()
+    old = ref.tree_inverse_weight(ref.tree_weight(to_np(h0), 3), 3.)["a"]
+    new = ref.tree_inverse_weight(ref.tree_weight(to_np(h1), 3), 3.)["a"]
+    want = new if sum_mode == "deferred" else old
+    assert np.array_equal(bits(got), bits(want))
+    # an in-place write the counter sees: deferred mode raises, eager mode kept the old value
+    d2 = to_dev(h0, cuda)
+    s2 = tu.tree_add(tu.tree_zeros_like(d2), tu.tree_weight(d2, 3))
+    d2["a"].add_(1.0)
+    if sum_mode == "deferred":
+        with pytest.raises(RuntimeError, match="modified"):
+            tu.tree_inverse_weight(s2, 3.)
+    else:
+        assert np.array_equal(bits(tu.tree_inverse_weight(s2, 3.)["a"].cpu().numpy()), bits(old))
+
+
+def test_deferred_chain_budget_is_bounded_by_free_memory(cuda, sum_mode):
+    """the automatic per-chain budget is min(4 GiB, free/8); a tiny explicit
+    budget folds the older part of the chain early with the same bits."""
+    if sum_mode != "deferred":
+        pytest.skip("deferred mode only")
+    b = tu._defer_budget(torch.device(cuda))
+    free, _ = torch.cuda.mem_get_info()
+    assert 64 << 20 <= b <= 4 << 30 and b <= max(64 << 20, free // 4)
+    g = torch.Generator().manual_seed(42)
+    hs = [rand_tree({"a": (4096,)}, g) for _ in range(9)]
+    ds = [to_dev(h, cuda) for h in hs]
+    try:
+        tu.set_deferred_sums(True, budget_bytes=3 * 4096 * 4)  # at most 3 deltas per fold
+        s = tu.tree_zeros_like(ds[0])
+        for k, d in enumerate(ds):
+            s = tu.tree_add(s, tu.tree_weight(d, k + 1))
+        assert type(s) is tu.PendingSum and s._n <= 3
+        got = tu.tree_inverse_weight(s, 45.)["a"].cpu().numpy()
+    finally:
+        tu.set_deferred_sums(True, budget_bytes=0)
+    want = tmap(lambda x: np.zeros(x.shape, np.float32), to_np(hs[0]))
+    for k, h in enumerate(hs):
+        want = ref.tree_add(want, ref.tree_weight(to_np(h), k + 1))
+    assert np.array_equal(bits(got), bits(ref.tree_inverse_weight(want, 45.)["a"]))

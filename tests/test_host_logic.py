@@ -192,3 +192,25 @@ def test_bf16_semantics_switch_and_leaf_rule():
         tu.set_bf16_semantics("f32")
     with pytest.raises(ValueError):
         tu.set_bf16_semantics("bf16")
+
+
+def test_server_schedule_and_frozen_mask_host_side():
+    """ScalarOrSchedule (optimizers.py:114): the descriptor of the step whose incremented
+    count is c carries f32(-lr(c - 1)) (optax.scale_by_schedule reads the count before
+    incrementing it); ignore_grads_haiku (optimizers.py:69-109) marks the frozen leaves in
+    flatten order and raises KeyError for a name the params do not have."""
+    from fedjax_amd import pytree, server
+    sched = lambda c: 0.1 * 0.5 ** c
+    opt = server.sgd(sched)
+    for c in (1, 2, 3):
+        assert opt.descriptor(c).neg_lr == np.float32(-sched(c - 1))
+    assert server.sgd(0.3).descriptor(7).neg_lr == np.float32(-0.3)
+    params = {"linear_1": {"w": np.zeros(3)}, "linear_2": {"w": np.zeros(3), "b": np.zeros(3)}}
+    _, td = pytree.flatten(params)
+    ig = server.ignore_grads_haiku(server.adam(sched), [("linear_1", "w"), ("linear_2", "b")])
+    assert ig.kind == server.adam(0.1).kind and ig.frozen == (("linear_1", "w"), ("linear_2", "b"))
+    # flatten order: linear_1/w, linear_2/b, linear_2/w
+    assert server._frozen_leaves(ig, params, td).tolist() == [True, True, False]
+    assert server._frozen_leaves(server.adam(0.1), params, td).tolist() == [False] * 3
+    with pytest.raises(KeyError):
+        server._frozen_leaves(server.ignore_grads_haiku(ig, [("linear_3", "w")]), params, td)

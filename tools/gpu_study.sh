@@ -104,5 +104,51 @@ case "$STUDY" in
     timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $O/trace -o run --output-format csv -- \
       python tools/time_pytree.py > $O/trace.log 2>&1 || die trace
     ;;
+  c5_rehearse)
+    # configs[4]: rank 0's share (1024 of 8192 clients x 125 M bf16) through the full sharded
+    # step on a world-1 RCCL communicator: fold -> f32 partial -> reduce -> bf16 cast
+    timeout -k 10 900 python bench.py --workload c5 --rehearse-shard 8 --steps ${STEPS:-10} --warmup 3 \
+      > $O/c5_rehearse.json 2> $O/c5_rehearse.err || die c5_rehearse
+    cat $O/c5_rehearse.json
+    ;;
+  narrow_pmc)
+    # k_dense_narrow (variant 18) counters at the two verdict shapes; SQ / GRBM / TCC in separate passes
+    for s in "16384 4096" "4096 16384"; do
+      n=$(echo $s | tr ' ' x)
+      B="python tools/sweep.py $s f32 1 5"
+      SWEEP_VARIANTS=${NARROW_VARIANTS:-18} timeout -s KILL 90 rocprofv3 --kernel-trace -d $O/$n/trace -o run \
+        --output-format csv -- $B > $O/$n.log 2>&1 || die "trace $n"
+      SWEEP_VARIANTS=${NARROW_VARIANTS:-18} timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT \
+        SQ_BUSY_CU_CYCLES SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY \
+        -d $O/$n/pmcA -o run --output-format csv -- $B >> $O/$n.log 2>&1 || die "pmcA $n"
+      SWEEP_VARIANTS=${NARROW_VARIANTS:-18} timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE \
+        -d $O/$n/pmcB -o run --output-format csv -- $B >> $O/$n.log 2>&1 || die "pmcB $n"
+      SWEEP_VARIANTS=${NARROW_VARIANTS:-18} timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS \
+        SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU \
+        -d $O/$n/pmcC -o run --output-format csv -- $B >> $O/$n.log 2>&1 || die "pmcC $n"
+      python tools/pmc_table.py ${NARROW_KERNEL:-k_dense_narrow} $O/table_$n.json $O/$n/trace $O/$n/pmcA \
+        $O/$n/pmcB $O/$n/pmcC > /dev/null
+    done
+    cat $O/table_*.json
+    ;;
+  stripe)
+    # k_dense_stripe (variants 19-22) parity, then the narrow-shape sweep against k_dense_narrow (18)
+    timeout -k 10 600 $PT tests/test_gpu_parity.py -k "stripe or variants_bitwise or narrow_fold" \
+      > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit 1
+    for s in "16384 4096 f32" "4096 16384 f32" "2048 32768 f32" "1024 65536 f32" "512 131072 f32" \
+             "256 262144 f32" "4096 32768 bf16" "1024 4096 f32" "128 16384 f32" "65536 1024 f32"; do
+      SWEEP_BALANCED_ONLY=1 SWEEP_VARIANTS=${SWEEP_VARIANTS:-2,18,19,20,21,22} timeout -k 10 120 \
+        python tools/sweep.py $s 3 5 || die "sweep $s"
+    done > $O/sweep.jsonl
+    cat $O/sweep.jsonl
+    ;;
+  r03tests)
+    # round-3 GPU tests: inference tensors, server ignore/schedules, norm combine orders, configs[4] share
+    timeout -k 10 900 $PT tests/test_gpu_inference_tensors.py tests/test_gpu_server_ext.py \
+      tests/test_gpu_tree_ops.py -k "norm_combine or data_writes or chain_budget or f32_in_bf16 or inference \
+      or ignore or schedule or frozen or configs4_rank0" tests/test_gpu_parity.py \
+      "tests/test_gpu_fullsize.py::test_configs4_rank0_share_native_pipeline" > $O/tests.log 2>&1
+    rc=$?; tail -5 $O/tests.log; [ $rc -eq 0 ] || exit 1
+    ;;
   *) echo "unknown study $STUDY"; exit 2 ;;
 esac

@@ -26,7 +26,7 @@ res = {}
 VARIANTS = [int(v) for v in os.environ.get("SWEEP_VARIANTS", ",".join(map(str, range(1, 16)))).split(",")]
 for _ in range(rounds):
     for v in VARIANTS:
-        for bal in (False, True):
+        for bal in ((True,) if os.environ.get("SWEEP_BALANCED_ONLY") else (False, True)):
             nt = True
             f = lambda: kernels.weighted_sum_dense(x, w, scale=0.5, out=out, nontemporal=nt, variant=v,
                                                    balanced=bal)
