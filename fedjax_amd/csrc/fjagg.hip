@@ -1222,6 +1222,7 @@ int launch_narrow(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, 
 }
 
 constexpr int kStripeVariant = 19;  // k_dense_stripe (fjstripe.hip): 19 auto width, 20 / 21 / 22 = 64 / 32 / 16
+constexpr int64_t kStripeMinClients = 512;
 
 int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, int64_t K,
                 int64_t P, const void* w, float scale, uint8_t* y, int flags, hipStream_t s,
@@ -1234,7 +1235,13 @@ int dense_exact(int in, int acc, int out, const uint8_t* x, int64_t ld_bytes, in
   if (variant >= kNumVariants) return fail(FJAGG_EINVAL, "unknown kernel variant %d", variant);
   // a narrow parameter axis with many clients: the LDS-staged kernel (k_dense_narrow);
   // from 256 Ki f32 up the 16-byte kernels keep enough loads in flight (profiles/r02i_*)
-  if (variant == 0 && gy == 1 && K >= 16 && P * ib <= (512 << 10)) variant = kNarrowVariant;
+  // with >= 512 clients the stripe pipeline (fjstripe.hip) is faster still at every swept
+  // narrow shape (profiles/r03b_stripe_sweep.jsonl); below that k_dense_narrow's shorter
+  // pipeline wins
+  if (variant == 0 && gy == 1 && K >= 16 && P * ib <= (512 << 10))
+    variant = (K >= kStripeMinClients && !(flags & FJAGG_HOST_TABLES) && fjagg_stripe_ok(x, ld_bytes, P, w, ib))
+                  ? kStripeVariant
+                  : kNarrowVariant;
   if (variant == 0) variant = pick_variant(P / V, K);
   if (variant == kNarrowVariant && (flags & FJAGG_HOST_TABLES))  // (fjagg_wsum_dense checks this first)
     return fail(FJAGG_EUNSUPPORTED, "FJAGG_HOST_TABLES: the narrow kernel takes device weights");
@@ -1511,15 +1518,19 @@ int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, c
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16 && in_dtype != FJAGG_I32)
     return fail(FJAGG_EINVAL, "bad dtype %d", in_dtype);
   if (L < 0 || L >= (1 << 22)) return fail(FJAGG_EINVAL, "bad leaf count %d", L);
-  if (flags & FJAGG_NARROW) {  // stripes of kNarrowCols elements of every leaf (k_ptrs_narrow)
+  if (flags & FJAGG_NARROW) {
+    // stripes of kNarrowCols elements of every leaf (k_ptrs_narrow), or of C = 64 / 32 / 16
+    // elements with FJAGG_VARIANT(20 / 21 / 22) (k_ptrs_stripe)
+    const int variant = (flags >> 8) & 0xff;
+    const int64_t width = variant == 20 ? 64 : variant == 21 ? 32 : variant == 22 ? 16 : kNarrowCols;
     int64_t nblk = 0;
     for (int l = 0; l < L; ++l) {
       if (leaf_n[l] < 0 || leaf_n[l] >= (1ll << 40))
         return fail(FJAGG_EINVAL, "leaf %d: %lld elements unsupported", l, (long long)leaf_n[l]);
-      for (int64_t e = 0; e < leaf_n[l]; e += kNarrowCols, ++nblk) {
+      for (int64_t e = 0; e < leaf_n[l]; e += width, ++nblk) {
         if (nblk < blocks_cap) {
           blocks[2 * nblk] = ((int64_t)l << 40) | e;
-          blocks[2 * nblk + 1] = e + kNarrowCols < leaf_n[l] ? e + kNarrowCols : leaf_n[l];
+          blocks[2 * nblk + 1] = e + width < leaf_n[l] ? e + width : leaf_n[l];
         }
       }
     }
@@ -1632,6 +1643,12 @@ int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* im
   }
   if (flags & FJAGG_NARROW) {
     if (ws) return fail(FJAGG_EINVAL, "FJAGG_NARROW plans fold only (no fused norms)");
+    const int variant = (flags >> 8) & 0xff;
+    if (variant >= 20 && variant <= 22) {  // k_ptrs_stripe over C-element stripes (fjstripe.hip)
+      if (flags & FJAGG_UNALIGNED) return fail(FJAGG_EINVAL, "stripe plans need 16-byte aligned pointers");
+      return fjagg_launch_ptrs_stripe(variant == 20 ? 64 : variant == 21 ? 32 : 16, in_dtype, acc_dtype, out_dtype,
+                                      nt, image_dev, L, K, nblk, w_dev, scale, ds, ac, s);
+    }
 #define FJ_CASE(I, A, O, ACCT)                                                                          \
     if (in_dtype == I && acc_dtype == A && out_dtype == O)                                              \
       return launch_ptrs_narrow<I, ACCT, O>(nt, image_dev, L, K, nblk, w_dev, scale, ds, ac, s);

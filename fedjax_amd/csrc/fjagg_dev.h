@@ -154,6 +154,17 @@ __device__ __forceinline__ typename Unit<IN, V>::Raw load_unit_ptr(const uint8_t
   }
 }
 
+// One 16-byte unit through a GLOBAL (address space 1) pointer: global_load, counted in
+// vmcnt only. (A generic pointer becomes a flat load, which also counts in lgkmcnt, so every
+// LDS wait of the kernel would wait for it too.)
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+template <bool NT>
+__device__ __forceinline__ u32x4 load16_global(const uint8_t* p) {
+  gu32x4* g = (gu32x4*)(reinterpret_cast<uintptr_t>(p));
+  if constexpr (NT) return __builtin_nontemporal_load(g);
+  else return *g;
+}
+
 template <int IN, class ACC, int V>
 __device__ __forceinline__ void decode(typename Unit<IN, V>::Raw r, typename ACC::T (&o)[V]) {
   if constexpr (V == 1) {
@@ -288,3 +299,9 @@ __attribute__((visibility("hidden"))) int fjagg_launch_stripe(int variant, int i
                                                               const uint8_t* x, int64_t ld_bytes, int64_t K,
                                                               int64_t P, const void* w, float scale, uint8_t* y,
                                                               int flags, hipStream_t s);
+// fjstripe.hip: k_ptrs_stripe launch over a FJAGG_NARROW plan of C-element stripes
+// (C = 64 / 32 / 16: FJAGG_VARIANT 20 / 21 / 22); every client and output pointer 16-byte aligned.
+__attribute__((visibility("hidden"))) int fjagg_launch_ptrs_stripe(int C, int in, int acc, int out, bool nt,
+                                                                   const int64_t* img, int L, int64_t K,
+                                                                   int64_t nblk, const void* w, float scale,
+                                                                   int dsc, int acm, hipStream_t s);

@@ -389,7 +389,25 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     }();
     const bool narrow = !with_l2 && K >= 16 && total * 4 <= narrow_max;
     const uint8_t* mask = any_elem && !narrow ? elem.data() : nullptr;
-    const int pflags = narrow ? FJAGG_NARROW : 0;
+    // every pointer 16-byte aligned: the stripe pipeline (k_ptrs_stripe, fjstripe.hip) with
+    // the width of tree_util._stripe_variant_for; FJAGG_STRIPE_PYTREE=0 keeps k_ptrs_narrow
+    static const bool stripe_on = [] {
+      const char* e = getenv("FJAGG_STRIPE_PYTREE");
+      return !(e && e[0] == '0' && e[1] == 0);
+    }();
+    int svar = 0;
+    if (narrow && stripe_on && !any_elem && K >= 512) {  // (fjagg.hip kStripeMinClients)
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+      int64_t s64 = 0, s32 = 0;
+      for (Py_ssize_t l = 0; l < L; ++l) {
+        s64 += (leaf_n[l] + 63) / 64;
+        s32 += (leaf_n[l] + 31) / 32;
+      }
+      svar = s64 >= cus ? 20 : s32 >= cus ? 21 : 22;
+    }
+    const int pflags = narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0;
     const int64_t nblk = plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);
     if (nblk < 0) Py_RETURN_NONE;
     // plan image (fjagg.h): in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk] | f32 weights
@@ -408,7 +426,7 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     };
     const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
     const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0) |
-                      (narrow ? FJAGG_NARROW : 0);
+                      (narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0);
     at::Tensor ws;  // fused l2 norms: per-workgroup partials, from torch's allocator (stream-ordered)
     float* l2p = nullptr;
     if (with_l2) {

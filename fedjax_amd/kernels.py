@@ -76,6 +76,17 @@ def _require_device(*ts: torch.Tensor) -> torch.device:
     return dev
 
 
+def stripe_variant(total_cols: int, cus: int) -> int:
+    """The stripe width k_dense_stripe / k_ptrs_stripe use for ``total_cols`` columns
+    (fjstripe.hip stripe_cols): 64 while every CU still gets a stripe, then 32, else 16,
+    as FJAGG_VARIANT 20 / 21 / 22."""
+    if (total_cols + 63) // 64 >= cus:
+        return 20
+    if (total_cols + 31) // 32 >= cus:
+        return 21
+    return 22
+
+
 def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[float] = None,
                        out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None,
                        accumulate: bool = False, mode: str = "exact",
@@ -183,18 +194,21 @@ def split_workspace_bytes(K: int, P: int) -> int:
     return int(_lib.load().fjagg_split_workspace_bytes(K, P))
 
 
-def ptrs_plan(in_code: int, leaf_n: Sequence[int], unaligned, narrow: bool = False) -> np.ndarray:
+def ptrs_plan(in_code: int, leaf_n: Sequence[int], unaligned, narrow: bool = False,
+              stripe_variant: int = 0) -> np.ndarray:
     """Workgroup table of the pytree kernel (host int64 array, 2 words per workgroup).
 
     ``unaligned``: a bool for the whole launch (True = element units everywhere; launch
     with ``unaligned=True``), or a per-leaf boolean array: the marked leaves take
     element units, the others 16-byte units (``fjagg_ptrs_plan_leaves``; launch with
     ``unaligned=False``). ``narrow``: 64-element stripes for k_ptrs_narrow (any
-    alignment; launch with ``FJAGG_NARROW``)."""
+    alignment; launch with ``FJAGG_NARROW``); with ``stripe_variant`` 20 / 21 / 22:
+    64 / 32 / 16-element stripes for k_ptrs_stripe (16-byte aligned pointers; launch with
+    ``FJAGG_NARROW | FJAGG_VARIANT(stripe_variant)``)."""
     lib = _lib.load()
     n = np.ascontiguousarray(leaf_n, dtype=np.int64)
     if narrow:
-        flags, mask = _lib.NARROW, None
+        flags, mask = _lib.NARROW | ((stripe_variant & 0xFF) << 8), None
     elif isinstance(unaligned, (bool, np.bool_)):
         flags, mask = (_lib.UNALIGNED if unaligned else 0), None
     else:
@@ -214,11 +228,13 @@ def ptrs_plan(in_code: int, leaf_n: Sequence[int], unaligned, narrow: bool = Fal
 def weighted_sum_ptrs(in_code: int, acc_code: int, out_code: int, image_dev: torch.Tensor,
                       L: int, K: int, nblk: int, w_dev: torch.Tensor, scale: Optional[float],
                       accumulate: bool = False, unaligned: bool = False,
-                      nontemporal: bool = False) -> None:
-    """Launch the pytree kernel over a device plan image (see include/fjagg.h)."""
+                      nontemporal: bool = False, narrow: bool = False, stripe_variant: int = 0) -> None:
+    """Launch the pytree kernel over a device plan image (see include/fjagg.h); ``narrow`` /
+    ``stripe_variant`` as the plan was built (:func:`ptrs_plan`)."""
     dev = _require_device(image_dev, w_dev)
     flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
     flags |= (_lib.UNALIGNED if unaligned else 0) | (_lib.NONTEMPORAL if nontemporal else 0)
+    flags |= (_lib.NARROW | ((stripe_variant & 0xFF) << 8)) if narrow else 0
     _lib.call("fjagg_wsum_ptrs", in_code, acc_code, out_code, image_dev.data_ptr(), L, K, nblk,
               w_dev.data_ptr(), float(scale if scale is not None else 1.0), flags,
               _stream_handle(dev))

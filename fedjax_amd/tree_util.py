@@ -272,8 +272,12 @@ def _fold(rows, weights, *, scale=None,
             in_ptrs = np.array([[rows[k][l].data_ptr() for l in ls] for k in range(K)], dtype=np.int64)
         out_ptrs = np.array([outs[l].data_ptr() for l in ls], dtype=np.int64)
         narrow = _narrow(K, leaf_n, in_c) and l2sq is None
+        svar = 0
         if narrow:
-            blocks, unaligned = _ptrs_plan(in_c, leaf_n, "narrow", device), False
+            # k_ptrs_stripe when every pointer is 16-byte aligned (k_ptrs_narrow otherwise)
+            if _STRIPE_PYTREE and K >= 512 and not ((in_ptrs & 15).any() or (out_ptrs & 15).any()):
+                svar = _stripe_variant_for(leaf_n, device)
+            blocks, unaligned = _ptrs_plan(in_c, leaf_n, ("narrow", svar), device), False
         else:
             blocks, unaligned = _leaf_plan(in_c, leaf_n, in_ptrs, out_ptrs, device)
         if packed is not None:
@@ -291,7 +295,7 @@ def _fold(rows, weights, *, scale=None,
         nt = (total_bytes >= NONTEMPORAL_MIN_BYTES) if nontemporal is None else nontemporal
         flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
         flags |= (_lib.UNALIGNED if unaligned else 0) | (_lib.NONTEMPORAL if nt else 0)
-        flags |= _lib.NARROW if narrow else 0
+        flags |= (_lib.NARROW | ((svar & 0xFF) << 8)) if narrow else 0
         nblk = len(blocks) // 2
         sc = float(np.float32(scale) if scale is not None else 1.0)
         stream = torch.cuda.current_stream(device).cuda_stream
@@ -352,15 +356,39 @@ def _narrow(K: int, leaf_n: np.ndarray, in_c: int) -> bool:
     return K >= 16 and int(leaf_n.sum()) * (2 if in_c == _lib.BF16 else 4) <= _NARROW_MAX_BYTES
 
 
+# Narrow plans over 16-byte aligned leaves run the stripe pipeline (k_ptrs_stripe,
+# fjstripe.hip) instead of k_ptrs_narrow; FJAGG_STRIPE_PYTREE=0 keeps k_ptrs_narrow (A/B).
+_STRIPE_PYTREE = os.environ.get("FJAGG_STRIPE_PYTREE", "1") != "0"
+_CUS = {}
+
+
+def _stripe_variant_for(leaf_n: np.ndarray, device: torch.device) -> int:
+    """FJAGG_VARIANT of the stripe width for these leaves (kernels.stripe_variant over the
+    stripes of every leaf: each leaf starts a new stripe)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    cus = _CUS.get(idx)
+    if cus is None:
+        cus = _CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    for v, c in ((20, 64), (21, 32)):
+        if int(((leaf_n + c - 1) // c).sum()) >= cus:
+            return v
+    return 22
+
+
 def _ptrs_plan(in_c: int, leaf_n: np.ndarray, unaligned, device: torch.device) -> np.ndarray:
-    """Cached :func:`kernels.ptrs_plan`; ``unaligned`` is a bool, a per-leaf mask, or
-    "narrow" (the k_ptrs_narrow stripes)."""
-    key = (in_c, leaf_n.tobytes(), unaligned if isinstance(unaligned, (bool, str)) else
+    """Cached :func:`kernels.ptrs_plan`; ``unaligned`` is a bool, a per-leaf mask,
+    "narrow" (the k_ptrs_narrow stripes) or ("narrow", v) (v = 20 / 21 / 22: the
+    k_ptrs_stripe stripes; 0: k_ptrs_narrow's)."""
+    key = (in_c, leaf_n.tobytes(), unaligned if isinstance(unaligned, (bool, str, tuple)) else
            np.asarray(unaligned, dtype=np.uint8).tobytes(), device)
     blocks = _PLANS.get(key)
     if blocks is None:
-        blocks = (kernels.ptrs_plan(in_c, leaf_n, False, narrow=True) if isinstance(unaligned, str)
-                  else kernels.ptrs_plan(in_c, leaf_n, unaligned))
+        if isinstance(unaligned, tuple):  # ("narrow", stripe variant or 0)
+            blocks = kernels.ptrs_plan(in_c, leaf_n, False, narrow=True, stripe_variant=unaligned[1])
+        elif isinstance(unaligned, str):
+            blocks = kernels.ptrs_plan(in_c, leaf_n, False, narrow=True)
+        else:
+            blocks = kernels.ptrs_plan(in_c, leaf_n, unaligned)
         if len(_PLANS) < 1024:
             _PLANS[key] = blocks
     return blocks

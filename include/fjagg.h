@@ -67,7 +67,11 @@ enum fjagg_flags {
                                  resident grid (tuning / A-B only) */
   FJAGG_NARROW = 1 << 5,      /* pytree path, plan AND launch: 64-element stripes per workgroup,
                                  client rows staged through LDS (k_ptrs_narrow) — for small
-                                 leaves and many clients; fold only (no fused norms) */
+                                 leaves and many clients; fold only (no fused norms). With
+                                 FJAGG_VARIANT(20 / 21 / 22) in both calls: stripes of 64 / 32 / 16
+                                 elements folded by the stripe pipeline (k_ptrs_stripe: LDS-
+                                 transposed products, one fold wave per stripe); every client and
+                                 output pointer must then be 16-byte aligned */
   FJAGG_HOST_TABLES = 1 << 6, /* the weights (and on the pytree path the plan image) are HOST
                                  pointers: the launch copies them into the kernel arguments, so
                                  no upload or staging copy runs on the stream before the fold and
@@ -83,7 +87,9 @@ enum fjagg_flags {
 #define FJAGG_KARG_MAX_WEIGHTS 1024 /* dense path: 4 KiB of weights */
 #define FJAGG_KARG_MAX_WORDS 3584   /* pytree path: 28 KiB = image words + ceil(K/2) weight words */
 /* bits 8..15 of flags select a kernel shape of the dense path: 0 = automatic,
- * 1..11 = fixed (units per lane, clients in flight, waves/SIMD) for tuning; see fjagg.hip */
+ * 1..17 = fixed (units per lane, clients in flight, waves/SIMD) for tuning, 18 = the
+ * LDS-staged narrow fold, 19 = the stripe pipeline (fjstripe.hip) with automatic stripe
+ * width, 20 / 21 / 22 = with 64 / 32 / 16 columns; see fjagg.hip */
 #define FJAGG_VARIANT(v) (((v)&0xff) << 8)
 
 enum fjagg_mode {

@@ -1096,3 +1096,56 @@ def test_l2_of_int_and_mixed_leaves_and_many_clients(cuda):
     assert norms.shape == (K,)
     npt.assert_allclose(host(norms)[:8], [np.sqrt(3) * (k % 7) for k in range(8)], rtol=1e-6)
     assert torch.equal(m["w"], tu.tree_mean(list(zip(trees, [1] * K)))["w"])
+
+
+@pytest.mark.parametrize("K,sizes,dt", [
+    (4096, [32, 288, 64, 18432, 128, 20000, 62, 7936 - 2], "f32"),  # a small CNN, many clients
+    (300, [5, 64, 1000, 3], "f32"), (1000, [4099, 17], "bf16"), (777, [100, 2000], "i32"),
+    (16, [64 * 300], "f32")])
+def test_ptrs_stripe_plan_bitwise(K, sizes, dt, cuda, coracle):
+    """k_ptrs_stripe (FJAGG_NARROW | FJAGG_VARIANT(20 / 21 / 22)): C-element stripes of every
+    leaf (leaves not multiples of C, shorter than C, tiles not full), client rows from the
+    K x L pointer table staged in LDS by the fold wave, accumulate mode — bitwise the
+    k_ptrs_narrow plan (variant 0) and, for f32, the oracle."""
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "i32": torch.int32}[dt]
+    in_c = kernels.dtype_code(tdt)
+    g = torch.Generator().manual_seed(K + len(sizes))
+    leaves = []
+    for k in range(K):
+        row = []
+        for n in sizes:
+            x = (torch.rand(n, generator=g) * 2 - 1) * 0.01
+            row.append((x * 1e6).to(torch.int32).to(cuda) if dt == "i32" else x.to(tdt).to(cuda))
+        leaves.append(row)
+    L = len(sizes)
+    leaf_n = np.array(sizes, dtype=np.int64)
+    in_ptrs = np.array([[t.data_ptr() for t in r] for r in leaves], dtype=np.int64)
+    assert not (in_ptrs & 15).any()
+    if dt == "i32":
+        acc_c, out_dt = _lib.I32, torch.int32
+        w = torch.tensor([int(v) for v in ref.fedavg_weights(K, seed=9)], dtype=torch.int32, device=cuda)
+        scale = None
+    else:
+        acc_c, out_dt = _lib.F32, tdt
+        w = torch.tensor(np.float32(ref.fedavg_weights(K, seed=9)), device=cuda)
+        scale = 0.125
+    res = {}
+    for acc in (False, True):
+        for v in (0, 20, 21, 22):
+            outs = [torch.full((n,), 3, dtype=out_dt, device=cuda) for n in sizes]
+            out_ptrs = np.array([o.data_ptr() for o in outs], dtype=np.int64)
+            blocks = kernels.ptrs_plan(in_c, leaf_n, False, narrow=True, stripe_variant=v)
+            image = np.concatenate([in_ptrs.ravel(), out_ptrs, leaf_n, blocks])
+            img = torch.from_numpy(image).to(cuda)
+            kernels.weighted_sum_ptrs(in_c, acc_c, kernels.dtype_code(out_dt), img, L, K, len(blocks) // 2, w, scale,
+                                      accumulate=acc, narrow=True, stripe_variant=v)
+            torch.cuda.synchronize()
+            res[(acc, v)] = [o.view(torch.uint8).cpu().numpy() for o in outs]
+        for v in (20, 21, 22):
+            for a, b in zip(res[(acc, 0)], res[(acc, v)]):
+                assert np.array_equal(a, b), (acc, v)
+    if dt == "f32":
+        for l, n in enumerate(sizes):
+            xs = np.stack([leaves[k][l].cpu().numpy() for k in range(K)])
+            want = coracle.wsum_f32(xs, host(w), scale=np.float32(0.125))
+            assert np.array_equal(res[(False, 20)][l].view(np.uint32), bits(want)), l

@@ -136,7 +136,8 @@ case "$STUDY" in
     timeout -k 10 600 $PT tests/test_gpu_parity.py -k "stripe or variants_bitwise or narrow_fold" \
       > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit 1
     for s in "16384 4096 f32" "4096 16384 f32" "2048 32768 f32" "1024 65536 f32" "512 131072 f32" \
-             "256 262144 f32" "4096 32768 bf16" "1024 4096 f32" "128 16384 f32" "65536 1024 f32"; do
+             "256 262144 f32" "4096 32768 bf16" "1024 4096 f32" "128 16384 f32" "65536 1024 f32" \
+             "64 65536 f32" "16 65536 f32" "32 16384 f32" "8192 8192 f32" "1024 131072 bf16" "256 32768 f32"; do
       SWEEP_BALANCED_ONLY=1 SWEEP_VARIANTS=${SWEEP_VARIANTS:-2,18,19,20,21,22} timeout -k 10 120 \
         python tools/sweep.py $s 3 5 || die "sweep $s"
     done > $O/sweep.jsonl
@@ -149,6 +150,18 @@ case "$STUDY" in
       or ignore or schedule or frozen or configs4_rank0" tests/test_gpu_parity.py \
       "tests/test_gpu_fullsize.py::test_configs4_rank0_share_native_pipeline" > $O/tests.log 2>&1
     rc=$?; tail -5 $O/tests.log; [ $rc -eq 0 ] || exit 1
+    ;;
+  stripe_tree)
+    # k_ptrs_stripe parity, then tree_mean over small models with many clients: stripe vs narrow
+    timeout -k 10 900 $PT tests/test_gpu_parity.py -k "ptrs_stripe or narrow or golden" tests/test_gpu_fuzz.py \
+      > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit 1
+    for sp in 0 1; do
+      for mx in 262144 524288; do
+        FJAGG_STRIPE_PYTREE=$sp FJAGG_NARROW_MAX_BYTES=$mx timeout -k 10 300 python tools/time_narrow_pytree.py \
+          > $O/time_sp${sp}_max${mx}.jsonl 2> $O/time_sp${sp}_max${mx}.err || die "time sp=$sp max=$mx"
+      done
+    done
+    grep -H . $O/time_*.jsonl
     ;;
   *) echo "unknown study $STUDY"; exit 2 ;;
 esac
