@@ -28,6 +28,7 @@ from __future__ import annotations
 import ctypes
 import numbers
 import os
+import time
 import weakref
 from typing import Any, Iterable, List, Optional, Sequence, Tuple
 
@@ -313,6 +314,14 @@ def _fold(rows, weights, *, scale=None,
 _ENTRY_ADDRS = None  # (plan_leaves, wsum_ptrs, wsum_l2_ptrs, l2 workspace bytes) addresses for fjhost.fold_table
 
 
+def _native_fold_addrs() -> None:
+    global _ENTRY_ADDRS
+    lib = _lib.load()
+    _ENTRY_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
+                         for f in ("fjagg_ptrs_plan_leaves", "fjagg_wsum_ptrs", "fjagg_wsum_l2_ptrs",
+                                   "fjagg_wsum_l2_ptrs_workspace_bytes"))
+
+
 def _native_fold(table: "_Table", packed: "_Weights", scale, out=None,
                  accumulate: bool = False, l2sq: Optional[torch.Tensor] = None) -> Optional[List[torch.Tensor]]:
     """The common case of :func:`_fold` in one native call (fjhost.fold_table): float32
@@ -321,12 +330,8 @@ def _native_fold(table: "_Table", packed: "_Weights", scale, out=None,
     also every client's squared l2 norm (fjagg_wsum_l2_ptrs). It builds the same plan
     image and launches the same kernel as the Python path below; None when the case does
     not hold (nothing launched)."""
-    global _ENTRY_ADDRS
     if _ENTRY_ADDRS is None:
-        lib = _lib.load()
-        _ENTRY_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
-                             for f in ("fjagg_ptrs_plan_leaves", "fjagg_wsum_ptrs", "fjagg_wsum_l2_ptrs",
-                                       "fjagg_wsum_l2_ptrs_workspace_bytes"))
+        _native_fold_addrs()
     dev = table.row0[0].device
     if dev.type != "cuda":
         return None
@@ -458,11 +463,12 @@ def _pack_weights(weights: List[Any]) -> Optional[_Weights]:
     return _Weights(f32, i32, kinds, total)
 
 
-def _client_table(trees: Sequence[PyTree]):
+def _client_table(trees: Sequence[PyTree], first=None):
     """(treedef, rows) like :func:`_client_rows`; rows is a :class:`_Table` when every
     client's leaves are already contiguous device tensors of client 0's dtypes and
-    shapes on client 0's device (the common case, checked natively), else lists."""
-    leaves0, td = pytree.flatten(trees[0])
+    shapes on client 0's device (the common case, checked natively), else lists.
+    ``first``: pytree.flatten(trees[0]) when already computed."""
+    leaves0, td = pytree.flatten(trees[0]) if first is None else first
     device = _find_device(leaves0)
     idx = _device_index(device)
     row0 = [_device_leaf(x, device, idx) for x in leaves0]
@@ -1041,6 +1047,84 @@ def _collect_pairs(pairs):
     return trees, weights, sum_weight
 
 
+# A synchronous tree_mean on an idle GPU waits for the whole host walk (every client's
+# leaves checked, K x L pointers) before the fold starts. When the stream is idle the call
+# folds the first _PIPELINE_FRAC of the clients as soon as their pointers are gathered and
+# walks the rest while that launch runs; the second launch accumulates into the first's
+# sums and applies 1/W (accumulate mode: the same per-element sequence, the same bits).
+# A busy stream gets one launch (the host work hides behind the queued kernels anyway).
+# The idle probe (hipStreamQuery) puts a marker on the stream, ~3 us of GPU time per call
+# when calls run back to back, so it is gated by a host-side estimate: the time the folds
+# this module issued would finish at the 8 TB/s peak; before that the stream is busy with
+# them and is not probed. FJAGG_PIPELINE_FRAC=0 turns the pipeline off (A/B runs).
+_PIPELINE_FRAC = float(os.environ.get("FJAGG_PIPELINE_FRAC", "0.25"))
+_PIPELINE_MIN_BYTES = 64 << 20  # below this the first launch is too short to hide the walk
+
+
+_PEAK_BYTES_PER_S = 8.0e12
+_BUSY_UNTIL = [0.0]  # perf_counter() time before which this module's issued folds cannot have finished
+
+
+def _stream_idle(stream: torch.cuda.Stream) -> bool:
+    return stream.query()
+
+
+def _tree_mean_pipelined(trees: List[PyTree], packed: "_Weights", W, first) -> Optional[PyTree]:
+    """tree_mean of float32 device pytrees in two launches overlapping the host walk (see
+    _PIPELINE_FRAC); None (nothing launched, or a first launch whose outputs are dropped)
+    when the case does not hold, and the caller then takes the one-launch path, which also
+    raises the reference's errors. ``first``: pytree.flatten(trees[0])."""
+    leaves0, td = first
+    if not leaves0:
+        return None
+    x0 = leaves0[0]
+    if type(x0) is not torch.Tensor or not x0.is_cuda:
+        return None
+    device = x0.device
+    idx = x0.get_device()
+    n = 0
+    for x in leaves0:
+        if type(x) is not torch.Tensor or x.dtype is not torch.float32 or x.get_device() != idx \
+                or not x.is_contiguous():
+            return None
+        n += x.numel()
+    K = len(trees)
+    if 4 * n <= _NARROW_MAX_BYTES or 4 * n * K < _PIPELINE_MIN_BYTES:
+        return None
+    now = time.perf_counter()
+    busy = now < _BUSY_UNTIL[0]
+    _BUSY_UNTIL[0] = max(now, _BUSY_UNTIL[0]) + 4 * n * K / _PEAK_BYTES_PER_S  # this call's fold, either way
+    stream = torch.cuda.current_stream(device)
+    if busy or not _stream_idle(stream):
+        return None  # kernels still queued: the walk already overlaps them
+    spec = pytree.native_spec(td)
+    if spec is None:
+        return None
+    host = _lib.host()
+    k1 = min(K - 1, max(1, int(K * _PIPELINE_FRAC)))
+    ptrs = np.empty((K, len(leaves0)), dtype=np.int64)
+    if host.gather_rows(trees[:k1], 1, spec, leaves0, idx, ptrs) != 0:
+        return None
+    if _ENTRY_ADDRS is None:
+        _native_fold_addrs()
+    plan, wsum, *_ = _ENTRY_ADDRS
+    nt_min = 0.0 if 4 * n * K >= NONTEMPORAL_MIN_BYTES else float("inf")  # the whole job's bytes decide
+    s = stream.cuda_stream
+    got = host.fold_table(leaves0, ptrs[:k1], packed.f32[:k1], 1.0, False, nt_min, idx, s, plan, wsum)
+    if got is None:
+        return None
+    _lib.check(got[0], "fjagg_wsum_ptrs")
+    outs = got[1]
+    if host.gather_rows(trees, k1, spec, leaves0, idx, ptrs) != 0:
+        return None
+    got = host.fold_table(leaves0, ptrs[k1:], packed.f32[k1:], float(np.float32(_inverse(W))), True, nt_min,
+                          idx, s, plan, wsum, outs, 1)
+    if got is None:
+        return None
+    _lib.check(got[0], "fjagg_wsum_ptrs")
+    return pytree.unflatten(td, outs)
+
+
 # tree_mean over a one-shot iterable holds at most this many bytes of client deltas
 # (float32 leaves) before folding them into the running sum (see tree_mean).
 STREAM_BUDGET_BYTES = 4 << 30
@@ -1066,7 +1150,13 @@ def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
     trees, weights, sum_weight = _collect_pairs(pytrees_and_weights)
     if not trees:
         return None  # tree_util.py:96 maps over None
-    td, rows = _client_table(trees)
+    first = None
+    if _PIPELINE_FRAC > 0.0 and len(trees) >= 8 and isinstance(weights, _Weights):
+        first = pytree.flatten(trees[0])
+        got = _tree_mean_pipelined(trees, weights, sum_weight, first)
+        if got is not None:
+            return got
+    td, rows = _client_table(trees, first)
     if not rows[0]:
         return pytree.unflatten(td, [])
     inv = _inverse(sum_weight)

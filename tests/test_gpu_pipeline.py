@@ -1,0 +1,114 @@
+"""tree_mean on an idle stream folds in two launches that overlap the host walk
+(tree_util._tree_mean_pipelined): the first launch folds clients [0, k1) as soon as their
+pointers are gathered, the second accumulates [k1, K) into the same sums and applies 1/W.
+Accumulate mode keeps the per-element sequence of fedjax/core/tree_util.py:85-96, so the
+result must be bitwise the one-launch fold and the oracle's; errors must be the one-launch
+path's (the second walk falls back to it)."""
+import numpy as np
+import pytest
+import torch
+
+from fedjax_amd import _lib, tree_util as tu
+from oracle import tree_util_ref as ref
+
+pytestmark = pytest.mark.gpu
+EMNIST = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "conv2_d_1": {"b": (64,), "w": (3, 3, 32, 64)},
+          "linear": {"b": (128,), "w": (9216, 128)}, "linear_1": {"b": (62,), "w": (128, 62)}}
+
+
+def _tmap(f, t):
+    return {k: _tmap(f, v) for k, v in t.items()} if isinstance(t, dict) else f(t)
+
+
+def _clients(K, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return [_tmap(lambda s: torch.rand(s, device="cuda", generator=g) - 0.5, EMNIST) for _ in range(K)]
+
+
+def _flat(tree):
+    return np.concatenate([x.detach().cpu().numpy().ravel() for x in ref.flatten(tree)[0]])
+
+
+def _launches():
+    return _lib.host().image_paths()["kernel_args"]
+
+
+@pytest.fixture
+def frac(monkeypatch):
+    def set_(v):
+        monkeypatch.setattr(tu, "_PIPELINE_FRAC", v)
+    return set_
+
+
+@pytest.mark.parametrize("K", [16, 29, 128])
+def test_pipelined_tree_mean_bitwise(K, frac, cuda):
+    clients = _clients(K, seed=K)
+    weights = np.random.RandomState(K).randint(1, 501, size=K).tolist()
+    weights[3] = 2.5  # a float weight among ints (weak float kinds)
+    pairs = list(zip(clients, weights))
+    frac(0.0)
+    one = _flat(tu.tree_mean(pairs))
+    for f in (0.01, 0.33, 0.5, 0.99):
+        frac(f)
+        torch.cuda.synchronize()  # idle stream: the pipelined path
+        n0 = _launches()
+        got = _flat(tu.tree_mean(pairs))
+        assert _launches() - n0 == 2, f"frac {f}: expected the two-launch pipeline"
+        np.testing.assert_array_equal(got.view(np.uint32), one.view(np.uint32))
+    if K == 29:  # the oracle on every element (29 x 1.2 M)
+        host = [(_tmap(lambda x: x.cpu().numpy(), c), w) for c, w in pairs]
+        want = np.concatenate([np.asarray(x).ravel() for x in ref.flatten(ref.tree_mean(host))[0]])
+        np.testing.assert_array_equal(one.view(np.uint32), want.astype(np.float32).view(np.uint32))
+
+
+def test_busy_stream_takes_one_launch(frac, cuda):
+    if not hasattr(torch.cuda, "_sleep"):
+        pytest.skip("torch.cuda._sleep unavailable")
+    frac(0.33)
+    K = 16
+    pairs = list(zip(_clients(K), [1.0 + k for k in range(K)]))
+    ref_out = _flat(tu.tree_mean(pairs))
+    torch.cuda.synchronize()
+    torch.cuda._sleep(50_000_000)  # keeps the stream busy while tree_mean is issued
+    n0 = _launches()
+    out = tu.tree_mean(pairs)
+    assert _launches() - n0 == 1
+    np.testing.assert_array_equal(_flat(out).view(np.uint32), ref_out.view(np.uint32))
+
+
+@pytest.mark.parametrize("where", [2, 13])  # before / after the first chunk's clients (k1 = 5)
+def test_pipelined_errors_are_the_one_launch_paths(where, frac, cuda):
+    frac(0.33)
+    K = 16
+    clients = _clients(K)
+    clients[where]["linear"]["w"] = torch.zeros(9216, 127, device="cuda")
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError, match="shape"):
+        tu.tree_mean(list(zip(clients, [1] * K)))
+    clients = _clients(K)
+    clients[where]["linear"]["b"] = clients[where]["linear"]["b"].to(torch.bfloat16)
+    torch.cuda.synchronize()
+    with pytest.raises(TypeError, match="dtype"):
+        tu.tree_mean(list(zip(clients, [1] * K)))
+
+
+def test_pipelined_declines_what_it_does_not_cover(frac, cuda):
+    """numpy-scalar weights, host leaves, a small delta (the narrow plans): one launch,
+    the same bits as with the pipeline off."""
+    frac(0.33)
+    K = 16
+    clients = _clients(K)
+    cases = {
+        "numpy weights": list(zip(clients, [np.float32(1 + k) for k in range(K)])),
+        "host client 0": [(_tmap(lambda x: x.cpu(), clients[0]), 1)] + [(c, 1) for c in clients[1:]],
+        "small delta": [({"w": c["linear_1"]["w"]}, 1 + k) for k, c in enumerate(clients)],
+    }
+    for name, pairs in cases.items():
+        frac(0.0)
+        want = _flat(tu.tree_mean(pairs))
+        frac(0.33)
+        torch.cuda.synchronize()
+        n0 = _launches()
+        got = _flat(tu.tree_mean(pairs))
+        assert _launches() - n0 <= 1, name
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32), err_msg=name)

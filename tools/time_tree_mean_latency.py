@@ -1,7 +1,10 @@
 """Single-call latency of tree_mean at configs[1] (128 clients x EMNIST-CNN, one allocation
 per client leaf): the device is idle before each call and the call is waited for, as a
 server that aggregates once per round sees it. Also the pipelined rate (calls back to back)
-for comparison. Prints one JSON line (microseconds, medians)."""
+for comparison. Prints one JSON line per pipeline fraction (microseconds, medians):
+    python tools/time_tree_mean_latency.py [FRAC ...]   (tree_util._PIPELINE_FRAC values,
+    measured in interleaved rounds; default: the module's own; a negative FRAC = |FRAC|
+    with the idle probe answering "busy": the probe's own cost, never pipelined)"""
 import json
 import os
 import sys
@@ -21,11 +24,7 @@ def tmap(f, t):
     return {k: tmap(f, v) for k, v in t.items()} if isinstance(t, dict) else f(t)
 
 
-def main(K=128, reps=100):
-    dev = torch.device("cuda:0")
-    g = torch.Generator(device=dev).manual_seed(0)
-    clients = [tmap(lambda s: torch.rand(s, device=dev, generator=g), SHAPES) for _ in range(K)]
-    pairs = list(zip(clients, np.random.RandomState(1).randint(1, 501, size=K).tolist()))
+def measure(pairs, reps):
     pc = time.perf_counter
     single, issue = [], []
     for i in range(reps + 10):
@@ -45,10 +44,31 @@ def main(K=128, reps=100):
         tu.tree_mean(pairs)
     torch.cuda.synchronize()
     piped = (pc() - t0) / reps * 1e6
-    print(json.dumps({"K": K, "single_call_us": round(float(np.median(single)), 1),
-                      "single_call_host_issue_us": round(float(np.median(issue)), 1),
-                      "pipelined_us_per_call": round(piped, 1)}))
+    return single, issue, piped
+
+
+def main(fracs, K=128, reps=100, rounds=3):
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    clients = [tmap(lambda s: torch.rand(s, device=dev, generator=g), SHAPES) for _ in range(K)]
+    pairs = list(zip(clients, np.random.RandomState(1).randint(1, 501, size=K).tolist()))
+    res = {f: ([], [], []) for f in fracs}
+    idle = tu._stream_idle
+    for _ in range(rounds):
+        for f in fracs:
+            if f is not None:
+                tu._PIPELINE_FRAC = abs(f)
+                tu._stream_idle = (lambda s: False) if f < 0 else idle
+            s, i, p = measure(pairs, reps)
+            res[f][0].extend(s)
+            res[f][1].extend(i)
+            res[f][2].append(p)
+    for f, (s, i, p) in res.items():
+        print(json.dumps({"K": K, "pipeline_frac": tu._PIPELINE_FRAC if f is None else f,
+                          "single_call_us": round(float(np.median(s)), 1),
+                          "single_call_host_issue_us": round(float(np.median(i)), 1),
+                          "back_to_back_us_per_call": round(float(np.median(p)), 1)}), flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    main([float(a) for a in sys.argv[1:]] or [None])
