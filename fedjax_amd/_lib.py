@@ -1,7 +1,8 @@
 """ctypes binding of ``libfjagg.so`` — the C ABI declared in ``include/fjagg.h``
 (aggregation), ``include/fjcomp.h`` (compression aggregators) and
 ``include/fjcomm.h`` (client-sharded aggregation over RCCL, timing events) and
-``include/fjtree.h`` (per-call tree ops, leaf table in the kernel arguments).
+``include/fjtree.h`` (per-call tree ops, leaf table in the kernel arguments) and
+``include/fjopt.h`` (the adafactor server step).
 
 The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950) into
 ``fedjax_amd/_build/libfjagg.so``. It links against the HIP runtime by soname
@@ -105,6 +106,10 @@ _SIGNATURES = {
     "fjtree_abi_version": (_i32, []),
     "fjtree_workspace_bytes": (_i64, [_vp]),
     "fjtree_fold_leaves": (_i32, [_vp, _vp]),
+    # include/fjopt.h
+    "fjopt_abi_version": (_i32, []),
+    "fjopt_adafactor_plan": (_i64, [_vp, _i32, _vp, _vp, _i64, _vp]),
+    "fjopt_adafactor_step": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
 }
 SYMBOLS = tuple(_SIGNATURES)
 
@@ -120,6 +125,24 @@ class ServerOpt(ctypes.Structure):
 
 OPT_SGD, OPT_MOMENTUM, OPT_ADAM, OPT_ADAGRAD, OPT_RMSPROP, OPT_YOGI = 1, 2, 3, 4, 5, 6
 OPT_F_MOMENTUM = 1
+
+
+class AfLeaf(ctypes.Structure):
+    """struct fjopt_af_leaf (include/fjopt.h)."""
+    _fields_ = [("g", _vp), ("p", _vp), ("v_row", _vp), ("v_col", _vp), ("v", _vp), ("m", _vp), ("n", _i64),
+                ("dims", _i64 * 5), ("factored", _i32), ("d0_is_lo", _i32), ("decay_weights", _i32),
+                ("reserved", _i32)]
+
+
+class AfHparams(ctypes.Structure):
+    """struct fjopt_af_hparams (include/fjopt.h)."""
+    _fields_ = [("decay_rate_t", _f32), ("one_minus_decay", _f32), ("eps", _f32), ("clip", _i32),
+                ("clip_threshold", _f32), ("has_lr", _i32), ("lr", _f32), ("param_scale", _i32),
+                ("min_scale", _f32), ("momentum", _i32), ("mom_decay", _f32), ("one_minus_mom", _f32),
+                ("weight_decay", _i32), ("wd", _f32)]
+
+
+OPT_ABI_VERSION = 1
 
 
 class TreeLeaves(ctypes.Structure):

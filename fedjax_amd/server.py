@@ -3,8 +3,8 @@
 The step after the mean in every FedJAX algorithm is the server update
 (examples/fed_avg.py:97-101, fedjax/algorithms/fed_avg.py:150-154):
 ``opt_state, params = server_optimizer.apply(mean_delta, opt_state, params)``
-with any of ``fedjax.optimizers.sgd``, ``adam``, ``adagrad``, ``rmsprop`` (not centered)
-or ``yogi`` (fedjax/core/optimizers.py:117-281, optax).
+with any of ``fedjax.optimizers.sgd``, ``adam``, ``adagrad``, ``rmsprop`` (not centered),
+``yogi`` or ``adafactor`` (fedjax/core/optimizers.py:117-348, optax).
 :func:`fused_mean_update` folds the round's client deltas and applies that update
 in the same kernel (``fjagg_server_update_dense``): the mean stays in registers,
 params / momentum / second moments are read and written once.
@@ -16,6 +16,8 @@ a schedule is evaluated on the host once per round, at optax's pre-increment ste
 (``optax.scale_by_schedule``), into the kernel's descriptor. :func:`ignore_grads_haiku`
 (optimizers.py:69-109) freezes haiku parameters: their leaves are left out of the fused
 launch, so params and optimizer state pass through untouched.
+:func:`adafactor` needs whole-leaf reductions (factored second moments, block RMS), so
+it runs after the fold as its own short launch chain over all leaves (include/fjopt.h).
 Bitwise parity holds against the numpy restatement in tests/test_gpu_parity.py;
 against XLA it is unpinned (XLA:CPU may contract mul+add, and evaluates
 ``b1 ** count`` with its own pow).
@@ -137,7 +139,7 @@ def yogi(learning_rate: float, b1: float = 0.9, b2: float = 0.999, eps: float = 
     return ServerOptimizer(_lib.OPT_YOGI, learning_rate, b1=b1, b2=b2, eps=eps, init_m=1e-6, init_v=1e-6)
 
 
-def ignore_grads_haiku(optimizer: ServerOptimizer, non_trainable_names: List[Tuple[str, str]]) -> ServerOptimizer:
+def ignore_grads_haiku(optimizer, non_trainable_names: List[Tuple[str, str]]):
     """fedjax.optimizers.ignore_grads_haiku (optimizers.py:69-109): ``optimizer`` with the
     haiku parameters ``params[module_name][name]`` for every pair in ``non_trainable_names``
     frozen. The reference maps them to ``None`` for the update and puts the old values
@@ -147,7 +149,7 @@ def ignore_grads_haiku(optimizer: ServerOptimizer, non_trainable_names: List[Tup
     return dataclasses.replace(optimizer, frozen=tuple((str(m), str(n)) for m, n in non_trainable_names))
 
 
-def _frozen_leaves(opt: ServerOptimizer, params, treedef) -> np.ndarray:
+def _frozen_leaves(opt, params, treedef) -> np.ndarray:
     """bool [L]: leaf l (flatten order of ``treedef``) is one of opt.frozen. ``params`` is
     a haiku-style ``{module_name: {name: leaf}}`` mapping, as the reference requires."""
     L = treedef.num_leaves
@@ -175,6 +177,11 @@ def fused_mean_update(slab: ClientDeltaSlab, weights: Sequence, opt: ServerOptim
     """
     if params.dtype != torch.float32 or params.numel() != slab.num_params or not params.is_contiguous():
         raise ValueError(f"params must be a contiguous float32 tensor of {slab.num_params} elements")
+    if isinstance(opt, Adafactor):  # needs whole-leaf reductions: the mean first, then the step
+        # (state = opt.init(slab.unflatten(params)): optax's per-leaf statistics)
+        mean = mean_out if mean_out is not None else torch.empty_like(params)
+        slab.mean(weights, out=mean)
+        return opt.apply(slab.unflatten(mean), state, slab.unflatten(params))[0]
     W = 0.0
     for x in weights:
         W += tree_util._host_weight(x)
@@ -224,6 +231,19 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
     (``fjagg_server_update_ptrs``) — examples/fed_avg.py:82 + :97-101. ``state`` is
     ``opt.init(params)``; returns the new state. ``mean_out`` (optional pytree of float32
     leaves) also receives the mean."""
+    if isinstance(opt, Adafactor):  # needs whole-leaf reductions: the mean first, then the step
+        mean = tree_util.tree_mean(pytrees_and_weights) if mean_out is None else None
+        if mean_out is not None:
+            trees, weights, W = tree_util._collect_pairs(pytrees_and_weights)
+            if not trees:
+                raise ValueError("no clients to aggregate")
+            td, rows = tree_util._client_table(trees)
+            tree_util._fold(rows, weights, scale=tree_util._inverse(W), out=pytree.flatten_as(td, mean_out),
+                            validated=True)
+            mean = mean_out
+        elif mean is None:
+            raise ValueError("no clients to aggregate")
+        return opt.apply(mean, state, params)[0]
     trees, weights, W = tree_util._collect_pairs(pytrees_and_weights)
     if not trees:
         raise ValueError("no clients to aggregate")
@@ -291,5 +311,188 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
     return new
 
 
-__all__ = ["ServerOptimizer", "adagrad", "adam", "fused_mean_update", "fused_tree_mean_update", "ignore_grads_haiku",
-           "rmsprop", "sgd", "yogi"]
+# --------------------------------------------------------------------------- adafactor
+def _factored_dims(shape, factored: bool, min_dim_size_to_factor: int):
+    """optax factorized._factored_dims: (d1, d0) = the second-largest and the largest axis
+    (numpy argsort order, as optax computes it), or None."""
+    if not factored or len(shape) < 2:
+        return None
+    sorted_dims = np.argsort(shape)
+    if shape[sorted_dims[-2]] < min_dim_size_to_factor:
+        return None
+    return int(sorted_dims[-2]), int(sorted_dims[-1])
+
+
+@dataclasses.dataclass(frozen=True)
+class Adafactor:
+    """fedjax.optimizers.adafactor (optimizers.py:284-348): optax.adafactor's chain
+    (include/fjopt.h) on the GPU, ``fjopt_adafactor_step`` over every leaf at once.
+
+    ``init(params)`` gives optax's state shapes (per leaf ``v_row`` / ``v_col`` for factored
+    leaves, ``v`` otherwise, each with a (1,) placeholder for the other kind, and the ema
+    ``m`` when ``momentum`` is set); ``apply(grads, state, params)`` updates ``params`` and
+    the state tensors in place and returns ``(state, params)`` (the reference's
+    ``Optimizer.apply`` returns new arrays). Params, grads and state are float32 device
+    tensors. Means are float64 sums in a fixed order (parity unpinned)."""
+    learning_rate: Union[None, float, Callable[[int], float]]
+    min_dim_size_to_factor: int = 128
+    decay_rate: float = 0.8
+    decay_offset: int = 0
+    multiply_by_parameter_scale: bool = True
+    clipping_threshold: Optional[float] = 1.0
+    momentum: Optional[float] = None
+    dtype_momentum: torch.dtype = torch.float32
+    weight_decay_rate: Optional[float] = None
+    eps: float = 1e-30
+    factored: bool = True
+    weight_decay_mask: object = None
+    frozen: Tuple[Tuple[str, str], ...] = ()
+    _plans: dict = dataclasses.field(default_factory=dict, compare=False, repr=False)
+
+    def init(self, params) -> dict:
+        leaves, td = pytree.flatten(params)
+        vr, vc, v, m = [], [], [], []
+        for p in leaves:
+            if not (isinstance(p, torch.Tensor) and p.dtype == torch.float32):
+                raise TypeError("adafactor takes float32 tensor params")
+            z1 = torch.zeros(1, dtype=torch.float32, device=p.device)
+            fd = _factored_dims(tuple(p.shape), self.factored, self.min_dim_size_to_factor)
+            if fd is not None:
+                d1, d0 = fd
+                vr.append(torch.zeros(tuple(np.delete(p.shape, d0)), dtype=torch.float32, device=p.device))
+                vc.append(torch.zeros(tuple(np.delete(p.shape, d1)), dtype=torch.float32, device=p.device))
+                v.append(z1)
+            else:
+                vr.append(z1)
+                vc.append(z1.clone())
+                v.append(torch.zeros_like(p))
+            if self.momentum is not None:
+                m.append(torch.zeros_like(p))
+        st = {"count": 0, "v_row": pytree.unflatten(td, vr), "v_col": pytree.unflatten(td, vc),
+              "v": pytree.unflatten(td, v)}
+        if self.momentum is not None:
+            if self.dtype_momentum != torch.float32:
+                raise NotImplementedError("the fused adafactor keeps a float32 momentum (dtype_momentum)")
+            st["m"] = pytree.unflatten(td, m)
+        return st
+
+    def hparams(self, count: int) -> _lib.AfHparams:
+        """struct fjopt_af_hparams of the step taken at (pre-increment) count ``count``."""
+        f32 = np.float32
+        h = _lib.AfHparams()
+        d = f32(1) - np.power(f32(count - self.decay_offset + 1), f32(-self.decay_rate))  # _decay_rate_pow
+        h.decay_rate_t, h.one_minus_decay, h.eps = d, f32(1) - d, f32(self.eps)
+        h.clip = int(self.clipping_threshold is not None)
+        h.clip_threshold = f32(self.clipping_threshold or 1.0)
+        h.has_lr = int(self.learning_rate is not None)
+        if self.learning_rate is not None:  # scale_by_schedule reads its pre-increment count
+            lr = self.learning_rate(count) if callable(self.learning_rate) else self.learning_rate
+            h.lr = f32(np.asarray(lr, dtype=np.float64))
+        h.param_scale, h.min_scale = int(bool(self.multiply_by_parameter_scale)), f32(1e-3)
+        h.momentum = int(self.momentum is not None)
+        if self.momentum is not None:
+            h.mom_decay, h.one_minus_mom = f32(self.momentum), f32(1.0 - self.momentum)
+        h.weight_decay = int(self.weight_decay_rate is not None)
+        h.wd = f32(self.weight_decay_rate or 0.0)
+        return h
+
+    def _mask(self, params, td) -> List[bool]:
+        if self.weight_decay_rate is None or self.weight_decay_mask is None:
+            return [True] * td.num_leaves
+        mask = self.weight_decay_mask(params) if callable(self.weight_decay_mask) else self.weight_decay_mask
+        flags = pytree.flatten_as(td, mask)  # a full tree of booleans (prefix trees are not supported)
+        return [bool(f) for f in flags]
+
+    def apply(self, grads, state: dict, params):
+        """One step: ``(state, params)`` with params and state updated in place."""
+        p, td = pytree.flatten(params)
+        g = pytree.flatten_as(td, grads)
+        vr = pytree.flatten_as(td, state["v_row"])
+        vc = pytree.flatten_as(td, state["v_col"])
+        v = pytree.flatten_as(td, state["v"])
+        m = pytree.flatten_as(td, state["m"]) if self.momentum is not None else [None] * len(p)
+        count = int(state["count"])
+        hp = self.hparams(count)
+        if p:
+            device = p[0].device
+            mask = self._mask(params, td)
+            frozen = _frozen_leaves(self, params, td)  # ignore_grads_haiku: left out of the step
+            key, recs = [hp.clip, hp.param_scale, hp.momentum], []
+            for l, (pl, gl) in enumerate(zip(p, g)):
+                if frozen[l]:
+                    continue
+                for what, t in (("grads", gl), ("params", pl)):
+                    if not (isinstance(t, torch.Tensor) and t.dtype == torch.float32 and t.is_contiguous()
+                            and t.device == device and t.shape == pl.shape):
+                        raise ValueError(f"leaf {l}: {what} must be contiguous float32 tensors on {device} "
+                                         f"shaped like the params")
+                rec = _lib.AfLeaf()
+                rec.g, rec.p, rec.n = gl.data_ptr(), pl.data_ptr(), pl.numel()
+                shape = tuple(pl.shape)
+                fd = _factored_dims(shape, self.factored, self.min_dim_size_to_factor)
+                if fd is not None:
+                    d1, d0 = fd
+                    lo, hi = min(d0, d1), max(d0, d1)
+                    prod = lambda s: int(np.prod(s, dtype=np.int64))
+                    dims = (prod(shape[:lo]), shape[lo], prod(shape[lo + 1:hi]), shape[hi], prod(shape[hi + 1:]))
+                    if tuple(vr[l].shape) != tuple(np.delete(shape, d0)) or \
+                            tuple(vc[l].shape) != tuple(np.delete(shape, d1)):
+                        raise ValueError(f"leaf {l}: state v_row / v_col do not have optax's factored shapes")
+                    rec.factored, rec.d0_is_lo = 1, int(d0 == lo)
+                    rec.v_row, rec.v_col = vr[l].data_ptr(), vc[l].data_ptr()
+                else:
+                    dims = (1, pl.numel(), 1, 1, 1)
+                    if v[l].shape != pl.shape:
+                        raise ValueError(f"leaf {l}: state v must have the params' shape")
+                    rec.v = v[l].data_ptr()
+                for s_ in (vr[l], vc[l], v[l]) + ((m[l],) if m[l] is not None else ()):
+                    if s_.dtype != torch.float32 or not s_.is_contiguous() or s_.device != device:
+                        raise ValueError(f"leaf {l}: state must be contiguous float32 tensors on {device}")
+                if m[l] is not None:
+                    if m[l].shape != pl.shape:
+                        raise ValueError(f"leaf {l}: state m must have the params' shape")
+                    rec.m = m[l].data_ptr()
+                rec.dims[:] = dims
+                rec.decay_weights = int(mask[l])
+                recs.append(rec)
+                key.append(bytes(rec))
+            key = tuple(key)
+            plan = self._plans.get(key) if recs else ()
+            if plan is None:
+                arr = (_lib.AfLeaf * len(recs))(*recs)
+                ws_bytes = ctypes.c_int64()
+                lib = _lib.load()
+                words = int(lib.fjopt_adafactor_plan(arr, len(recs), ctypes.byref(hp), None, 0, ctypes.byref(ws_bytes)))
+                table = np.zeros(max(words, 1), dtype=np.int64)
+                if words >= 0:
+                    words = int(lib.fjopt_adafactor_plan(arr, len(recs), ctypes.byref(hp), table.ctypes.data,
+                                                         table.size, ctypes.byref(ws_bytes)))
+                _lib.check(min(words, 0), "fjopt_adafactor_plan")
+                table_dev = torch.from_numpy(table).pin_memory().to(device, non_blocking=True)
+                ws = torch.empty(int(ws_bytes.value), dtype=torch.uint8, device=device)
+                if len(self._plans) >= 8:
+                    self._plans.clear()
+                plan = self._plans[key] = (table, table_dev, ws)
+            if not recs:
+                return dict(state, count=count + 1), params
+            table, table_dev, ws = plan
+            _lib.call("fjopt_adafactor_step", table.ctypes.data, table_dev.data_ptr(), ctypes.byref(hp),
+                      ws.data_ptr(), ws.numel(), torch.cuda.current_stream(device).cuda_stream)
+        new = dict(state)
+        new["count"] = count + 1
+        return new, params
+
+
+def adafactor(learning_rate, min_dim_size_to_factor: int = 128, decay_rate: float = 0.8, decay_offset: int = 0,
+              multiply_by_parameter_scale: bool = True, clipping_threshold: Optional[float] = 1.0,
+              momentum: Optional[float] = None, dtype_momentum=torch.float32,
+              weight_decay_rate: Optional[float] = None, eps: float = 1e-30, factored: bool = True,
+              weight_decay_mask=None) -> Adafactor:
+    """fedjax.optimizers.adafactor (optimizers.py:284-348), same arguments and defaults."""
+    return Adafactor(learning_rate, min_dim_size_to_factor, decay_rate, decay_offset, multiply_by_parameter_scale,
+                     clipping_threshold, momentum, dtype_momentum, weight_decay_rate, eps, factored,
+                     weight_decay_mask)
+
+
+__all__ = ["Adafactor", "ServerOptimizer", "adafactor", "adagrad", "adam", "fused_mean_update",
+           "fused_tree_mean_update", "ignore_grads_haiku", "rmsprop", "sgd", "yogi"]
