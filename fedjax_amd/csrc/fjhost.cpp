@@ -14,10 +14,10 @@
 // errors (ValueError / TypeError). So this module never decides an error itself.
 //
 // Entry points (all positional):
-//   gather_rows(trees, k0, spec, row0, dev_index, ptrs) -> int
-//       Walk trees[k0:] against `spec` (pytree.native_spec of client 0's TreeDef) and
-//       write the device pointer of client k's leaf l to ptrs[k*L + l] (int64 buffer),
-//       for k = k0 .. len(trees)-1, L = len(row0). Every leaf must be a torch.Tensor on
+//   gather_rows(trees, k0, spec, row0, dev_index, ptrs[, k1]) -> int
+//       Walk trees[k0:k1] (k1 defaults to len(trees)) against `spec` (pytree.native_spec
+//       of client 0's TreeDef) and write the device pointer of client k's leaf l to
+//       ptrs[k*L + l] (int64 buffer), for k = k0 .. k1-1, L = len(row0). Every leaf must be a torch.Tensor on
 //       cuda:dev_index (-1: host tensors, for the CPU tests), strided and contiguous,
 //       with row0[l]'s dtype and shape. Also writes row0's pointers to row 0 when k0 == 1.
 //       Returns 0, or -(k+1) for the first client k that does not match.
@@ -160,13 +160,15 @@ int walk(PyObject* spec, PyObject* x, Walk& w) {
 
 PyObject* gather_rows(PyObject*, PyObject* args) {
   PyObject *trees, *spec, *row0, *ptrs;
-  Py_ssize_t k0;
+  Py_ssize_t k0, k1 = -1;
   int dev;
-  if (!PyArg_ParseTuple(args, "O!nOO!iO", &PyList_Type, &trees, &k0, &spec, &PyList_Type, &row0, &dev, &ptrs))
+  if (!PyArg_ParseTuple(args, "O!nOO!iO|n", &PyList_Type, &trees, &k0, &spec, &PyList_Type, &row0, &dev, &ptrs,
+                        &k1))
     return nullptr;
   const Py_ssize_t K = PyList_GET_SIZE(trees), L = PyList_GET_SIZE(row0);
-  if (k0 < 0 || k0 > K) {
-    PyErr_SetString(PyExc_ValueError, "gather_rows: k0 out of range");
+  if (k1 < 0) k1 = K;
+  if (k0 < 0 || k0 > k1 || k1 > K) {
+    PyErr_SetString(PyExc_ValueError, "gather_rows: need 0 <= k0 <= k1 <= len(trees)");
     return nullptr;
   }
   Py_buffer buf;
@@ -197,7 +199,7 @@ PyObject* gather_rows(PyObject*, PyObject* args) {
       if (k0 == 1) out[l] = reinterpret_cast<int64_t>(t.data_ptr());
     }
     Walk w{&dtypes, &sizes, static_cast<c10::DeviceIndex>(dev), nullptr, 0};
-    for (Py_ssize_t k = k0; k < K; ++k) {
+    for (Py_ssize_t k = k0; k < k1; ++k) {
       w.out = out + k * L;
       w.leaf = 0;
       int rc = walk(spec, PyList_GET_ITEM(trees, k), w);

@@ -1049,18 +1049,24 @@ def _collect_pairs(pairs):
 
 # A synchronous tree_mean on an idle GPU waits for the whole host walk (every client's
 # leaves checked, K x L pointers) before the fold starts. When the stream is idle the call
-# folds the first _PIPELINE_FRAC of the clients as soon as their pointers are gathered and
-# walks the rest while that launch runs; the second launch accumulates into the first's
-# sums and applies 1/W (accumulate mode: the same per-element sequence, the same bits).
+# walks the clients in chunks and launches each chunk's fold as soon as its pointers are
+# gathered, accumulating into the first chunk's sums, with 1/W applied by the last launch
+# (accumulate mode: the same per-element sequence, the same bits). Two shapes:
+#   * the fold is the longer part (configs[1]: ~0.35 us of walk vs ~0.6 us of fold per
+#     client): two launches, the first over _PIPELINE_FRAC of the clients;
+#   * the walk is the longer part (many clients, many leaves per client): launches of
+#     >= _PIPELINE_CHUNK clients, each chunk's fold hidden behind the next chunk's walk.
+# Deltas of <= 256 KiB (the narrow plans, whose images are uploaded per launch) are not
+# pipelined: there the per-launch upload costs more than the overlap gives.
 # A busy stream gets one launch (the host work hides behind the queued kernels anyway).
 # The idle probe (hipStreamQuery) puts a marker on the stream, ~3 us of GPU time per call
 # when calls run back to back, so it is gated by a host-side estimate: the time the folds
 # this module issued would finish at the 8 TB/s peak; before that the stream is busy with
 # them and is not probed. FJAGG_PIPELINE_FRAC=0 turns the pipeline off (A/B runs).
 _PIPELINE_FRAC = float(os.environ.get("FJAGG_PIPELINE_FRAC", "0.25"))
+_PIPELINE_CHUNK = int(os.environ.get("FJAGG_PIPELINE_CHUNK", "512"))
 _PIPELINE_MIN_BYTES = 64 << 20  # below this the first launch is too short to hide the walk
-
-
+_WALK_NS_PER_LEAF = 35.0  # native walk + checks per (client, leaf), MI355X host
 _PEAK_BYTES_PER_S = 8.0e12
 _BUSY_UNTIL = [0.0]  # perf_counter() time before which this module's issued folds cannot have finished
 
@@ -1069,9 +1075,24 @@ def _stream_idle(stream: torch.cuda.Stream) -> bool:
     return stream.query()
 
 
+_CHUNK_WALK_US = 60.0  # walk per chunk that amortises a launch's host cost (~15-20 us with its plan image)
+
+
+def _pipeline_bounds(K: int, n: int, L: int) -> List[int]:
+    """Chunk ends [k_1, ..., K] of the pipelined fold (see _PIPELINE_FRAC). Walk-bound
+    calls take chunks of at least _PIPELINE_CHUNK clients and at least _CHUNK_WALK_US of
+    walk each (profiles/r03g_pipeline/)."""
+    walk_ns, fold_ns = _WALK_NS_PER_LEAF * L, 4.0 * n / _PEAK_BYTES_PER_S * 1e9
+    if walk_ns > fold_ns and _PIPELINE_CHUNK > 0:
+        c = max(_PIPELINE_CHUNK, int(np.ceil(_CHUNK_WALK_US * 1e3 / walk_ns)))
+        if K > c:
+            return list(range(c, K, c)) + [K]
+    return [min(K - 1, max(1, int(K * _PIPELINE_FRAC))), K]
+
+
 def _tree_mean_pipelined(trees: List[PyTree], packed: "_Weights", W, first) -> Optional[PyTree]:
-    """tree_mean of float32 device pytrees in two launches overlapping the host walk (see
-    _PIPELINE_FRAC); None (nothing launched, or a first launch whose outputs are dropped)
+    """tree_mean of float32 device pytrees in chunked launches overlapping the host walk
+    (see _PIPELINE_FRAC); None (nothing launched, or launches whose outputs are dropped)
     when the case does not hold, and the caller then takes the one-launch path, which also
     raises the reference's errors. ``first``: pytree.flatten(trees[0])."""
     leaves0, td = first
@@ -1089,6 +1110,8 @@ def _tree_mean_pipelined(trees: List[PyTree], packed: "_Weights", W, first) -> O
             return None
         n += x.numel()
     K = len(trees)
+    # small deltas (<= _NARROW_MAX_BYTES) fold through plan images uploaded per launch: chunked
+    # launches there cost more than the overlap gives (profiles/r03g_pipeline/narrow2.jsonl)
     if 4 * n <= _NARROW_MAX_BYTES or 4 * n * K < _PIPELINE_MIN_BYTES:
         return None
     now = time.perf_counter()
@@ -1101,27 +1124,24 @@ def _tree_mean_pipelined(trees: List[PyTree], packed: "_Weights", W, first) -> O
     if spec is None:
         return None
     host = _lib.host()
-    k1 = min(K - 1, max(1, int(K * _PIPELINE_FRAC)))
-    ptrs = np.empty((K, len(leaves0)), dtype=np.int64)
-    if host.gather_rows(trees[:k1], 1, spec, leaves0, idx, ptrs) != 0:
-        return None
     if _ENTRY_ADDRS is None:
         _native_fold_addrs()
     plan, wsum, *_ = _ENTRY_ADDRS
     nt_min = 0.0 if 4 * n * K >= NONTEMPORAL_MIN_BYTES else float("inf")  # the whole job's bytes decide
     s = stream.cuda_stream
-    got = host.fold_table(leaves0, ptrs[:k1], packed.f32[:k1], 1.0, False, nt_min, idx, s, plan, wsum)
-    if got is None:
-        return None
-    _lib.check(got[0], "fjagg_wsum_ptrs")
-    outs = got[1]
-    if host.gather_rows(trees, k1, spec, leaves0, idx, ptrs) != 0:
-        return None
-    got = host.fold_table(leaves0, ptrs[k1:], packed.f32[k1:], float(np.float32(_inverse(W))), True, nt_min,
-                          idx, s, plan, wsum, outs, 1)
-    if got is None:
-        return None
-    _lib.check(got[0], "fjagg_wsum_ptrs")
+    ptrs = np.empty((K, len(leaves0)), dtype=np.int64)
+    scale = float(np.float32(_inverse(W)))
+    outs, done = None, 0  # clients [0, done) folded; client 0's row comes from the gather at k0 = 1
+    for k1 in _pipeline_bounds(K, n, len(leaves0)):
+        if host.gather_rows(trees, max(done, 1), spec, leaves0, idx, ptrs, k1) != 0:
+            return None
+        last = k1 == K
+        got = host.fold_table(leaves0, ptrs[done:k1], packed.f32[done:k1], scale if last else 1.0, last, nt_min,
+                              idx, s, plan, wsum, outs, 0 if outs is None else 1)
+        if got is None:
+            return None
+        _lib.check(got[0], "fjagg_wsum_ptrs")
+        outs, done = got[1], k1
     return pytree.unflatten(td, outs)
 
 

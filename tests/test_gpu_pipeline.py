@@ -1,6 +1,6 @@
-"""tree_mean on an idle stream folds in two launches that overlap the host walk
+"""tree_mean on an idle stream folds in chunked launches that overlap the host walk
 (tree_util._tree_mean_pipelined): the first launch folds clients [0, k1) as soon as their
-pointers are gathered, the second accumulates [k1, K) into the same sums and applies 1/W.
+pointers are gathered, later ones accumulate into the same sums, the last applies 1/W.
 Accumulate mode keeps the per-element sequence of fedjax/core/tree_util.py:85-96, so the
 result must be bitwise the one-launch fold and the oracle's; errors must be the one-launch
 path's (the second walk falls back to it)."""
@@ -29,8 +29,16 @@ def _flat(tree):
     return np.concatenate([x.detach().cpu().numpy().ravel() for x in ref.flatten(tree)[0]])
 
 
-def _launches():
-    return _lib.host().image_paths()["kernel_args"]
+def _launches():  # fold_table launches (image in the kernel arguments or uploaded)
+    p = _lib.host().image_paths()
+    return p["kernel_args"] + p["uploaded"]
+
+
+@pytest.fixture
+def chunk(monkeypatch):
+    def set_(v):
+        monkeypatch.setattr(tu, "_PIPELINE_CHUNK", v)
+    return set_
 
 
 @pytest.fixture
@@ -57,6 +65,32 @@ def test_pipelined_tree_mean_bitwise(K, frac, cuda):
         np.testing.assert_array_equal(got.view(np.uint32), one.view(np.uint32))
     if K == 29:  # the oracle on every element (29 x 1.2 M)
         host = [(_tmap(lambda x: x.cpu().numpy(), c), w) for c, w in pairs]
+        want = np.concatenate([np.asarray(x).ravel() for x in ref.flatten(ref.tree_mean(host))[0]])
+        np.testing.assert_array_equal(one.view(np.uint32), want.astype(np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("K,c", [(1500, 512), (1500, 100), (600, 256)])
+def test_chunked_pipeline_small_model_bitwise(K, c, frac, chunk, cuda, monkeypatch):
+    """A small model (48,670 params: the walk, not the fold, is the longer part), with the
+    narrow-delta exclusion lifted: launches of c clients, each accumulating into the first's
+    sums (stripe / narrow plans per chunk)."""
+    monkeypatch.setattr(tu, "_CHUNK_WALK_US", 0.0)  # chunks of exactly c clients
+    monkeypatch.setattr(tu, "_NARROW_MAX_BYTES", 0)  # (the fold still picks its narrow plans natively)
+    g = torch.Generator(device="cuda").manual_seed(K + c)
+    shapes = {"w": (784, 62), "b": (62,)}
+    clients = [{k: torch.rand(s, device="cuda", generator=g) - 0.5 for k, s in shapes.items()} for _ in range(K)]
+    pairs = list(zip(clients, np.random.RandomState(c).randint(1, 501, size=K).tolist()))
+    frac(0.0)
+    one = _flat(tu.tree_mean(pairs))
+    frac(0.25)
+    chunk(c)
+    torch.cuda.synchronize()
+    n0 = _launches()
+    got = _flat(tu.tree_mean(pairs))
+    assert _launches() - n0 == -(-K // c)
+    np.testing.assert_array_equal(got.view(np.uint32), one.view(np.uint32))
+    if K == 600:
+        host = [({k: v.cpu().numpy() for k, v in t.items()}, w) for t, w in pairs]
         want = np.concatenate([np.asarray(x).ravel() for x in ref.flatten(ref.tree_mean(host))[0]])
         np.testing.assert_array_equal(one.view(np.uint32), want.astype(np.float32).view(np.uint32))
 

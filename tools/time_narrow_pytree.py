@@ -2,10 +2,13 @@
 kernel): an EMNIST logistic-regression-sized tree {w: (784, 62), b: (62,)} (48,670 params)
 and a 2-layer MLP {l1/w: (784, 128), l1/b, l2/w: (128, 62), l2/b} (108,606 params), each
 (client, leaf) its own allocation. Prints one JSON line per shape: GPU ms per call (events
-around back-to-back calls) and GB/s of client deltas."""
+around back-to-back calls), GB/s of client deltas, and the median wall time of one
+synchronous call on an idle GPU. The FJAGG_PIPELINE_* environment selects the host pipeline
+(tree_util._tree_mean_pipelined; FJAGG_PIPELINE_FRAC=0: off)."""
 import json
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -42,8 +45,17 @@ def main():
             e.record()
             e.synchronize()
             ms = s.elapsed_time(e) / reps
+            sync = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                tu.tree_mean(pairs)
+                torch.cuda.synchronize()
+                sync.append((time.perf_counter() - t0) * 1e3)
             print(json.dumps({"model": name, "clients": K, "params": P, "ms_per_call": round(ms, 4),
-                              "GBs": round(K * P * 4 / ms / 1e6, 1)}), flush=True)
+                              "GBs": round(K * P * 4 / ms / 1e6, 1),
+                              "sync_call_ms": round(float(np.median(sync)), 4),
+                              "pipeline": [tu._PIPELINE_FRAC, tu._PIPELINE_CHUNK]}), flush=True)
             del clients, pairs
 
 
