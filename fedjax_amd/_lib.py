@@ -124,7 +124,7 @@ class ServerOpt(ctypes.Structure):
 
 
 OPT_SGD, OPT_MOMENTUM, OPT_ADAM, OPT_ADAGRAD, OPT_RMSPROP, OPT_YOGI = 1, 2, 3, 4, 5, 6
-OPT_F_MOMENTUM = 1
+OPT_F_MOMENTUM, OPT_F_CENTERED = 1, 2
 
 
 class AfLeaf(ctypes.Structure):

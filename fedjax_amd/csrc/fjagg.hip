@@ -116,14 +116,22 @@ struct OptEpi {
       const float ss = __fadd_rn(__fmul_rn(g, g), v[e]);
       v[e] = ss;
       u = __fmul_rn(ss > 0.0f ? rsqrt_rn(__fadd_rn(ss, o.eps)) : 0.0f, g);
-    } else if (o.kind == FJAGG_OPT_RMSPROP) {  // optax.scale_by_rms [+ optax.trace]
+    } else if (o.kind == FJAGG_OPT_RMSPROP) {  // optax.rmsprop: scale_by_rms | scale_by_stddev, lr, [trace]
       const float nu = __fadd_rn(__fmul_rn(o.one_minus_b2, __fmul_rn(g, g)), __fmul_rn(o.b2, v[e]));
       v[e] = nu;
-      u = __fmul_rn(g, rsqrt_rn(__fadd_rn(nu, o.eps)));
-      if (o.flags & FJAGG_OPT_F_MOMENTUM) {
-        const float t = __fadd_rn(u, __fmul_rn(o.decay, m[e]));
+      float den = nu;
+      if (o.flags & FJAGG_OPT_F_CENTERED) {  // scale_by_stddev: mu = (1 - decay) g + decay mu
+        const float mu = __fadd_rn(__fmul_rn(o.one_minus_b2, g), __fmul_rn(o.b2, m[e]));
+        m[e] = mu;
+        den = __fsub_rn(nu, __fmul_rn(mu, mu));
+      }
+      u = __fmul_rn(g, rsqrt_rn(__fadd_rn(den, o.eps)));
+      if (o.flags & FJAGG_OPT_F_MOMENTUM) {  // the trace follows scale_by_learning_rate in this chain
+        const float s = __fmul_rn(o.neg_lr, u);
+        const float t = __fadd_rn(s, __fmul_rn(o.decay, m[e]));
         m[e] = t;
-        u = o.nesterov ? __fadd_rn(u, __fmul_rn(o.decay, t)) : t;
+        params[e] = __fadd_rn(p, o.nesterov ? __fadd_rn(s, __fmul_rn(o.decay, t)) : t);
+        return;
       }
     } else {  // optax.scale_by_yogi: nu - (1 - b2) * sign(nu - g^2) * g^2, no bias correction
       const float mu = __fadd_rn(__fmul_rn(o.one_minus_b1, g), __fmul_rn(o.b1, m[e]));
@@ -1699,9 +1707,15 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
 namespace {
 bool opt_needs_m(const fjagg_server_opt& o) {
   return o.kind == FJAGG_OPT_MOMENTUM || o.kind == FJAGG_OPT_ADAM || o.kind == FJAGG_OPT_YOGI ||
-         (o.kind == FJAGG_OPT_RMSPROP && (o.flags & FJAGG_OPT_F_MOMENTUM));
+         (o.kind == FJAGG_OPT_RMSPROP && (o.flags & (FJAGG_OPT_F_MOMENTUM | FJAGG_OPT_F_CENTERED)));
 }
 bool opt_needs_v(const fjagg_server_opt& o) { return o.kind >= FJAGG_OPT_ADAM; }
+bool opt_valid(const fjagg_server_opt* o) {
+  if (!o || o->kind < FJAGG_OPT_SGD || o->kind > FJAGG_OPT_YOGI) return false;
+  const int known = o->kind == FJAGG_OPT_RMSPROP ? (FJAGG_OPT_F_MOMENTUM | FJAGG_OPT_F_CENTERED) : FJAGG_OPT_F_MOMENTUM;
+  if (o->flags & ~known) return false;
+  return (o->flags & (FJAGG_OPT_F_MOMENTUM | FJAGG_OPT_F_CENTERED)) != (FJAGG_OPT_F_MOMENTUM | FJAGG_OPT_F_CENTERED);
+}
 }  // namespace
 extern "C" {
 
@@ -1711,8 +1725,7 @@ int fjagg_server_update_ptrs(int in_dtype, const int64_t* image_dev, int L, int6
   g_err[0] = 0;
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16)
     return fail(FJAGG_EUNSUPPORTED, "server update: f32 or bf16 deltas");
-  if (!opt || opt->kind < FJAGG_OPT_SGD || opt->kind > FJAGG_OPT_YOGI || (opt->flags & ~FJAGG_OPT_F_MOMENTUM))
-    return fail(FJAGG_EINVAL, "server update: bad optimizer descriptor");
+  if (!opt_valid(opt)) return fail(FJAGG_EINVAL, "server update: bad optimizer descriptor");
   if (K < 1) return fail(FJAGG_EINVAL, "need K >= 1");
   if (nblk == 0) return FJAGG_OK;
   if (nblk < 0 || nblk > 0x7fffffff || !image_dev || !w_dev || !state_dev || L < 1)
@@ -1771,8 +1784,7 @@ int fjagg_server_update_dense(int in_dtype, const void* x_dev, int64_t ld, int64
   g_err[0] = 0;
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16)
     return fail(FJAGG_EUNSUPPORTED, "server update: f32 or bf16 deltas");
-  if (!opt || opt->kind < FJAGG_OPT_SGD || opt->kind > FJAGG_OPT_YOGI || (opt->flags & ~FJAGG_OPT_F_MOMENTUM))
-    return fail(FJAGG_EINVAL, "server update: bad optimizer descriptor");
+  if (!opt_valid(opt)) return fail(FJAGG_EINVAL, "server update: bad optimizer descriptor");
   if (K < 1 || P < 1 || ld < P) return fail(FJAGG_EINVAL, "bad shape (K=%lld, P=%lld)", (long long)K, (long long)P);
   if (P * elem_bytes(in_dtype) > kMaxRowBytes) return fail(FJAGG_EUNSUPPORTED, "rows > 1 GiB");
   if (!x_dev || !w_dev || !params_dev) return fail(FJAGG_EINVAL, "null pointer argument");

@@ -3,7 +3,7 @@
 The step after the mean in every FedJAX algorithm is the server update
 (examples/fed_avg.py:97-101, fedjax/algorithms/fed_avg.py:150-154):
 ``opt_state, params = server_optimizer.apply(mean_delta, opt_state, params)``
-with any of ``fedjax.optimizers.sgd``, ``adam``, ``adagrad``, ``rmsprop`` (not centered),
+with any of ``fedjax.optimizers.sgd``, ``adam``, ``adagrad``, ``rmsprop`` (centered without momentum too),
 ``yogi`` or ``adafactor`` (fedjax/core/optimizers.py:117-348, optax).
 :func:`fused_mean_update` folds the round's client deltas and applies that update
 in the same kernel (``fjagg_server_update_dense``): the mean stays in registers,
@@ -55,6 +55,7 @@ class ServerOptimizer:
     init_m: float = 0.0
     init_v: float = 0.0
     frozen: Tuple[Tuple[str, str], ...] = ()
+    centered: bool = False
 
     def lr(self, count: int) -> float:
         """The learning rate of the step whose INCREMENTED count is ``count``: a schedule is
@@ -66,7 +67,7 @@ class ServerOptimizer:
 
     def needs_m(self) -> bool:
         return self.kind in (_lib.OPT_MOMENTUM, _lib.OPT_ADAM, _lib.OPT_YOGI) or (
-            self.kind == _lib.OPT_RMSPROP and self.momentum is not None)
+            self.kind == _lib.OPT_RMSPROP and (self.momentum is not None or self.centered))
 
     def needs_v(self) -> bool:
         return self.kind >= _lib.OPT_ADAM
@@ -103,7 +104,10 @@ class ServerOptimizer:
         d.bc1 = f32(1) - np.power(f32(self.b1), f32(count))
         d.bc2 = f32(1) - np.power(f32(self.b2), f32(count))
         d.eps, d.eps_root = f32(self.eps), f32(self.eps_root)
-        d.flags = _lib.OPT_F_MOMENTUM if (self.kind == _lib.OPT_RMSPROP and self.momentum is not None) else 0
+        d.flags = 0
+        if self.kind == _lib.OPT_RMSPROP:
+            d.flags = (_lib.OPT_F_MOMENTUM if self.momentum is not None else 0) | (
+                _lib.OPT_F_CENTERED if self.centered else 0)
         return d
 
 
@@ -126,11 +130,14 @@ def adagrad(learning_rate: float, initial_accumulator_value: float = 0.1, eps: f
 
 def rmsprop(learning_rate: float, decay: float = 0.9, eps: float = 1e-8, initial_scale: float = 0.,
             centered: bool = False, momentum: Optional[float] = None, nesterov: bool = False) -> ServerOptimizer:
-    """fedjax.optimizers.rmsprop (optimizers.py:181-224): optax.scale_by_rms [+ trace]."""
-    if centered:
-        raise NotImplementedError("centered rmsprop (optax.scale_by_stddev) has no fused server step")
+    """fedjax.optimizers.rmsprop (optimizers.py:181-224) = optax.rmsprop: scale_by_rms
+    (centered: scale_by_stddev, state m = mu), scale_by_learning_rate, then [trace] of the
+    lr-scaled update (state m = the trace)."""
+    if centered and momentum is not None:
+        raise NotImplementedError("centered rmsprop with momentum keeps three states (mu, nu, trace); the fused "
+                                  "server step has two")
     return ServerOptimizer(_lib.OPT_RMSPROP, learning_rate, momentum=momentum, nesterov=nesterov, b2=decay,
-                           eps=eps, init_v=initial_scale)
+                           eps=eps, init_v=initial_scale, centered=bool(centered))
 
 
 def yogi(learning_rate: float, b1: float = 0.9, b2: float = 0.999, eps: float = 1e-3) -> ServerOptimizer:

@@ -227,9 +227,14 @@ enum fjagg_opt_kind {
   FJAGG_OPT_RMSPROP = 5,  /* optimizers.py:181-224, optax.scale_by_rms (v) [+ trace (m)]     */
   FJAGG_OPT_YOGI = 6      /* optimizers.py:253-281, optax.scale_by_yogi (m, v)               */
 };
-/* RMSPROP: b2 / one_minus_b2 = decay / 1 - decay; flags & FJAGG_OPT_F_MOMENTUM adds
- * optax.trace(decay = this struct's `decay`, nesterov) after the rescale. */
+/* RMSPROP: b2 / one_minus_b2 = decay / 1 - decay. optax.rmsprop's chain is the rescale,
+ * then scale_by_learning_rate, then (flags & FJAGG_OPT_F_MOMENTUM) optax.trace(decay = this
+ * struct's `decay`, nesterov) of the lr-scaled update (m holds that trace), then
+ * apply_updates. flags & FJAGG_OPT_F_CENTERED: the rescale is optax.scale_by_stddev
+ * (m holds mu: u = g * rsqrt(nu - mu*mu + eps)); not combinable with the momentum flag
+ * (a third state). */
 #define FJAGG_OPT_F_MOMENTUM 1
+#define FJAGG_OPT_F_CENTERED 2
 typedef struct fjagg_server_opt {
   int kind;
   int nesterov;

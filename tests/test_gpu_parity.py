@@ -764,12 +764,17 @@ def _np_server_step(opt, d, g, p, m, v):
     elif opt.kind == 4:  # optax.scale_by_rss
         v = g * g + v
         u = np.where(v > 0, rsqrt(v + f(d.eps)), f(0)) * g
-    elif opt.kind == 5:  # optax.scale_by_rms [+ trace]
+    elif opt.kind == 5:  # optax.rmsprop: scale_by_rms | scale_by_stddev, scale_by_learning_rate, [trace]
         v = f(d.one_minus_b2) * (g * g) + f(d.b2) * v
-        u = g * rsqrt(v + f(d.eps))
-        if opt.momentum is not None:
-            m = u + f(d.decay) * m
-            u = u + f(d.decay) * m if opt.nesterov else m
+        den = v
+        if opt.centered:  # scale_by_stddev: mu = (1 - decay) g + decay mu; rsqrt(nu - mu^2 + eps)
+            m = f(d.one_minus_b2) * g + f(d.b2) * m
+            den = v - m * m
+        u = g * rsqrt(den + f(d.eps))
+        if opt.momentum is not None:  # the trace of the lr-scaled update
+            s_ = f(d.neg_lr) * u
+            m = s_ + f(d.decay) * m
+            return p + (s_ + f(d.decay) * m if opt.nesterov else m), m, v
     else:  # optax.scale_by_yogi
         m = f(d.one_minus_b1) * g + f(d.b1) * m
         v = v - (f(d.one_minus_b2) * np.sign(v - g * g)).astype(f) * (g * g)
@@ -783,6 +788,7 @@ OPTIMIZERS = [lambda s: s.sgd(0.5), lambda s: s.sgd(0.1, momentum=0.9),
               lambda s: s.adagrad(0.1), lambda s: s.adagrad(0.3, initial_accumulator_value=0.0, eps=1e-7),
               lambda s: s.rmsprop(0.01), lambda s: s.rmsprop(0.01, decay=0.8, initial_scale=1.0, momentum=0.5),
               lambda s: s.rmsprop(0.01, momentum=0.9, nesterov=True),
+              lambda s: s.rmsprop(0.01, centered=True), lambda s: s.rmsprop(0.02, decay=0.7, centered=True, initial_scale=1.0),
               lambda s: s.yogi(0.01), lambda s: s.yogi(0.05, b1=0.5, b2=0.99, eps=1e-4)]
 
 
