@@ -255,6 +255,16 @@ def test_random_case_matches_oracle(cuda, seed, monkeypatch):
         want = ref.tree_mean(list(zip(np_trees, ws)))
         want_sum = ref.tree_sum(np_trees)
     _same(tu.tree_mean(list(zip(trees, ws))), want, "tree_mean(list)")
+    # the idle-stream pipeline (tree_util._tree_mean_pipelined) forced on whatever this case
+    # is: chunks of about a third of the clients, each accumulating into the first's sums
+    with monkeypatch.context() as mp:
+        mp.setattr(tu, "_PIPELINE_MIN_BYTES", 0)
+        mp.setattr(tu, "_NARROW_MAX_BYTES", 0)
+        mp.setattr(tu, "_CHUNK_WALK_US", 0.0)
+        mp.setattr(tu, "_PIPELINE_CHUNK", max(1, K // 3))
+        mp.setattr(tu, "_BUSY_UNTIL", [0.0])
+        torch.cuda.synchronize()
+        _same(tu.tree_mean(list(zip(trees, ws))), want, "tree_mean(list), pipelined")
     # generator input: chunks of about two clients' worth of deltas
     per = max(1, sum(int(np.prod(s)) for s in c["shapes"])) * 4
     monkeypatch.setattr(tu, "STREAM_BUDGET_BYTES", 2 * per + 1)
