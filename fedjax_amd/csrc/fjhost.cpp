@@ -53,6 +53,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/csrc/autograd/python_variable.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -306,6 +307,135 @@ typedef int (*WsumL2Fn)(int, int, int, const int64_t*, int, int64_t, int64_t, co
                         int64_t, void*);
 constexpr int kF32 = 0, kScale = 1, kAccumulate = 2, kNontemporal = 4;  // fjagg.h enums
 
+// The launch part of fold_table for a gathered table: K x L pointers `in` (row 0 = row0's
+// leaves), float32 weights wf[K]. outs: empty = fresh outputs shaped like row0 (appended),
+// else the destinations (float32, contiguous, row0's shapes and device). Returns 0 with the
+// library status in *rc (launched), 1 when the case does not hold (nothing launched).
+// Throws on torch errors.
+int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K, const float* wf, double scale,
+              bool has_scale, double nt_min_bytes, int dev, unsigned long long stream, PlanFn plan, WsumFn wsum,
+              std::vector<at::Tensor>& outs, bool accumulate, WsumL2Fn l2fn, L2WsFn l2ws, float* l2p, int* rc,
+              Stamp& st) {
+  const int64_t L = static_cast<int64_t>(row0.size());
+  const bool with_l2 = l2p != nullptr;
+  if (L < 1 || K < 1 || (accumulate && outs.empty())) return 1;
+  // fast case only: float32 leaves (fold type and output type are then float32 for any
+  // weights). A leaf with a client pointer off 16 bytes walks element units (per-leaf
+  // plan); the outputs are fresh allocations, so aligned.
+  std::vector<int64_t> leaf_n(L);
+  int64_t total = 0;
+  for (int64_t l = 0; l < L; ++l) {
+    const at::Tensor& t = row0[l];
+    if (t.scalar_type() != at::kFloat) return 1;
+    leaf_n[l] = t.numel();
+    total += leaf_n[l];
+  }
+  if (total == 0) return 1;  // only empty leaves: the Python path (no launch at all)
+  std::vector<int64_t> lbits(L, 0);
+  for (int64_t k = 0; k < K; ++k)
+    for (int64_t l = 0; l < L; ++l) lbits[l] |= in[k * L + l];
+  st.lap(kTChecks);
+  const bool fresh = outs.empty();
+  if (!fresh) {  // caller's destinations: float32, contiguous, row0's shape and device
+    if (static_cast<int64_t>(outs.size()) != L) return 1;
+    for (int64_t l = 0; l < L; ++l) {
+      const at::Tensor& d = outs[l];
+      if (d.scalar_type() != at::kFloat || !d.is_contiguous() || d.sizes() != row0[l].sizes() ||
+          d.device() != row0[l].device())
+        return 1;
+    }
+  }
+  std::vector<uint8_t> elem(L, 0);
+  bool any_elem = false;
+  for (int64_t l = 0; l < L; ++l) {
+    if (fresh) outs.push_back(at::empty(row0[l].sizes(), row0[l].options()));
+    elem[l] = ((lbits[l] | reinterpret_cast<int64_t>(outs[l].data_ptr())) & 15) != 0;
+    any_elem = any_elem || elem[l];
+  }
+  st.lap(kTOutputs);
+  // a small delta and many clients: k_ptrs_narrow's LDS-staged stripes (any alignment;
+  // the rule of tree_util._narrow), not with fused norms
+  static const int64_t narrow_max = [] {  // FJAGG_NARROW_MAX_BYTES, as tree_util._NARROW_MAX_BYTES
+    const char* e = getenv("FJAGG_NARROW_MAX_BYTES");
+    return e ? (int64_t)atoll(e) : (int64_t)(256 << 10);
+  }();
+  const bool narrow = !with_l2 && K >= 16 && total * 4 <= narrow_max;
+  const uint8_t* mask = any_elem && !narrow ? elem.data() : nullptr;
+  // every pointer 16-byte aligned: the stripe pipeline (k_ptrs_stripe, fjstripe.hip) with
+  // the width of tree_util._stripe_variant_for; FJAGG_STRIPE_PYTREE=0 keeps k_ptrs_narrow
+  static const bool stripe_on = [] {
+    const char* e = getenv("FJAGG_STRIPE_PYTREE");
+    return !(e && e[0] == '0' && e[1] == 0);
+  }();
+  int svar = 0;
+  if (narrow && stripe_on && !any_elem && K >= 512) {  // (fjagg.hip kStripeMinClients)
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    int64_t s64 = 0, s32 = 0;
+    for (int64_t l = 0; l < L; ++l) {
+      s64 += (leaf_n[l] + 63) / 64;
+      s32 += (leaf_n[l] + 31) / 32;
+    }
+    svar = s64 >= cus ? 20 : s32 >= cus ? 21 : 22;
+  }
+  const int pflags = narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0;
+  const int64_t nblk = plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);
+  if (nblk < 0) return 1;
+  // plan image (fjagg.h): in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk] | f32 weights
+  const int64_t nw = (K + 1) / 2, n = K * L + 2 * L + 2 * nblk + nw;
+  st.lap(kTPlan);
+  auto fill = [&](int64_t* p) {
+    std::memcpy(p, in, sizeof(int64_t) * K * L);
+    for (int64_t l = 0; l < L; ++l) {
+      p[K * L + l] = reinterpret_cast<int64_t>(outs[l].data_ptr());
+      p[K * L + L + l] = leaf_n[l];
+    }
+    if (plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) return false;
+    p[n - 1] = 0;
+    std::memcpy(p + n - nw, wf, 4 * K);
+    return true;
+  };
+  const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
+  const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0) |
+                    (narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0);
+  at::Tensor ws;  // fused l2 norms: per-workgroup partials, from torch's allocator (stream-ordered)
+  if (with_l2) {
+    const int64_t need = l2ws(K, nblk);
+    if (need < 0) return 1;
+    ws = at::empty({need > 4 ? need : 4}, outs[0].options().dtype(at::kByte));
+  }
+  auto launch = [&](const int64_t* image, const int64_t* w, int fl) {
+    if (with_l2)
+      return l2fn(kF32, kF32, kF32, image, static_cast<int>(L), K, nblk, w, static_cast<float>(scale), l2p, fl,
+                  ws.data_ptr(), ws.numel(), reinterpret_cast<void*>(stream));
+    return wsum(kF32, kF32, kF32, image, static_cast<int>(L), K, nblk, w, static_cast<float>(scale), fl,
+                reinterpret_cast<void*>(stream));
+  };
+  *rc = FJAGG_EUNSUPPORTED;
+  if (!narrow && n <= FJAGG_KARG_MAX_WORDS) {
+    // the image and weights travel in the kernel arguments (FJAGG_HOST_TABLES): no pinned
+    // staging buffer and no upload on the stream in front of the fold
+    thread_local std::vector<int64_t> host_img;
+    host_img.resize(static_cast<size_t>(n));
+    if (!fill(host_img.data())) return 1;
+    st.lap(kTImage);
+    *rc = launch(host_img.data(), host_img.data() + (n - nw), flags | FJAGG_HOST_TABLES);
+    if (*rc != FJAGG_EUNSUPPORTED) ++g_image_karg;
+  }
+  if (*rc == FJAGG_EUNSUPPORTED) {  // too large for the kernel arguments: pinned image + stream-ordered upload
+    at::Tensor img = at::empty({n}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+    if (!fill(img.data_ptr<int64_t>())) return 1;
+    st.lap(kTImage);
+    at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);
+    st.lap(kTUpload);
+    const int64_t* dp = dimg.data_ptr<int64_t>();
+    *rc = launch(dp, dp + (n - nw), flags);
+    ++g_image_upload;
+  }
+  st.lap(kTLaunch);
+  return 0;
+}
+
 PyObject* fold_table(PyObject*, PyObject* args) {
   PyObject *row0, *ptrs, *wf, *dst = Py_None, *l2sq = Py_None;
   double scale, nt_min_bytes;
@@ -336,137 +466,37 @@ PyObject* fold_table(PyObject*, PyObject* args) {
   if (L < 1 || bp.len % (8 * L) != 0) Py_RETURN_NONE;
   const int64_t K = bp.len / (8 * L);
   if (K < 1 || bw.len < 4 * K) Py_RETURN_NONE;
-  const auto* in = static_cast<const int64_t*>(bp.buf);
   Stamp st;
   ++g_timer_calls;
   try {
+    std::vector<at::Tensor> r0, outs;
+    r0.reserve(L);
+    for (Py_ssize_t l = 0; l < L; ++l) {
+      PyObject* x = PyList_GET_ITEM(row0, l);
+      if (!THPVariable_Check(x)) Py_RETURN_NONE;
+      r0.push_back(THPVariable_Unpack(x));
+    }
+    if (dst != Py_None) {
+      for (Py_ssize_t l = 0; l < L; ++l) {
+        PyObject* o = PyList_GET_ITEM(dst, l);
+        if (!THPVariable_Check(o)) Py_RETURN_NONE;
+        outs.push_back(THPVariable_Unpack(o));
+      }
+    }
+    float* l2p = nullptr;
     if (with_l2) {
       const at::Tensor& q = THPVariable_Unpack(l2sq);
       if (q.scalar_type() != at::kFloat || q.numel() != K || !q.is_contiguous() || !q.is_cuda() ||
           q.get_device() != dev)
         Py_RETURN_NONE;
+      l2p = q.data_ptr<float>();
     }
-    // fast case only: float32 leaves (fold type and output type are then float32 for any
-    // weights). A leaf with a client pointer off 16 bytes walks element units (per-leaf
-    // plan); the outputs are fresh allocations, so aligned.
-    std::vector<int64_t> leaf_n(L);
-    int64_t total = 0;
-    for (Py_ssize_t l = 0; l < L; ++l) {
-      const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(row0, l));
-      if (t.scalar_type() != at::kFloat) Py_RETURN_NONE;
-      leaf_n[l] = t.numel();
-      total += leaf_n[l];
-    }
-    if (total == 0) Py_RETURN_NONE;  // only empty leaves: the Python path (no launch at all)
-    std::vector<int64_t> lbits(L, 0);
-    for (int64_t k = 0; k < K; ++k)
-      for (Py_ssize_t l = 0; l < L; ++l) lbits[l] |= in[k * L + l];
-    st.lap(kTChecks);
-    std::vector<at::Tensor> outs;
-    outs.reserve(L);
-    std::vector<uint8_t> elem(L, 0);
-    bool any_elem = false;
-    for (Py_ssize_t l = 0; l < L; ++l) {
-      const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(row0, l));
-      if (dst != Py_None) {  // caller's destinations: float32, contiguous, row0's shape and device
-        PyObject* o = PyList_GET_ITEM(dst, l);
-        if (!THPVariable_Check(o)) Py_RETURN_NONE;
-        const at::Tensor& d = THPVariable_Unpack(o);
-        if (d.scalar_type() != at::kFloat || !d.is_contiguous() || d.sizes() != t.sizes() || d.device() != t.device())
-          Py_RETURN_NONE;
-        outs.push_back(d);
-      } else {
-        outs.push_back(at::empty(t.sizes(), t.options()));
-      }
-      elem[l] = ((lbits[l] | reinterpret_cast<int64_t>(outs.back().data_ptr())) & 15) != 0;
-      any_elem = any_elem || elem[l];
-    }
-    st.lap(kTOutputs);
-    auto plan = reinterpret_cast<PlanFn>(plan_addr);
-    // a small delta and many clients: k_ptrs_narrow's LDS-staged stripes (any alignment;
-    // the rule of tree_util._narrow), not with fused norms
-    static const int64_t narrow_max = [] {  // FJAGG_NARROW_MAX_BYTES, as tree_util._NARROW_MAX_BYTES
-      const char* e = getenv("FJAGG_NARROW_MAX_BYTES");
-      return e ? (int64_t)atoll(e) : (int64_t)(256 << 10);
-    }();
-    const bool narrow = !with_l2 && K >= 16 && total * 4 <= narrow_max;
-    const uint8_t* mask = any_elem && !narrow ? elem.data() : nullptr;
-    // every pointer 16-byte aligned: the stripe pipeline (k_ptrs_stripe, fjstripe.hip) with
-    // the width of tree_util._stripe_variant_for; FJAGG_STRIPE_PYTREE=0 keeps k_ptrs_narrow
-    static const bool stripe_on = [] {
-      const char* e = getenv("FJAGG_STRIPE_PYTREE");
-      return !(e && e[0] == '0' && e[1] == 0);
-    }();
-    int svar = 0;
-    if (narrow && stripe_on && !any_elem && K >= 512) {  // (fjagg.hip kStripeMinClients)
-      int cus = 0;
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-        cus = 256;
-      int64_t s64 = 0, s32 = 0;
-      for (Py_ssize_t l = 0; l < L; ++l) {
-        s64 += (leaf_n[l] + 63) / 64;
-        s32 += (leaf_n[l] + 31) / 32;
-      }
-      svar = s64 >= cus ? 20 : s32 >= cus ? 21 : 22;
-    }
-    const int pflags = narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0;
-    const int64_t nblk = plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);
-    if (nblk < 0) Py_RETURN_NONE;
-    // plan image (fjagg.h): in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk] | f32 weights
-    const int64_t nw = (K + 1) / 2, n = K * L + 2 * L + 2 * nblk + nw;
-    st.lap(kTPlan);
-    auto fill = [&](int64_t* p) {
-      std::memcpy(p, in, sizeof(int64_t) * K * L);
-      for (Py_ssize_t l = 0; l < L; ++l) {
-        p[K * L + l] = reinterpret_cast<int64_t>(outs[l].data_ptr());
-        p[K * L + L + l] = leaf_n[l];
-      }
-      if (plan(kF32, pflags, leaf_n.data(), mask, static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) return false;
-      p[n - 1] = 0;
-      std::memcpy(p + n - nw, bw.buf, 4 * K);
-      return true;
-    };
-    const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
-    const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0) |
-                      (narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0);
-    at::Tensor ws;  // fused l2 norms: per-workgroup partials, from torch's allocator (stream-ordered)
-    float* l2p = nullptr;
-    if (with_l2) {
-      const int64_t need = reinterpret_cast<L2WsFn>(l2ws_addr)(K, nblk);
-      if (need < 0) Py_RETURN_NONE;
-      ws = at::empty({need > 4 ? need : 4}, outs[0].options().dtype(at::kByte));
-      l2p = THPVariable_Unpack(l2sq).data_ptr<float>();
-    }
-    auto launch = [&](const int64_t* image, const int64_t* w, int fl) {
-      if (with_l2)
-        return reinterpret_cast<WsumL2Fn>(l2_addr)(kF32, kF32, kF32, image, static_cast<int>(L), K, nblk, w,
-                                                   static_cast<float>(scale), l2p, fl, ws.data_ptr(), ws.numel(),
-                                                   reinterpret_cast<void*>(stream));
-      return reinterpret_cast<WsumFn>(wsum_addr)(kF32, kF32, kF32, image, static_cast<int>(L), K, nblk, w,
-                                                 static_cast<float>(scale), fl, reinterpret_cast<void*>(stream));
-    };
-    int rc = FJAGG_EUNSUPPORTED;
-    if (!narrow && n <= FJAGG_KARG_MAX_WORDS) {
-      // the image and weights travel in the kernel arguments (FJAGG_HOST_TABLES): no pinned
-      // staging buffer and no upload on the stream in front of the fold
-      thread_local std::vector<int64_t> host_img;
-      host_img.resize(static_cast<size_t>(n));
-      if (!fill(host_img.data())) Py_RETURN_NONE;
-      st.lap(kTImage);
-      rc = launch(host_img.data(), host_img.data() + (n - nw), flags | FJAGG_HOST_TABLES);
-      if (rc != FJAGG_EUNSUPPORTED) ++g_image_karg;
-    }
-    if (rc == FJAGG_EUNSUPPORTED) {  // too large for the kernel arguments: pinned image + stream-ordered upload
-      at::Tensor img = at::empty({n}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
-      if (!fill(img.data_ptr<int64_t>())) Py_RETURN_NONE;
-      st.lap(kTImage);
-      at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);
-      st.lap(kTUpload);
-      const int64_t* dp = dimg.data_ptr<int64_t>();
-      rc = launch(dp, dp + (n - nw), flags);
-      ++g_image_upload;
-    }
-    st.lap(kTLaunch);
+    int rc = 0;
+    if (fold_core(r0, static_cast<const int64_t*>(bp.buf), K, static_cast<const float*>(bw.buf), scale,
+                  has_scale != 0, nt_min_bytes, dev, stream, reinterpret_cast<PlanFn>(plan_addr),
+                  reinterpret_cast<WsumFn>(wsum_addr), outs, accumulate != 0, reinterpret_cast<WsumL2Fn>(l2_addr),
+                  reinterpret_cast<L2WsFn>(l2ws_addr), l2p, &rc, st) != 0)
+      Py_RETURN_NONE;
     PyObject* list = PyList_New(L);
     if (!list) return nullptr;
     for (Py_ssize_t l = 0; l < L; ++l) PyList_SET_ITEM(list, l, THPVariable_Wrap(std::move(outs[l])));
@@ -957,6 +987,216 @@ PyObject* leaf_fold(PyObject*, PyObject* args) {
   }
 }
 
+// ------------------------------------------------------------------ tree_mean, whole call
+// tree_mean(list of (pytree, weight)) in one native call for the common case: exact dict /
+// list / tuple / None nodes over float32 CUDA tensors (contiguous, client 0's shapes, one
+// device), Python int / float weights. The same launches as the Python path
+// (gather_rows + fold_weights + fold_table), and the idle-stream pipeline of
+// tree_util._tree_mean_pipelined. Anything else is "not this case": None (nothing launched,
+// or launches whose outputs are dropped) and the Python path runs, raising the reference's
+// errors.
+
+// Walk program of tree x (the format of pytree.native_spec: 0 leaf, 1 None, (2, sorted keys,
+// children) dict, (3|4, n, children) list / tuple) with its tensor leaves in flatten order
+// and the sorted key list of every dict in pre-order (for rebuild). nullptr: not the fast
+// case when no Python error is set.
+struct SpecBuild {
+  std::vector<PyObject*> leaves;  // borrowed
+  std::vector<PyObject*> keys;    // owned
+  ~SpecBuild() {
+    for (PyObject* k : keys) Py_DECREF(k);
+  }
+};
+
+PyObject* spec_of(PyObject* x, SpecBuild& b, int depth) {
+  if (depth > 64) return nullptr;
+  if (Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(THPVariableClass)) {
+    b.leaves.push_back(x);
+    return PyLong_FromLong(kLeaf);
+  }
+  if (x == Py_None) return PyLong_FromLong(kNone);
+  const bool is_dict = PyDict_CheckExact(x), is_list = PyList_CheckExact(x), is_tuple = PyTuple_CheckExact(x);
+  if (!is_dict && !is_list && !is_tuple) return nullptr;
+  PyObject* keys = nullptr;
+  Py_ssize_t n;
+  if (is_dict) {
+    keys = PyDict_Keys(x);
+    if (!keys) return nullptr;
+    b.keys.push_back(keys);
+    if (PyList_Sort(keys) != 0) {  // unorderable keys: the Python path decides
+      PyErr_Clear();
+      return nullptr;
+    }
+    n = PyList_GET_SIZE(keys);
+  } else {
+    n = Py_SIZE(x);
+  }
+  PyObject* children = PyTuple_New(n);
+  if (!children) return nullptr;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* c = is_dict ? PyDict_GetItem(x, PyList_GET_ITEM(keys, i))
+                          : (is_list ? PyList_GET_ITEM(x, i) : PyTuple_GET_ITEM(x, i));
+    PyObject* cs = c ? spec_of(c, b, depth + 1) : nullptr;
+    if (!cs) {
+      Py_DECREF(children);
+      return nullptr;
+    }
+    PyTuple_SET_ITEM(children, i, cs);
+  }
+  PyObject* aux = is_dict ? PyList_AsTuple(keys) : PyLong_FromSsize_t(n);
+  if (!aux) {
+    Py_DECREF(children);
+    return nullptr;
+  }
+  return Py_BuildValue("(lNN)", is_dict ? (long)kDict : is_list ? (long)kList : (long)kTuple, aux, children);
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// mean_pairs(pairs, may_pipeline, frac, chunk, chunk_walk_us, walk_ns_per_leaf, min_bytes,
+//            narrow_max, nt_min_bytes, plan_fn, wsum_fn) -> (rc, tree, job_bytes) | None
+// may_pipeline: the caller's host-side estimate says the stream may be idle (then the
+// stream is probed). The chunking is tree_util._pipeline_bounds's.
+PyObject* mean_pairs(PyObject*, PyObject* args) {
+  PyObject* pairs;
+  int may_pipeline;
+  double frac, chunk_walk_us, walk_ns, nt_min;
+  long long chunk, min_bytes, narrow_max;
+  unsigned long long plan_addr, wsum_addr;
+  if (!PyArg_ParseTuple(args, "OpdLddLLdKK", &pairs, &may_pipeline, &frac, &chunk, &chunk_walk_us, &walk_ns,
+                        &min_bytes, &narrow_max, &nt_min, &plan_addr, &wsum_addr))
+    return nullptr;
+  if (!PyList_CheckExact(pairs) && !PyTuple_CheckExact(pairs)) Py_RETURN_NONE;
+  const Py_ssize_t K = Py_SIZE(pairs);
+  if (K < 1) Py_RETURN_NONE;
+  PyObject* const* items = PyList_CheckExact(pairs) ? &PyList_GET_ITEM(pairs, 0) : &PyTuple_GET_ITEM(pairs, 0);
+  Stamp st;
+  ++g_timer_calls;
+  try {
+    std::vector<PyObject*> trees(K);
+    std::vector<float> wf(K);
+    double W = 0.0;
+    for (Py_ssize_t k = 0; k < K; ++k) {  // `for pytree, weight in pytrees_and_weights` (tree_util.py:89)
+      PyObject* pr = items[k];
+      PyObject *t, *w;
+      if (PyTuple_CheckExact(pr) && PyTuple_GET_SIZE(pr) == 2) {
+        t = PyTuple_GET_ITEM(pr, 0);
+        w = PyTuple_GET_ITEM(pr, 1);
+      } else if (PyList_CheckExact(pr) && PyList_GET_SIZE(pr) == 2) {
+        t = PyList_GET_ITEM(pr, 0);
+        w = PyList_GET_ITEM(pr, 1);
+      } else {
+        Py_RETURN_NONE;
+      }
+      double d;
+      if (PyLong_CheckExact(w)) {
+        int overflow = 0;
+        long long v = PyLong_AsLongLongAndOverflow(w, &overflow);
+        if (PyErr_Occurred()) PyErr_Clear();
+        if (overflow || v >= (1LL << 53) || v <= -(1LL << 53)) Py_RETURN_NONE;
+        d = static_cast<double>(v);
+      } else if (PyFloat_CheckExact(w)) {
+        d = PyFloat_AS_DOUBLE(w);
+      } else {
+        Py_RETURN_NONE;
+      }
+      trees[k] = t;
+      wf[k] = static_cast<float>(d);
+      W += d;  // tree_util.py:95
+    }
+    SpecBuild sb;
+    PyObject* spec = spec_of(trees[0], sb, 0);
+    if (!spec) {
+      if (PyErr_Occurred()) return nullptr;
+      Py_RETURN_NONE;
+    }
+    struct Ref {
+      PyObject* o;
+      ~Ref() { Py_DECREF(o); }
+    } spec_ref{spec};
+    const int64_t L = static_cast<int64_t>(sb.leaves.size());
+    if (L < 1) Py_RETURN_NONE;
+    std::vector<at::Tensor> row0;
+    row0.reserve(L);
+    std::vector<at::ScalarType> dtypes;
+    std::vector<c10::IntArrayRef> sizes;
+    int64_t n = 0;
+    int dev = -1;
+    for (PyObject* x : sb.leaves) {
+      const at::Tensor& t = THPVariable_Unpack(x);
+      if (t.layout() != c10::kStrided || !t.is_cuda() || t.scalar_type() != at::kFloat || !t.is_contiguous())
+        Py_RETURN_NONE;
+      if (dev < 0) dev = t.get_device();
+      if (t.get_device() != dev) Py_RETURN_NONE;
+      row0.push_back(t);
+      n += t.numel();
+    }
+    if (n == 0) Py_RETURN_NONE;
+    for (const at::Tensor& t : row0) {
+      dtypes.push_back(t.scalar_type());
+      sizes.push_back(t.sizes());
+    }
+    const double job_bytes = 4.0 * static_cast<double>(n) * static_cast<double>(K);
+    const unsigned long long stream =
+        reinterpret_cast<unsigned long long>(c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(dev)).stream());
+    // chunk ends (tree_util._pipeline_bounds), pipelined only on an idle stream
+    std::vector<int64_t> bounds;
+    if (may_pipeline && frac > 0.0 && K >= 8 && 4 * n > narrow_max && job_bytes >= static_cast<double>(min_bytes) &&
+        hipStreamQuery(reinterpret_cast<hipStream_t>(stream)) == hipSuccess) {
+      const double wns = walk_ns * L, fns = 4.0 * n / 8.0e12 * 1e9;
+      int64_t c = 0;
+      if (wns > fns && chunk > 0) {
+        c = std::max<int64_t>(chunk, static_cast<int64_t>(std::ceil(chunk_walk_us * 1e3 / wns)));
+        if (K <= c) c = 0;
+      }
+      if (c > 0) {
+        for (int64_t k1 = c; k1 < K; k1 += c) bounds.push_back(k1);
+      } else {
+        bounds.push_back(std::min<int64_t>(K - 1, std::max<int64_t>(1, static_cast<int64_t>(K * frac))));
+      }
+    }
+    bounds.push_back(K);
+    st.lap(kTChecks);
+    std::vector<int64_t> ptrs(static_cast<size_t>(K * L));
+    for (int64_t l = 0; l < L; ++l) ptrs[l] = reinterpret_cast<int64_t>(row0[l].data_ptr());
+    Walk w{&dtypes, &sizes, static_cast<c10::DeviceIndex>(dev), nullptr, 0};
+    const double scale = W > 0.0 ? 1.0 / W : 0.0;  // tree_util.py:37,60
+    const double ntm = job_bytes >= nt_min ? 0.0 : HUGE_VAL;  // the whole job's bytes decide
+    std::vector<at::Tensor> outs;
+    int64_t done = 0;
+    int rc = 0;
+    for (int64_t k1 : bounds) {
+      for (int64_t k = std::max<int64_t>(done, 1); k < k1; ++k) {
+        w.out = ptrs.data() + k * L;
+        w.leaf = 0;
+        const int r = walk(spec, trees[k], w);
+        if (r < 0) return nullptr;
+        if (r > 0 || w.leaf != static_cast<size_t>(L)) Py_RETURN_NONE;
+      }
+      const bool last = k1 == K;
+      if (fold_core(row0, ptrs.data() + done * L, k1 - done, wf.data() + done, last ? scale : 1.0, last, ntm, dev,
+                    stream, reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs,
+                    !outs.empty(), nullptr, nullptr, nullptr, &rc, st) != 0)
+        Py_RETURN_NONE;
+      if (rc != 0) return Py_BuildValue("(iOd)", rc, Py_None, job_bytes);
+      done = k1;
+    }
+    std::vector<PyObject*> wrapped(L);
+    for (int64_t l = 0; l < L; ++l) wrapped[l] = THPVariable_Wrap(std::move(outs[l]));
+    size_t i = 0, ki = 0;
+    PyObject* tree = rebuild(trees[0], wrapped.data(), i, sb.keys, ki);
+    for (PyObject* o : wrapped) Py_XDECREF(o);  // (rebuild took the ones it used)
+    if (!tree) return nullptr;
+    st.lap(kTWrap);
+    return Py_BuildValue("(iNd)", rc, tree, job_bytes);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 PyObject* image_paths(PyObject*, PyObject*) {
   return Py_BuildValue("{s:L,s:L}", "kernel_args", g_image_karg, "uploaded", g_image_upload);
 }
@@ -992,6 +1232,7 @@ PyMethodDef kMethods[] = {
     {"table_from_caps", table_from_caps, METH_VARARGS, "pointer table of captured leaves, version check"},
     {"leaf_fold", leaf_fold, METH_VARARGS, "fjtree_fold_leaves over 1-2 operand trees (see fjhost.cpp)"},
     {"fold_table", fold_table, METH_VARARGS, "plan image + output leaves + fjagg_wsum_ptrs launch (see fjhost.cpp)"},
+    {"mean_pairs", mean_pairs, METH_VARARGS, "tree_mean of (pytree, weight) pairs in one native call (see fjhost.cpp)"},
     {nullptr, nullptr, 0, nullptr},
 };
 

@@ -1071,6 +1071,28 @@ _PEAK_BYTES_PER_S = 8.0e12
 _BUSY_UNTIL = [0.0]  # perf_counter() time before which this module's issued folds cannot have finished
 
 
+# The whole call in one native function (fjhost.mean_pairs) for the common case — plain
+# dict / list / tuple pytrees of float32 CUDA tensors, Python-number weights: the same
+# launches as below (gather, fold_table, the pipeline), without the Python walk of client 0,
+# the pair collection and the unflatten. FJAGG_NATIVE_MEAN=0 keeps the Python path (A/B).
+_NATIVE_MEAN = os.environ.get("FJAGG_NATIVE_MEAN", "1") != "0"
+
+
+def _native_mean(pairs) -> Optional[PyTree]:
+    if _ENTRY_ADDRS is None:
+        _native_fold_addrs()
+    now = time.perf_counter()
+    got = _lib.host().mean_pairs(pairs, _PIPELINE_FRAC > 0.0 and now >= _BUSY_UNTIL[0], _PIPELINE_FRAC,
+                                 _PIPELINE_CHUNK, _CHUNK_WALK_US, _WALK_NS_PER_LEAF, _PIPELINE_MIN_BYTES,
+                                 _NARROW_MAX_BYTES, float(NONTEMPORAL_MIN_BYTES), _ENTRY_ADDRS[0], _ENTRY_ADDRS[1])
+    if got is None:
+        return None
+    rc, tree, job_bytes = got
+    _BUSY_UNTIL[0] = max(now, _BUSY_UNTIL[0]) + job_bytes / _PEAK_BYTES_PER_S
+    _lib.check(rc, "fjagg_wsum_ptrs")
+    return tree
+
+
 def _stream_idle(stream: torch.cuda.Stream) -> bool:
     return stream.query()
 
@@ -1167,6 +1189,10 @@ def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
     """
     if type(pytrees_and_weights) is not list and type(pytrees_and_weights) is not tuple:
         return _tree_mean_stream(iter(pytrees_and_weights))
+    if _NATIVE_MEAN and pytrees_and_weights:
+        got = _native_mean(pytrees_and_weights)
+        if got is not None:
+            return got
     trees, weights, sum_weight = _collect_pairs(pytrees_and_weights)
     if not trees:
         return None  # tree_util.py:96 maps over None

@@ -146,3 +146,48 @@ def test_pipelined_declines_what_it_does_not_cover(frac, cuda):
         got = _flat(tu.tree_mean(pairs))
         assert _launches() - n0 <= 1, name
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32), err_msg=name)
+
+
+def test_native_whole_call_equals_python_path(frac, cuda, monkeypatch):
+    """fjhost.mean_pairs (the whole tree_mean call natively) against the Python path
+    (FJAGG_NATIVE_MEAN off): bitwise, for dict / list / tuple / None nodes, pairs given as
+    tuples or lists, int and float weights, pipelined or not; declined cases (a namedtuple
+    node, a numpy weight, a bf16 leaf) still give the Python path's result."""
+    import collections
+    g = torch.Generator(device="cuda").manual_seed(7)
+    r = lambda *s: torch.rand(*s, device="cuda", generator=g) - 0.5
+    NT = collections.namedtuple("NT", "a b")
+    K = 12
+    cases = {
+        "nested": [({"z": [r(70_000), None, (r(3), r(5, 2))], "a": {"q": r(8), "p": r(100_000)}}, 1 + k)
+                   for k in range(K)],
+        "list pairs, float weights": [[[r(90_000), r(4)], 0.5 + k] for k in range(K)],
+        "emnist": list(zip(_clients(K, seed=3), [7] * K)),
+        "namedtuple": [(NT(r(80_000), r(3)), k + 1) for k in range(K)],
+        "numpy weight": [({"w": r(80_000)}, np.float32(k + 1)) for k in range(K)],
+        "bf16": [({"w": r(80_000).to(torch.bfloat16)}, k + 1) for k in range(K)],
+    }
+    for name, pairs in cases.items():
+        monkeypatch.setattr(tu, "_NATIVE_MEAN", False)
+        frac(0.0)
+        want = tu.tree_mean(pairs)
+        monkeypatch.setattr(tu, "_NATIVE_MEAN", True)
+        for f in (0.0, 0.5):
+            frac(f)
+            monkeypatch.setattr(tu, "_PIPELINE_MIN_BYTES", 0)
+            torch.cuda.synchronize()
+            got = tu.tree_mean(pairs)
+            assert ref.flatten(got)[1] == ref.flatten(want)[1], name
+            assert type(got) is type(want), name
+            for a, b in zip(ref.flatten(got)[0], ref.flatten(want)[0]):
+                assert a.dtype == b.dtype and a.shape == b.shape, name
+                assert torch.equal(a.view(torch.int16 if a.dtype == torch.bfloat16 else torch.int32),
+                                   b.view(torch.int16 if b.dtype == torch.bfloat16 else torch.int32)), name
+    # structure / shape / dtype errors: the Python path's
+    bad = [({"w": r(80_000)}, 1) for _ in range(K)]
+    bad[9] = ({"w": r(80_001)}, 1)
+    with pytest.raises(ValueError):
+        tu.tree_mean(bad)
+    bad[9] = ({"v": r(80_000)}, 1)
+    with pytest.raises(ValueError):
+        tu.tree_mean(bad)
