@@ -130,7 +130,9 @@ def dropin_surface(dev, calls=20):
       ``mean_aggregator().apply`` (calls back to back);
     * configs[1] as 128 EMNIST-CNN pytrees, every (client, leaf) its own allocation,
       through ``tree_mean``: calls back to back, and one synchronous call on an idle GPU
-      (the latency a server aggregating once per round sees).
+      (the latency a server aggregating once per round sees);
+    * the same clients through the library algorithms' running sum (fed_avg.py:132-146),
+      one synchronous round.
 
     GB/s = the K*P*4 algorithmic bytes of client deltas / the time per call."""
     import fedjax_amd
@@ -200,8 +202,25 @@ def dropin_surface(dev, calls=20):
     ms = float(np.median(single)) * 1e3
     res["c1_tree_mean_sync_call_ms"] = round(ms, 4)
     res["c1_tree_mean_sync_call_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+    # the library algorithms' running sum (fedjax/algorithms/fed_avg.py:132-146): one
+    # synchronous round of tree_add(s, tree_weight(delta, n)) x K + tree_inverse_weight
+    W = float(sum(w for _, w in pairs))
+    loop = []
+    for _ in range(calls):
+        torch.cuda.synchronize()
+        t0 = pc()
+        s = tu.tree_zeros_like(pairs[0][0])
+        for t, w in pairs:
+            s = tu.tree_add(s, tu.tree_weight(t, w))
+        mean = tu.tree_inverse_weight(s, W)
+        torch.cuda.synchronize()
+        loop.append(pc() - t0)
+    del s, mean
+    ms = float(np.median(loop)) * 1e3
+    res["c1_library_loop_round_ms"] = round(ms, 4)
+    res["c1_library_loop_round_GBs"] = round(K * P * 4 / ms / 1e6, 1)
     res["note"] = ("caller-held pytrees, separate allocations; timed after the headline, outside its "
-                   "timed region; GB/s = K*P*4 client-delta bytes per call")
+                   "timed region; GB/s = K*P*4 client-delta bytes per call (library loop: per round)")
     del pairs
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
