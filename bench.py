@@ -202,6 +202,19 @@ def dropin_surface(dev, calls=20):
     ms = float(np.median(single)) * 1e3
     res["c1_tree_mean_sync_call_ms"] = round(ms, 4)
     res["c1_tree_mean_sync_call_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+    # the same clients through the Aggregator surface (aggregator.py:61-75), one synchronous call
+    agg, single = fedjax_amd.aggregators.mean_aggregator(), []
+    triples = [(f"c{k}", t, w) for k, (t, w) in enumerate(pairs)]
+    for _ in range(n):
+        torch.cuda.synchronize()
+        t0 = pc()
+        agg.apply(triples, state)
+        torch.cuda.synchronize()
+        single.append(pc() - t0)
+    ms = float(np.median(single)) * 1e3
+    res["c1_mean_aggregator_apply_sync_call_ms"] = round(ms, 4)
+    res["c1_mean_aggregator_apply_sync_call_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+    del triples
     # the library algorithms' running sum (fedjax/algorithms/fed_avg.py:132-146): one
     # synchronous round of tree_add(s, tree_weight(delta, n)) x K + tree_inverse_weight
     W = float(sum(w for _, w in pairs))

@@ -1238,6 +1238,12 @@ def _tree_mean_stream(it) -> PyTree:
                 done = True
                 break
             chunk.append(nxt)
+        if done and out is None and _NATIVE_MEAN:
+            # the whole iterable fit one chunk (mean_aggregator().apply over resident clients):
+            # the one-call native path, as tree_mean(list) takes
+            got = _native_mean(chunk)
+            if got is not None:
+                return got
         trees = [t for t, _ in chunk]
         weights = [w for _, w in chunk]
         for i, w in enumerate(weights):
