@@ -542,8 +542,12 @@ _STALE = -100  # fjhost.leaf_fold: a captured operand changed since tree_weight
 _NORMS: "collections.deque" = None  # (capture, l2sq, l2) of the last fused tree_add calls
 
 
+_HOST = None  # the _fjhost module (set with _TREE_ADDRS: the per-call paths skip _lib.host())
+
+
 def _tree_addrs():
-    global _TREE_ADDRS, _NORMS
+    global _TREE_ADDRS, _NORMS, _HOST
+    _HOST = _lib.host()
     if _TREE_ADDRS is None:
         import collections
         lib = _lib.load()
@@ -648,18 +652,25 @@ _F32_EXACT_INT = 1 << 53
 # Deferred running sums (PendingSum): on by default; see set_deferred_sums.
 # budget_bytes None = automatic: min(4 GiB, 1/8 of the device's free memory when the
 # process first defers a sum on it), see _defer_budget
-_DEFER = {"enabled": True, "budget_bytes": None, "max_clients": 4095}
+_DEFER = {"enabled": True, "budget_bytes": None, "max_clients": 4095,
+          # fold the pending part early once it holds this much (and >= flush_clients links):
+          # that launch runs while the caller's loop goes on, and fewer deltas stay referenced
+          "flush_bytes": 256 << 20, "flush_clients": 16}
 _AUTO_BUDGET = {}  # device index -> automatic budget in bytes
 
 
 def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = None,
-                      max_clients: Optional[int] = None) -> None:
+                      max_clients: Optional[int] = None, flush_bytes: Optional[int] = None,
+                      flush_clients: Optional[int] = None) -> None:
     """Configure how ``tree_add(s, tree_weight(x, n))`` runs.
 
     Enabled (default): the sum is deferred (:class:`PendingSum`) and folded by ONE
     pytree-kernel launch when it is used, at most ``budget_bytes`` of pending deltas or
     ``max_clients`` (<= 4095) clients per launch (an older part of the chain is folded
-    first when a limit would be passed, so memory stays bounded). Disabled: every call is
+    first when a limit would be passed, so memory stays bounded). Once the pending part
+    holds >= 256 MiB of deltas in >= 16 clients it is folded at the next ``tree_add``
+    (``flush_bytes`` / ``flush_clients``): that launch overlaps the rest of the caller's
+    loop, and the deltas it covers are released. Any split gives the same bits. Disabled: every call is
     one fused launch (fjtree_fold_leaves), which also suits loops that update delta
     tensors in place between clients. Both give the reference's bits.
 
@@ -668,7 +679,8 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
     default budget is therefore min(4 GiB, 1/8 of the device memory free when the process
     first defers a sum there), per chain; a loop that keeps several running sums at once
     holds up to that much per sum — pass a smaller ``budget_bytes`` (or disable deferral)
-    on a device close to full. ``budget_bytes=0`` restores the automatic value.
+    on a device close to full. ``budget_bytes=0`` restores the automatic value. A new
+    budget applies to running sums started after the call.
 
     Semantics: deferral holds each delta by reference, guarded by torch's in-place
     version counter (a modified delta makes the fold raise). Writes that bypass that
@@ -680,6 +692,10 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
         _DEFER["budget_bytes"] = int(budget_bytes) if int(budget_bytes) > 0 else None
     if max_clients is not None:
         _DEFER["max_clients"] = min(4095, max(1, int(max_clients)))
+    if flush_bytes is not None:
+        _DEFER["flush_bytes"] = max(0, int(flush_bytes))
+    if flush_clients is not None:
+        _DEFER["flush_clients"] = max(1, int(flush_clients))
 
 
 def _defer_budget(device: torch.device) -> int:
@@ -699,10 +715,10 @@ class _Chain:
     """The linear run of PendingSum links one norm buffer serves: float32 [2, n] on the
     device, row 0 = squared l2 norms, row 1 = l2 norms of the clients, by link index."""
 
-    __slots__ = ("tip", "buf")
+    __slots__ = ("tip", "buf", "budget")
 
     def __init__(self):
-        self.tip, self.buf = None, None
+        self.tip, self.buf, self.budget = None, None, None  # budget: _defer_budget, on first use
 
 
 class _Ticket:
@@ -907,20 +923,24 @@ def _defer(sum_side, item, item_weight, item_cap):
         ref = sum_side._value if sum_side._value is not None else sum_side._ref
     else:
         ref, parent, root = sum_side, None, sum_side
-    cap = _lib.host().append_check(ref, item, item_cap)
+    host = _HOST if _HOST is not None else _lib.host()
+    cap = host.append_check(ref, item, item_cap)
     if cap is None:
         return None
     if type(cap) is int:
         raise RuntimeError("a pytree passed to tree_weight was modified (a leaf replaced or updated in "
                            "place) before its weighted value was used; the reference computes "
                            "tree_weight eagerly")
-    if parent is not None and parent._value is None and (
-            parent._n + 1 > _DEFER["max_clients"] or
-            parent._bytes + cap[2] > _defer_budget(cap[0][0].device)):
-        parent.materialize()  # bound the chain: fold what is pending, continue from it
+    if parent is not None and parent._value is None:
+        budget = parent._chain.budget
+        if budget is None:
+            budget = parent._chain.budget = _defer_budget(cap[0][0].device)
+        if (parent._n + 1 > _DEFER["max_clients"] or parent._bytes + cap[2] > budget or
+                (parent._bytes >= _DEFER["flush_bytes"] and parent._n >= _DEFER["flush_clients"])):
+            parent.materialize()  # bound the chain: fold what is pending, continue from it
     bcap = None
     if parent is None or parent._value is not None:  # this link starts a run: capture its base
-        bcap = _lib.host().capture(root if parent is None else parent._value, -1)
+        bcap = host.capture(root if parent is None else parent._value, -1)
     node = PendingSum(root, parent, cap, item_weight, ref, bcap)
     _LAST = weakref.ref(node)
     return node
@@ -932,11 +952,12 @@ def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
     Float32 device pytrees (<= 64 leaves) with a Python-number weight give a
     :class:`WeightedTree` (deferred, fused into the tree_add that consumes it);
     anything else is computed now by the pytree kernel."""
-    w = _host_weight(weight)
+    tw = type(weight)
+    w = weight if (tw is float or tw is int) else _host_weight(weight)
     if (type(w) is float or (type(w) is int and -_F32_EXACT_INT < w < _F32_EXACT_INT)):
         if _TREE_ADDRS is None:
             _tree_addrs()
-        cap = _lib.host().capture(pytree_, -1)
+        cap = _HOST.capture(pytree_, -1)
         if cap is not None:
             return WeightedTree(pytree_, w, cap)
     return _fold_trees([pytree_], [w])

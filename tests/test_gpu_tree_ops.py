@@ -410,3 +410,44 @@ def test_deferred_chain_budget_is_bounded_by_free_memory(cuda, sum_mode):
     for k, h in enumerate(hs):
         want = ref.tree_add(want, ref.tree_weight(to_np(h), k + 1))
     assert np.array_equal(bits(got), bits(ref.tree_inverse_weight(want, 45.)["a"]))
+
+
+def test_early_flush_of_the_running_sum(cuda, sum_mode):
+    """The deferred chain folds its pending part once it holds flush_bytes in flush_clients
+    links (set_deferred_sums): the literal loop with the per-client norm of fed_avg.py:
+    137-144 keeps the reference's bits for the mean, and each norm is the same value the
+    one-launch chain gives."""
+    if sum_mode != "deferred":
+        pytest.skip("deferred mode only")
+    g = torch.Generator().manual_seed(23)
+    shapes = {"w": (3000,), "b": {"c": (17,)}}
+    K = 23
+    xs = [to_dev(rand_tree(shapes, g), cuda) for _ in range(K)]
+    ws = [int(v) for v in np.random.RandomState(4).randint(1, 50, size=K)]
+
+    def loop():
+        s, norms = tu.tree_zeros_like(xs[0]), []
+        for x, w in zip(xs, ws):
+            s = tu.tree_add(s, tu.tree_weight(x, w))
+            norms.append(tu.tree_l2_norm(x))
+        mean = tu.tree_inverse_weight(s, float(sum(ws)))
+        return leaves_np(mean), [float(n) for n in norms]
+
+    base_mean, base_norms = loop()  # defaults: one fold (23 small clients < 256 MiB)
+    acc = tmap(lambda s: np.zeros(s, np.float32), shapes)
+    for x, w in zip(xs, ws):
+        acc = ref.tree_add(acc, ref.tree_weight(to_np(x), w))
+    want = [a.reshape(-1) for a in pytree.leaves_of(ref.tree_inverse_weight(acc, float(sum(ws))))]
+    for a, b in zip(base_mean, want):
+        assert np.array_equal(bits(a), bits(b))
+    for fb, fc in [(1, 1), (12_100 * 3, 2), (40_000, 5)]:
+        tu.set_deferred_sums(True, flush_bytes=fb, flush_clients=fc)
+        try:
+            mean, norms = loop()
+        finally:
+            tu.set_deferred_sums(True, flush_bytes=256 << 20, flush_clients=16)
+        for a, b in zip(mean, want):
+            assert np.array_equal(bits(a), bits(b)), (fb, fc)
+        n64 = [float(np.sqrt(sum(float(np.dot(v.astype(np.float64), v.astype(np.float64)))
+                                 for v in leaves_np(x)))) for x in xs]
+        np.testing.assert_allclose(norms, n64, rtol=2e-6)
