@@ -1075,7 +1075,16 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
   Stamp st;
   ++g_timer_calls;
   try {
-    std::vector<PyObject*> trees(K);
+    // the trees are held by new references for the call: key comparisons during the walks
+    // can run Python code, which could otherwise drop the caller's last reference
+    struct Held {
+      std::vector<PyObject*> v;
+      ~Held() {
+        for (PyObject* o : v) Py_XDECREF(o);
+      }
+    } held;
+    held.v.assign(K, nullptr);
+    std::vector<PyObject*>& trees = held.v;
     std::vector<float> wf(K);
     double W = 0.0;
     for (Py_ssize_t k = 0; k < K; ++k) {  // `for pytree, weight in pytrees_and_weights` (tree_util.py:89)
@@ -1102,6 +1111,7 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
       } else {
         Py_RETURN_NONE;
       }
+      Py_INCREF(t);
       trees[k] = t;
       wf[k] = static_cast<float>(d);
       W += d;  // tree_util.py:95

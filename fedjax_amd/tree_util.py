@@ -654,8 +654,11 @@ _F32_EXACT_INT = 1 << 53
 # process first defers a sum on it), see _defer_budget
 _DEFER = {"enabled": True, "budget_bytes": None, "max_clients": 4095,
           # fold the pending part early once it holds this much (and >= flush_clients links):
-          # that launch runs while the caller's loop goes on, and fewer deltas stay referenced
-          "flush_bytes": 256 << 20, "flush_clients": 16}
+          # that launch runs while the caller's loop goes on, and fewer deltas stay referenced.
+          # A flush costs ~30-50 us of host time, so it pays once the fold it starts early is
+          # long: at configs[1] 256 MiB flushes made a 128-client round slower (0.48 -> 0.54
+          # ms, profiles/r03s_library_loop/); 1 GiB never triggers there
+          "flush_bytes": 1 << 30, "flush_clients": 16}
 _AUTO_BUDGET = {}  # device index -> automatic budget in bytes
 
 
@@ -668,7 +671,7 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
     pytree-kernel launch when it is used, at most ``budget_bytes`` of pending deltas or
     ``max_clients`` (<= 4095) clients per launch (an older part of the chain is folded
     first when a limit would be passed, so memory stays bounded). Once the pending part
-    holds >= 256 MiB of deltas in >= 16 clients it is folded at the next ``tree_add``
+    holds >= 1 GiB of deltas in >= 16 clients it is folded at the next ``tree_add``
     (``flush_bytes`` / ``flush_clients``): that launch overlaps the rest of the caller's
     loop, and the deltas it covers are released. Any split gives the same bits. Disabled: every call is
     one fused launch (fjtree_fold_leaves), which also suits loops that update delta

@@ -433,7 +433,7 @@ def test_early_flush_of_the_running_sum(cuda, sum_mode):
         mean = tu.tree_inverse_weight(s, float(sum(ws)))
         return leaves_np(mean), [float(n) for n in norms]
 
-    base_mean, base_norms = loop()  # defaults: one fold (23 small clients < 256 MiB)
+    base_mean, base_norms = loop()  # defaults: one fold (23 small clients < 1 GiB)
     acc = tmap(lambda s: np.zeros(s, np.float32), shapes)
     for x, w in zip(xs, ws):
         acc = ref.tree_add(acc, ref.tree_weight(to_np(x), w))
@@ -445,7 +445,7 @@ def test_early_flush_of_the_running_sum(cuda, sum_mode):
         try:
             mean, norms = loop()
         finally:
-            tu.set_deferred_sums(True, flush_bytes=256 << 20, flush_clients=16)
+            tu.set_deferred_sums(True, flush_bytes=1 << 30, flush_clients=16)
         for a, b in zip(mean, want):
             assert np.array_equal(bits(a), bits(b)), (fb, fc)
         n64 = [float(np.sqrt(sum(float(np.dot(v.astype(np.float64), v.astype(np.float64)))

@@ -30,6 +30,8 @@ def rounds(deltas, weights, params, n):
 
 
 def main(K=128):
+    if len(sys.argv) > 1:  # flush_bytes of the deferred chain (tree_util.set_deferred_sums)
+        tu.set_deferred_sums(True, flush_bytes=int(sys.argv[1]))
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     deltas = [tmap(lambda s: torch.rand(s, device=dev, generator=g) - 0.5, SHAPES) for _ in range(K)]
@@ -38,7 +40,9 @@ def main(K=128):
     rounds(deltas, weights, params, 5)
     t0 = time.perf_counter()
     rounds(deltas, weights, params, 50)
-    print(f"round_ms {(time.perf_counter() - t0) / 50 * 1e3:.4f}", flush=True)
+    print(f"round_ms {(time.perf_counter() - t0) / 50 * 1e3:.4f} flush_bytes {tu._DEFER['flush_bytes']}", flush=True)
+    if os.environ.get("CPROF", "1") == "0":
+        return
     pr = cProfile.Profile()
     pr.enable()
     rounds(deltas, weights, params, 50)
