@@ -1207,6 +1207,170 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
   }
 }
 
+// server_pairs(pairs, params, m, v, mean_out, desc_addr, nt_min_bytes, plan_fn, update_fn)
+//   -> rc | None
+// server.fused_tree_mean_update for the common case in one native call: the pairs as in
+// mean_pairs (float32 CUDA deltas, Python-number weights, plain containers), and params /
+// m / v / mean_out (None where absent) trees of client 0's structure with contiguous float32
+// leaves of the deltas' shapes on the same device. Builds the plan image of
+// fjagg_server_update_ptrs (in_ptrs | params | leaf_n | blocks | f32 weights | m | v | mean;
+// per-leaf element units where a pointer is off 16 bytes), uploads it through pinned memory
+// and launches on the current stream. None: not this case (nothing launched).
+typedef int (*UpdFn)(int, const int64_t*, int, int64_t, int64_t, const float*, float, const void*, const int64_t*,
+                     int, void*);
+
+PyObject* server_pairs(PyObject*, PyObject* args) {
+  PyObject *pairs, *params, *mt, *vt, *mo;
+  double nt_min;
+  unsigned long long desc_addr, plan_addr, upd_addr;
+  if (!PyArg_ParseTuple(args, "OOOOOKdKK", &pairs, &params, &mt, &vt, &mo, &desc_addr, &nt_min, &plan_addr,
+                        &upd_addr))
+    return nullptr;
+  if (!PyList_CheckExact(pairs) && !PyTuple_CheckExact(pairs)) Py_RETURN_NONE;
+  const Py_ssize_t K = Py_SIZE(pairs);
+  if (K < 1) Py_RETURN_NONE;
+  PyObject* const* items = PyList_CheckExact(pairs) ? &PyList_GET_ITEM(pairs, 0) : &PyTuple_GET_ITEM(pairs, 0);
+  try {
+    struct Held {
+      std::vector<PyObject*> v;
+      ~Held() {
+        for (PyObject* o : v) Py_XDECREF(o);
+      }
+    } held;
+    held.v.assign(K, nullptr);
+    std::vector<PyObject*>& trees = held.v;
+    std::vector<float> wf(K);
+    double W = 0.0;
+    for (Py_ssize_t k = 0; k < K; ++k) {
+      PyObject* pr = items[k];
+      PyObject *t, *w;
+      if (PyTuple_CheckExact(pr) && PyTuple_GET_SIZE(pr) == 2) {
+        t = PyTuple_GET_ITEM(pr, 0);
+        w = PyTuple_GET_ITEM(pr, 1);
+      } else if (PyList_CheckExact(pr) && PyList_GET_SIZE(pr) == 2) {
+        t = PyList_GET_ITEM(pr, 0);
+        w = PyList_GET_ITEM(pr, 1);
+      } else {
+        Py_RETURN_NONE;
+      }
+      double d;
+      if (PyLong_CheckExact(w)) {
+        int overflow = 0;
+        long long iv = PyLong_AsLongLongAndOverflow(w, &overflow);
+        if (PyErr_Occurred()) PyErr_Clear();
+        if (overflow || iv >= (1LL << 53) || iv <= -(1LL << 53)) Py_RETURN_NONE;
+        d = static_cast<double>(iv);
+      } else if (PyFloat_CheckExact(w)) {
+        d = PyFloat_AS_DOUBLE(w);
+      } else {
+        Py_RETURN_NONE;
+      }
+      Py_INCREF(t);
+      trees[k] = t;
+      wf[k] = static_cast<float>(d);
+      W += d;  // tree_util.py:95
+    }
+    SpecBuild sb;
+    PyObject* spec = spec_of(trees[0], sb, 0);
+    if (!spec) {
+      if (PyErr_Occurred()) return nullptr;
+      Py_RETURN_NONE;
+    }
+    struct Ref {
+      PyObject* o;
+      ~Ref() { Py_DECREF(o); }
+    } spec_ref{spec};
+    const int64_t L = static_cast<int64_t>(sb.leaves.size());
+    if (L < 1) Py_RETURN_NONE;
+    std::vector<at::ScalarType> dtypes;
+    std::vector<c10::IntArrayRef> sizes;
+    std::vector<at::Tensor> row0;
+    int dev = -1;
+    for (PyObject* x : sb.leaves) {
+      const at::Tensor& t = THPVariable_Unpack(x);
+      if (t.layout() != c10::kStrided || !t.is_cuda() || t.scalar_type() != at::kFloat || !t.is_contiguous())
+        Py_RETURN_NONE;
+      if (dev < 0) dev = t.get_device();
+      if (t.get_device() != dev) Py_RETURN_NONE;
+      row0.push_back(t);
+    }
+    std::vector<int64_t> leaf_n(L);
+    int64_t total = 0;
+    for (int64_t l = 0; l < L; ++l) {
+      dtypes.push_back(at::kFloat);
+      sizes.push_back(row0[l].sizes());
+      leaf_n[l] = row0[l].numel();
+      total += leaf_n[l];
+    }
+    if (total == 0) Py_RETURN_NONE;
+    // params / state / mean_out leaves: client 0's structure, float32, contiguous, its shapes
+    Walk w{&dtypes, &sizes, static_cast<c10::DeviceIndex>(dev), nullptr, 0};
+    std::vector<int64_t> pp(L, 0), st(3 * L, 0);
+    PyObject* side[4] = {params, mt, vt, mo};
+    for (int i = 0; i < 4; ++i) {
+      if (side[i] == Py_None) {
+        if (i == 0) Py_RETURN_NONE;
+        continue;
+      }
+      w.out = i == 0 ? pp.data() : st.data() + (i - 1) * L;
+      w.leaf = 0;
+      const int r = walk(spec, side[i], w);
+      if (r < 0) return nullptr;
+      if (r > 0 || w.leaf != static_cast<size_t>(L)) Py_RETURN_NONE;
+    }
+    // every client's leaf pointers
+    std::vector<int64_t> ptrs(static_cast<size_t>(K * L));
+    for (int64_t l = 0; l < L; ++l) ptrs[l] = reinterpret_cast<int64_t>(row0[l].data_ptr());
+    for (Py_ssize_t k = 1; k < K; ++k) {
+      w.out = ptrs.data() + k * L;
+      w.leaf = 0;
+      const int r = walk(spec, trees[k], w);
+      if (r < 0) return nullptr;
+      if (r > 0 || w.leaf != static_cast<size_t>(L)) Py_RETURN_NONE;
+    }
+    // per-leaf element units where any pointer of the leaf is off 16 bytes
+    std::vector<uint8_t> elem(L, 0);
+    bool any_elem = false;
+    for (int64_t l = 0; l < L; ++l) {
+      int64_t bits = pp[l] | st[l] | st[L + l] | st[2 * L + l];
+      for (Py_ssize_t k = 0; k < K; ++k) bits |= ptrs[k * L + l];
+      elem[l] = (bits & 15) != 0;
+      any_elem = any_elem || elem[l];
+    }
+    auto plan = reinterpret_cast<PlanFn>(plan_addr);
+    const uint8_t* mask = any_elem ? elem.data() : nullptr;
+    const int64_t nblk = plan(kF32, 0, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);
+    if (nblk < 1) Py_RETURN_NONE;
+    const int64_t nw = (K + 1) / 2, n = K * L + 2 * L + 2 * nblk + nw + 3 * L;
+    at::Tensor img = at::empty({n}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+    int64_t* p = img.data_ptr<int64_t>();
+    std::memcpy(p, ptrs.data(), sizeof(int64_t) * K * L);
+    std::memcpy(p + K * L, pp.data(), sizeof(int64_t) * L);
+    std::memcpy(p + K * L + L, leaf_n.data(), sizeof(int64_t) * L);
+    if (plan(kF32, 0, leaf_n.data(), mask, static_cast<int>(L), p + K * L + 2 * L, nblk) != nblk) Py_RETURN_NONE;
+    int64_t* wp = p + K * L + 2 * L + 2 * nblk;
+    wp[nw - 1] = 0;
+    std::memcpy(wp, wf.data(), 4 * K);
+    std::memcpy(wp + nw, st.data(), sizeof(int64_t) * 3 * L);
+    at::Tensor dimg = img.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)), /*non_blocking=*/true);
+    const int64_t* dp = dimg.data_ptr<int64_t>();
+    const double job_bytes = 4.0 * static_cast<double>(total) * static_cast<double>(K);
+    const int flags = job_bytes >= nt_min ? kNontemporal : 0;
+    const float scale = static_cast<float>(W > 0.0 ? 1.0 / W : 0.0);  // tree_util.py:37,60
+    const unsigned long long stream =
+        reinterpret_cast<unsigned long long>(c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(dev)).stream());
+    const int rc = reinterpret_cast<UpdFn>(upd_addr)(kF32, dp, static_cast<int>(L), K, nblk,
+                                                      reinterpret_cast<const float*>(dp + K * L + 2 * L + 2 * nblk),
+                                                      scale, reinterpret_cast<const void*>(desc_addr),
+                                                      dp + K * L + 2 * L + 2 * nblk + nw, flags,
+                                                      reinterpret_cast<void*>(stream));
+    return PyLong_FromLong(rc);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 PyObject* image_paths(PyObject*, PyObject*) {
   return Py_BuildValue("{s:L,s:L}", "kernel_args", g_image_karg, "uploaded", g_image_upload);
 }
@@ -1243,6 +1407,7 @@ PyMethodDef kMethods[] = {
     {"leaf_fold", leaf_fold, METH_VARARGS, "fjtree_fold_leaves over 1-2 operand trees (see fjhost.cpp)"},
     {"fold_table", fold_table, METH_VARARGS, "plan image + output leaves + fjagg_wsum_ptrs launch (see fjhost.cpp)"},
     {"mean_pairs", mean_pairs, METH_VARARGS, "tree_mean of (pytree, weight) pairs in one native call (see fjhost.cpp)"},
+    {"server_pairs", server_pairs, METH_VARARGS, "fused_tree_mean_update in one native call (see fjhost.cpp)"},
     {nullptr, nullptr, 0, nullptr},
 };
 

@@ -230,6 +230,19 @@ def fused_mean_update(slab: ClientDeltaSlab, weights: Sequence, opt: ServerOptim
     return new
 
 
+_UPDATE_ADDRS = None
+
+
+def _update_addrs():
+    """(fjagg_ptrs_plan_leaves, fjagg_server_update_ptrs) addresses for fjhost.server_pairs."""
+    global _UPDATE_ADDRS
+    if _UPDATE_ADDRS is None:
+        lib = _lib.load()
+        _UPDATE_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
+                              for f in ("fjagg_ptrs_plan_leaves", "fjagg_server_update_ptrs"))
+    return _UPDATE_ADDRS
+
+
 def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, state: dict, *,
                            mean_out=None, nontemporal: Optional[bool] = None) -> dict:
     """:func:`fused_mean_update` on the pytree path: ``tree_mean`` of the clients' delta
@@ -251,6 +264,19 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
         elif mean is None:
             raise ValueError("no clients to aggregate")
         return opt.apply(mean, state, params)[0]
+    if (not opt.frozen and nontemporal is None and type(pytrees_and_weights) in (list, tuple)
+            and pytrees_and_weights):
+        # the common case in one native call (fjhost.server_pairs): same image, same launch
+        count = state["count"] + 1
+        desc = opt.descriptor(count)
+        rc = _lib.host().server_pairs(pytrees_and_weights, params, state.get("m"), state.get("v"), mean_out,
+                                      ctypes.addressof(desc), float(tree_util.NONTEMPORAL_MIN_BYTES),
+                                      *_update_addrs())
+        if rc is not None:
+            _lib.check(rc, "fjagg_server_update_ptrs")
+            new = dict(state)
+            new["count"] = count
+            return new
     trees, weights, W = tree_util._collect_pairs(pytrees_and_weights)
     if not trees:
         raise ValueError("no clients to aggregate")

@@ -138,3 +138,38 @@ def test_learning_rate_schedule(make, cuda, coracle):
         gm = coracle.wsum_f32(xh, np.float32(wi), scale=ref.mean_scale(wi))
         p_np, m_np, v_np = _np_server_step(opt, d, gm, p_np, m_np, v_np)
         assert np.array_equal(bits(host(params)), bits(p_np)), rnd
+
+
+@pytest.mark.parametrize("make", [lambda s: s.adam(1e-3), lambda s: s.sgd(0.1, momentum=0.9),
+                                  lambda s: s.rmsprop(0.01, centered=True)])
+def test_native_server_step_equals_python_path(make, cuda):
+    """fused_tree_mean_update's one-call native path (fjhost.server_pairs) against the Python
+    path (taken when ``nontemporal`` is given; the cache policy changes no bits): params,
+    state and mean_out bitwise, with a leaf at a 4-byte offset (element units) and float
+    weights among ints."""
+    opt = make(server)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    K = 9
+    slab = torch.rand(K, 70_001 + 129, device="cuda", generator=g) - 0.5
+    clients = [{"a": slab[k, 1:70_001].view(7, 10_000), "b": {"c": slab[k, 70_001:70_129]}} for k in range(K)]
+    weights = [3, 1.5, 4, 1, 5, 9, 2, 6, 5]
+    pairs = list(zip(clients, weights))
+    p0 = {"a": torch.randn(7, 10_000, device="cuda", generator=g), "b": {"c": torch.randn(128, device="cuda",
+                                                                                         generator=g)}}
+    runs = []
+    for nt in (None, False):
+        params = {"a": p0["a"].clone(), "b": {"c": p0["b"]["c"].clone()}}
+        st = opt.init(params)
+        mo = {"a": torch.empty_like(p0["a"]), "b": {"c": torch.empty_like(p0["b"]["c"])}}
+        for _ in range(3):
+            st = server.fused_tree_mean_update(pairs, opt, params, st, mean_out=mo, nontemporal=nt)
+        runs.append((params, st, mo))
+    (pa, sa, ma), (pb, sb, mb) = runs
+    assert sa["count"] == sb["count"] == 3
+    leaves = lambda t: [host(x) for x in fedjax_amd.pytree.leaves_of(t)]
+    for x, y in zip(leaves(pa) + leaves(ma), leaves(pb) + leaves(mb)):
+        npt.assert_array_equal(bits(x), bits(y))
+    for key in ("m", "v"):
+        if key in sa:
+            for x, y in zip(leaves(sa[key]), leaves(sb[key])):
+                npt.assert_array_equal(bits(x), bits(y))
