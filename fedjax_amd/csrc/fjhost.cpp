@@ -1056,7 +1056,10 @@ double now_s() {
 }
 
 // mean_pairs(pairs, may_pipeline, frac, chunk, chunk_walk_us, walk_ns_per_leaf, min_bytes,
-//            narrow_max, nt_min_bytes, plan_fn, wsum_fn) -> (rc, tree, job_bytes) | None
+//            narrow_max, nt_min_bytes, plan_fn, wsum_fn[, wsum_l2_fn, l2_ws_bytes_fn])
+//   -> (rc, tree, job_bytes, l2sq | None) | None
+// With the l2 entry points every client's squared l2 norm over all leaves comes from the
+// launch that folds it (fjagg_wsum_l2_ptrs; K <= 4096, the caller checks).
 // may_pipeline: the caller's host-side estimate says the stream may be idle (then the
 // stream is probed). The chunking is tree_util._pipeline_bounds's.
 PyObject* mean_pairs(PyObject*, PyObject* args) {
@@ -1064,10 +1067,11 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
   int may_pipeline;
   double frac, chunk_walk_us, walk_ns, nt_min;
   long long chunk, min_bytes, narrow_max;
-  unsigned long long plan_addr, wsum_addr;
-  if (!PyArg_ParseTuple(args, "OpdLddLLdKK", &pairs, &may_pipeline, &frac, &chunk, &chunk_walk_us, &walk_ns,
-                        &min_bytes, &narrow_max, &nt_min, &plan_addr, &wsum_addr))
+  unsigned long long plan_addr, wsum_addr, l2_addr = 0, l2ws_addr = 0;
+  if (!PyArg_ParseTuple(args, "OpdLddLLdKK|KK", &pairs, &may_pipeline, &frac, &chunk, &chunk_walk_us, &walk_ns,
+                        &min_bytes, &narrow_max, &nt_min, &plan_addr, &wsum_addr, &l2_addr, &l2ws_addr))
     return nullptr;
+  const bool with_l2 = l2_addr != 0 && l2ws_addr != 0;  // tree_mean_with_l2_norms: + every client's l2sq
   if (!PyList_CheckExact(pairs) && !PyTuple_CheckExact(pairs)) Py_RETURN_NONE;
   const Py_ssize_t K = Py_SIZE(pairs);
   if (K < 1) Py_RETURN_NONE;
@@ -1175,6 +1179,8 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
     const double scale = W > 0.0 ? 1.0 / W : 0.0;  // tree_util.py:37,60
     const double ntm = job_bytes >= nt_min ? 0.0 : HUGE_VAL;  // the whole job's bytes decide
     std::vector<at::Tensor> outs;
+    at::Tensor l2sq;  // float32 [K] (with_l2): client k's squared norm from the launch that folds it
+    if (with_l2) l2sq = at::empty({K}, row0[0].options());
     int64_t done = 0;
     int rc = 0;
     for (int64_t k1 : bounds) {
@@ -1188,9 +1194,11 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
       const bool last = k1 == K;
       if (fold_core(row0, ptrs.data() + done * L, k1 - done, wf.data() + done, last ? scale : 1.0, last, ntm, dev,
                     stream, reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs,
-                    !outs.empty(), nullptr, nullptr, nullptr, &rc, st) != 0)
+                    !outs.empty(), with_l2 ? reinterpret_cast<WsumL2Fn>(l2_addr) : nullptr,
+                    with_l2 ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr,
+                    with_l2 ? l2sq.data_ptr<float>() + done : nullptr, &rc, st) != 0)
         Py_RETURN_NONE;
-      if (rc != 0) return Py_BuildValue("(iOd)", rc, Py_None, job_bytes);
+      if (rc != 0) return Py_BuildValue("(iOdO)", rc, Py_None, job_bytes, Py_None);
       done = k1;
     }
     std::vector<PyObject*> wrapped(L);
@@ -1200,7 +1208,12 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
     for (PyObject* o : wrapped) Py_XDECREF(o);  // (rebuild took the ones it used)
     if (!tree) return nullptr;
     st.lap(kTWrap);
-    return Py_BuildValue("(iNd)", rc, tree, job_bytes);
+    PyObject* l2 = with_l2 ? THPVariable_Wrap(std::move(l2sq)) : (Py_INCREF(Py_None), Py_None);
+    if (!l2) {
+      Py_DECREF(tree);
+      return nullptr;
+    }
+    return Py_BuildValue("(iNdN)", rc, tree, job_bytes, l2);
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;

@@ -1102,19 +1102,22 @@ _BUSY_UNTIL = [0.0]  # perf_counter() time before which this module's issued fol
 _NATIVE_MEAN = os.environ.get("FJAGG_NATIVE_MEAN", "1") != "0"
 
 
-def _native_mean(pairs) -> Optional[PyTree]:
+def _native_mean(pairs, with_l2: bool = False):
+    """fjhost.mean_pairs: the tree (with_l2: (tree, l2sq)), or None when not its case."""
     if _ENTRY_ADDRS is None:
         _native_fold_addrs()
     now = time.perf_counter()
+    extra = (_ENTRY_ADDRS[2], _ENTRY_ADDRS[3]) if with_l2 else ()
     got = _lib.host().mean_pairs(pairs, _PIPELINE_FRAC > 0.0 and now >= _BUSY_UNTIL[0], _PIPELINE_FRAC,
                                  _PIPELINE_CHUNK, _CHUNK_WALK_US, _WALK_NS_PER_LEAF, _PIPELINE_MIN_BYTES,
-                                 _NARROW_MAX_BYTES, float(NONTEMPORAL_MIN_BYTES), _ENTRY_ADDRS[0], _ENTRY_ADDRS[1])
+                                 _NARROW_MAX_BYTES, float(NONTEMPORAL_MIN_BYTES), _ENTRY_ADDRS[0], _ENTRY_ADDRS[1],
+                                 *extra)
     if got is None:
         return None
-    rc, tree, job_bytes = got
+    rc, tree, job_bytes, l2sq = got
     _BUSY_UNTIL[0] = max(now, _BUSY_UNTIL[0]) + job_bytes / _PEAK_BYTES_PER_S
-    _lib.check(rc, "fjagg_wsum_ptrs")
-    return tree
+    _lib.check(rc, "fjagg_wsum_l2_ptrs" if with_l2 else "fjagg_wsum_ptrs")
+    return (tree, l2sq) if with_l2 else tree
 
 
 def _stream_idle(stream: torch.cuda.Stream) -> bool:
@@ -1301,6 +1304,11 @@ def tree_mean_with_l2_norms(pytrees_and_weights: Iterable[Tuple[PyTree, float]])
     The mean is bitwise :func:`tree_mean`'s. The norms (float32 [K] on the device) sum
     squares in f32 in a fixed order; float leaves of one dtype.
     Returns ``(None, None)`` for no clients."""
+    if (_NATIVE_MEAN and type(pytrees_and_weights) in (list, tuple)
+            and 0 < len(pytrees_and_weights) <= _L2_MAX_CLIENTS):
+        got = _native_mean(pytrees_and_weights, with_l2=True)
+        if got is not None:
+            return got[0], torch.sqrt(got[1])
     trees, weights, sum_weight = _collect_pairs(pytrees_and_weights)
     if not trees:
         return None, None

@@ -191,3 +191,21 @@ def test_native_whole_call_equals_python_path(frac, cuda, monkeypatch):
     bad[9] = ({"v": r(80_000)}, 1)
     with pytest.raises(ValueError):
         tu.tree_mean(bad)
+
+
+def test_native_mean_with_l2_norms_equals_python_path(frac, cuda, monkeypatch):
+    """tree_mean_with_l2_norms through fjhost.mean_pairs (one launch, or the pipelined
+    chunks, each giving its clients' norms) against the Python path: mean and norms bitwise."""
+    K = 40
+    pairs = list(zip(_clients(K, seed=9), [1 + (k % 7) for k in range(K)]))
+    monkeypatch.setattr(tu, "_NATIVE_MEAN", False)
+    want_mean, want_norms = tu.tree_mean_with_l2_norms(pairs)
+    monkeypatch.setattr(tu, "_NATIVE_MEAN", True)
+    for f in (0.0, 0.3):
+        frac(f)
+        torch.cuda.synchronize()
+        n0 = _launches()
+        mean, norms = tu.tree_mean_with_l2_norms(pairs)
+        assert _launches() - n0 == (1 if f == 0.0 else 2)
+        np.testing.assert_array_equal(_flat(mean).view(np.uint32), _flat(want_mean).view(np.uint32))
+        np.testing.assert_array_equal(norms.cpu().numpy().view(np.uint32), want_norms.cpu().numpy().view(np.uint32))
