@@ -1091,35 +1091,43 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
     std::vector<PyObject*>& trees = held.v;
     std::vector<float> wf(K);
     double W = 0.0;
-    for (Py_ssize_t k = 0; k < K; ++k) {  // `for pytree, weight in pytrees_and_weights` (tree_util.py:89)
-      PyObject* pr = items[k];
-      PyObject *t, *w;
-      if (PyTuple_CheckExact(pr) && PyTuple_GET_SIZE(pr) == 2) {
-        t = PyTuple_GET_ITEM(pr, 0);
-        w = PyTuple_GET_ITEM(pr, 1);
-      } else if (PyList_CheckExact(pr) && PyList_GET_SIZE(pr) == 2) {
-        t = PyList_GET_ITEM(pr, 0);
-        w = PyList_GET_ITEM(pr, 1);
-      } else {
-        Py_RETURN_NONE;
+    // pairs [parsed, k1) -> trees, f32 weights, W (tree_util.py:89,95, in order); parsed
+    // chunk by chunk, so the first launch does not wait for the whole list. false: a pair
+    // or weight this path does not take (the caller's Python path then does)
+    Py_ssize_t parsed = 0;
+    auto parse = [&](Py_ssize_t k1) {
+      for (; parsed < k1; ++parsed) {  // `for pytree, weight in pytrees_and_weights`
+        PyObject* pr = items[parsed];
+        PyObject *t, *w;
+        if (PyTuple_CheckExact(pr) && PyTuple_GET_SIZE(pr) == 2) {
+          t = PyTuple_GET_ITEM(pr, 0);
+          w = PyTuple_GET_ITEM(pr, 1);
+        } else if (PyList_CheckExact(pr) && PyList_GET_SIZE(pr) == 2) {
+          t = PyList_GET_ITEM(pr, 0);
+          w = PyList_GET_ITEM(pr, 1);
+        } else {
+          return false;
+        }
+        double d;
+        if (PyLong_CheckExact(w)) {
+          int overflow = 0;
+          long long v = PyLong_AsLongLongAndOverflow(w, &overflow);
+          if (PyErr_Occurred()) PyErr_Clear();
+          if (overflow || v >= (1LL << 53) || v <= -(1LL << 53)) return false;
+          d = static_cast<double>(v);
+        } else if (PyFloat_CheckExact(w)) {
+          d = PyFloat_AS_DOUBLE(w);
+        } else {
+          return false;
+        }
+        Py_INCREF(t);
+        trees[parsed] = t;
+        wf[parsed] = static_cast<float>(d);
+        W += d;  // tree_util.py:95
       }
-      double d;
-      if (PyLong_CheckExact(w)) {
-        int overflow = 0;
-        long long v = PyLong_AsLongLongAndOverflow(w, &overflow);
-        if (PyErr_Occurred()) PyErr_Clear();
-        if (overflow || v >= (1LL << 53) || v <= -(1LL << 53)) Py_RETURN_NONE;
-        d = static_cast<double>(v);
-      } else if (PyFloat_CheckExact(w)) {
-        d = PyFloat_AS_DOUBLE(w);
-      } else {
-        Py_RETURN_NONE;
-      }
-      Py_INCREF(t);
-      trees[k] = t;
-      wf[k] = static_cast<float>(d);
-      W += d;  // tree_util.py:95
-    }
+      return true;
+    };
+    if (!parse(1)) Py_RETURN_NONE;
     SpecBuild sb;
     PyObject* spec = spec_of(trees[0], sb, 0);
     if (!spec) {
@@ -1176,7 +1184,6 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
     std::vector<int64_t> ptrs(static_cast<size_t>(K * L));
     for (int64_t l = 0; l < L; ++l) ptrs[l] = reinterpret_cast<int64_t>(row0[l].data_ptr());
     Walk w{&dtypes, &sizes, static_cast<c10::DeviceIndex>(dev), nullptr, 0};
-    const double scale = W > 0.0 ? 1.0 / W : 0.0;  // tree_util.py:37,60
     const double ntm = job_bytes >= nt_min ? 0.0 : HUGE_VAL;  // the whole job's bytes decide
     std::vector<at::Tensor> outs;
     at::Tensor l2sq;  // float32 [K] (with_l2): client k's squared norm from the launch that folds it
@@ -1184,6 +1191,7 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
     int64_t done = 0;
     int rc = 0;
     for (int64_t k1 : bounds) {
+      if (!parse(k1)) Py_RETURN_NONE;
       for (int64_t k = std::max<int64_t>(done, 1); k < k1; ++k) {
         w.out = ptrs.data() + k * L;
         w.leaf = 0;
@@ -1191,8 +1199,9 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
         if (r < 0) return nullptr;
         if (r > 0 || w.leaf != static_cast<size_t>(L)) Py_RETURN_NONE;
       }
-      const bool last = k1 == K;
-      if (fold_core(row0, ptrs.data() + done * L, k1 - done, wf.data() + done, last ? scale : 1.0, last, ntm, dev,
+      const bool last = k1 == K;  // (then every weight is parsed: W is complete)
+      const double scale = last ? (W > 0.0 ? 1.0 / W : 0.0) : 1.0;  // tree_util.py:37,60
+      if (fold_core(row0, ptrs.data() + done * L, k1 - done, wf.data() + done, scale, last, ntm, dev,
                     stream, reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs,
                     !outs.empty(), with_l2 ? reinterpret_cast<WsumL2Fn>(l2_addr) : nullptr,
                     with_l2 ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr,

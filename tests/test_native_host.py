@@ -128,3 +128,30 @@ def test_leaf_versions_track_in_place_updates():
     assert H.leaf_versions(trees, spec, L, v1) == -3
     with pytest.raises(ValueError):
         H.leaf_versions(trees, spec, L, np.empty(2, dtype=np.int64))
+
+
+def _mean_pairs(pairs):
+    """fjhost.mean_pairs with the tree_util knobs; plan / launch addresses are never
+    reached on the host (every case here declines first)."""
+    return _lib.host().mean_pairs(pairs, False, 0.25, 512, 60.0, 35.0, 64 << 20, 256 << 10, float(256 << 20), 0, 0)
+
+
+@pytest.mark.parametrize("pairs", [
+    [],                                                                 # no clients
+    [({"w": torch.zeros(5)}, 1)] * 3,                                   # host tensors
+    [({"w": torch.zeros(5)}, np.float32(1))] * 3,                       # a numpy weight
+    [({"w": torch.zeros(5)}, True)] * 3,                                # a bool weight
+    [({"w": torch.zeros(5)}, 2 ** 60)] * 3,                             # a weight past 2**53
+    [({"w": torch.zeros(5)},)] * 3,                                     # not a pair
+    [({1: torch.zeros(5), "a": torch.zeros(5)}, 1)] * 3,                # unorderable dict keys
+    [(collections.OrderedDict(w=torch.zeros(5)), 1)] * 3,              # a node kind it does not take
+    [({"w": np.zeros(5, np.float32)}, 1)] * 3,                          # a numpy leaf
+    [({"w": None}, 1)] * 3,                                             # no leaves
+])
+def test_native_whole_call_declines(pairs):
+    """tree_mean's one-call native path (fjhost.mean_pairs) answers None, launching
+    nothing and raising nothing, for every input it does not take: the Python path then
+    runs (and raises the reference's errors where there are any)."""
+    assert _mean_pairs(pairs) is None
+    assert _mean_pairs(tuple(pairs)) is None
+    assert _lib.host().server_pairs(pairs, {"w": torch.zeros(5)}, None, None, None, 0, 0.0, 0, 0) is None
