@@ -522,6 +522,67 @@ struct PWalk {
   }
 };
 
+// The sorted key list of dict x (a new reference, or nullptr with *unorderable set when
+// sorting raised — the error is cleared — or with a Python error set). Per-call tree ops
+// walk one client pytree after another, every one a dict with the same key objects in the
+// same insertion order: a small cache keyed by those key pointers (held by strong
+// references, so a pointer is never a reused address) gives the sorted list without a
+// PyDict_Keys + sort per dict node per call. Guarded by the GIL like every entry point.
+PyObject* sorted_keys(PyObject* x, bool* unorderable) {
+  struct Entry {
+    std::vector<PyObject*> order;  // strong references, insertion order
+    PyObject* sorted;              // strong reference
+  };
+  static std::vector<Entry> cache;
+  static size_t next_slot = 0;
+  constexpr size_t kCap = 64;
+  *unorderable = false;
+  const Py_ssize_t n = PyDict_GET_SIZE(x);
+  for (const Entry& e : cache) {
+    if (static_cast<Py_ssize_t>(e.order.size()) != n) continue;
+    Py_ssize_t pos = 0, i = 0;
+    PyObject *k, *v;
+    bool same = true;
+    while (PyDict_Next(x, &pos, &k, &v)) {
+      if (k != e.order[i++]) {
+        same = false;
+        break;
+      }
+    }
+    if (same) {
+      Py_INCREF(e.sorted);
+      return e.sorted;
+    }
+  }
+  PyObject* keys = PyDict_Keys(x);
+  if (!keys) return nullptr;
+  if (PyList_Sort(keys) != 0) {
+    PyErr_Clear();
+    Py_DECREF(keys);
+    *unorderable = true;
+    return nullptr;
+  }
+  Entry e;
+  Py_ssize_t pos = 0;
+  PyObject *k, *v;
+  while (PyDict_Next(x, &pos, &k, &v)) {
+    Py_INCREF(k);
+    e.order.push_back(k);
+  }
+  Py_INCREF(keys);
+  e.sorted = keys;
+  if (cache.size() < kCap) {
+    cache.push_back(std::move(e));
+  } else {  // replace round-robin
+    Entry& old = cache[next_slot];
+    for (PyObject* o : old.order) Py_DECREF(o);
+    Py_DECREF(old.sorted);
+    old = std::move(e);
+    next_slot = (next_slot + 1) % kCap;
+  }
+  return keys;
+}
+
 // 0: walked; 1: not the fast case / structures differ; -1: Python error set.
 int pwalk(PyObject* const* xs, PWalk& w, int depth) {
   if (depth > 64) return 1;
@@ -546,13 +607,10 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
     const Py_ssize_t n = PyDict_GET_SIZE(x0);
     for (int k = 1; k < K; ++k)
       if (!PyDict_CheckExact(xs[k]) || PyDict_GET_SIZE(xs[k]) != n) return 1;
-    PyObject* keys = PyDict_Keys(x0);
-    if (!keys) return -1;
+    bool unorderable = false;
+    PyObject* keys = sorted_keys(x0, &unorderable);
+    if (!keys) return unorderable ? 1 : -1;  // unorderable keys: the Python path decides
     w.keys.push_back(keys);
-    if (PyList_Sort(keys) != 0) {  // unorderable keys: the Python path decides
-      PyErr_Clear();
-      return 1;
-    }
     for (Py_ssize_t i = 0; i < n; ++i) {
       PyObject* key = PyList_GET_ITEM(keys, i);
       for (int k = 0; k < K; ++k) {
@@ -1020,13 +1078,10 @@ PyObject* spec_of(PyObject* x, SpecBuild& b, int depth) {
   PyObject* keys = nullptr;
   Py_ssize_t n;
   if (is_dict) {
-    keys = PyDict_Keys(x);
-    if (!keys) return nullptr;
+    bool unorderable = false;
+    keys = sorted_keys(x, &unorderable);
+    if (!keys) return nullptr;  // (unorderable keys: no error set, the Python path decides)
     b.keys.push_back(keys);
-    if (PyList_Sort(keys) != 0) {  // unorderable keys: the Python path decides
-      PyErr_Clear();
-      return nullptr;
-    }
     n = PyList_GET_SIZE(keys);
   } else {
     n = Py_SIZE(x);
