@@ -517,6 +517,7 @@ struct PWalk {
   int K = 0;
   std::vector<PyObject*> leaves[FJTREE_MAX_OPERANDS];  // borrowed, flatten order
   std::vector<PyObject*> keys;                         // owned sorted key lists, pre-order
+  std::vector<int64_t>* sig = nullptr;  // optional: operand 0's structure (kinds, lengths, key objects)
   ~PWalk() {
     for (PyObject* k : keys) Py_DECREF(k);
   }
@@ -595,11 +596,13 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
       if (w.leaves[k].size() >= FJTREE_MAX_LEAVES) return 1;
       w.leaves[k].push_back(xs[k]);
     }
+    if (w.sig) w.sig->push_back(kLeaf);
     return 0;
   }
   if (x0 == Py_None) {
     for (int k = 1; k < K; ++k)
       if (xs[k] != Py_None) return 1;
+    if (w.sig) w.sig->push_back(kNone);
     return 0;
   }
   PyObject* vals[FJTREE_MAX_OPERANDS];
@@ -611,6 +614,11 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
     PyObject* keys = sorted_keys(x0, &unorderable);
     if (!keys) return unorderable ? 1 : -1;  // unorderable keys: the Python path decides
     w.keys.push_back(keys);
+    if (w.sig) {
+      w.sig->push_back(kDict);
+      w.sig->push_back(n);
+      for (Py_ssize_t i = 0; i < n; ++i) w.sig->push_back(reinterpret_cast<int64_t>(PyList_GET_ITEM(keys, i)));
+    }
     for (Py_ssize_t i = 0; i < n; ++i) {
       PyObject* key = PyList_GET_ITEM(keys, i);
       for (int k = 0; k < K; ++k) {
@@ -629,6 +637,10 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
   const Py_ssize_t n = Py_SIZE(x0);
   for (int k = 1; k < K; ++k)
     if (Py_TYPE(xs[k]) != Py_TYPE(x0) || Py_SIZE(xs[k]) != n) return 1;
+  if (w.sig) {
+    w.sig->push_back(is_list ? kList : kTuple);
+    w.sig->push_back(n);
+  }
   for (Py_ssize_t i = 0; i < n; ++i) {
     for (int k = 0; k < K; ++k) vals[k] = is_list ? PyList_GET_ITEM(xs[k], i) : PyTuple_GET_ITEM(xs[k], i);
     if (int rc = pwalk(vals, w, depth + 1)) return rc;
@@ -740,16 +752,45 @@ typedef int (*TreeFoldFn)(const fjtree_leaves*, void*);
 typedef int64_t (*TreeWsFn)(const fjtree_leaves*);
 constexpr int kStale = -100;
 
-// capture(tree, dev) -> (leaves_tuple, version_sum, nbytes) | None   (dev = -1: the first leaf's)
+struct SigHash {
+  size_t operator()(const std::vector<int64_t>& v) const {
+    uint64_t h = 1469598103934665603ull;
+    for (int64_t x : v) h = (h ^ static_cast<uint64_t>(x)) * 1099511628211ull;
+    return static_cast<size_t>(h ^ (h >> 29));
+  }
+};
+
+// The structure token of a captured tree: equal tokens <=> the same node kinds, lengths,
+// dict key OBJECTS (in sorted order), device and leaf shapes. Interned per process; the
+// table holds strong references to the key objects, so a key's address is never reused
+// while its entry exists. -1 once the table is full (the caller then walks both trees).
+int64_t structure_token(const std::vector<int64_t>& sig, const PWalk& w) {
+  static auto* table = new std::unordered_map<std::vector<int64_t>, int64_t, SigHash>();
+  constexpr size_t kMaxTokens = 4096;
+  auto it = table->find(sig);
+  if (it != table->end()) return it->second;
+  if (table->size() >= kMaxTokens) return -1;
+  for (PyObject* kl : w.keys)  // keep the key objects alive for as long as the entry exists
+    for (Py_ssize_t i = 0; i < PyList_GET_SIZE(kl); ++i) Py_INCREF(PyList_GET_ITEM(kl, i));
+  const int64_t tok = static_cast<int64_t>(table->size());
+  table->emplace(sig, tok);
+  return tok;
+}
+
+// capture(tree, dev) -> (leaves_tuple, version_sum, nbytes, token) | None   (dev = -1: the first leaf's)
 //     tree_weight's lazy result holds its input's leaves (strong references, flatten order)
-//     and their version sum, so tree_add can check that nothing changed in between.
+//     and their version sum, so the fold can check that nothing changed in between; token
+//     (structure_token) lets tree_add match two captured trees' structures without a walk.
 PyObject* capture(PyObject*, PyObject* args) {
   PyObject* tree;
   int dev;
   if (!PyArg_ParseTuple(args, "Oi", &tree, &dev)) return nullptr;
   try {
+    thread_local std::vector<int64_t> sig;
+    sig.clear();
     PWalk w;
     w.K = 1;
+    w.sig = &sig;
     int rc = pwalk(&tree, w, 0);
     if (rc < 0) return nullptr;
     int64_t vs = 0;
@@ -766,12 +807,18 @@ PyObject* capture(PyObject*, PyObject* args) {
     PyObject* tup = PyTuple_New(L);
     if (!tup) return nullptr;
     int64_t nbytes = 0;
+    sig.push_back(dev);
     for (Py_ssize_t l = 0; l < L; ++l) {
       Py_INCREF(w.leaves[0][l]);
       PyTuple_SET_ITEM(tup, l, w.leaves[0][l]);
-      nbytes += 4 * THPVariable_Unpack(w.leaves[0][l]).numel();
+      const at::Tensor& t = THPVariable_Unpack(w.leaves[0][l]);
+      nbytes += 4 * t.numel();
+      sig.push_back(t.dim());
+      for (int64_t s : t.sizes()) sig.push_back(s);
     }
-    return Py_BuildValue("(NLL)", tup, static_cast<long long>(vs), static_cast<long long>(nbytes));
+    const int64_t tok = structure_token(sig, w);
+    return Py_BuildValue("(NLLL)", tup, static_cast<long long>(vs), static_cast<long long>(nbytes),
+                         static_cast<long long>(tok));
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;

@@ -601,8 +601,13 @@ class WeightedTree:
     other use computes it: indexing, iteration, attribute access and every pytree walk of
     this package (``pytree.flatten``, ``tree_util.*``) see the weighted pytree itself, and
     ``materialize()`` returns it. The input's leaf objects and their in-place versions are
-    captured at ``tree_weight``: if a leaf is replaced or modified before the weighted
-    value is used, using it raises RuntimeError (the reference's arrays are immutable).
+    captured at ``tree_weight``. A deferred running sum (``tree_add`` into a sum of the
+    same structure) takes the captured leaves, so a leaf replaced in the input afterwards
+    does not change the sum — the value the reference's eager tree_weight computed; a
+    captured leaf modified in place makes the sum's fold raise RuntimeError. Any other use
+    (including ``tree_add`` with deferral off)
+    raises RuntimeError when a leaf was replaced or modified in between (the reference's
+    arrays are immutable).
     The guard is torch's in-place version counter: writes that bypass it (through
     ``tensor.data``, or by native code writing the tensor's memory) are not seen, and the
     deferred multiply then reads the new values. Inference tensors, which have no version
@@ -785,7 +790,7 @@ class PendingSum:
     ``delta_l2_norm`` of fed_avg.py:142-144 without another pass over the delta.
 
     The deltas stay referenced until the fold (bounded by :func:`set_deferred_sums`). A
-    delta modified in place after it was added makes the fold raise RuntimeError (the
+    delta modified in place after its tree_weight makes the fold raise RuntimeError (the
     reference's arrays are immutable); loops that reuse delta buffers should call
     ``set_deferred_sums(False)``. The check is torch's in-place version counter, so a
     write that bypasses it — through ``tensor.data``, or by native code / a kernel writing
@@ -796,12 +801,13 @@ class PendingSum:
     """
 
     __slots__ = ("_root", "_parent", "_cap", "_weight", "_n", "_bytes", "_value", "_chain", "_idx", "_ticket",
-                 "_ref", "_bcap", "__weakref__")
+                 "_ref", "_bcap", "_tok", "__weakref__")
 
-    def __init__(self, root, parent, cap, weight, ref, bcap=None):
+    def __init__(self, root, parent, cap, weight, ref, bcap=None, tok=-1):
         self._root, self._parent, self._cap, self._weight, self._value = root, parent, cap, weight, None
         self._ref = ref  # a tree with the sum's structure (the chain's base): O(1) structure checks
         self._bcap = bcap  # capture of the base tree when this link starts a run (parent not pending)
+        self._tok = tok  # the sum's structure token (fjhost.capture), -1 if unknown
         self._ticket = None
         live = parent is not None and parent._value is None
         self._n = 1 + (parent._n if live else 0)
@@ -873,8 +879,8 @@ def _fold_chain(base, links, scale):
                            "Call fedjax_amd.tree_util.set_deferred_sums(False) for loops that do this")
     if bad > 0:
         raise RuntimeError(f"client {bad - 1} of a pending tree_add sum was modified (a leaf updated in place) "
-                           "after it was added; the reference sums each delta's value at tree_add. Add "
-                           "copies, or call fedjax_amd.tree_util.set_deferred_sums(False)")
+                           "after its tree_weight / tree_add; the reference sums each delta's value at that "
+                           "call. Add copies, or call fedjax_amd.tree_util.set_deferred_sums(False)")
     packed = _pack_weights([1] + [n._weight for n in links])
     waiting = [n for n in links if n._ticket is not None and n._ticket.node is not None]
     l2sq = None
@@ -919,32 +925,46 @@ def _lazy_norm(pytree_, row: int):
 
 
 def _defer(sum_side, item, item_weight, item_cap):
-    """PendingSum for tree_add(sum_side, weighted item), or None when not applicable."""
+    """PendingSum for tree_add(sum_side, weighted item), or None when not applicable.
+
+    When the item comes from tree_weight (``item_cap``, its capture) and the sum's structure
+    token equals the capture's, the structures and leaf shapes are known to match without a
+    walk: the link holds the captured leaves — the values tree_weight saw, as the
+    reference's eager tree_weight would — and the fold checks their versions. Otherwise
+    ``fjhost.append_check`` walks the sum and the item together."""
     global _LAST
+    host = _HOST if _HOST is not None else _lib.host()
     if type(sum_side) is PendingSum:
         parent, root = sum_side, None
-        ref = sum_side._value if sum_side._value is not None else sum_side._ref
+        live = sum_side._value is None
+        ref = sum_side._ref if live else sum_side._value
     else:
-        ref, parent, root = sum_side, None, sum_side
-    host = _HOST if _HOST is not None else _lib.host()
-    cap = host.append_check(ref, item, item_cap)
-    if cap is None:
-        return None
-    if type(cap) is int:
-        raise RuntimeError("a pytree passed to tree_weight was modified (a leaf replaced or updated in "
-                           "place) before its weighted value was used; the reference computes "
-                           "tree_weight eagerly")
-    if parent is not None and parent._value is None:
+        ref, parent, root, live = sum_side, None, sum_side, False
+    bcap = None
+    if live:
+        tok = parent._tok
+    else:  # this link starts a run: capture its base (its leaves, versions and structure token)
+        bcap = host.capture(ref, -1)
+        tok = bcap[3] if bcap is not None else -1
+    if item_cap is not None and tok >= 0 and item_cap[3] == tok:
+        cap = item_cap
+    else:
+        cap = host.append_check(ref, item, item_cap)
+        if cap is None:
+            return None
+        if type(cap) is int:
+            raise RuntimeError("a pytree passed to tree_weight was modified (a leaf replaced or updated in "
+                               "place) before its weighted value was used; the reference computes "
+                               "tree_weight eagerly")
+    if live:
         budget = parent._chain.budget
         if budget is None:
             budget = parent._chain.budget = _defer_budget(cap[0][0].device)
         if (parent._n + 1 > _DEFER["max_clients"] or parent._bytes + cap[2] > budget or
                 (parent._bytes >= _DEFER["flush_bytes"] and parent._n >= _DEFER["flush_clients"])):
             parent.materialize()  # bound the chain: fold what is pending, continue from it
-    bcap = None
-    if parent is None or parent._value is not None:  # this link starts a run: capture its base
-        bcap = host.capture(root if parent is None else parent._value, -1)
-    node = PendingSum(root, parent, cap, item_weight, ref, bcap)
+            bcap = host.capture(parent._value, -1)
+    node = PendingSum(root, parent, cap, item_weight, ref, bcap, tok)
     _LAST = weakref.ref(node)
     return node
 

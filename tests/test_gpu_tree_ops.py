@@ -152,17 +152,25 @@ def test_weighted_tree_materializes_on_use(cuda):
     assert np.array_equal(bits(both["a"].cpu().numpy()), bits(wb))
 
 
-def test_modified_delta_raises(cuda):
+def test_modified_delta_raises(cuda, sum_mode):
     d = {"a": torch.ones(100, device=cuda)}
     s = {"a": torch.zeros(100, device=cuda)}
     wt = tu.tree_weight(d, 2)
-    d["a"].add_(1.0)  # in place, before the weighted value is used
+    d["a"].add_(1.0)  # in place, before the weighted value is used: the sum refuses
     with pytest.raises(RuntimeError, match="modified"):
-        tu.tree_add(s, wt)
+        tu.tree_add(s, wt).materialize()  # (a deferred sum raises at its fold)
     wt = tu.tree_weight(d, 2)
     d["a"] = torch.zeros(100, device=cuda)  # leaf replaced
-    with pytest.raises(RuntimeError, match="modified"):
-        tu.tree_add(s, wt)
+    if sum_mode == "deferred":  # the deferred sum holds the captured leaves: the value tree_weight saw
+        got = tu.tree_add(s, wt)
+        assert torch.equal(got["a"], torch.full((100,), 4.0, device=cuda))
+    else:  # one launch per tree_add over the input as it is now: refused
+        with pytest.raises(RuntimeError, match="modified"):
+            tu.tree_add(s, wt)
+    wt = tu.tree_weight(d, 2)
+    d["a"] = torch.ones(100, device=cuda)  # replaced, then the weighted value itself is used: refused
+    with pytest.raises(RuntimeError, match="changed structure|modified"):
+        wt.materialize()
     # the fused-norm cache does not answer for a modified delta
     d = {"a": torch.ones(100, device=cuda)}
     tu.tree_add(s, tu.tree_weight(d, 2))
@@ -223,7 +231,7 @@ def test_literal_loop_configs1_bitwise_and_host_cost(K, cuda, sum_mode):
 def test_pending_sum_chain_semantics(cuda, sum_mode):
     """PendingSum keeps every intermediate sum valid (s1 stays s0 + x1 after s2 is built),
     folds in bounded chunks under the budget, applies tree_inverse_weight's scale in the
-    same launch, and refuses a delta modified after it was added."""
+    same launch, and refuses a delta modified in place after its tree_weight."""
     if sum_mode != "deferred":
         pytest.skip("deferred mode only")
     g = torch.Generator().manual_seed(11)

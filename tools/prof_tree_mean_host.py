@@ -22,7 +22,7 @@ def tmap(f, t):
     return {k: tmap(f, v) for k, v in t.items()} if isinstance(t, dict) else f(t)
 
 
-def main(K=128, reps=200):
+def main(K=128, reps=200, sync=False):
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     clients = [tmap(lambda s: torch.rand(s, device=dev, generator=g), SHAPES) for _ in range(K)]
@@ -45,15 +45,22 @@ def main(K=128, reps=200):
         if i >= 20:
             for k, v in zip(ph, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4)):
                 ph[k].append(v * 1e6)
-        if i % 50 == 0:
+        if sync or i % 50 == 0:
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     from fedjax_amd import _lib
+    _lib.host().host_timers()  # reset: the phases below are of the timed calls only
+    for i in range(reps):
+        td, rows = tu._client_table(trees)
+        if sync:
+            torch.cuda.synchronize()
+        tu._fold(rows, w, scale=tu._inverse(W), validated=True)
+    torch.cuda.synchronize()
     inner = {k: round(v, 2) for k, v in _lib.host().host_timers().items()}
-    print(json.dumps({"workload": "configs[1] tree_mean host phases (us, median)",
+    print(json.dumps({"workload": f"configs[1] tree_mean host phases (us, median), K={K}, sync={sync}",
                       **{k: round(float(np.median(v)), 2) for k, v in ph.items()},
                       "fold_table_phases_us_mean": inner}), flush=True)
 
 
-if __name__ == "__main__":
-    main()
+if __name__ == "__main__":  # argv: K, then "sync" (idle GPU before every call)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 128, sync="sync" in sys.argv[2:])
