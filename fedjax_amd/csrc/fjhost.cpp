@@ -932,7 +932,13 @@ PyObject* norm_view(PyObject*, PyObject* args) {
   }
   try {
     const at::Tensor& b = THPVariable_Unpack(buf);
-    return THPVariable_Wrap(b.select(0, row).select(0, index), reinterpret_cast<PyTypeObject*>(type));
+    if (b.dim() != 2 || row < 0 || row >= b.size(0) || index < 0 || index >= b.size(1)) {
+      PyErr_SetString(PyExc_IndexError, "norm_view: index out of range");
+      return nullptr;
+    }
+    // one view op (b[row, index]) instead of two selects
+    return THPVariable_Wrap(b.as_strided({}, {}, b.storage_offset() + row * b.stride(0) + index * b.stride(1)),
+                            reinterpret_cast<PyTypeObject*>(type));
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;

@@ -909,7 +909,7 @@ def _lazy_norm(pytree_, row: int):
     node = _LAST() if _LAST is not None else None
     if node is None or node._value is not None or node._cap is None:
         return None
-    host = _lib.host()
+    host = _HOST if _HOST is not None else _lib.host()
     if not host.matches(pytree_, node._cap[0], node._cap[1]):
         return None
     ch = node._chain

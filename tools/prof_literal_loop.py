@@ -71,6 +71,20 @@ def main(K=128, rounds=15):
            "round_issue_ms": round(float(np.median(per["round_issue"])), 4),
            "round_wall_ms": round(float(np.median(per["round_wall"])), 4)}
     print(json.dumps(res), flush=True)
+    if os.environ.get("CPROF", "0") == "1":  # where the per-call host time goes
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(20):
+            s = tu.tree_zeros_like(params)
+            for d, n in zip(deltas, weights):
+                s = tu.tree_add(s, tu.tree_weight(d, n))
+                tu.tree_l2_norm(d)
+            tu.tree_inverse_weight(s, float(sum(weights)))
+        torch.cuda.synchronize()
+        pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(16)
 
 
 if __name__ == "__main__":
