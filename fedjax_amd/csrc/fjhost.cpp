@@ -986,6 +986,105 @@ PyObject* table_from_caps(PyObject*, PyObject* args) {
   }
 }
 
+// fold_caps(base, caps, weights, scale, has_scale, nt_min_bytes, plan_fn, wsum_fn, wsum_l2_fn,
+//           l2_ws_bytes_fn, l2sq) -> (rc, tree) | k | None
+//     A deferred running sum's fold (tree_util._fold_chain) in one call: caps[0] is the
+//     captured base, caps[1..] the links' captures (leaves_tuple, version_sum, ...), weights
+//     the K Python-number weights. Checks every capture's versions (k: the first stale one;
+//     0 also when `base` no longer has the captured leaf count), builds the pointer table and
+//     launches fold_core on the current stream; the result tree has base's structure (dict
+//     keys sorted). l2sq: None or float32 [K] for every operand's squared norm. None: not this
+//     case (nothing launched).
+PyObject* fold_caps(PyObject*, PyObject* args) {
+  PyObject *base, *caps, *weights, *l2sq;
+  double scale, nt_min;
+  int has_scale;
+  unsigned long long plan_addr, wsum_addr, l2_addr, l2ws_addr;
+  if (!PyArg_ParseTuple(args, "OO!O!dpdKKKKO", &base, &PyList_Type, &caps, &PyList_Type, &weights, &scale,
+                        &has_scale, &nt_min, &plan_addr, &wsum_addr, &l2_addr, &l2ws_addr, &l2sq))
+    return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(caps);
+  if (K < 1 || PyList_GET_SIZE(weights) != K) Py_RETURN_NONE;
+  Stamp st;
+  ++g_timer_calls;
+  try {
+    std::vector<float> wf(K);
+    for (Py_ssize_t k = 0; k < K; ++k)
+      if (!f32_weight(PyList_GET_ITEM(weights, k), &wf[k])) Py_RETURN_NONE;
+    PyObject* cap0 = PyList_GET_ITEM(caps, 0);
+    if (!PyTuple_Check(cap0) || PyTuple_GET_SIZE(cap0) < 2 || !PyTuple_Check(PyTuple_GET_ITEM(cap0, 0)))
+      Py_RETURN_NONE;
+    const Py_ssize_t L = PyTuple_GET_SIZE(PyTuple_GET_ITEM(cap0, 0));
+    if (L < 1) Py_RETURN_NONE;
+    PWalk w;  // base's structure now (for the result tree); its leaf objects are not used
+    w.K = 1;
+    const int wr = pwalk(&base, w, 0);
+    if (wr < 0) return nullptr;
+    if (wr > 0) Py_RETURN_NONE;
+    if (static_cast<Py_ssize_t>(w.leaves[0].size()) != L) return PyLong_FromLong(0);
+    std::vector<int64_t> ptrs(static_cast<size_t>(K * L));
+    std::vector<at::Tensor> row0;
+    row0.reserve(L);
+    int dev = -1;
+    for (Py_ssize_t k = 0; k < K; ++k) {
+      PyObject* cap = PyList_GET_ITEM(caps, k);
+      if (!PyTuple_Check(cap) || PyTuple_GET_SIZE(cap) < 2) Py_RETURN_NONE;
+      PyObject* tup = PyTuple_GET_ITEM(cap, 0);
+      if (!PyTuple_Check(tup) || PyTuple_GET_SIZE(tup) != L) return PyLong_FromSsize_t(k);
+      int64_t vs = 0;
+      for (Py_ssize_t l = 0; l < L; ++l) {
+        PyObject* o = PyTuple_GET_ITEM(tup, l);
+        if (!THPVariable_Check(o)) Py_RETURN_NONE;
+        const at::Tensor& t = THPVariable_Unpack(o);
+        if (k == 0) {
+          if (t.scalar_type() != at::kFloat || !t.is_cuda() || !t.is_contiguous()) Py_RETURN_NONE;
+          if (dev < 0) dev = t.get_device();
+          if (t.get_device() != dev) Py_RETURN_NONE;
+          row0.push_back(t);
+        } else if (t.scalar_type() != at::kFloat || !t.is_cuda() || t.get_device() != dev || !t.is_contiguous() ||
+                   t.sizes() != row0[l].sizes()) {
+          Py_RETURN_NONE;  // (captures of one chain match by construction; the Python path decides)
+        }
+        vs += version_of(t);
+        ptrs[k * L + l] = reinterpret_cast<int64_t>(t.data_ptr());
+      }
+      const long long want = PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1));
+      if (want == -1 && PyErr_Occurred()) return nullptr;
+      if (vs != want) return PyLong_FromSsize_t(k);
+    }
+    float* l2p = nullptr;
+    if (l2sq != Py_None) {
+      if (!THPVariable_Check(l2sq)) Py_RETURN_NONE;
+      const at::Tensor& q = THPVariable_Unpack(l2sq);
+      if (q.scalar_type() != at::kFloat || q.numel() != K || !q.is_contiguous() || !q.is_cuda() ||
+          q.get_device() != dev)
+        Py_RETURN_NONE;
+      l2p = q.data_ptr<float>();
+    }
+    const unsigned long long stream =
+        reinterpret_cast<unsigned long long>(c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(dev)).stream());
+    std::vector<at::Tensor> outs;
+    int rc = 0;
+    if (fold_core(row0, ptrs.data(), K, wf.data(), scale, has_scale != 0, nt_min, dev, stream,
+                  reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs, false,
+                  l2p ? reinterpret_cast<WsumL2Fn>(l2_addr) : nullptr, l2p ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr,
+                  l2p, &rc, st) != 0)
+      Py_RETURN_NONE;
+    if (rc != 0) return Py_BuildValue("(iO)", rc, Py_None);
+    std::vector<PyObject*> wrapped(L);
+    for (Py_ssize_t l = 0; l < L; ++l) wrapped[l] = THPVariable_Wrap(std::move(outs[l]));
+    size_t i = 0, ki = 0;
+    PyObject* tree = rebuild(base, wrapped.data(), i, w.keys, ki);
+    for (PyObject* o : wrapped) Py_XDECREF(o);  // (rebuild took the ones it used)
+    if (!tree) return nullptr;
+    st.lap(kTWrap);
+    return Py_BuildValue("(iN)", rc, tree);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 // leaf_fold(trees, weights, caps, scale, flags, norm_operand, dev, stream, fold_fn, ws_fn)
 //     -> (rc, out_tree | None, l2sq | None, l2 | None) | None
 // dev = -1: the first leaf's device; stream = 0: torch's current stream on it.
@@ -1534,6 +1633,7 @@ PyMethodDef kMethods[] = {
     {"append_check", append_check, METH_VARARGS, "deferred tree_add: structure + capture check in one walk"},
     {"norm_view", norm_view, METH_VARARGS, "0-d view of buf[row, index] as a tensor subclass"},
     {"table_from_caps", table_from_caps, METH_VARARGS, "pointer table of captured leaves, version check"},
+    {"fold_caps", fold_caps, METH_VARARGS, "a deferred running sum's fold from its captures, one call"},
     {"leaf_fold", leaf_fold, METH_VARARGS, "fjtree_fold_leaves over 1-2 operand trees (see fjhost.cpp)"},
     {"fold_table", fold_table, METH_VARARGS, "plan image + output leaves + fjagg_wsum_ptrs launch (see fjhost.cpp)"},
     {"mean_pairs", mean_pairs, METH_VARARGS, "tree_mean of (pytree, weight) pairs in one native call (see fjhost.cpp)"},

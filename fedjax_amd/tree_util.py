@@ -853,10 +853,34 @@ pytree.register_lazy_type(PendingSum, PendingSum.materialize)
 _LAST = None  # weakref to the most recent PendingSum link (tree_l2_norm of its delta is lazy)
 
 
+_FOLD_CAPS = os.environ.get("FJAGG_FOLD_CAPS", "1") != "0"  # 0: the Python path below (A/B runs)
+
+
 def _fold_chain(base, links, scale):
     """fl(...fl(fl(base*1) + fl(x_1 w_1)) ... + fl(x_k w_k)) [* f32(scale)]: one pytree-kernel
     launch over the base tree's leaves and the captured leaves of every link; with the
-    per-client squared norms from the same pass when a lazy norm view waits on a link."""
+    per-client squared norms from the same pass when a lazy norm view waits on a link.
+    A captured base (the common case) goes through one native call (fjhost.fold_caps: the
+    version checks, the pointer table, the launch and the result tree)."""
+    bcap = links[0]._bcap
+    if _FOLD_CAPS and bcap is not None:
+        waiting = [n for n in links if n._ticket is not None and n._ticket.node is not None]
+        l2sq = None
+        if waiting:
+            l2sq = torch.empty(1 + len(links), dtype=torch.float32, device=bcap[0][0].device)
+        if _ENTRY_ADDRS is None:
+            _native_fold_addrs()
+        sc = float(np.float32(scale)) if scale is not None else 1.0
+        got = (_HOST or _lib.host()).fold_caps(base, [bcap] + [n._cap for n in links], [1] + [n._weight for n in links], sc,
+                              scale is not None, float(NONTEMPORAL_MIN_BYTES), *_ENTRY_ADDRS, l2sq)
+        if type(got) is int:
+            _stale_chain(got)
+        if got is not None:
+            rc, tree = got
+            _lib.check(rc, "fjagg_wsum_ptrs")
+            if waiting:
+                _fill_norms(links, waiting, l2sq)
+            return tree
     leaves0, td = pytree.flatten(base)
     L = len(leaves0)
     caps = [n._cap for n in links]
@@ -873,14 +897,8 @@ def _fold_chain(base, links, scale):
         ptrs[0] = [x.data_ptr() for x in leaves0]
         bad = _lib.host().table_from_caps(caps, ptrs[1:])
         bad = bad + 1 if bad >= 0 else bad
-    if bad == 0:
-        raise RuntimeError("the running sum passed to tree_add was modified (a leaf replaced or updated in "
-                           "place) before the pending sum was used; the reference adds its value at tree_add. "
-                           "Call fedjax_amd.tree_util.set_deferred_sums(False) for loops that do this")
-    if bad > 0:
-        raise RuntimeError(f"client {bad - 1} of a pending tree_add sum was modified (a leaf updated in place) "
-                           "after its tree_weight / tree_add; the reference sums each delta's value at that "
-                           "call. Add copies, or call fedjax_amd.tree_util.set_deferred_sums(False)")
+    if bad >= 0:
+        _stale_chain(bad)
     packed = _pack_weights([1] + [n._weight for n in links])
     waiting = [n for n in links if n._ticket is not None and n._ticket.node is not None]
     l2sq = None
@@ -888,20 +906,37 @@ def _fold_chain(base, links, scale):
         l2sq = torch.empty(1 + len(links), dtype=torch.float32, device=leaves0[0].device)
     outs = _fold(_Table(list(leaves0), ptrs), packed, scale=scale, validated=True, l2sq=l2sq)
     if waiting:
-        # per chain, the links form one run of consecutive indices: two small launches each
-        j = 0
-        while j < len(links):
-            ch, j0 = links[j]._chain, j
-            while j < len(links) and links[j]._chain is ch and links[j]._idx == links[j0]._idx + (j - j0):
-                j += 1
-            if ch.buf is not None:
-                i0, i1 = links[j0]._idx, links[j0]._idx + (j - j0)
-                ch.buf[0, i0:i1].copy_(l2sq[1 + j0:1 + j])
-                torch.sqrt(l2sq[1 + j0:1 + j], out=ch.buf[1, i0:i1])
-        for n in waiting:
-            n._ticket.node = None
-            n._ticket = None
+        _fill_norms(links, waiting, l2sq)
     return pytree.unflatten(td, outs)
+
+
+def _stale_chain(bad: int):
+    """Raise for operand ``bad`` of a chain's fold (0: the base) found modified."""
+    if bad == 0:
+        raise RuntimeError("the running sum passed to tree_add was modified (a leaf replaced or updated in "
+                           "place) before the pending sum was used; the reference adds its value at tree_add. "
+                           "Call fedjax_amd.tree_util.set_deferred_sums(False) for loops that do this")
+    raise RuntimeError(f"client {bad - 1} of a pending tree_add sum was modified (a leaf updated in place) "
+                       "after its tree_weight / tree_add; the reference sums each delta's value at that "
+                       "call. Add copies, or call fedjax_amd.tree_util.set_deferred_sums(False)")
+
+
+def _fill_norms(links, waiting, l2sq):
+    """Copy the fold's per-operand squared norms (l2sq[1 + j] for link j) into the chains'
+    norm buffers the waiting lazy views read, and release the views' tickets."""
+    # per chain, the links form one run of consecutive indices: two small launches each
+    j = 0
+    while j < len(links):
+        ch, j0 = links[j]._chain, j
+        while j < len(links) and links[j]._chain is ch and links[j]._idx == links[j0]._idx + (j - j0):
+            j += 1
+        if ch.buf is not None:
+            i0, i1 = links[j0]._idx, links[j0]._idx + (j - j0)
+            ch.buf[0, i0:i1].copy_(l2sq[1 + j0:1 + j])
+            torch.sqrt(l2sq[1 + j0:1 + j], out=ch.buf[1, i0:i1])
+    for n in waiting:
+        n._ticket.node = None
+        n._ticket = None
 
 
 def _lazy_norm(pytree_, row: int):

@@ -459,3 +459,59 @@ def test_early_flush_of_the_running_sum(cuda, sum_mode):
         n64 = [float(np.sqrt(sum(float(np.dot(v.astype(np.float64), v.astype(np.float64)))
                                  for v in leaves_np(x)))) for x in xs]
         np.testing.assert_allclose(norms, n64, rtol=2e-6)
+
+
+def test_native_chain_fold_equals_python_path(cuda, sum_mode, monkeypatch):
+    """A deferred sum's fold through fjhost.fold_caps (one native call) against the Python
+    path (_FOLD_CAPS off): the literal loop's mean and lazy norms bitwise, with early
+    flushes (several folds per round), a nested / list / None structure, and the stale
+    errors (base and client) raised the same way."""
+    if sum_mode != "deferred":
+        pytest.skip("deferred mode only")
+    g = torch.Generator().manual_seed(21)
+    shapes = {"z": [(70,), None, ((3,), (5, 2))], "a": {"q": (8,), "p": (1001,)}}
+
+    def dev_tree(t):
+        if isinstance(t, dict):
+            return {k: dev_tree(v) for k, v in t.items()}
+        if isinstance(t, list):
+            return [dev_tree(v) for v in t]
+        if isinstance(t, tuple) and t and not isinstance(t[0], int):
+            return tuple(dev_tree(v) for v in t)
+        if t is None:
+            return None
+        return (torch.rand(t, generator=g) - 0.5).to(cuda)
+
+    K = 37
+    deltas = [dev_tree(shapes) for _ in range(K)]
+    weights = [1 + (k % 9) for k in range(K)]
+    weights[4] = 0.75
+    params = tu.tree_zeros_like(deltas[0])
+
+    def run(native, flush):
+        monkeypatch.setattr(tu, "_FOLD_CAPS", native)
+        tu.set_deferred_sums(True, flush_bytes=flush, flush_clients=4)
+        try:
+            mean, norms = literal_loop(tu, params, deltas, weights)
+            return [x.cpu() for x in pytree.leaves_of(mean)], torch.stack(norms).cpu(), ref.flatten(mean)[1]
+        finally:
+            tu.set_deferred_sums(True, flush_bytes=1 << 30, flush_clients=16)
+
+    want, want_n, want_td = run(False, 1 << 30)
+    for flush in (1 << 30, 20_000):  # one fold per round / a fold every ~5 clients
+        got, got_n, got_td = run(True, flush)
+        assert got_td == want_td
+        for a, b in zip(got, want):
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+        assert torch.equal(got_n.view(torch.int32), want_n.view(torch.int32))
+    monkeypatch.setattr(tu, "_FOLD_CAPS", True)
+    s = tu.tree_add(tu.tree_zeros_like(deltas[0]), tu.tree_weight(deltas[1], 2))
+    s = tu.tree_add(s, tu.tree_weight(deltas[2], 3))
+    deltas[2]["a"]["q"].add_(1.0)
+    with pytest.raises(RuntimeError, match="client 1 of a pending tree_add sum was modified"):
+        s.materialize()
+    base = tu.tree_zeros_like(deltas[0])
+    s = tu.tree_add(base, tu.tree_weight(deltas[3], 2))
+    base["a"]["p"].add_(1.0)
+    with pytest.raises(RuntimeError, match="running sum passed to tree_add was modified"):
+        tu.tree_inverse_weight(s, 2.0)
