@@ -1041,9 +1041,11 @@ PyObject* fold_caps(PyObject*, PyObject* args) {
           if (dev < 0) dev = t.get_device();
           if (t.get_device() != dev) Py_RETURN_NONE;
           row0.push_back(t);
-        } else if (t.scalar_type() != at::kFloat || !t.is_cuda() || t.get_device() != dev || !t.is_contiguous() ||
-                   t.sizes() != row0[l].sizes()) {
-          Py_RETURN_NONE;  // (captures of one chain match by construction; the Python path decides)
+        } else if (t.numel() != row0[l].numel()) {
+          // the links' captures were checked against the chain's structure when they were
+          // taken (dtype, device, layout, shape); dtype and device cannot change, and an
+          // in-place reshape bumps the version. The element count guards the fold's reads.
+          Py_RETURN_NONE;
         }
         vs += version_of(t);
         ptrs[k * L + l] = reinterpret_cast<int64_t>(t.data_ptr());
