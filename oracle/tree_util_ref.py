@@ -14,6 +14,7 @@ Restates google/fedjax 0.0.17 ``fedjax/core/tree_util.py`` op for op:
 * ``tree_mean``              tree_util.py:76-96   weighted fold, W summed in Python
 * ``tree_size``              tree_util.py:99-102
 * ``tree_l2_squared/norm``   tree_util.py:105-114
+* ``tree_clip_by_global_norm`` tree_util.py:117-133
 * ``mean_aggregator``        fedjax/aggregators/aggregator.py:61-75
 
 and the JAX dtype rules those lines run under (x64 disabled, the jax default):
@@ -221,6 +222,15 @@ def tree_l2_squared(pytree) -> np.float32:
 def tree_l2_norm(pytree) -> np.float32:
     """tree_util.py:111-114."""
     return np.float32(np.sqrt(np.float32(tree_l2_squared(pytree))))
+
+
+def tree_clip_by_global_norm(pytree, max_norm):
+    """tree_util.py:117-133 under jax.jit: max_norm is a weakly typed f32 argument,
+    ``scale = min(1, max_norm / norm)`` in float32, then ``scale * t`` per leaf."""
+    norm = tree_l2_norm(pytree)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        scale = np.minimum(np.float32(1), np.float32(max_norm) / norm)
+    return tree_map(lambda l: (np.float32(scale) * canonical_leaf(l)).astype(np.float32), pytree)
 
 
 # ----------------------------------------------------------------------------

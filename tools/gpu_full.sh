@@ -6,7 +6,7 @@ set -u
 TAG=${1:-r01}
 OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
 run() { local name=$1 lim=$2 a1=$3; shift 3; timeout -k 10 "$lim" "$@"; local rc=$?; echo "[$name] rc=$rc"; if [ $rc -eq 0 ] || { [ $a1 = 1 ] && [ $rc -eq 1 ]; }; then return 0; fi; exit $rc; }
-run gpu-tests 900 1 bash -c "python -u -m pytest tests -q -m gpu -rf --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/${TAG}_gpu_tests.log 2>&1"
+run gpu-tests 900 1 bash -c "python -u -m pytest tests -q -m gpu -rfs --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/${TAG}_gpu_tests.log 2>&1"
 tail -2 $OUT/${TAG}_gpu_tests.log
 run smoke 300 0 bash -c "python -c 'import __graft_entry__ as g; g.smoke()' > $OUT/${TAG}_smoke.log 2>&1"
 tail -1 $OUT/${TAG}_smoke.log

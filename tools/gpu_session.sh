@@ -20,10 +20,10 @@ step() {  # name limit allow_rc1 cmd...
   exit $rc
 }
 if [ -n "$KEXPR" ]; then
-  step gpu-tests 900 1 python -u -m pytest tests -x -v -m gpu -k "$KEXPR" --timeout 300 --timeout-method thread \
+  step gpu-tests 900 1 python -u -m pytest tests -x -v -m gpu -k "$KEXPR" --timeout 300 --timeout-method thread -rs \
     -p no:cacheprovider > "$OUT/${TAG}_gpu_tests.log" 2>&1
 else
-  step gpu-tests 1100 1 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -rf \
+  step gpu-tests 1100 1 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -rfs \
     -p no:cacheprovider > "$OUT/${TAG}_gpu_tests.log" 2>&1
 fi
 tail -5 "$OUT/${TAG}_gpu_tests.log"
