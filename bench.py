@@ -64,6 +64,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def phase(rank, name):
+    """One stderr line per phase of a rank's run (communicator init, each auto-tune
+    candidate, warmup, timed loop, e2e, done), and the rank's current phase in the file a
+    spawning parent named in FJ_BENCH_PHASES (spawn_ranks reads them on a timeout to name
+    the ranks that had not finished, and where each one stopped)."""
+    log(f"[bench rank {rank}] {name}")
+    d = os.environ.get("FJ_BENCH_PHASES")
+    if d:
+        try:
+            with open(os.path.join(d, f"rank{rank}"), "w") as f:
+                f.write(name)
+        except OSError:
+            pass
+
+
 def fedavg_weights(K, seed=1):
     return np.random.RandomState(seed).randint(1, 501, size=K).tolist()
 
@@ -250,17 +265,48 @@ def _free_port() -> int:
     return port
 
 
+def rank_timeout(args) -> float:
+    """Seconds a spawned N-rank run may take before spawn_ranks kills it: process start,
+    rendezvous and communicator init (300 s), plus every step the ranks run — warmup,
+    timed steps, the exchange auto-tune (24 candidates x 7 steps) and the e2e repeats —
+    at a pessimistic 0.5 TB/s per rank for that rank's share of the deltas, times 4."""
+    K, P, dtype, _ = WORKLOADS[args.workload]
+    K = args.clients or K
+    esize = torch.empty((), dtype=dtype).element_size()
+    per_rank_s = (K + args.gpus - 1) // args.gpus * P * esize / 0.5e12
+    steps = args.warmup + args.steps + 24 * 7 + 6
+    return 300.0 + 4.0 * steps * per_rank_s
+
+
+def _rank_phases(d: str, nproc: int):
+    out = {}
+    for r in range(nproc):
+        try:
+            with open(os.path.join(d, f"rank{r}")) as f:
+                out[r] = f.read().strip() or "started"
+        except OSError:
+            out[r] = "not started"
+    return out
+
+
 def spawn_ranks(nproc: int, argv, script: str = None, timeout: float = None) -> int:
     """Run ``script argv`` as ``nproc`` ranks of one node and forward rank 0's JSON line.
 
     A bare ``python bench.py --gpus N`` (no WORLD_SIZE in the environment) lands here
     before anything touches the GPU. The ranks are children of this process
-    (``python -m torch.distributed.run``, rendezvous on 127.0.0.1): nothing is exec'd.
-    Every rank's stderr passes through; stdout is collected and only the JSON line
-    (rank 0's) is printed. Returns the launcher's exit status, non-zero if any rank
-    failed or no JSON line came back. Rank 0 writes its line to the file named in
-    FJ_BENCH_JSON (emit_json); the shared stdout pipe is the fallback for scripts that
-    do not."""
+    (``python -m torch.distributed.run``, rendezvous on 127.0.0.1, in a process group of
+    their own): nothing is exec'd. Every rank's stderr passes through; stdout is collected
+    and only the JSON line (rank 0's) is printed. Returns the launcher's exit status,
+    non-zero if any rank failed or no JSON line came back. Rank 0 writes its line to the
+    file named in FJ_BENCH_JSON (emit_json); the shared stdout pipe is the fallback for
+    scripts that do not.
+
+    ``timeout`` (seconds, None = none): past it the whole process group is terminated
+    (SIGTERM, then SIGKILL after 10 s), the ranks that had not reached their "done" phase
+    are named with the last phase each one wrote (FJ_BENCH_PHASES, bench.phase), and the
+    return status is 124."""
+    import shutil
+    import signal
     import subprocess
     import tempfile
 
@@ -269,18 +315,35 @@ def spawn_ranks(nproc: int, argv, script: str = None, timeout: float = None) -> 
            *argv]
     fd, json_path = tempfile.mkstemp(prefix="fj_bench_", suffix=".json")
     os.close(fd)
-    env = dict(os.environ, FJ_BENCH_LAUNCHER="bench.py -> torch.distributed.run child", FJ_BENCH_JSON=json_path)
-    log("+", " ".join(cmd))
+    phase_dir = tempfile.mkdtemp(prefix="fj_bench_phases_")
+    env = dict(os.environ, FJ_BENCH_LAUNCHER="bench.py -> torch.distributed.run child", FJ_BENCH_JSON=json_path,
+               FJ_BENCH_PHASES=phase_dir)
+    log("+", " ".join(cmd) + (f"   (timeout {timeout:.0f} s)" if timeout else ""))
     try:
+        proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, start_new_session=True)
         try:
-            proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, timeout=timeout)
+            out, _ = proc.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
-            log(f"spawned ranks did not finish within {timeout} s")
+            phases = _rank_phases(phase_dir, nproc)
+            stuck = [r for r, p in phases.items() if p != "done"]
+            log(f"bench: spawned ranks did not finish within {timeout:.0f} s; ranks {stuck} had not finished "
+                f"(last phase per rank: {phases}); terminating the launcher's process group")
+            for sig, wait in ((signal.SIGTERM, 10), (signal.SIGKILL, 10)):
+                try:
+                    os.killpg(proc.pid, sig)  # the group this call started (start_new_session)
+                except ProcessLookupError:
+                    break
+                try:
+                    proc.wait(timeout=wait)
+                    break
+                except subprocess.TimeoutExpired:
+                    continue
             return 124
         with open(json_path) as f:
             filed = f.read().strip()
     finally:
         os.unlink(json_path)
+        shutil.rmtree(phase_dir, ignore_errors=True)
     if proc.returncode != 0:
         log(f"rank launcher exited with status {proc.returncode}")
         return proc.returncode
@@ -288,7 +351,7 @@ def spawn_ranks(nproc: int, argv, script: str = None, timeout: float = None) -> 
         lines = [filed]
     else:  # a script that does not write FJ_BENCH_JSON: rank 0's JSON object on the shared pipe
         lines = []
-        for ln in proc.stdout.decode(errors="replace").splitlines():
+        for ln in out.decode(errors="replace").splitlines():
             i = ln.find('{"')  # another rank's unterminated banner can precede the JSON
             if i >= 0:
                 try:
@@ -325,6 +388,73 @@ def load_traffic(workload):
     return d.get("hbm_bytes_per_launch")
 
 
+# host RAM one rank may pin for its shard in the e2e leg (a configs[4] shard is 256 GB)
+E2E_MAX_PINNED_BYTES = 64 << 30
+
+
+def host_resident_rate(x, w_local, sharded_step, out, scale, nt, dev, rank, sharded, job_bytes, reps=3):
+    """The deployment rate (north star): every rank's client deltas start in
+    its own pinned host memory and go over its own PCIe link (H2D into the resident slab),
+    then the fold — at N>1 the whole sharded step, fold + RCCL reduce — and the mean comes
+    back to the host (D2H on rank 0). Rate = all clients' bytes / the max-over-ranks wall
+    time of ``reps`` such rounds. Every rank decides together whether its shard fits the
+    pinned budget (one all_reduce), so either all ranks run the leg or none does."""
+    from fedjax_amd import kernels
+
+    nbytes = x.shape[0] * x.shape[1] * x.element_size()
+    ok = nbytes <= E2E_MAX_PINNED_BYTES
+    xh = None
+    if ok:
+        try:
+            xh = torch.empty(x.shape, dtype=x.dtype).pin_memory()
+            xh.copy_(x.cpu())
+        except RuntimeError as e:  # pinned allocation refused: skip the leg on every rank
+            log(f"[bench rank {rank}] e2e: pinned host buffer of {nbytes / 2**30:.1f} GiB refused ({e})")
+            ok, xh = False, None
+    if sharded:
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag.item())
+    if not ok:
+        return {"e2e_host_resident_GBs": None,
+                "e2e_note": f"skipped: a rank's shard ({nbytes / 2**30:.1f} GiB) exceeds the "
+                            f"{E2E_MAX_PINNED_BYTES >> 30} GiB pinned-host budget or was refused"}
+    yh = torch.empty(out.shape, dtype=out.dtype).pin_memory()
+    wd = torch.from_numpy(np.float32(w_local)).to(dev)
+
+    def one():
+        x.copy_(xh, non_blocking=True)
+        if sharded:
+            sharded_step()
+        else:
+            kernels.weighted_sum_dense(x, wd, scale=scale, out=out, nontemporal=nt)
+        if rank == 0:
+            yh.copy_(out, non_blocking=True)
+
+    one()  # warm (first pinned transfers map the buffers)
+    torch.cuda.synchronize()
+    if sharded:
+        dist.barrier()
+    ts = time.perf_counter()
+    for _ in range(reps):
+        one()
+    torch.cuda.synchronize()
+    if sharded:
+        dist.barrier()
+    t = time.perf_counter() - ts
+    if sharded:
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    del xh
+    return {"e2e_host_resident_GBs": round(job_bytes * reps / t / 1e9, 2),
+            "e2e_ms_per_round": round(t / reps * 1e3, 4),
+            "e2e_note": "each rank's deltas in its own pinned host memory -> its own PCIe link (H2D) -> "
+                        + (f"fold + {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} exchange"
+                           if sharded else "fold") + " -> mean D2H on rank 0; "
+                        "bytes = all clients' deltas; max over ranks"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -340,7 +470,12 @@ def main():
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the drop-in surface sub-record (mean_aggregator().apply / tree_mean over "
                          "caller-held pytrees, timed after the headline)")
-    ap.add_argument("--e2e", action="store_true", help="also time host-resident deltas (H2D + fold + D2H)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="N=1: also time host-resident deltas (H2D + fold + D2H); on by default at N>1")
+    ap.add_argument("--no-e2e", action="store_true", help="N>1: skip the host-resident end-to-end leg")
+    ap.add_argument("--timeout", type=float, default=0,
+                    help="bare --gpus N: seconds before the spawned ranks are killed (0 = derived from the "
+                         "workload and steps, rank_timeout)")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--all-ranks", action="store_true",
                     help="every rank needs the mean: all_reduce only (default: the mean is needed on rank 0, and "
@@ -374,7 +509,8 @@ def main():
         # bare `python bench.py --gpus N`: one rank per GPU as child processes (nothing in
         # this process touches the GPU runtime, not even a device count — the ranks check
         # that there are enough GPUs — and nothing is exec'd)
-        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:]))
+        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:],
+                                     timeout=args.timeout if args.timeout > 0 else rank_timeout(args)))
     # stdout carries exactly one line, rank 0's JSON: native libraries write banners to fd 1
     # (RCCL's version block, gloo's connection notes), so fd 1 is pointed at stderr for the
     # rest of the run and the JSON goes to a saved copy of the original stdout
@@ -403,6 +539,7 @@ def main():
         nshard = args.rehearse_shard
     sharded = nshard > 1
     if sharded:
+        phase(rank, f"init process group ({args.backend}, world {world})")
         if args.backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
@@ -427,6 +564,7 @@ def main():
     vw = 16 // esize
     ld = (P + vw - 1) // vw * vw
     x = torch.empty(Kl, ld, dtype=dtype, device=dev)[:, :P]
+    phase(rank, f"fill {Kl} clients x {P} params")
     kernels.fill_synth(x, seed=0, k0=k0)  # the same global client k on every N
     w_local = [weights[k] for k in range(k0, k1)]
     out = torch.empty(P, dtype=dtype if not sharded else torch.float32, device=dev)
@@ -468,6 +606,7 @@ def main():
     # HIP fold + torch.distributed collective (ProcessGroupNCCL)
     comm = None
     if sharded and args.backend == "nccl" and args.engine in ("auto", "native") and not args.with_norms:
+        phase(rank, "native RCCL communicator init")
         try:
             comm = fd.RcclCommunicator(device=dev)
         except Exception as e:  # noqa: BLE001 - the torch engine still runs
@@ -545,18 +684,21 @@ def main():
                     if len(fd.bucket_edges(P, b)) < (b if isinstance(b, int) else len(b)):
                         continue  # P too small for that many aligned buckets
                     engine, collective, buckets = eng, col, b
+                    phase(rank, f"auto-tune candidate {eng}/{col}/{fd.bucket_name(b)}")
                     wall(2)
                     tune[(eng, col, b)] = wall(5) / 5 * 1e3
         engine, collective, buckets = min(tune, key=tune.get)
         tune = {f"{e}/{c}/{fd.bucket_name(b)}": t for (e, c, b), t in tune.items()}
         log(f"exchange auto-tune (ms/step, max over ranks): {tune} -> "
             f"{engine}/{collective}/{fd.bucket_name(buckets)}")
+    phase(rank, f"warmup ({args.warmup} steps)")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     if sharded:
         dist.barrier()
     torch.cuda.synchronize()
+    phase(rank, f"timed loop ({args.steps} steps)")
     events = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -577,20 +719,10 @@ def main():
     achieved = bytes_per_launch / mean_kernel_s / 1e9
 
     e2e = None
-    if args.e2e and not sharded:
-        xh = torch.empty(K, P, dtype=dtype).pin_memory()
-        xh.copy_(x.cpu())
-        yh = torch.empty(P, dtype=out.dtype).pin_memory()
-        wd = torch.from_numpy(np.float32(w_local)).to(dev)
-        torch.cuda.synchronize()
-        ts = time.perf_counter()
-        for _ in range(3):
-            x.copy_(xh, non_blocking=True)
-            kernels.weighted_sum_dense(x, wd, scale=scale, out=out, nontemporal=nt)
-            yh.copy_(out, non_blocking=True)
-        torch.cuda.synchronize()
-        e2e = K * P * esize * 3 / (time.perf_counter() - ts) / 1e9
-        del xh
+    if (args.e2e or (sharded and not args.no_e2e)) and args.server == "none" and not args.with_norms:
+        phase(rank, "e2e: host-resident deltas (pinned H2D + fold [+ reduce] + D2H)")
+        e2e = host_resident_rate(x, w_local, step if sharded else None, out, scale, nt, dev, rank, sharded,
+                                 K * P * esize if nshard == world else Kl * P * esize)
 
     if rank == 0:
         value = (K if nshard == world else Kl) * P * esize * args.steps / elapsed / 1e9
@@ -638,7 +770,7 @@ def main():
                          "mean_launch_ms": round(mean_kernel_s * 1e3, 4)},
         }
         if e2e is not None:
-            res["e2e_host_resident_GBs"] = round(e2e, 2)
+            res.update(e2e)
         if nshard != world:
             res["rehearsal_projected_whole_job_GBs"] = round(value * nshard, 2)
         if (not sharded and not args.no_dropin and args.workload == "c3" and not args.clients
@@ -652,6 +784,7 @@ def main():
         comm.close()
     if sharded:
         dist.destroy_process_group()
+    phase(rank, "done")
 
 
 def single_process(args):

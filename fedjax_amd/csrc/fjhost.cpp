@@ -47,6 +47,7 @@
 //       path then handles it.
 
 #include <Python.h>
+#include <structmember.h>
 
 #include <ATen/ATen.h>
 #include <c10/hip/HIPFunctions.h>
@@ -69,7 +70,7 @@ namespace {
 
 // Host phase timers of fold_table (host_timers() reads and resets them): where the
 // per-call host time of tree_mean goes (tools/prof_tree_mean_host.py).
-enum { kTChecks, kTOutputs, kTPlan, kTImage, kTUpload, kTLaunch, kTWrap, kTPhases };
+enum { kTSpec, kTChecks, kTOutputs, kTPlan, kTImage, kTUpload, kTLaunch, kTWrap, kTFirstLaunch, kTPhases };
 double g_timers[kTPhases] = {};
 long long g_timer_calls = 0;
 // how fold_table's plan images reached the kernel: in the kernel arguments, or through a
@@ -307,6 +308,28 @@ typedef int (*WsumL2Fn)(int, int, int, const int64_t*, int, int64_t, int64_t, co
                         int64_t, void*);
 constexpr int kF32 = 0, kScale = 1, kAccumulate = 2, kNontemporal = 4;  // fjagg.h enums
 
+// Fresh output leaves shaped like row0: ONE allocation, each leaf its own tensor (own
+// TensorImpl and version counter) over a 256-byte aligned slice — one allocator call instead
+// of one per leaf on the path to the first launch. A single leaf is a plain allocation.
+void carve_outputs(const std::vector<at::Tensor>& row0, std::vector<at::Tensor>& outs) {
+  const size_t L = row0.size();
+  if (L == 1) {
+    outs.push_back(at::empty(row0[0].sizes(), row0[0].options()));
+    return;
+  }
+  thread_local std::vector<int64_t> offs;
+  offs.assign(L + 1, 0);
+  for (size_t l = 0; l < L; ++l) offs[l + 1] = offs[l] + (row0[l].numel() + 63) / 64 * 64;
+  at::Tensor flat = at::empty({std::max<int64_t>(offs[L], 1)}, row0[0].options());
+  for (size_t l = 0; l < L; ++l) {
+    at::Tensor t = at::detail::make_tensor<c10::TensorImpl>(c10::Storage(flat.storage()), flat.key_set(),
+                                                            flat.dtype());
+    t.unsafeGetTensorImpl()->set_storage_offset(offs[l]);
+    t.unsafeGetTensorImpl()->set_sizes_contiguous(row0[l].sizes());
+    outs.push_back(std::move(t));
+  }
+}
+
 // The launch part of fold_table for a gathered table: K x L pointers `in` (row 0 = row0's
 // leaves), float32 weights wf[K]. outs: empty = fresh outputs shaped like row0 (appended),
 // else the destinations (float32, contiguous, row0's shapes and device). Returns 0 with the
@@ -347,8 +370,8 @@ int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K,
   }
   std::vector<uint8_t> elem(L, 0);
   bool any_elem = false;
+  if (fresh) carve_outputs(row0, outs);
   for (int64_t l = 0; l < L; ++l) {
-    if (fresh) outs.push_back(at::empty(row0[l].sizes(), row0[l].options()));
     elem[l] = ((lbits[l] | reinterpret_cast<int64_t>(outs[l].data_ptr())) & 15) != 0;
     any_elem = any_elem || elem[l];
   }
@@ -781,16 +804,15 @@ int64_t structure_token(const std::vector<int64_t>& sig, const PWalk& w) {
 //     tree_weight's lazy result holds its input's leaves (strong references, flatten order)
 //     and their version sum, so the fold can check that nothing changed in between; token
 //     (structure_token) lets tree_add match two captured trees' structures without a walk.
-PyObject* capture(PyObject*, PyObject* args) {
-  PyObject* tree;
-  int dev;
-  if (!PyArg_ParseTuple(args, "Oi", &tree, &dev)) return nullptr;
+// New reference: the capture tuple, Py_None (not the fast case), or nullptr (Python error).
+PyObject* capture_impl(PyObject* tree, int dev) {
   try {
     thread_local std::vector<int64_t> sig;
     sig.clear();
     PWalk w;
     w.K = 1;
     w.sig = &sig;
+    w.leaves[0].reserve(16);
     int rc = pwalk(&tree, w, 0);
     if (rc < 0) return nullptr;
     int64_t vs = 0;
@@ -817,12 +839,30 @@ PyObject* capture(PyObject*, PyObject* args) {
       for (int64_t s : t.sizes()) sig.push_back(s);
     }
     const int64_t tok = structure_token(sig, w);
-    return Py_BuildValue("(NLLL)", tup, static_cast<long long>(vs), static_cast<long long>(nbytes),
-                         static_cast<long long>(tok));
+    PyObject* out = PyTuple_New(4);
+    PyObject* a = PyLong_FromLongLong(vs);
+    PyObject* b = PyLong_FromLongLong(nbytes);
+    PyObject* c = PyLong_FromLongLong(tok);
+    if (!out || !a || !b || !c) {
+      Py_XDECREF(out), Py_XDECREF(a), Py_XDECREF(b), Py_XDECREF(c), Py_DECREF(tup);
+      return nullptr;
+    }
+    PyTuple_SET_ITEM(out, 0, tup);
+    PyTuple_SET_ITEM(out, 1, a);
+    PyTuple_SET_ITEM(out, 2, b);
+    PyTuple_SET_ITEM(out, 3, c);
+    return out;
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
   }
+}
+
+PyObject* capture(PyObject*, PyObject* args) {
+  PyObject* tree;
+  int dev;
+  if (!PyArg_ParseTuple(args, "Oi", &tree, &dev)) return nullptr;
+  return capture_impl(tree, dev);
 }
 
 // matches(tree, leaves_tuple, version_sum) -> bool: the same leaf objects, unmodified.
@@ -995,23 +1035,18 @@ PyObject* table_from_caps(PyObject*, PyObject* args) {
 //     launches fold_core on the current stream; the result tree has base's structure (dict
 //     keys sorted). l2sq: None or float32 [K] for every operand's squared norm. None: not this
 //     case (nothing launched).
-PyObject* fold_caps(PyObject*, PyObject* args) {
-  PyObject *base, *caps, *weights, *l2sq;
-  double scale, nt_min;
-  int has_scale;
-  unsigned long long plan_addr, wsum_addr, l2_addr, l2ws_addr;
-  if (!PyArg_ParseTuple(args, "OO!O!dpdKKKKO", &base, &PyList_Type, &caps, &PyList_Type, &weights, &scale,
-                        &has_scale, &nt_min, &plan_addr, &wsum_addr, &l2_addr, &l2ws_addr, &l2sq))
-    return nullptr;
-  const Py_ssize_t K = PyList_GET_SIZE(caps);
-  if (K < 1 || PyList_GET_SIZE(weights) != K) Py_RETURN_NONE;
+PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const* weights, Py_ssize_t K, double scale,
+                         bool has_scale, double nt_min, unsigned long long plan_addr, unsigned long long wsum_addr,
+                         unsigned long long l2_addr, unsigned long long l2ws_addr, PyObject* l2sq) {
+  if (K < 1) Py_RETURN_NONE;
   Stamp st;
   ++g_timer_calls;
   try {
-    std::vector<float> wf(K);
+    thread_local std::vector<float> wf;
+    wf.resize(K);
     for (Py_ssize_t k = 0; k < K; ++k)
-      if (!f32_weight(PyList_GET_ITEM(weights, k), &wf[k])) Py_RETURN_NONE;
-    PyObject* cap0 = PyList_GET_ITEM(caps, 0);
+      if (!f32_weight(weights[k], &wf[k])) Py_RETURN_NONE;
+    PyObject* cap0 = caps[0];
     if (!PyTuple_Check(cap0) || PyTuple_GET_SIZE(cap0) < 2 || !PyTuple_Check(PyTuple_GET_ITEM(cap0, 0)))
       Py_RETURN_NONE;
     const Py_ssize_t L = PyTuple_GET_SIZE(PyTuple_GET_ITEM(cap0, 0));
@@ -1022,12 +1057,13 @@ PyObject* fold_caps(PyObject*, PyObject* args) {
     if (wr < 0) return nullptr;
     if (wr > 0) Py_RETURN_NONE;
     if (static_cast<Py_ssize_t>(w.leaves[0].size()) != L) return PyLong_FromLong(0);
-    std::vector<int64_t> ptrs(static_cast<size_t>(K * L));
+    thread_local std::vector<int64_t> ptrs;
+    ptrs.resize(static_cast<size_t>(K * L));
     std::vector<at::Tensor> row0;
     row0.reserve(L);
     int dev = -1;
     for (Py_ssize_t k = 0; k < K; ++k) {
-      PyObject* cap = PyList_GET_ITEM(caps, k);
+      PyObject* cap = caps[k];
       if (!PyTuple_Check(cap) || PyTuple_GET_SIZE(cap) < 2) Py_RETURN_NONE;
       PyObject* tup = PyTuple_GET_ITEM(cap, 0);
       if (!PyTuple_Check(tup) || PyTuple_GET_SIZE(tup) != L) return PyLong_FromSsize_t(k);
@@ -1041,10 +1077,11 @@ PyObject* fold_caps(PyObject*, PyObject* args) {
           if (dev < 0) dev = t.get_device();
           if (t.get_device() != dev) Py_RETURN_NONE;
           row0.push_back(t);
-        } else if (t.numel() != row0[l].numel()) {
+        } else if (t.numel() != row0[l].numel() || t.scalar_type() != at::kFloat || !t.is_contiguous()) {
           // the links' captures were checked against the chain's structure when they were
-          // taken (dtype, device, layout, shape); dtype and device cannot change, and an
-          // in-place reshape bumps the version. The element count guards the fold's reads.
+          // taken (dtype, device, layout, shape); an in-place reshape bumps the version, but
+          // a `.data` reassignment does not: the element count, dtype and layout guard the
+          // fold's reads, the Python path then raises or recomputes
           Py_RETURN_NONE;
         }
         vs += version_of(t);
@@ -1067,7 +1104,7 @@ PyObject* fold_caps(PyObject*, PyObject* args) {
         reinterpret_cast<unsigned long long>(c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(dev)).stream());
     std::vector<at::Tensor> outs;
     int rc = 0;
-    if (fold_core(row0, ptrs.data(), K, wf.data(), scale, has_scale != 0, nt_min, dev, stream,
+    if (fold_core(row0, ptrs.data(), K, wf.data(), scale, has_scale, nt_min, dev, stream,
                   reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs, false,
                   l2p ? reinterpret_cast<WsumL2Fn>(l2_addr) : nullptr, l2p ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr,
                   l2p, &rc, st) != 0)
@@ -1085,6 +1122,20 @@ PyObject* fold_caps(PyObject*, PyObject* args) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
   }
+}
+
+PyObject* fold_caps(PyObject*, PyObject* args) {
+  PyObject *base, *caps, *weights, *l2sq;
+  double scale, nt_min;
+  int has_scale;
+  unsigned long long plan_addr, wsum_addr, l2_addr, l2ws_addr;
+  if (!PyArg_ParseTuple(args, "OO!O!dpdKKKKO", &base, &PyList_Type, &caps, &PyList_Type, &weights, &scale,
+                        &has_scale, &nt_min, &plan_addr, &wsum_addr, &l2_addr, &l2ws_addr, &l2sq))
+    return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(caps);
+  if (K < 1 || PyList_GET_SIZE(weights) != K) Py_RETURN_NONE;
+  return fold_caps_impl(base, &PyList_GET_ITEM(caps, 0), &PyList_GET_ITEM(weights, 0), K, scale, has_scale != 0,
+                        nt_min, plan_addr, wsum_addr, l2_addr, l2ws_addr, l2sq);
 }
 
 // leaf_fold(trees, weights, caps, scale, flags, norm_operand, dev, stream, fold_fn, ws_fn)
@@ -1260,6 +1311,27 @@ PyObject* spec_of(PyObject* x, SpecBuild& b, int depth) {
   return Py_BuildValue("(lNN)", is_dict ? (long)kDict : is_list ? (long)kList : (long)kTuple, aux, children);
 }
 
+// chunk ends of mean_pairs' fold-bound pipeline as fractions of K (pipeline_fracs(); empty:
+// the single `frac` argument)
+std::vector<double> g_pipeline_fracs;
+
+PyObject* pipeline_fracs(PyObject*, PyObject* arg) {
+  PyObject* seq = PySequence_Fast(arg, "pipeline_fracs: a sequence of floats");
+  if (!seq) return nullptr;
+  std::vector<double> v;
+  for (Py_ssize_t i = 0; i < PySequence_Fast_GET_SIZE(seq); ++i) {
+    const double f = PyFloat_AsDouble(PySequence_Fast_GET_ITEM(seq, i));
+    if (f == -1.0 && PyErr_Occurred()) {
+      Py_DECREF(seq);
+      return nullptr;
+    }
+    v.push_back(f);
+  }
+  Py_DECREF(seq);
+  g_pipeline_fracs.swap(v);
+  Py_RETURN_NONE;
+}
+
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1286,6 +1358,7 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
   if (K < 1) Py_RETURN_NONE;
   PyObject* const* items = PyList_CheckExact(pairs) ? &PyList_GET_ITEM(pairs, 0) : &PyTuple_GET_ITEM(pairs, 0);
   Stamp st;
+  const auto t_entry = st.t;
   ++g_timer_calls;
   try {
     // the trees are held by new references for the call: key comparisons during the walks
@@ -1384,12 +1457,18 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
       }
       if (c > 0) {
         for (int64_t k1 = c; k1 < K; k1 += c) bounds.push_back(k1);
+      } else if (!g_pipeline_fracs.empty()) {  // pipeline_fracs(): several first chunks
+        int64_t prev = 0;
+        for (double f : g_pipeline_fracs) {
+          const int64_t k1 = std::min<int64_t>(K - 1, std::max<int64_t>(prev + 1, static_cast<int64_t>(K * f)));
+          if (k1 > prev && k1 < K) bounds.push_back(k1), prev = k1;
+        }
       } else {
         bounds.push_back(std::min<int64_t>(K - 1, std::max<int64_t>(1, static_cast<int64_t>(K * frac))));
       }
     }
     bounds.push_back(K);
-    st.lap(kTChecks);
+    st.lap(kTSpec);
     std::vector<int64_t> ptrs(static_cast<size_t>(K * L));
     for (int64_t l = 0; l < L; ++l) ptrs[l] = reinterpret_cast<int64_t>(row0[l].data_ptr());
     Walk w{&dtypes, &sizes, static_cast<c10::DeviceIndex>(dev), nullptr, 0};
@@ -1417,6 +1496,9 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
                     with_l2 ? l2sq.data_ptr<float>() + done : nullptr, &rc, st) != 0)
         Py_RETURN_NONE;
       if (rc != 0) return Py_BuildValue("(iOdO)", rc, Py_None, job_bytes, Py_None);
+      if (done == 0)
+        g_timers[kTFirstLaunch] +=
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_entry).count();
       done = k1;
     }
     std::vector<PyObject*> wrapped(L);
@@ -1602,12 +1684,442 @@ PyObject* server_pairs(PyObject*, PyObject* args) {
   }
 }
 
+// ------------------------------------------------------------------ lazy results, natively
+// tree_util.WeightedTree, PendingSum and _Chain are Python subclasses of the three base
+// types below: their fields are these C members, their methods stay Python. The two hot
+// calls of the library running-sum loop (fedjax/algorithms/fed_avg.py:137-138, and the six
+// other algorithms of SURVEY §8f row 1) — tree_weight(delta, n) and tree_add(s, that) — are
+// METH_FASTCALL functions here that build those objects directly; tree_util installs them as
+// tree_util.tree_weight / tree_add (fast_install). Anything but the fast case calls the
+// Python function they replace, which then decides exactly as before.
+
+struct WTObject {
+  PyObject_HEAD
+  PyObject* tree;
+  PyObject* weight;
+  PyObject* cap;
+  PyObject* value;
+};
+
+struct ChainObject {
+  PyObject_HEAD
+  PyObject* tip;
+  PyObject* buf;
+  PyObject* budget;
+};
+
+struct PSObject {
+  PyObject_HEAD
+  PyObject* root;
+  PyObject* parent;
+  PyObject* cap;
+  PyObject* weight;
+  PyObject* value;
+  PyObject* chain;
+  PyObject* ticket;
+  PyObject* ref;
+  PyObject* bcap;
+  long long n, bytes, idx, tok;
+  PyObject* weakreflist;
+};
+
+#define FJ_OBJ_MEMBER(T, f) {const_cast<char*>("_" #f), T_OBJECT, offsetof(T, f), 0, nullptr}
+#define FJ_LL_MEMBER(T, f) {const_cast<char*>("_" #f), T_LONGLONG, offsetof(T, f), 0, nullptr}
+
+PyMemberDef kWTMembers[] = {FJ_OBJ_MEMBER(WTObject, tree), FJ_OBJ_MEMBER(WTObject, weight),
+                            FJ_OBJ_MEMBER(WTObject, cap), FJ_OBJ_MEMBER(WTObject, value), {nullptr}};
+PyMemberDef kChainMembers[] = {{const_cast<char*>("tip"), T_OBJECT, offsetof(ChainObject, tip), 0, nullptr},
+                               {const_cast<char*>("buf"), T_OBJECT, offsetof(ChainObject, buf), 0, nullptr},
+                               {const_cast<char*>("budget"), T_OBJECT, offsetof(ChainObject, budget), 0, nullptr},
+                               {nullptr}};
+PyMemberDef kPSMembers[] = {FJ_OBJ_MEMBER(PSObject, root),   FJ_OBJ_MEMBER(PSObject, parent),
+                            FJ_OBJ_MEMBER(PSObject, cap),    FJ_OBJ_MEMBER(PSObject, weight),
+                            FJ_OBJ_MEMBER(PSObject, value),  FJ_OBJ_MEMBER(PSObject, chain),
+                            FJ_OBJ_MEMBER(PSObject, ticket), FJ_OBJ_MEMBER(PSObject, ref),
+                            FJ_OBJ_MEMBER(PSObject, bcap),   FJ_LL_MEMBER(PSObject, n),
+                            FJ_LL_MEMBER(PSObject, bytes),   FJ_LL_MEMBER(PSObject, idx),
+                            FJ_LL_MEMBER(PSObject, tok),
+                            {const_cast<char*>("__weaklistoffset__"), T_PYSSIZET, offsetof(PSObject, weakreflist),
+                             READONLY, nullptr},
+                            {nullptr}};
+
+int wt_traverse(PyObject* o, visitproc visit, void* arg) {
+  auto* x = reinterpret_cast<WTObject*>(o);
+  Py_VISIT(Py_TYPE(o));
+  Py_VISIT(x->tree);
+  Py_VISIT(x->weight);
+  Py_VISIT(x->cap);
+  Py_VISIT(x->value);
+  return 0;
+}
+int wt_clear(PyObject* o) {
+  auto* x = reinterpret_cast<WTObject*>(o);
+  Py_CLEAR(x->tree);
+  Py_CLEAR(x->weight);
+  Py_CLEAR(x->cap);
+  Py_CLEAR(x->value);
+  return 0;
+}
+void wt_dealloc(PyObject* o) {
+  PyTypeObject* tp = Py_TYPE(o);
+  PyObject_GC_UnTrack(o);
+  wt_clear(o);
+  tp->tp_free(o);
+  Py_DECREF(tp);
+}
+
+int chain_traverse(PyObject* o, visitproc visit, void* arg) {
+  auto* x = reinterpret_cast<ChainObject*>(o);
+  Py_VISIT(Py_TYPE(o));
+  Py_VISIT(x->tip);
+  Py_VISIT(x->buf);
+  Py_VISIT(x->budget);
+  return 0;
+}
+int chain_clear(PyObject* o) {
+  auto* x = reinterpret_cast<ChainObject*>(o);
+  Py_CLEAR(x->tip);
+  Py_CLEAR(x->buf);
+  Py_CLEAR(x->budget);
+  return 0;
+}
+void chain_dealloc(PyObject* o) {
+  PyTypeObject* tp = Py_TYPE(o);
+  PyObject_GC_UnTrack(o);
+  chain_clear(o);
+  tp->tp_free(o);
+  Py_DECREF(tp);
+}
+
+int ps_traverse(PyObject* o, visitproc visit, void* arg) {
+  auto* x = reinterpret_cast<PSObject*>(o);
+  Py_VISIT(Py_TYPE(o));
+  Py_VISIT(x->root);
+  Py_VISIT(x->parent);
+  Py_VISIT(x->cap);
+  Py_VISIT(x->weight);
+  Py_VISIT(x->value);
+  Py_VISIT(x->chain);
+  Py_VISIT(x->ticket);
+  Py_VISIT(x->ref);
+  Py_VISIT(x->bcap);
+  return 0;
+}
+int ps_clear(PyObject* o) {
+  auto* x = reinterpret_cast<PSObject*>(o);
+  Py_CLEAR(x->root);
+  Py_CLEAR(x->parent);
+  Py_CLEAR(x->cap);
+  Py_CLEAR(x->weight);
+  Py_CLEAR(x->value);
+  Py_CLEAR(x->chain);
+  Py_CLEAR(x->ticket);
+  Py_CLEAR(x->ref);
+  Py_CLEAR(x->bcap);
+  return 0;
+}
+void ps_dealloc(PyObject* o) {
+  PyTypeObject* tp = Py_TYPE(o);
+  PyObject_GC_UnTrack(o);
+  if (reinterpret_cast<PSObject*>(o)->weakreflist) PyObject_ClearWeakRefs(o);
+  ps_clear(o);
+  tp->tp_free(o);
+  Py_DECREF(tp);
+}
+
+PyType_Slot kWTSlots[] = {{Py_tp_dealloc, reinterpret_cast<void*>(wt_dealloc)},
+                          {Py_tp_traverse, reinterpret_cast<void*>(wt_traverse)},
+                          {Py_tp_clear, reinterpret_cast<void*>(wt_clear)},
+                          {Py_tp_members, kWTMembers},
+                          {Py_tp_new, reinterpret_cast<void*>(PyType_GenericNew)},
+                          {Py_tp_doc, const_cast<char*>("fields of tree_util.WeightedTree")},
+                          {0, nullptr}};
+PyType_Slot kChainSlots[] = {{Py_tp_dealloc, reinterpret_cast<void*>(chain_dealloc)},
+                             {Py_tp_traverse, reinterpret_cast<void*>(chain_traverse)},
+                             {Py_tp_clear, reinterpret_cast<void*>(chain_clear)},
+                             {Py_tp_members, kChainMembers},
+                             {Py_tp_new, reinterpret_cast<void*>(PyType_GenericNew)},
+                             {Py_tp_doc, const_cast<char*>("fields of tree_util._Chain")},
+                             {0, nullptr}};
+PyType_Slot kPSSlots[] = {{Py_tp_dealloc, reinterpret_cast<void*>(ps_dealloc)},
+                          {Py_tp_traverse, reinterpret_cast<void*>(ps_traverse)},
+                          {Py_tp_clear, reinterpret_cast<void*>(ps_clear)},
+                          {Py_tp_members, kPSMembers},
+                          {Py_tp_new, reinterpret_cast<void*>(PyType_GenericNew)},
+                          {Py_tp_doc, const_cast<char*>("fields of tree_util.PendingSum")},
+                          {0, nullptr}};
+constexpr unsigned kBaseFlags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_BASETYPE | Py_TPFLAGS_HAVE_GC;
+PyType_Spec kWTSpec = {"_fjhost.WeightedBase", sizeof(WTObject), 0, kBaseFlags, kWTSlots};
+PyType_Spec kChainSpec = {"_fjhost.ChainBase", sizeof(ChainObject), 0, kBaseFlags, kChainSlots};
+PyType_Spec kPSSpec = {"_fjhost.PendingBase", sizeof(PSObject), 0, kBaseFlags, kPSSlots};
+
+struct FastState {
+  PyTypeObject* wt = nullptr;     // tree_util.WeightedTree
+  PyTypeObject* ps = nullptr;     // tree_util.PendingSum
+  PyTypeObject* chain = nullptr;  // tree_util._Chain
+  PyObject* py_tree_weight = nullptr;  // the Python functions the fast calls fall back to
+  PyObject* py_tree_add = nullptr;
+  // tree_util.set_deferred_sums
+  bool defer = true;
+  long long max_clients = 4095, flush_bytes = 1LL << 30, flush_clients = 16;
+  PyObject* last = nullptr;  // weak reference to the most recent PendingSum link
+};
+FastState g_fast;
+
+// fast_install(WeightedTree, PendingSum, _Chain, py_tree_weight, py_tree_add)
+PyObject* fast_install(PyObject*, PyObject* args) {
+  PyObject *wt, *ps, *ch, *ftw, *fta;
+  if (!PyArg_ParseTuple(args, "O!O!O!OO", &PyType_Type, &wt, &PyType_Type, &ps, &PyType_Type, &ch, &ftw, &fta))
+    return nullptr;
+  if (!PyCallable_Check(ftw) || !PyCallable_Check(fta)) {
+    PyErr_SetString(PyExc_TypeError, "fast_install: fallbacks must be callable");
+    return nullptr;
+  }
+  Py_INCREF(wt), Py_INCREF(ps), Py_INCREF(ch), Py_INCREF(ftw), Py_INCREF(fta);
+  Py_XSETREF(g_fast.wt, reinterpret_cast<PyTypeObject*>(wt));
+  Py_XSETREF(g_fast.ps, reinterpret_cast<PyTypeObject*>(ps));
+  Py_XSETREF(g_fast.chain, reinterpret_cast<PyTypeObject*>(ch));
+  Py_XSETREF(g_fast.py_tree_weight, ftw);
+  Py_XSETREF(g_fast.py_tree_add, fta);
+  Py_RETURN_NONE;
+}
+
+// fast_config(enabled, max_clients, flush_bytes, flush_clients): tree_util.set_deferred_sums
+PyObject* fast_config(PyObject*, PyObject* args) {
+  int en;
+  long long mc, fb, fc;
+  if (!PyArg_ParseTuple(args, "pLLL", &en, &mc, &fb, &fc)) return nullptr;
+  g_fast.defer = en != 0;
+  g_fast.max_clients = mc;
+  g_fast.flush_bytes = fb;
+  g_fast.flush_clients = fc;
+  Py_RETURN_NONE;
+}
+
+// set_last(node) / last() -> node | None: the most recent PendingSum link (weakly held),
+// whose delta a following tree_l2_norm may take from the chain's fold (tree_util._lazy_norm)
+PyObject* set_last(PyObject*, PyObject* node) {
+  PyObject* wr = PyWeakref_NewRef(node, nullptr);
+  if (!wr) return nullptr;
+  Py_XSETREF(g_fast.last, wr);
+  Py_RETURN_NONE;
+}
+PyObject* last(PyObject*, PyObject*) {
+  PyObject* o = g_fast.last ? PyWeakref_GetObject(g_fast.last) : Py_None;
+  Py_INCREF(o);
+  return o;
+}
+
+// Python int / float weight that tree_weight defers (|int| < 2**53: exact in float32's path)
+inline int deferrable_weight(PyObject* w) {
+  if (PyFloat_CheckExact(w)) return 1;
+  if (!PyLong_CheckExact(w)) return 0;
+  int of = 0;
+  const long long v = PyLong_AsLongLongAndOverflow(w, &of);
+  if (v == -1 && PyErr_Occurred()) return -1;
+  return (!of && v > -(1LL << 53) && v < (1LL << 53)) ? 1 : 0;
+}
+
+// tree_weight(pytree, weight): tree_util.tree_weight (tree_util.py:29-32). A Python-number
+// weight and a pytree of float32 device tensors give a WeightedTree holding the capture;
+// anything else is the Python function's.
+PyObject* fast_tree_weight(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
+  if (!g_fast.wt || !g_fast.py_tree_weight) {
+    PyErr_SetString(PyExc_RuntimeError, "fedjax_amd.tree_util is not installed (fast_install)");
+    return nullptr;
+  }
+  if (nargs == 2 && kwnames == nullptr) {
+    const int ok = deferrable_weight(args[1]);
+    if (ok < 0) return nullptr;
+    if (ok) {
+      PyObject* cap = capture_impl(args[0], -1);
+      if (!cap) return nullptr;
+      if (cap != Py_None) {
+        auto* o = reinterpret_cast<WTObject*>(g_fast.wt->tp_alloc(g_fast.wt, 0));
+        if (!o) {
+          Py_DECREF(cap);
+          return nullptr;
+        }
+        Py_INCREF(args[0]);
+        o->tree = args[0];
+        Py_INCREF(args[1]);
+        o->weight = args[1];
+        o->cap = cap;
+        return reinterpret_cast<PyObject*>(o);
+      }
+      Py_DECREF(cap);
+    }
+  }
+  return PyObject_Vectorcall(g_fast.py_tree_weight, args, nargs, kwnames);
+}
+
+// tree_add(left, right): tree_util.tree_add (tree_util.py:47-50). The fast case is the
+// running sum's append, s = tree_add(s, tree_weight(x, n)) with s a live PendingSum at the
+// tip of its chain, the capture's structure token equal to the sum's, and no chain limit
+// reached (tree_util._defer's checks): the new link is built here, exactly as PendingSum's
+// __init__ builds it. Anything else is the Python function's.
+PyObject* fast_tree_add(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
+  if (!g_fast.ps || !g_fast.py_tree_add) {
+    PyErr_SetString(PyExc_RuntimeError, "fedjax_amd.tree_util is not installed (fast_install)");
+    return nullptr;
+  }
+  if (nargs == 2 && kwnames == nullptr && g_fast.defer && Py_TYPE(args[1]) == g_fast.wt &&
+      Py_TYPE(args[0]) == g_fast.ps) {
+    auto* r = reinterpret_cast<WTObject*>(args[1]);
+    auto* p = reinterpret_cast<PSObject*>(args[0]);
+    auto* ch = reinterpret_cast<ChainObject*>(p->chain);
+    if (r->tree && r->tree != Py_None && r->cap && PyTuple_CheckExact(r->cap) && PyTuple_GET_SIZE(r->cap) >= 4 &&
+        (!p->value || p->value == Py_None) && p->tok >= 0 && ch && Py_TYPE(ch) == g_fast.chain &&
+        ch->tip == args[0] && ch->budget && PyLong_CheckExact(ch->budget)) {
+      const long long tok = PyLong_AsLongLong(PyTuple_GET_ITEM(r->cap, 3));
+      const long long nb = PyLong_AsLongLong(PyTuple_GET_ITEM(r->cap, 2));
+      const long long budget = PyLong_AsLongLong(ch->budget);
+      if (PyErr_Occurred()) return nullptr;
+      if (tok == p->tok && p->n + 1 <= g_fast.max_clients && p->bytes + nb <= budget &&
+          !(p->bytes >= g_fast.flush_bytes && p->n >= g_fast.flush_clients)) {
+        auto* q = reinterpret_cast<PSObject*>(g_fast.ps->tp_alloc(g_fast.ps, 0));
+        if (!q) return nullptr;
+        Py_INCREF(p);
+        q->parent = args[0];
+        Py_INCREF(r->cap);
+        q->cap = r->cap;
+        Py_INCREF(r->weight);
+        q->weight = r->weight;
+        Py_INCREF(ch);
+        q->chain = reinterpret_cast<PyObject*>(ch);
+        Py_XINCREF(p->ref);
+        q->ref = p->ref;
+        q->n = p->n + 1;
+        q->bytes = p->bytes + nb;
+        q->idx = p->idx + 1;
+        q->tok = p->tok;
+        Py_INCREF(q);
+        Py_XSETREF(ch->tip, reinterpret_cast<PyObject*>(q));
+        PyObject* wr = PyWeakref_NewRef(reinterpret_cast<PyObject*>(q), nullptr);
+        if (!wr) {
+          Py_DECREF(q);
+          return nullptr;
+        }
+        Py_XSETREF(g_fast.last, wr);
+        return reinterpret_cast<PyObject*>(q);
+      }
+    }
+  }
+  return PyObject_Vectorcall(g_fast.py_tree_add, args, nargs, kwnames);
+}
+
+// zeros_like(tree) -> tree | None: tree_util.tree_zeros_like (tree_util.py:41-44) for a plain
+// dict / list / tuple / None pytree of float32 device tensors (<= 64 leaves, one device): ONE
+// zeroed allocation, and every leaf its own tensor over a 256-byte aligned slice of it (its
+// own TensorImpl and in-place version counter, not a view: writing one leaf does not bump
+// the others' versions). The result's dict keys are sorted, as jax.tree.map builds them.
+// None: not this case (the Python path decides).
+PyObject* zeros_like(PyObject*, PyObject* tree) {
+  try {
+    PWalk w;
+    w.K = 1;
+    w.leaves[0].reserve(16);
+    const int rc = pwalk(&tree, w, 0);
+    if (rc < 0) return nullptr;
+    const size_t L = w.leaves[0].size();
+    if (rc > 0 || L == 0) Py_RETURN_NONE;
+    std::vector<int64_t> offs(L + 1, 0);
+    int dev = -1;
+    for (size_t l = 0; l < L; ++l) {
+      const at::Tensor& t = THPVariable_Unpack(w.leaves[0][l]);
+      if (t.layout() != c10::kStrided || t.scalar_type() != at::kFloat || !t.is_cuda()) Py_RETURN_NONE;
+      if (dev < 0) dev = t.get_device();
+      if (t.get_device() != dev) Py_RETURN_NONE;
+      offs[l + 1] = offs[l] + (t.numel() + 63) / 64 * 64;
+    }
+    const at::Tensor& t0 = THPVariable_Unpack(w.leaves[0][0]);
+    at::Tensor flat = at::zeros({std::max<int64_t>(offs[L], 1)}, t0.options());
+    std::vector<PyObject*> wrapped(L, nullptr);
+    struct Drop {
+      std::vector<PyObject*>& v;
+      ~Drop() {
+        for (PyObject* o : v) Py_XDECREF(o);  // (rebuild takes the ones it uses)
+      }
+    } drop{wrapped};
+    for (size_t l = 0; l < L; ++l) {
+      at::Tensor leaf = at::detail::make_tensor<c10::TensorImpl>(c10::Storage(flat.storage()), flat.key_set(),
+                                                                 flat.dtype());
+      leaf.unsafeGetTensorImpl()->set_storage_offset(offs[l]);
+      leaf.unsafeGetTensorImpl()->set_sizes_contiguous(THPVariable_Unpack(w.leaves[0][l]).sizes());
+      wrapped[l] = THPVariable_Wrap(std::move(leaf));
+      if (!wrapped[l]) return nullptr;
+    }
+    size_t i = 0, ki = 0;
+    return rebuild(tree, wrapped.data(), i, w.keys, ki);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
+// fold_chain(node, scale, has_scale, nt_min_bytes, plan_fn, wsum_fn, wsum_l2_fn, l2_ws_bytes_fn)
+//     -> (rc, tree) | k | None
+// tree_util._fold_chain for a PendingSum link, walked natively: the unfolded links from the
+// nearest folded ancestor (or the chain's root), the base (the root's tree, or the folded
+// ancestor's value), then fold_caps over [base capture, link captures] with weights
+// [1, n_1 .. n_k]. None (nothing launched) when the run has no captured base or a lazy norm
+// waits on one of its links (the Python path also fills the norms); k: capture k is stale.
+PyObject* fold_chain(PyObject*, PyObject* args) {
+  PyObject* node;
+  double scale, nt_min;
+  int has_scale;
+  unsigned long long plan_addr, wsum_addr, l2_addr, l2ws_addr;
+  if (!PyArg_ParseTuple(args, "OdpdKKKK", &node, &scale, &has_scale, &nt_min, &plan_addr, &wsum_addr, &l2_addr,
+                        &l2ws_addr))
+    return nullptr;
+  if (!g_fast.ps || Py_TYPE(node) != g_fast.ps) Py_RETURN_NONE;
+  thread_local std::vector<PSObject*> links;
+  links.clear();
+  PyObject* base = nullptr;
+  for (auto* p = reinterpret_cast<PSObject*>(node);;) {
+    if (p->value && p->value != Py_None) {
+      base = p->value;
+      break;
+    }
+    if (p->ticket && p->ticket != Py_None) Py_RETURN_NONE;  // a lazy norm waits: the Python path
+    links.push_back(p);
+    if (!p->parent || p->parent == Py_None) {
+      base = p->root;
+      break;
+    }
+    if (Py_TYPE(p->parent) != g_fast.ps) Py_RETURN_NONE;
+    p = reinterpret_cast<PSObject*>(p->parent);
+  }
+  if (links.empty() || !base) Py_RETURN_NONE;
+  std::reverse(links.begin(), links.end());
+  PyObject* bcap = links[0]->bcap;
+  if (!bcap || bcap == Py_None) Py_RETURN_NONE;
+  const Py_ssize_t K = static_cast<Py_ssize_t>(links.size()) + 1;
+  thread_local std::vector<PyObject*> caps, weights;
+  caps.resize(K);
+  weights.resize(K);
+  static PyObject* one = PyLong_FromLong(1);
+  caps[0] = bcap;
+  weights[0] = one;
+  for (Py_ssize_t j = 1; j < K; ++j) {
+    caps[j] = links[j - 1]->cap;
+    weights[j] = links[j - 1]->weight;
+    if (!caps[j] || !weights[j]) Py_RETURN_NONE;
+  }
+  Py_INCREF(base);  // (the walk's references are borrowed from the chain, which `node` holds)
+  PyObject* got = fold_caps_impl(base, caps.data(), weights.data(), K, scale, has_scale != 0, nt_min, plan_addr,
+                                 wsum_addr, l2_addr, l2ws_addr, Py_None);
+  Py_DECREF(base);
+  return got;
+}
+
 PyObject* image_paths(PyObject*, PyObject*) {
   return Py_BuildValue("{s:L,s:L}", "kernel_args", g_image_karg, "uploaded", g_image_upload);
 }
 
 PyObject* host_timers(PyObject*, PyObject*) {
-  static const char* names[kTPhases] = {"checks", "outputs", "plan", "image", "upload", "launch", "wrap"};
+  static const char* names[kTPhases] = {"spec",  "checks", "outputs", "plan",           "image",
+                                        "upload", "launch", "wrap",    "first_launch_at"};
   PyObject* d = PyDict_New();
   if (!d) return nullptr;
   for (int i = 0; i < kTPhases; ++i) {
@@ -1640,6 +2152,23 @@ PyMethodDef kMethods[] = {
     {"fold_table", fold_table, METH_VARARGS, "plan image + output leaves + fjagg_wsum_ptrs launch (see fjhost.cpp)"},
     {"mean_pairs", mean_pairs, METH_VARARGS, "tree_mean of (pytree, weight) pairs in one native call (see fjhost.cpp)"},
     {"server_pairs", server_pairs, METH_VARARGS, "fused_tree_mean_update in one native call (see fjhost.cpp)"},
+    {"zeros_like", zeros_like, METH_O, "tree_zeros_like of a float32 device pytree: one allocation, own leaves"},
+    {"pipeline_fracs", pipeline_fracs, METH_O, "chunk ends (fractions of K) of tree_mean's fold-bound pipeline"},
+    {"fold_chain", fold_chain, METH_VARARGS, "a PendingSum's deferred fold, its links walked natively"},
+    {"fast_install", fast_install, METH_VARARGS, "register tree_util's lazy classes and Python fallbacks"},
+    {"fast_config", fast_config, METH_VARARGS, "deferred-sum settings (tree_util.set_deferred_sums)"},
+    {"set_last", set_last, METH_O, "remember the most recent PendingSum link (weakly)"},
+    {"last", last, METH_NOARGS, "the most recent PendingSum link, or None"},
+    {"tree_weight", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_tree_weight)),
+     METH_FASTCALL | METH_KEYWORDS,
+     "tree_weight(pytree, weight)\n--\n\nWeights tree leaves by weight (fedjax/core/tree_util.py:29-32).\n\n"
+     "Float32 device pytrees (<= 64 leaves) with a Python-number weight give a WeightedTree\n"
+     "(deferred, fused into the tree_add that consumes it); anything else is computed now\n"
+     "by the pytree kernel (fedjax_amd.tree_util._tree_weight_py)."},
+    {"tree_add", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_tree_add)), METH_FASTCALL | METH_KEYWORDS,
+     "tree_add(left, right)\n--\n\nAdds two trees together (fedjax/core/tree_util.py:47-50).\n\n"
+     "The running sum s = tree_add(s, tree_weight(x, n)) appends to a deferred PendingSum\n"
+     "(one launch folds the round); every other case is fedjax_amd.tree_util._tree_add_py."},
     {nullptr, nullptr, 0, nullptr},
 };
 
@@ -1648,4 +2177,18 @@ PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_fjhost", "native host side of th
 
 }  // namespace
 
-PyMODINIT_FUNC PyInit__fjhost(void) { return PyModule_Create(&kModule); }
+PyMODINIT_FUNC PyInit__fjhost(void) {
+  PyObject* m = PyModule_Create(&kModule);
+  if (!m) return nullptr;
+  const std::pair<const char*, PyType_Spec*> types[] = {
+      {"WeightedBase", &kWTSpec}, {"ChainBase", &kChainSpec}, {"PendingBase", &kPSSpec}};
+  for (const auto& t : types) {
+    PyObject* tp = PyType_FromSpec(t.second);
+    if (!tp || PyModule_AddObject(m, t.first, tp) != 0) {
+      Py_XDECREF(tp);
+      Py_DECREF(m);
+      return nullptr;
+    }
+  }
+  return m;
+}

@@ -542,12 +542,8 @@ _STALE = -100  # fjhost.leaf_fold: a captured operand changed since tree_weight
 _NORMS: "collections.deque" = None  # (capture, l2sq, l2) of the last fused tree_add calls
 
 
-_HOST = None  # the _fjhost module (set with _TREE_ADDRS: the per-call paths skip _lib.host())
-
-
 def _tree_addrs():
-    global _TREE_ADDRS, _NORMS, _HOST
-    _HOST = _lib.host()
+    global _TREE_ADDRS, _NORMS
     if _TREE_ADDRS is None:
         import collections
         lib = _lib.load()
@@ -593,7 +589,10 @@ def _leaf_fold(trees, weights, caps, scale=None, norm_operand=-1, no_out=False):
     return out, sq, l2
 
 
-class WeightedTree:
+_HOST = _lib.host()  # the _fjhost module: native walks, and the base types of the lazy results below
+
+
+class WeightedTree(_HOST.WeightedBase):
     """``tree_weight(tree, w)`` of a pytree of float32 device tensors, not yet computed.
 
     The multiply is deferred so that ``tree_add(s, tree_weight(x, n))`` — the running sum
@@ -616,7 +615,7 @@ class WeightedTree:
     type matters.
     """
 
-    __slots__ = ("_tree", "_weight", "_cap", "_value")
+    __slots__ = ()  # fields _tree, _weight, _cap, _value: fjhost's WeightedBase
 
     def __init__(self, tree, weight, cap):
         self._tree, self._weight, self._cap, self._value = tree, weight, cap, None
@@ -704,6 +703,7 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
         _DEFER["flush_bytes"] = max(0, int(flush_bytes))
     if flush_clients is not None:
         _DEFER["flush_clients"] = max(1, int(flush_clients))
+    _HOST.fast_config(_DEFER["enabled"], _DEFER["max_clients"], _DEFER["flush_bytes"], _DEFER["flush_clients"])
 
 
 def _defer_budget(device: torch.device) -> int:
@@ -719,11 +719,11 @@ def _defer_budget(device: torch.device) -> int:
     return got
 
 
-class _Chain:
+class _Chain(_HOST.ChainBase):
     """The linear run of PendingSum links one norm buffer serves: float32 [2, n] on the
     device, row 0 = squared l2 norms, row 1 = l2 norms of the clients, by link index."""
 
-    __slots__ = ("tip", "buf", "budget")
+    __slots__ = ()  # fields tip, buf, budget: fjhost's ChainBase
 
     def __init__(self):
         self.tip, self.buf, self.budget = None, None, None  # budget: _defer_budget, on first use
@@ -774,7 +774,7 @@ def _flush_views(x) -> None:
             _flush_views(y)
 
 
-class PendingSum:
+class PendingSum(_HOST.PendingBase):
     """``s = tree_add(s, tree_weight(x, n))`` repeated over clients, not yet computed.
 
     FedJAX's algorithms build the round's running sum this way, one client at a time
@@ -800,8 +800,9 @@ class PendingSum:
     ``materialize()`` where the concrete container type matters.
     """
 
-    __slots__ = ("_root", "_parent", "_cap", "_weight", "_n", "_bytes", "_value", "_chain", "_idx", "_ticket",
-                 "_ref", "_bcap", "_tok", "__weakref__")
+    # fields _root, _parent, _cap, _weight, _n, _bytes, _value, _chain, _idx, _ticket, _ref, _bcap,
+    # _tok and weak-reference support: fjhost's PendingBase (fjhost.tree_add builds links natively)
+    __slots__ = ()
 
     def __init__(self, root, parent, cap, weight, ref, bcap=None, tok=-1):
         self._root, self._parent, self._cap, self._weight, self._value = root, parent, cap, weight, None
@@ -834,8 +835,7 @@ class PendingSum:
 
     def materialize(self) -> PyTree:
         if self._value is None:
-            base, links = self._links()
-            self._value = _fold_chain(base, links, None)
+            self._value = _fold_pending(self, None)
             self._root = self._parent = self._cap = self._ref = self._bcap = None  # the deltas can go
         return self._value
 
@@ -850,10 +850,28 @@ class PendingSum:
 
 
 pytree.register_lazy_type(PendingSum, PendingSum.materialize)
-_LAST = None  # weakref to the most recent PendingSum link (tree_l2_norm of its delta is lazy)
 
 
 _FOLD_CAPS = os.environ.get("FJAGG_FOLD_CAPS", "1") != "0"  # 0: the Python path below (A/B runs)
+
+
+def _fold_pending(node: "PendingSum", scale):
+    """The fold of a PendingSum's unfolded links [* f32(scale)]: fjhost.fold_chain walks the
+    links natively and folds them in one launch (fold_caps); when a lazy norm waits on a
+    link, or the run has no captured base, the Python walk below (_fold_chain) does it."""
+    if _FOLD_CAPS:
+        if _ENTRY_ADDRS is None:
+            _native_fold_addrs()
+        got = _HOST.fold_chain(node, float(np.float32(scale)) if scale is not None else 1.0, scale is not None,
+                               float(NONTEMPORAL_MIN_BYTES), *_ENTRY_ADDRS)
+        if type(got) is int:
+            _stale_chain(got)
+        if got is not None:
+            rc, tree = got
+            _lib.check(rc, "fjagg_wsum_ptrs")
+            return tree
+    base, links = node._links()
+    return _fold_chain(base, links, scale)
 
 
 def _fold_chain(base, links, scale):
@@ -871,7 +889,7 @@ def _fold_chain(base, links, scale):
         if _ENTRY_ADDRS is None:
             _native_fold_addrs()
         sc = float(np.float32(scale)) if scale is not None else 1.0
-        got = (_HOST or _lib.host()).fold_caps(base, [bcap] + [n._cap for n in links], [1] + [n._weight for n in links], sc,
+        got = _HOST.fold_caps(base, [bcap] + [n._cap for n in links], [1] + [n._weight for n in links], sc,
                               scale is not None, float(NONTEMPORAL_MIN_BYTES), *_ENTRY_ADDRS, l2sq)
         if type(got) is int:
             _stale_chain(got)
@@ -941,10 +959,10 @@ def _fill_norms(links, waiting, l2sq):
 
 def _lazy_norm(pytree_, row: int):
     """A _NormView of the delta just added to a deferred sum, or None."""
-    node = _LAST() if _LAST is not None else None
+    node = _HOST.last()  # the most recent PendingSum link (weakly held by fjhost)
     if node is None or node._value is not None or node._cap is None:
         return None
-    host = _HOST if _HOST is not None else _lib.host()
+    host = _HOST
     if not host.matches(pytree_, node._cap[0], node._cap[1]):
         return None
     ch = node._chain
@@ -967,8 +985,7 @@ def _defer(sum_side, item, item_weight, item_cap):
     walk: the link holds the captured leaves — the values tree_weight saw, as the
     reference's eager tree_weight would — and the fold checks their versions. Otherwise
     ``fjhost.append_check`` walks the sum and the item together."""
-    global _LAST
-    host = _HOST if _HOST is not None else _lib.host()
+    host = _HOST
     if type(sum_side) is PendingSum:
         parent, root = sum_side, None
         live = sum_side._value is None
@@ -1000,21 +1017,21 @@ def _defer(sum_side, item, item_weight, item_cap):
             parent.materialize()  # bound the chain: fold what is pending, continue from it
             bcap = host.capture(parent._value, -1)
     node = PendingSum(root, parent, cap, item_weight, ref, bcap, tok)
-    _LAST = weakref.ref(node)
+    host.set_last(node)
     return node
 
 
-def tree_weight(pytree_: PyTree, weight: float) -> PyTree:
+def _tree_weight_py(pytree_: PyTree, weight: float) -> PyTree:
     """Weights tree leaves by weight (tree_util.py:29-32).
 
     Float32 device pytrees (<= 64 leaves) with a Python-number weight give a
     :class:`WeightedTree` (deferred, fused into the tree_add that consumes it);
-    anything else is computed now by the pytree kernel."""
+    anything else is computed now by the pytree kernel. :func:`tree_weight` is the native
+    fjhost.tree_weight, which builds the WeightedTree itself in the fast case and calls
+    this function otherwise."""
     tw = type(weight)
     w = weight if (tw is float or tw is int) else _host_weight(weight)
     if (type(w) is float or (type(w) is int and -_F32_EXACT_INT < w < _F32_EXACT_INT)):
-        if _TREE_ADDRS is None:
-            _tree_addrs()
         cap = _HOST.capture(pytree_, -1)
         if cap is not None:
             return WeightedTree(pytree_, w, cap)
@@ -1029,10 +1046,9 @@ def tree_inverse_weight(pytree_: PyTree, weight: float) -> PyTree:
     """Weights tree leaves by ``1 / weight`` (tree_util.py:35-38); computed now. A
     :class:`PendingSum` is folded with the ``1/W`` scale in the same launch
     (``fl(s * f32(1/W))``, the reference's bits) — fed_avg.py:145-146 in one pass."""
-    inv = _inverse(_host_weight(weight))
+    inv = _inverse(weight if type(weight) is float or type(weight) is int else _host_weight(weight))
     if type(pytree_) is PendingSum and pytree_._value is None:
-        base, links = pytree_._links()
-        return _fold_chain(base, links, inv)
+        return _fold_pending(pytree_, inv)
     pytree_ = _eager(pytree_)
     if type(inv) is float:
         got = _leaf_fold([pytree_], [inv], [None])
@@ -1044,19 +1060,18 @@ def tree_inverse_weight(pytree_: PyTree, weight: float) -> PyTree:
 def tree_zeros_like(pytree_: PyTree) -> PyTree:
     """Creates a tree with zeros with same structure as the input (tree_util.py:41-44).
 
-    Float32 tensor leaves (the running-sum base of fed_avg.py:132) get one zeroed
-    allocation carved into 256-byte-aligned leaf views: one allocation and one memset
-    instead of one per leaf (the views are disjoint, so each leaf is its own array)."""
+    A plain pytree of float32 device tensors (the running-sum base of fed_avg.py:132) is
+    zeroed as ONE allocation (fjhost.zeros_like: one allocation and one memset instead of
+    one per leaf). Each leaf is still its own tensor with its own in-place version counter
+    over a 256-byte aligned slice of that storage, so writing one leaf never marks the
+    others modified. The slices share one storage: a leaf kept alive keeps the whole
+    buffer alive, and ``torch.save`` of a single leaf writes every leaf's bytes. Other
+    pytrees get one ``torch.zeros`` per leaf."""
+    got = _HOST.zeros_like(pytree_)
+    if got is not None:
+        return got
     leaves, td = pytree.flatten(pytree_)
     device = _find_device(leaves)
-    if leaves and all(type(x) is torch.Tensor and x.dtype is torch.float32 for x in leaves):
-        shapes = [x.shape for x in leaves]
-        sizes = [x.numel() for x in leaves]
-        offs = [0]
-        for n in sizes:
-            offs.append(offs[-1] + (n + 63) // 64 * 64)
-        flat = torch.zeros(offs[-1], dtype=torch.float32, device=device)
-        return pytree.unflatten(td, [flat[o:o + n].view(sh) for o, n, sh in zip(offs, sizes, shapes)])
     out = []
     for x in leaves:
         t = _to_tensor(x)
@@ -1067,11 +1082,14 @@ def tree_zeros_like(pytree_: PyTree) -> PyTree:
     return pytree.unflatten(td, out)
 
 
-def tree_add(left: PyTree, right: PyTree) -> PyTree:
+def _tree_add_py(left: PyTree, right: PyTree) -> PyTree:
     """Adds two trees together (tree_util.py:47-50): x*1 is exact, so a K=2 fold
     with unit weights is the reference's ``jnp.add``. A :class:`WeightedTree` operand
     is folded in the same launch (``fl(s + fl(x * f32(n)))``), which also sums the
-    squares of its input for a following ``tree_l2_norm`` of that input."""
+    squares of its input for a following ``tree_l2_norm`` of that input. :func:`tree_add`
+    is the native fjhost.tree_add, which appends the running sum's link itself in the
+    common case (tree_add(s, tree_weight(x, n)) with s a live deferred sum) and calls this
+    function otherwise."""
     tl, tr = type(left) is WeightedTree, type(right) is WeightedTree
     if tr and not tl and right._tree is not None and _DEFER["enabled"]:
         # the running sum of fed_avg.py:137-138: s = tree_add(s, tree_weight(x, n))
@@ -1110,6 +1128,15 @@ def tree_add(left: PyTree, right: PyTree) -> PyTree:
             _NORMS.appendleft((caps[norm_op], sq, l2))
         return out
     return _fold_trees([_eager(left), _eager(right)], [1, 1])
+
+
+# The hot pair of the running-sum loop, native (fjhost.tree_weight / fjhost.tree_add): the
+# fast case builds the WeightedTree / PendingSum link in C, everything else calls the Python
+# functions above. Per client this is one builtin call each instead of a Python frame, the
+# type tests and a Python object construction.
+_HOST.fast_install(WeightedTree, PendingSum, _Chain, _tree_weight_py, _tree_add_py)
+tree_weight = _HOST.tree_weight
+tree_add = _HOST.tree_add
 
 
 def tree_sum(pytrees: Iterable[PyTree]) -> PyTree:

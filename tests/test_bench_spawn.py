@@ -101,3 +101,40 @@ def test_bare_bench_refuses_nccl_without_gpus():
                        capture_output=True, text=True, timeout=120)
     assert p.returncode != 0
     assert "visible GPUs" in p.stderr
+
+
+def test_spawn_timeout_names_the_stalled_rank(tmp_path, capfd):
+    """A rank that stalls (here: rank 1 sleeps past the limit after its last phase line)
+    makes spawn_ranks kill the launcher's process group, return 124 within the timeout
+    (+ the 10 s grace), and name that rank with the phase it stopped in (VERDICT r3 #3)."""
+    import time
+
+    p = tmp_path / "rank.py"
+    p.write_text(textwrap.dedent("""
+        import os, sys, time
+        sys.path.insert(0, %r)
+        import bench
+        r = int(os.environ["RANK"])
+        bench.phase(r, "native RCCL communicator init")
+        if r == 1:
+            bench.phase(r, "auto-tune candidate native/reduce/1")
+            time.sleep(600)
+        bench.phase(r, "done")
+    """ % bench.ROOT))
+    t0 = time.monotonic()
+    rc = bench.spawn_ranks(2, [], script=str(p), timeout=15)
+    took = time.monotonic() - t0
+    err = capfd.readouterr().err
+    assert rc == 124
+    assert took < 15 + 25, took
+    assert "ranks [1] had not finished" in err, err
+    assert "auto-tune candidate native/reduce/1" in err
+
+
+def test_rank_timeout_scales_with_the_workload():
+    import argparse
+
+    a = argparse.Namespace(workload="c3", clients=0, gpus=8, warmup=5, steps=20)
+    c5 = argparse.Namespace(workload="c5", clients=0, gpus=8, warmup=5, steps=20)
+    assert 300 < bench.rank_timeout(a) < 400  # configs[3]: 2.1 GB per rank
+    assert bench.rank_timeout(c5) > bench.rank_timeout(a) + 300  # configs[4]: 256 GB per rank

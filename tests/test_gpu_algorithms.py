@@ -40,7 +40,7 @@ class _Recorder:
 
 
 def _gpu_round(fn, cuda, rec):
-    to_leaf = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, np.float32))).to(cuda)
+    to_leaf = lambda a: torch.from_numpy(np.array(a, dtype=np.float32)).to(cuda)  # (keeps 0-d shapes)
     to_weight = lambda w: torch.tensor(w, device=cuda)  # a jnp scalar array on the device
     return fn(rec, to_leaf, host, to_weight)
 

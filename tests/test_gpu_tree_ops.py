@@ -515,3 +515,42 @@ def test_native_chain_fold_equals_python_path(cuda, sum_mode, monkeypatch):
     base["a"]["p"].add_(1.0)
     with pytest.raises(RuntimeError, match="running sum passed to tree_add was modified"):
         tu.tree_inverse_weight(s, 2.0)
+
+
+def test_tree_zeros_like_one_allocation_own_leaves(cuda):
+    """tree_zeros_like of a float32 device pytree (fjhost.zeros_like): zeros of every leaf's
+    shape, dict keys sorted as jax.tree.map builds them, one storage, 256-byte aligned
+    disjoint slices, and each leaf its own tensor: an in-place write to one leaf bumps only
+    its own version counter (views shared one counter)."""
+    tree = {"z": torch.ones(5, 3, device=cuda), "a": [torch.ones(1001, device=cuda), None,
+                                                       (torch.ones((), device=cuda),)]}
+    z = tu.tree_zeros_like(tree)
+    assert list(z) == ["a", "z"]
+    leaves = pytree.leaves_of(z)
+    src = pytree.leaves_of(tree)
+    assert [x.shape for x in leaves] == [x.shape for x in src]
+    assert all(x.dtype == torch.float32 and x.device == src[0].device and x.is_contiguous() for x in leaves)
+    assert all(not x.any().item() for x in leaves)
+    assert z["a"][1] is None and isinstance(z["a"][2], tuple)
+    assert len({x.untyped_storage().data_ptr() for x in leaves}) == 1
+    ptrs = sorted((x.data_ptr(), x.numel() * 4) for x in leaves)
+    assert all(p % 256 == 0 for p, _ in ptrs)
+    assert all(p0 + n0 <= p1 for (p0, n0), (p1, _) in zip(ptrs, ptrs[1:]))
+    v = [x._version for x in leaves]
+    leaves[0].add_(1.0)
+    assert [x._version for x in leaves][1:] == v[1:] and leaves[0]._version > v[0]
+    assert all(not x.any().item() for x in leaves[1:])
+    # a running sum on that base is still guarded per leaf: modifying a sibling after
+    # tree_add does not make the fold raise, modifying the base leaf in place does
+    d = {"a": [torch.full((1001,), 2.0, device=cuda), None, (torch.full((), 2.0, device=cuda),)],
+         "z": torch.full((5, 3), 2.0, device=cuda)}
+    base = tu.tree_zeros_like(d)
+    s = tu.tree_add(base, tu.tree_weight(d, 3))
+    other = tu.tree_zeros_like(d)
+    other["z"].add_(1.0)
+    assert float(tu.tree_inverse_weight(s, 3.0)["z"][0, 0]) == 2.0
+    base2 = tu.tree_zeros_like(d)
+    s2 = tu.tree_add(base2, tu.tree_weight(d, 3))
+    base2["z"].add_(1.0)
+    with pytest.raises(RuntimeError, match="running sum passed to tree_add was modified"):
+        tu.tree_inverse_weight(s2, 3.0)
