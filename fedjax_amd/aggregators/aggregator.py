@@ -56,12 +56,12 @@ def mean_aggregator() -> Aggregator:
             _, param, weight = clients_params_and_weight
             return param, weight
 
-        if type(clients_params_and_weights) in (list, tuple):
-            # resident clients: the same pairs as a list, so tree_mean takes its one-call
-            # native path (a one-shot iterable keeps the lazy map and the streaming fold)
-            params_and_weights = [(param, weight) for _, param, weight in clients_params_and_weights]
-        else:
-            params_and_weights = map(extract_params_and_weight, clients_params_and_weights)
+        if type(clients_params_and_weights) in (list, tuple) and clients_params_and_weights:
+            # resident clients: the triples go to the one-call native path as they are
+            # (tree_util.mean_of_triples); a one-shot iterable keeps the lazy map and the
+            # streaming fold
+            return tree_util.mean_of_triples(clients_params_and_weights), state
+        params_and_weights = map(extract_params_and_weight, clients_params_and_weights)
         return tree_util.tree_mean(params_and_weights), state
 
     return Aggregator(init, apply)

@@ -1591,12 +1591,18 @@ int64_t fjagg_ptrs_plan_leaves(int in_dtype, int flags, const int64_t* leaf_n, c
 
 namespace {
 // FJAGG_HOST_TABLES on the pytree path: the host image and the K f32 weights are copied
-// into ONE kernel-argument struct (k_ptrs<..., kKargWords>), float32 leaves, 16-byte units.
-int launch_ptrs_karg(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w, float scale,
-                     int ds, int ac, float* ws, float* l2, hipStream_t s) {
+// into ONE kernel-argument struct (k_ptrs<..., NW>), float32 leaves, 16-byte units. The
+// struct comes in three sizes (NW = 1024, 2048, kKargWords words) and the launch takes the
+// smallest that holds the image: the host cost of a launch grows with its argument bytes
+// (tools/probe_launch_cost.hip: 3.3 us at 8 KiB, 4.4 at 16 KiB, 7.5 at 28 KiB per launch on
+// MI355X), and a synchronous tree_mean waits for its first launch.
+extern "C++" {
+template <int NW>
+int launch_ptrs_karg_n(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w, float scale,
+                       int ds, int ac, float* ws, float* l2, hipStream_t s) {
   constexpr int IN = FJAGG_F32, OUT = FJAGG_F32, V = 4;
   using ACC = AccF;
-  KargWords<kKargWords> ki;
+  KargWords<NW> ki;
   const int64_t nimg = K * L + 2 * (int64_t)L + 2 * nblk;
   std::memcpy(ki.w, img, sizeof(int64_t) * (size_t)nimg);
   ki.w[nimg + (K + 1) / 2 - 1] = 0;  // the odd weight slot, if any
@@ -1605,10 +1611,10 @@ int launch_ptrs_karg(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk
   if (ws) {
     const size_t smem = (size_t)(kThreads / 64) * K * sizeof(float);
     if (nt)
-      hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true, true, kKargWords>), grid, block, smem, s, nullptr, L,
+      hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true, true, NW>), grid, block, smem, s, nullptr, L,
                          K, nullptr, scale, ds, ac, ws, ki);
     else
-      hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true, true, kKargWords>), grid, block, smem, s, nullptr, L,
+      hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true, true, NW>), grid, block, smem, s, nullptr, L,
                          K, nullptr, scale, ds, ac, ws, ki);
     if (int rc = check_launch("k_ptrs (l2, kernel-argument image)")) return rc;
     hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s, ws, nblk, K,
@@ -1618,18 +1624,27 @@ int launch_ptrs_karg(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk
   // the schedule rule of launch_ptrs_t
   const bool burst = nblk < 2 * (int64_t)residency(reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true>)).cus;
   if (nt && burst)
-    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, true, kKargWords>), grid, block, 0, s, nullptr, L, K,
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, true, NW>), grid, block, 0, s, nullptr, L, K,
                        nullptr, scale, ds, ac, nullptr, ki);
   else if (nt)
-    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, false, kKargWords>), grid, block, 0, s, nullptr, L, K,
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, false, NW>), grid, block, 0, s, nullptr, L, K,
                        nullptr, scale, ds, ac, nullptr, ki);
   else if (burst)
-    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, true, kKargWords>), grid, block, 0, s, nullptr, L, K,
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, true, NW>), grid, block, 0, s, nullptr, L, K,
                        nullptr, scale, ds, ac, nullptr, ki);
   else
-    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, false, kKargWords>), grid, block, 0, s, nullptr, L, K,
+    hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, false, NW>), grid, block, 0, s, nullptr, L, K,
                        nullptr, scale, ds, ac, nullptr, ki);
   return check_launch("k_ptrs (kernel-argument image)");
+}
+}  // extern "C++"
+
+int launch_ptrs_karg(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w, float scale,
+                     int ds, int ac, float* ws, float* l2, hipStream_t s) {
+  const int64_t words = fjagg_karg_image_words(K, L, nblk);
+  if (words <= 1024) return launch_ptrs_karg_n<1024>(nt, img, L, K, nblk, w, scale, ds, ac, ws, l2, s);
+  if (words <= 2048) return launch_ptrs_karg_n<2048>(nt, img, L, K, nblk, w, scale, ds, ac, ws, l2, s);
+  return launch_ptrs_karg_n<kKargWords>(nt, img, L, K, nblk, w, scale, ds, ac, ws, l2, s);
 }
 
 int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,

@@ -1343,15 +1343,12 @@ double now_s() {
 // launch that folds it (fjagg_wsum_l2_ptrs; K <= 4096, the caller checks).
 // may_pipeline: the caller's host-side estimate says the stream may be idle (then the
 // stream is probed). The chunking is tree_util._pipeline_bounds's.
-PyObject* mean_pairs(PyObject*, PyObject* args) {
-  PyObject* pairs;
-  int may_pipeline;
-  double frac, chunk_walk_us, walk_ns, nt_min;
-  long long chunk, min_bytes, narrow_max;
-  unsigned long long plan_addr, wsum_addr, l2_addr = 0, l2ws_addr = 0;
-  if (!PyArg_ParseTuple(args, "OpdLddLLdKK|KK", &pairs, &may_pipeline, &frac, &chunk, &chunk_walk_us, &walk_ns,
-                        &min_bytes, &narrow_max, &nt_min, &plan_addr, &wsum_addr, &l2_addr, &l2ws_addr))
-    return nullptr;
+// triples: the items are mean_aggregator().apply's (client_id, params, weight) triples
+// (aggregator.py:61-75), read as (params, weight) without building the pairs list.
+PyObject* mean_pairs_impl(PyObject* pairs, bool triples, int may_pipeline, double frac, long long chunk,
+                          double chunk_walk_us, double walk_ns, long long min_bytes, long long narrow_max,
+                          double nt_min, unsigned long long plan_addr, unsigned long long wsum_addr,
+                          unsigned long long l2_addr, unsigned long long l2ws_addr) {
   const bool with_l2 = l2_addr != 0 && l2ws_addr != 0;  // tree_mean_with_l2_norms: + every client's l2sq
   if (!PyList_CheckExact(pairs) && !PyTuple_CheckExact(pairs)) Py_RETURN_NONE;
   const Py_ssize_t K = Py_SIZE(pairs);
@@ -1381,12 +1378,13 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
       for (; parsed < k1; ++parsed) {  // `for pytree, weight in pytrees_and_weights`
         PyObject* pr = items[parsed];
         PyObject *t, *w;
-        if (PyTuple_CheckExact(pr) && PyTuple_GET_SIZE(pr) == 2) {
-          t = PyTuple_GET_ITEM(pr, 0);
-          w = PyTuple_GET_ITEM(pr, 1);
-        } else if (PyList_CheckExact(pr) && PyList_GET_SIZE(pr) == 2) {
-          t = PyList_GET_ITEM(pr, 0);
-          w = PyList_GET_ITEM(pr, 1);
+        const Py_ssize_t o = triples ? 1 : 0, n = o + 2;
+        if (PyTuple_CheckExact(pr) && PyTuple_GET_SIZE(pr) == n) {
+          t = PyTuple_GET_ITEM(pr, o);
+          w = PyTuple_GET_ITEM(pr, o + 1);
+        } else if (PyList_CheckExact(pr) && PyList_GET_SIZE(pr) == n) {
+          t = PyList_GET_ITEM(pr, o);
+          w = PyList_GET_ITEM(pr, o + 1);
         } else {
           return false;
         }
@@ -1520,6 +1518,101 @@ PyObject* mean_pairs(PyObject*, PyObject* args) {
   }
 }
 
+PyObject* mean_pairs(PyObject*, PyObject* args) {
+  PyObject* pairs;
+  int may_pipeline;
+  double frac, chunk_walk_us, walk_ns, nt_min;
+  long long chunk, min_bytes, narrow_max;
+  unsigned long long plan_addr, wsum_addr, l2_addr = 0, l2ws_addr = 0;
+  if (!PyArg_ParseTuple(args, "OpdLddLLdKK|KK", &pairs, &may_pipeline, &frac, &chunk, &chunk_walk_us, &walk_ns,
+                        &min_bytes, &narrow_max, &nt_min, &plan_addr, &wsum_addr, &l2_addr, &l2ws_addr))
+    return nullptr;
+  return mean_pairs_impl(pairs, false, may_pipeline, frac, chunk, chunk_walk_us, walk_ns, min_bytes, narrow_max, nt_min,
+                         plan_addr, wsum_addr, l2_addr, l2ws_addr);
+}
+
+// ------------------------------------------------------------------ tree_mean as a builtin
+// tree_util.tree_mean (tree_util.py:76-96) for a resident list / tuple of pairs, and
+// mean_aggregator().apply's list of triples (aggregator.py:61-75), without a Python frame:
+// the configuration of tree_util._native_mean (mean_config), the same mean_pairs_impl, and
+// the host-side estimate of when the folds this process issued can have finished (the idle
+// probe's gate, tree_util._BUSY_UNTIL). Anything but that case calls the Python function.
+struct MeanConfig {
+  bool on = false;  // mean_config() ran (tree_util sets it on its first Python-path call)
+  double frac = 0.25, chunk_walk_us = 60.0, walk_ns = 35.0, nt_min = 256.0 * (1 << 20), peak = 8.0e12;
+  long long chunk = 512, min_bytes = 64LL << 20, narrow_max = 256 << 10;
+  unsigned long long plan = 0, wsum = 0;
+  double busy_until = 0.0;  // steady-clock seconds
+  PyObject* py_tree_mean = nullptr;
+  PyObject* py_mean_triples = nullptr;
+};
+MeanConfig g_mean;
+
+// mean_config(on, frac, chunk, chunk_walk_us, walk_ns, min_bytes, narrow_max, nt_min, peak, plan, wsum,
+//             py_tree_mean, py_mean_triples, busy_until)
+// busy_until: time.perf_counter() seconds (CLOCK_MONOTONIC, steady_clock's clock here)
+PyObject* mean_config(PyObject*, PyObject* args) {
+  int on;
+  PyObject *ftm, *fmt;
+  if (!PyArg_ParseTuple(args, "pdLddLLddKKOOd", &on, &g_mean.frac, &g_mean.chunk, &g_mean.chunk_walk_us,
+                        &g_mean.walk_ns, &g_mean.min_bytes, &g_mean.narrow_max, &g_mean.nt_min, &g_mean.peak,
+                        &g_mean.plan, &g_mean.wsum, &ftm, &fmt, &g_mean.busy_until))
+    return nullptr;
+  Py_INCREF(ftm), Py_INCREF(fmt);
+  Py_XSETREF(g_mean.py_tree_mean, ftm);
+  Py_XSETREF(g_mean.py_mean_triples, fmt);
+  g_mean.on = on != 0 && g_mean.plan && g_mean.wsum;
+  Py_RETURN_NONE;
+}
+
+PyObject* mean_fast(PyObject* arg, bool triples) {
+  const double now = now_s();
+  PyObject* got = mean_pairs_impl(arg, triples, g_mean.frac > 0.0 && now >= g_mean.busy_until, g_mean.frac,
+                                  g_mean.chunk, g_mean.chunk_walk_us, g_mean.walk_ns, g_mean.min_bytes,
+                                  g_mean.narrow_max, g_mean.nt_min, g_mean.plan, g_mean.wsum, 0, 0);
+  if (!got || got == Py_None) return got;
+  // (rc, tree, job_bytes, None)
+  const int rc = static_cast<int>(PyLong_AsLong(PyTuple_GET_ITEM(got, 0)));
+  const double job_bytes = PyFloat_AsDouble(PyTuple_GET_ITEM(got, 2));
+  g_mean.busy_until = std::max(now, g_mean.busy_until) + job_bytes / g_mean.peak;
+  if (rc != 0) {  // the Python path raises the library's error (FjaggError) for it
+    Py_DECREF(got);
+    Py_RETURN_NONE;
+  }
+  PyObject* tree = PyTuple_GET_ITEM(got, 1);
+  Py_INCREF(tree);
+  Py_DECREF(got);
+  return tree;
+}
+
+PyObject* fast_tree_mean(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
+  if (!g_mean.py_tree_mean) {
+    PyErr_SetString(PyExc_RuntimeError, "fedjax_amd.tree_util is not installed (mean_config)");
+    return nullptr;
+  }
+  if (g_mean.on && nargs == 1 && !kwnames && Py_SIZE(args[0]) > 0 &&
+      (PyList_CheckExact(args[0]) || PyTuple_CheckExact(args[0]))) {
+    PyObject* got = mean_fast(args[0], false);
+    if (got != Py_None) return got;  // (a tree, or nullptr with the error set)
+    Py_DECREF(got);
+  }
+  return PyObject_Vectorcall(g_mean.py_tree_mean, args, nargs, kwnames);
+}
+
+// mean_triples(clients) -> tree: tree_mean over (client_id, params, weight) triples
+PyObject* mean_triples(PyObject*, PyObject* clients) {
+  if (!g_mean.py_mean_triples) {
+    PyErr_SetString(PyExc_RuntimeError, "fedjax_amd.tree_util is not installed (mean_config)");
+    return nullptr;
+  }
+  if (g_mean.on && Py_SIZE(clients) > 0 && (PyList_CheckExact(clients) || PyTuple_CheckExact(clients))) {
+    PyObject* got = mean_fast(clients, true);
+    if (got != Py_None) return got;
+    Py_DECREF(got);
+  }
+  return PyObject_CallOneArg(g_mean.py_mean_triples, clients);
+}
+
 // server_pairs(pairs, params, m, v, mean_out, desc_addr, nt_min_bytes, plan_fn, update_fn)
 //   -> rc | None
 // server.fused_tree_mean_update for the common case in one native call: the pairs as in
@@ -1542,6 +1635,15 @@ PyObject* server_pairs(PyObject*, PyObject* args) {
   if (!PyList_CheckExact(pairs) && !PyTuple_CheckExact(pairs)) Py_RETURN_NONE;
   const Py_ssize_t K = Py_SIZE(pairs);
   if (K < 1) Py_RETURN_NONE;
+  {  // the state trees the rule reads: a missing one is never launched with a null
+     // table entry; the Python path raises ValueError for it
+    const auto* opt = reinterpret_cast<const fjagg_server_opt*>(desc_addr);
+    if (!opt) Py_RETURN_NONE;
+    const bool needs_m = opt->kind == FJAGG_OPT_MOMENTUM || opt->kind == FJAGG_OPT_ADAM || opt->kind == FJAGG_OPT_YOGI ||
+                         (opt->kind == FJAGG_OPT_RMSPROP && (opt->flags & (FJAGG_OPT_F_MOMENTUM | FJAGG_OPT_F_CENTERED)));
+    const bool needs_v = opt->kind >= FJAGG_OPT_ADAM;
+    if ((needs_m && mt == Py_None) || (needs_v && vt == Py_None)) Py_RETURN_NONE;
+  }
   PyObject* const* items = PyList_CheckExact(pairs) ? &PyList_GET_ITEM(pairs, 0) : &PyTuple_GET_ITEM(pairs, 0);
   try {
     struct Held {
@@ -2153,6 +2255,13 @@ PyMethodDef kMethods[] = {
     {"mean_pairs", mean_pairs, METH_VARARGS, "tree_mean of (pytree, weight) pairs in one native call (see fjhost.cpp)"},
     {"server_pairs", server_pairs, METH_VARARGS, "fused_tree_mean_update in one native call (see fjhost.cpp)"},
     {"zeros_like", zeros_like, METH_O, "tree_zeros_like of a float32 device pytree: one allocation, own leaves"},
+    {"mean_config", mean_config, METH_VARARGS, "configuration of the builtin tree_mean (tree_util._native_mean)"},
+    {"tree_mean", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_tree_mean)), METH_FASTCALL | METH_KEYWORDS,
+     "tree_mean(pytrees_and_weights)\n--\n\nReturns (weighted) mean of input trees and weights "
+     "(fedjax/core/tree_util.py:76-96).\n\nA resident list / tuple of (float32 device pytree, Python-number weight) "
+     "pairs is folded by one native call\n(the pytree kernel, pipelined with the walk on an idle GPU); every other "
+     "input is\nfedjax_amd.tree_util._tree_mean_py's (one-shot iterables stream in chunks)."},
+    {"mean_triples", mean_triples, METH_O, "tree_mean over (client_id, params, weight) triples (aggregator.py:61-75)"},
     {"pipeline_fracs", pipeline_fracs, METH_O, "chunk ends (fractions of K) of tree_mean's fold-bound pipeline"},
     {"fold_chain", fold_chain, METH_VARARGS, "a PendingSum's deferred fold, its links walked natively"},
     {"fast_install", fast_install, METH_VARARGS, "register tree_util's lazy classes and Python fallbacks"},

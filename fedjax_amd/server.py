@@ -189,6 +189,7 @@ def fused_mean_update(slab: ClientDeltaSlab, weights: Sequence, opt: ServerOptim
         mean = mean_out if mean_out is not None else torch.empty_like(params)
         slab.mean(weights, out=mean)
         return opt.apply(slab.unflatten(mean), state, slab.unflatten(params))[0]
+    _require_state(opt, state)
     W = 0.0
     for x in weights:
         W += tree_util._host_weight(x)
@@ -243,6 +244,16 @@ def _update_addrs():
     return _UPDATE_ADDRS
 
 
+def _require_state(opt: "ServerOptimizer", state: dict) -> None:
+    """The moments ``opt``'s rule reads must be in ``state`` (e.g. a state from
+    ``rmsprop(centered=False).init`` given to a centered rmsprop has no 'm'): raise instead
+    of launching the fused step with an absent state tree."""
+    for key, need in (("m", opt.needs_m()), ("v", opt.needs_v())):
+        if need and state.get(key) is None:
+            raise ValueError(f"optimizer state has no {key!r}, which this optimizer's update reads; "
+                             f"use opt.init(params) of the same optimizer")
+
+
 def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, state: dict, *,
                            mean_out=None, nontemporal: Optional[bool] = None) -> dict:
     """:func:`fused_mean_update` on the pytree path: ``tree_mean`` of the clients' delta
@@ -264,6 +275,7 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
         elif mean is None:
             raise ValueError("no clients to aggregate")
         return opt.apply(mean, state, params)[0]
+    _require_state(opt, state)
     if (not opt.frozen and nontemporal is None and type(pytrees_and_weights) in (list, tuple)
             and pytrees_and_weights):
         # the common case in one native call (fjhost.server_pairs): same image, same launch
@@ -450,7 +462,7 @@ class Adafactor:
             device = p[0].device
             mask = self._mask(params, td)
             frozen = _frozen_leaves(self, params, td)  # ignore_grads_haiku: left out of the step
-            key, recs = [hp.clip, hp.param_scale, hp.momentum], []
+            recs = []
             for l, (pl, gl) in enumerate(zip(p, g)):
                 if frozen[l]:
                     continue
@@ -488,29 +500,48 @@ class Adafactor:
                 rec.dims[:] = dims
                 rec.decay_weights = int(mask[l])
                 recs.append(rec)
-                key.append(bytes(rec))
-            key = tuple(key)
-            plan = self._plans.get(key) if recs else ()
+            # The plan is keyed on what shapes it (leaf shapes, factoring, flags, mask) and on
+            # the stream, not on the pointers: the mean delta is a fresh tensor every round
+            # (ADVICE r3). The pointers are rewritten into the cached table, and uploaded into
+            # its device copy on this stream, only when they change; the workspace belongs to
+            # the (plan, stream) entry, so calls on two streams never share one.
+            stream = torch.cuda.current_stream(device)
+            shape_key = []
+            for rec in recs:
+                z = _lib.AfLeaf.from_buffer_copy(rec)
+                z.g = z.p = z.v_row = z.v_col = z.v = z.m = None
+                shape_key.append(bytes(z))
+            key = (hp.clip, hp.param_scale, hp.momentum, hp.weight_decay, hp.has_lr, tuple(shape_key),
+                   device, stream.cuda_stream)
+            ptr_key = tuple(bytes(rec) for rec in recs)
+            if not recs:
+                return dict(state, count=count + 1), params
+            plan = self._plans.get(key)
+            lib = _lib.load()
+            arr = None
             if plan is None:
                 arr = (_lib.AfLeaf * len(recs))(*recs)
                 ws_bytes = ctypes.c_int64()
-                lib = _lib.load()
                 words = int(lib.fjopt_adafactor_plan(arr, len(recs), ctypes.byref(hp), None, 0, ctypes.byref(ws_bytes)))
-                table = np.zeros(max(words, 1), dtype=np.int64)
-                if words >= 0:
-                    words = int(lib.fjopt_adafactor_plan(arr, len(recs), ctypes.byref(hp), table.ctypes.data,
-                                                         table.size, ctypes.byref(ws_bytes)))
                 _lib.check(min(words, 0), "fjopt_adafactor_plan")
-                table_dev = torch.from_numpy(table).pin_memory().to(device, non_blocking=True)
-                ws = torch.empty(int(ws_bytes.value), dtype=torch.uint8, device=device)
+                table = np.zeros(max(words, 1), dtype=np.int64)
+                table_dev = torch.empty(table.size, dtype=torch.int64, device=device)
+                ws = torch.empty(max(int(ws_bytes.value), 1), dtype=torch.uint8, device=device)
                 if len(self._plans) >= 8:
                     self._plans.clear()
-                plan = self._plans[key] = (table, table_dev, ws)
-            if not recs:
-                return dict(state, count=count + 1), params
-            table, table_dev, ws = plan
+                plan = self._plans[key] = [None, table, table_dev, ws]
+            if plan[0] != ptr_key:  # new pointers: rewrite the host table, upload it on this stream
+                if arr is None:
+                    arr = (_lib.AfLeaf * len(recs))(*recs)
+                ws_bytes = ctypes.c_int64()
+                words = int(lib.fjopt_adafactor_plan(arr, len(recs), ctypes.byref(hp), plan[1].ctypes.data,
+                                                     plan[1].size, ctypes.byref(ws_bytes)))
+                _lib.check(min(words, 0), "fjopt_adafactor_plan")
+                plan[2].copy_(torch.from_numpy(plan[1]).pin_memory(), non_blocking=True)
+                plan[0] = ptr_key
+            _, table, table_dev, ws = plan
             _lib.call("fjopt_adafactor_step", table.ctypes.data, table_dev.data_ptr(), ctypes.byref(hp),
-                      ws.data_ptr(), ws.numel(), torch.cuda.current_stream(device).cuda_stream)
+                      ws.data_ptr(), ws.numel(), stream.cuda_stream)
         new = dict(state)
         new["count"] = count + 1
         return new, params

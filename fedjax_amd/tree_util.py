@@ -320,6 +320,18 @@ def _native_fold_addrs() -> None:
     _ENTRY_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
                          for f in ("fjagg_ptrs_plan_leaves", "fjagg_wsum_ptrs", "fjagg_wsum_l2_ptrs",
                                    "fjagg_wsum_l2_ptrs_workspace_bytes"))
+    _mean_config()
+
+
+def _mean_config() -> None:
+    """Configure the builtin tree_mean (fjhost.tree_mean / mean_triples): the same settings
+    _native_mean passes, the library's entry points once loaded (until then the builtin
+    calls the Python function, which loads them), and the Python fallbacks."""
+    on = _NATIVE_MEAN and _ENTRY_ADDRS is not None
+    _HOST.mean_config(on, _PIPELINE_FRAC, _PIPELINE_CHUNK, _CHUNK_WALK_US, _WALK_NS_PER_LEAF, _PIPELINE_MIN_BYTES,
+                      _NARROW_MAX_BYTES, float(NONTEMPORAL_MIN_BYTES), _PEAK_BYTES_PER_S,
+                      _ENTRY_ADDRS[0] if on else 0, _ENTRY_ADDRS[1] if on else 0, _tree_mean_py, _mean_triples_py,
+                      _BUSY_UNTIL[0])
 
 
 def _native_fold(table: "_Table", packed: "_Weights", scale, out=None,
@@ -1293,7 +1305,7 @@ def _tree_mean_pipelined(trees: List[PyTree], packed: "_Weights", W, first) -> O
 STREAM_BUDGET_BYTES = 4 << 30
 
 
-def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
+def _tree_mean_py(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
     """Returns (weighted) mean of input trees and weights (tree_util.py:76-96).
 
     All K clients are folded by ONE kernel launch per leaf-dtype group; the result
@@ -1328,6 +1340,20 @@ def tree_mean(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree:
         return pytree.unflatten(td, [])
     inv = _inverse(sum_weight)
     return pytree.unflatten(td, _fold(rows, weights, scale=inv, validated=True))
+
+
+def _mean_triples_py(clients) -> PyTree:
+    """tree_mean over mean_aggregator().apply's (client_id, params, weight) triples
+    (aggregator.py:61-75) when fjhost.mean_triples declines them."""
+    return _tree_mean_py([(param, weight) for _, param, weight in clients])
+
+
+# tree_mean is the native fjhost.tree_mean: a resident list / tuple of float32 device pytrees
+# with Python-number weights is one native call (no Python frame); everything else is
+# _tree_mean_py. mean_of_triples serves mean_aggregator().apply the same way.
+tree_mean = _HOST.tree_mean
+mean_of_triples = _HOST.mean_triples
+_mean_config()  # the fallbacks now; the library's entry points once _native_fold_addrs runs
 
 
 def _f32_tree_bytes(tree) -> Optional[int]:

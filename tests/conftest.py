@@ -31,6 +31,23 @@ def coracle():
     return co.load(_build_oracle())
 
 
+@pytest.fixture()
+def tu_settings(monkeypatch):
+    """Set fedjax_amd.tree_util's module settings (_PIPELINE_FRAC, _NATIVE_MEAN, ...) for one
+    test. The builtin tree_mean (fjhost.tree_mean) holds its own copy of them, so it is
+    re-configured (tree_util._mean_config) on every set and after the test's monkeypatches
+    are undone."""
+    from fedjax_amd import tree_util as tu
+
+    def set_(**kw):
+        for k, v in kw.items():
+            monkeypatch.setattr(tu, k, v)
+        tu._mean_config()
+    yield set_
+    monkeypatch.undo()
+    tu._mean_config()
+
+
 @pytest.fixture(scope="session")
 def cuda():
     import torch

@@ -263,8 +263,13 @@ def test_random_case_matches_oracle(cuda, seed, monkeypatch):
         mp.setattr(tu, "_CHUNK_WALK_US", 0.0)
         mp.setattr(tu, "_PIPELINE_CHUNK", max(1, K // 3))
         mp.setattr(tu, "_BUSY_UNTIL", [0.0])
-        torch.cuda.synchronize()
-        _same(tu.tree_mean(list(zip(trees, ws))), want, "tree_mean(list), pipelined")
+        tu._mean_config()  # (the builtin tree_mean's copy of these settings)
+        try:
+            torch.cuda.synchronize()
+            _same(tu.tree_mean(list(zip(trees, ws))), want, "tree_mean(list), pipelined")
+        finally:
+            mp.undo()
+            tu._mean_config()
     # generator input: chunks of about two clients' worth of deltas
     per = max(1, sum(int(np.prod(s)) for s in c["shapes"])) * 4
     monkeypatch.setattr(tu, "STREAM_BUDGET_BYTES", 2 * per + 1)

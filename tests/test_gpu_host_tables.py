@@ -115,12 +115,12 @@ def _emnist_clients(K, cuda, seed):
     return [tmap(lambda s: (torch.rand(s, generator=g) * 2 - 1).to(cuda), EMNIST) for _ in range(K)]
 
 
-def test_pytree_image_in_kernel_args_configs1(cuda, monkeypatch):
+def test_pytree_image_in_kernel_args_configs1(cuda, tu_settings):
     """configs[1] (128 clients x the 8 EMNIST-CNN leaves, separate allocations): tree_mean's
     native path carries the whole plan image (~13 KB) in the kernel arguments; the mean and
     the fused norms are bitwise the device-image launches of the Python path, and the mean
     is bitwise the oracle's."""
-    monkeypatch.setattr(tu, "_PIPELINE_FRAC", 0.0)  # one launch per call (tests/test_gpu_pipeline.py: two)
+    tu_settings(_PIPELINE_FRAC=0.0)  # one launch per call (tests/test_gpu_pipeline.py: two)
     K = 128
     trees = _emnist_clients(K, cuda, 1)
     weights = [int(v) for v in ref.fedavg_weights(K, seed=5)]
@@ -144,11 +144,11 @@ def test_pytree_image_in_kernel_args_configs1(cuda, monkeypatch):
         assert np.array_equal(u32(a), b.view(np.int32))
 
 
-def test_pytree_image_too_large_is_uploaded(cuda, monkeypatch):
+def test_pytree_image_too_large_is_uploaded(cuda, tu_settings):
     """An image beyond FJAGG_KARG_MAX_WORDS (here 640 clients x 8 leaves) takes the
     pinned upload; misaligned leaves (per-leaf element units) still fit the kernel
     arguments. Both bitwise the Python path."""
-    monkeypatch.setattr(tu, "_PIPELINE_FRAC", 0.0)  # one launch per call
+    tu_settings(_PIPELINE_FRAC=0.0)  # one launch per call
     host = _lib.host()
     g = torch.Generator(device="cpu").manual_seed(2)
     # 280 KB per client (above the narrow plan's 256 KiB), 5,120 client leaves

@@ -35,16 +35,16 @@ def _launches():  # fold_table launches (image in the kernel arguments or upload
 
 
 @pytest.fixture
-def chunk(monkeypatch):
+def chunk(tu_settings):
     def set_(v):
-        monkeypatch.setattr(tu, "_PIPELINE_CHUNK", v)
+        tu_settings(_PIPELINE_CHUNK=v)
     return set_
 
 
 @pytest.fixture
-def frac(monkeypatch):
+def frac(tu_settings):
     def set_(v):
-        monkeypatch.setattr(tu, "_PIPELINE_FRAC", v)
+        tu_settings(_PIPELINE_FRAC=v)
     return set_
 
 
@@ -70,12 +70,12 @@ def test_pipelined_tree_mean_bitwise(K, frac, cuda):
 
 
 @pytest.mark.parametrize("K,c", [(1500, 512), (1500, 100), (600, 256)])
-def test_chunked_pipeline_small_model_bitwise(K, c, frac, chunk, cuda, monkeypatch):
+def test_chunked_pipeline_small_model_bitwise(K, c, frac, chunk, cuda, tu_settings):
     """A small model (48,670 params: the walk, not the fold, is the longer part), with the
     narrow-delta exclusion lifted: launches of c clients, each accumulating into the first's
     sums (stripe / narrow plans per chunk)."""
-    monkeypatch.setattr(tu, "_CHUNK_WALK_US", 0.0)  # chunks of exactly c clients
-    monkeypatch.setattr(tu, "_NARROW_MAX_BYTES", 0)  # (the fold still picks its narrow plans natively)
+    tu_settings(_CHUNK_WALK_US=0.0)  # chunks of exactly c clients
+    tu_settings(_NARROW_MAX_BYTES=0)  # (the fold still picks its narrow plans natively)
     g = torch.Generator(device="cuda").manual_seed(K + c)
     shapes = {"w": (784, 62), "b": (62,)}
     clients = [{k: torch.rand(s, device="cuda", generator=g) - 0.5 for k, s in shapes.items()} for _ in range(K)]
@@ -148,7 +148,7 @@ def test_pipelined_declines_what_it_does_not_cover(frac, cuda):
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32), err_msg=name)
 
 
-def test_native_whole_call_equals_python_path(frac, cuda, monkeypatch):
+def test_native_whole_call_equals_python_path(frac, cuda, tu_settings):
     """fjhost.mean_pairs (the whole tree_mean call natively) against the Python path
     (FJAGG_NATIVE_MEAN off): bitwise, for dict / list / tuple / None nodes, pairs given as
     tuples or lists, int and float weights, pipelined or not; declined cases (a namedtuple
@@ -168,13 +168,13 @@ def test_native_whole_call_equals_python_path(frac, cuda, monkeypatch):
         "bf16": [({"w": r(80_000).to(torch.bfloat16)}, k + 1) for k in range(K)],
     }
     for name, pairs in cases.items():
-        monkeypatch.setattr(tu, "_NATIVE_MEAN", False)
+        tu_settings(_NATIVE_MEAN=False)
         frac(0.0)
         want = tu.tree_mean(pairs)
-        monkeypatch.setattr(tu, "_NATIVE_MEAN", True)
+        tu_settings(_NATIVE_MEAN=True)
         for f in (0.0, 0.5):
             frac(f)
-            monkeypatch.setattr(tu, "_PIPELINE_MIN_BYTES", 0)
+            tu_settings(_PIPELINE_MIN_BYTES=0)
             torch.cuda.synchronize()
             got = tu.tree_mean(pairs)
             assert ref.flatten(got)[1] == ref.flatten(want)[1], name
@@ -193,14 +193,14 @@ def test_native_whole_call_equals_python_path(frac, cuda, monkeypatch):
         tu.tree_mean(bad)
 
 
-def test_native_mean_with_l2_norms_equals_python_path(frac, cuda, monkeypatch):
+def test_native_mean_with_l2_norms_equals_python_path(frac, cuda, tu_settings):
     """tree_mean_with_l2_norms through fjhost.mean_pairs (one launch, or the pipelined
     chunks, each giving its clients' norms) against the Python path: mean and norms bitwise."""
     K = 40
     pairs = list(zip(_clients(K, seed=9), [1 + (k % 7) for k in range(K)]))
-    monkeypatch.setattr(tu, "_NATIVE_MEAN", False)
+    tu_settings(_NATIVE_MEAN=False)
     want_mean, want_norms = tu.tree_mean_with_l2_norms(pairs)
-    monkeypatch.setattr(tu, "_NATIVE_MEAN", True)
+    tu_settings(_NATIVE_MEAN=True)
     for f in (0.0, 0.3):
         frac(f)
         torch.cuda.synchronize()

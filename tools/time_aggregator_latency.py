@@ -15,6 +15,7 @@ triples = [(f"c{k}", tmap(lambda s: torch.rand(s, device=dev, generator=g), SHAP
 agg = fedjax_amd.aggregators.mean_aggregator(); st = agg.init()
 for native in (False, True, False, True):
     tu._NATIVE_MEAN = native
+    tu._mean_config()  # (the builtin tree_mean keeps its own copy)
     for _ in range(5): agg.apply(triples, st)
     ts = []
     for _ in range(100):

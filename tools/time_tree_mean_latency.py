@@ -58,6 +58,7 @@ def main(fracs, K=128, reps=100, rounds=3):
         for f in fracs:
             if f is not None:
                 tu._PIPELINE_FRAC = abs(f)
+                tu._mean_config()  # (the builtin tree_mean keeps its own copy)
                 tu._stream_idle = (lambda s: False) if f < 0 else idle
             s, i, p = measure(pairs, reps)
             res[f][0].extend(s)
