@@ -379,13 +379,49 @@ def emit_json(json_fd, res):
     os.write(json_fd, line.encode())
 
 
-def load_traffic(workload):
-    p = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+def load_traffic(workload, path=None):
+    """HBM bytes per launch of the dominant kernel from the PMC passes in
+    profiles/traffic_<workload>.json, with where they came from: the build (sha256 of the
+    libfjagg.so the counters ran) and whether it is the build running now. None: no file."""
+    p = path or os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     with open(p) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_summary import build_tag
+
+    now = build_tag()
+    src = {"file": os.path.relpath(p, ROOT), "measured_in_this_run": False,
+           "method": d.get("method", "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/gpu_full.sh)"),
+           "correction": d.get("correction"), "build": d.get("build", d.get("collected")),
+           "this_build": now, "same_build": d.get("build") == now, "collected": d.get("collected")}
+    return d.get("hbm_bytes_per_launch"), src
+
+
+def measure_traffic(workload, dst=None):
+    """--measure-traffic: the FETCH_SIZE and WRITE_SIZE passes run here, each as its own
+    rocprofv3 child over a short bench run of the same workload (no cpu baseline, no
+    drop-in), summarised by tools/pmc_summary.py into profiles/traffic_<workload>.json.
+    Returns (bytes per launch, source record) for this run's line."""
+    import subprocess
+    import tempfile
+
+    out = tempfile.mkdtemp(prefix="fj_pmc_")
+    cmd = [sys.executable, os.path.abspath(__file__), "--workload", workload, "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--no-dropin"]
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        log(f"[bench] PMC pass {counter}")
+        subprocess.run(["rocprofv3", "--pmc", counter, "-d", os.path.join(out, counter), "-o", "run",
+                        "--output-format", "csv", "--", *cmd], check=True, timeout=300,
+                       stdout=subprocess.DEVNULL)
+    dst = dst or os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), os.path.join(out, "FETCH_SIZE"),
+                    os.path.join(out, "WRITE_SIZE"), dst], check=True, timeout=120, stdout=subprocess.DEVNULL)
+    b, src = load_traffic(workload, dst)
+    if src is not None:
+        src["measured_in_this_run"] = True
+    return b, src
 
 
 # host RAM one rank may pin for its shard in the e2e leg (a configs[4] shard is 256 GB)
@@ -473,6 +509,12 @@ def main():
     ap.add_argument("--e2e", action="store_true",
                     help="N=1: also time host-resident deltas (H2D + fold + D2H); on by default at N>1")
     ap.add_argument("--no-e2e", action="store_true", help="N>1: skip the host-resident end-to-end leg")
+    ap.add_argument("--measure-traffic", action="store_true",
+                    help="N=1: run the FETCH_SIZE / WRITE_SIZE rocprofv3 passes from this run (child processes) "
+                         "and report their HBM bytes as roofline.traffic (default: profiles/traffic_<workload>.json "
+                         "with its build tag)")
+    ap.add_argument("--traffic-out", default="",
+                    help="--measure-traffic: where the summary goes (default profiles/traffic_<workload>.json)")
     ap.add_argument("--timeout", type=float, default=0,
                     help="bare --gpus N: seconds before the spawned ranks are killed (0 = derived from the "
                          "workload and steps, rank_timeout)")
@@ -724,6 +766,11 @@ def main():
         e2e = host_resident_rate(x, w_local, step if sharded else None, out, scale, nt, dev, rank, sharded,
                                  K * P * esize if nshard == world else Kl * P * esize)
 
+    traffic = (None, None)
+    if rank == 0 and not sharded and not args.with_norms and args.server == "none" and not args.variant \
+            and not args.clients:
+        traffic = (measure_traffic(args.workload, args.traffic_out or None) if args.measure_traffic
+                   else load_traffic(args.workload))
     if rank == 0:
         value = (K if nshard == world else Kl) * P * esize * args.steps / elapsed / 1e9
         res = {
@@ -762,8 +809,7 @@ def main():
                        "fused_server_step": args.server},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4),
-                         "traffic": load_traffic(args.workload) if (not sharded and not args.with_norms
-                                                                    and args.server == "none") else None,
+                         "traffic": traffic[0], "traffic_source": traffic[1],
                          "kernel": ("k_dense_opt fold + server " + args.server if args.server != "none" else
                                     "k_dense_l2 fold + per-client l2" if args.with_norms else "k_dense weighted fold"),
                          "bytes_per_launch": bytes_per_launch,

@@ -160,6 +160,99 @@ int walk(PyObject* spec, PyObject* x, Walk& w) {
   return 1;
 }
 
+// The leaf objects of x against spec, appended to objs (tensor leaves by exact type only; no
+// tensor field is read): 0 walked, 1 mismatch, -1 Python error set.
+int collect(PyObject* spec, PyObject* x, std::vector<PyObject*>& objs) {
+  if (PyLong_CheckExact(spec)) {
+    const long k = PyLong_AsLong(spec);
+    if (k == kLeaf) {
+      if (Py_TYPE(x) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) return 1;
+      objs.push_back(x);
+      return 0;
+    }
+    if (k == kNone) return x == Py_None ? 0 : 1;
+    return 1;
+  }
+  if (!PyTuple_CheckExact(spec) || PyTuple_GET_SIZE(spec) != 3) return 1;
+  const long kind = PyLong_AsLong(PyTuple_GET_ITEM(spec, 0));
+  PyObject* aux = PyTuple_GET_ITEM(spec, 1);
+  PyObject* children = PyTuple_GET_ITEM(spec, 2);
+  const Py_ssize_t n = PyTuple_GET_SIZE(children);
+  if (kind == kDict) {
+    if (!PyDict_CheckExact(x) || PyDict_GET_SIZE(x) != n) return 1;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      PyObject* v = PyDict_GetItemWithError(x, PyTuple_GET_ITEM(aux, i));  // borrowed
+      if (v == nullptr) {
+        if (PyErr_Occurred()) PyErr_Clear();  // e.g. an unhashable comparison: a mismatch
+        return 1;
+      }
+      if (int rc = collect(PyTuple_GET_ITEM(children, i), v, objs)) return rc;
+    }
+    return 0;
+  }
+  if (kind == kList || kind == kTuple) {
+    const bool ok = kind == kList ? PyList_CheckExact(x) : PyTuple_CheckExact(x);
+    if (!ok || Py_SIZE(x) != n) return 1;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      PyObject* v = kind == kList ? PyList_GET_ITEM(x, i) : PyTuple_GET_ITEM(x, i);
+      if (int rc = collect(PyTuple_GET_ITEM(children, i), v, objs)) return rc;
+    }
+    return 0;
+  }
+  return 1;
+}
+
+// Touch the lines a leaf check reads before the checks run: the TensorImpl of every
+// collected leaf, then (once those lines are on their way) every StorageImpl. A client's
+// tensors are scattered over the heap, so the walk of K x L leaves is bound by cache misses;
+// issuing a batch's misses together lets them overlap instead of being paid one by one.
+inline void prefetch_impls(const std::vector<PyObject*>& objs) {
+  for (PyObject* o : objs) {
+    const char* p = reinterpret_cast<const char*>(THPVariable_Unpack(o).unsafeGetTensorImpl());
+    __builtin_prefetch(p);
+    __builtin_prefetch(p + 64);
+    __builtin_prefetch(p + 128);
+    __builtin_prefetch(p + 192);
+  }
+  for (PyObject* o : objs)
+    __builtin_prefetch(THPVariable_Unpack(o).unsafeGetTensorImpl()->storage().unsafeGetStorageImpl());
+}
+
+// Clients trees[k0, k1) against spec: every leaf a strided tensor on cuda:dev (dev < 0: on
+// the host), of dtypes[l] / sizes[l], contiguous; its data pointer goes to rows[k * L + l].
+// Walked in batches of 16 clients (collect, prefetch, check). 0: all match; k + 1: client k
+// is the first that does not; -1: a Python error is set.
+int64_t gather_clients(PyObject* spec, PyObject* const* trees, int64_t k0, int64_t k1,
+                       const std::vector<at::ScalarType>& dtypes, const std::vector<c10::IntArrayRef>& sizes,
+                       c10::DeviceIndex dev, int64_t* rows) {
+  const size_t L = dtypes.size();
+  constexpr int64_t B = 16;
+  thread_local std::vector<PyObject*> objs;
+  for (int64_t b0 = k0; b0 < k1; b0 += B) {
+    const int64_t b1 = std::min(k1, b0 + B);
+    objs.clear();
+    for (int64_t k = b0; k < b1; ++k) {
+      const size_t before = objs.size();
+      const int rc = collect(spec, trees[k], objs);
+      if (rc < 0) return -1;
+      if (rc > 0 || objs.size() - before != L) return k + 1;
+    }
+    prefetch_impls(objs);
+    for (int64_t k = b0; k < b1; ++k) {
+      PyObject* const* row = objs.data() + (k - b0) * L;
+      int64_t* out = rows + k * L;
+      for (size_t l = 0; l < L; ++l) {
+        const at::Tensor& t = THPVariable_Unpack(row[l]);
+        if (t.layout() != c10::kStrided) return k + 1;
+        if (dev >= 0 ? (!t.is_cuda() || t.get_device() != dev) : !t.is_cpu()) return k + 1;
+        if (t.scalar_type() != dtypes[l] || t.sizes() != sizes[l] || !t.is_contiguous()) return k + 1;
+        out[l] = reinterpret_cast<int64_t>(t.data_ptr());
+      }
+    }
+  }
+  return 0;
+}
+
 PyObject* gather_rows(PyObject*, PyObject* args) {
   PyObject *trees, *spec, *row0, *ptrs;
   Py_ssize_t k0, k1 = -1;
@@ -200,15 +293,10 @@ PyObject* gather_rows(PyObject*, PyObject* args) {
       sizes.push_back(t.sizes());
       if (k0 == 1) out[l] = reinterpret_cast<int64_t>(t.data_ptr());
     }
-    Walk w{&dtypes, &sizes, static_cast<c10::DeviceIndex>(dev), nullptr, 0};
-    for (Py_ssize_t k = k0; k < k1; ++k) {
-      w.out = out + k * L;
-      w.leaf = 0;
-      int rc = walk(spec, PyList_GET_ITEM(trees, k), w);
-      if (rc < 0) return nullptr;
-      if (rc > 0 || w.leaf != static_cast<size_t>(L)) return PyLong_FromSsize_t(-(k + 1));
-    }
-    return PyLong_FromLong(0);
+    const int64_t r = gather_clients(spec, &PyList_GET_ITEM(trees, 0), k0, k1, dtypes, sizes,
+                                     static_cast<c10::DeviceIndex>(dev), out);
+    if (r < 0) return nullptr;
+    return PyLong_FromLongLong(-r);
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
@@ -1059,6 +1147,23 @@ PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const*
     if (static_cast<Py_ssize_t>(w.leaves[0].size()) != L) return PyLong_FromLong(0);
     thread_local std::vector<int64_t> ptrs;
     ptrs.resize(static_cast<size_t>(K * L));
+    {  // the K x L captured tensors' objects, then their TensorImpls and StorageImpls, requested
+       // before the checks below read them (gather_clients' batching, for the chain's captures)
+      thread_local std::vector<PyObject*> objs;
+      objs.clear();
+      for (Py_ssize_t k = 0; k < K; ++k) {
+        PyObject* cap = caps[k];
+        if (!PyTuple_Check(cap) || PyTuple_GET_SIZE(cap) < 2 || !PyTuple_Check(PyTuple_GET_ITEM(cap, 0))) break;
+        PyObject* tup = PyTuple_GET_ITEM(cap, 0);
+        for (Py_ssize_t l = 0; l < PyTuple_GET_SIZE(tup); ++l) {
+          objs.push_back(PyTuple_GET_ITEM(tup, l));
+          __builtin_prefetch(objs.back());
+        }
+      }
+      bool all_tensors = true;
+      for (PyObject* o : objs) all_tensors = all_tensors && THPVariable_Check(o);
+      if (all_tensors) prefetch_impls(objs);
+    }
     std::vector<at::Tensor> row0;
     row0.reserve(L);
     int dev = -1;
@@ -1469,7 +1574,6 @@ PyObject* mean_pairs_impl(PyObject* pairs, bool triples, int may_pipeline, doubl
     st.lap(kTSpec);
     std::vector<int64_t> ptrs(static_cast<size_t>(K * L));
     for (int64_t l = 0; l < L; ++l) ptrs[l] = reinterpret_cast<int64_t>(row0[l].data_ptr());
-    Walk w{&dtypes, &sizes, static_cast<c10::DeviceIndex>(dev), nullptr, 0};
     const double ntm = job_bytes >= nt_min ? 0.0 : HUGE_VAL;  // the whole job's bytes decide
     std::vector<at::Tensor> outs;
     at::Tensor l2sq;  // float32 [K] (with_l2): client k's squared norm from the launch that folds it
@@ -1478,13 +1582,10 @@ PyObject* mean_pairs_impl(PyObject* pairs, bool triples, int may_pipeline, doubl
     int rc = 0;
     for (int64_t k1 : bounds) {
       if (!parse(k1)) Py_RETURN_NONE;
-      for (int64_t k = std::max<int64_t>(done, 1); k < k1; ++k) {
-        w.out = ptrs.data() + k * L;
-        w.leaf = 0;
-        const int r = walk(spec, trees[k], w);
-        if (r < 0) return nullptr;
-        if (r > 0 || w.leaf != static_cast<size_t>(L)) Py_RETURN_NONE;
-      }
+      const int64_t r = gather_clients(spec, trees.data(), std::max<int64_t>(done, 1), k1, dtypes, sizes,
+                                       static_cast<c10::DeviceIndex>(dev), ptrs.data());
+      if (r < 0) return nullptr;
+      if (r > 0) Py_RETURN_NONE;
       const bool last = k1 == K;  // (then every weight is parsed: W is complete)
       const double scale = last ? (W > 0.0 ? 1.0 / W : 0.0) : 1.0;  // tree_util.py:37,60
       if (fold_core(row0, ptrs.data() + done * L, k1 - done, wf.data() + done, scale, last, ntm, dev,

@@ -8,9 +8,19 @@ usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT.json [kernel-substrin
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def build_tag(path=os.path.join(ROOT, "fedjax_amd", "_build", "libfjagg.so")) -> str:
+    """The identity of the kernel build the counters describe: sha256 of libfjagg.so."""
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def per_dispatch(d, counter, pat):
@@ -41,7 +51,9 @@ def main():
            "fetch_size_kib_median": f_med, "write_size_kib_median": w_med,
            "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
            "hbm_bytes_per_launch": read_b + write_b,
-           "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write = WRITE_SIZE x 1024"}
+           "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write = WRITE_SIZE x 1024",
+           "build": build_tag(), "collected": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, one pass each, median per dispatch"}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))

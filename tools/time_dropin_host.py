@@ -141,7 +141,7 @@ def main(rounds=30, K=128):
     # chunk schedules of the synchronous call's pipeline (fjhost.pipeline_fracs)
     sweep = {}
     for rep in range(2):  # the schedules interleaved, twice
-        for fr in [(), (0.125, 0.375), (0.1, 0.3), (0.15, 0.45), (0.0625, 0.25), (0.2,), (0.1, 0.25, 0.5)]:
+        for fr in [(), (0.1,), (0.15,), (0.2,), (0.3,), (0.1, 0.3), (0.15, 0.45)]:
             host.pipeline_fracs(list(fr))
             walls = []
             for _ in range(3 * rounds):
