@@ -888,10 +888,31 @@ int64_t structure_token(const std::vector<int64_t>& sig, const PWalk& w) {
   return tok;
 }
 
-// capture(tree, dev) -> (leaves_tuple, version_sum, nbytes, token) | None   (dev = -1: the first leaf's)
+// capture(tree, dev) -> (leaves_tuple, version_sum, nbytes, token, data_ptrs) | None   (dev = -1: the first
+//     leaf's)
 //     tree_weight's lazy result holds its input's leaves (strong references, flatten order)
 //     and their version sum, so the fold can check that nothing changed in between; token
 //     (structure_token) lets tree_add match two captured trees' structures without a walk.
+// The data pointers of a capture's leaves as bytes (int64 each), element 4 of the capture.
+// A `.data = other` reassignment keeps a tensor object and, with torch's set_data, its
+// version counter, but moves its storage: the folds compare these pointers with the
+// captured tensors' current ones and refuse a moved leaf as they refuse a modified one.
+PyObject* ptr_bytes(PyObject* const* leaves, Py_ssize_t L) {
+  PyObject* b = PyBytes_FromStringAndSize(nullptr, 8 * L);
+  if (!b) return nullptr;
+  auto* p = reinterpret_cast<int64_t*>(PyBytes_AS_STRING(b));
+  for (Py_ssize_t l = 0; l < L; ++l) p[l] = reinterpret_cast<int64_t>(THPVariable_Unpack(leaves[l]).data_ptr());
+  return b;
+}
+
+// captured data pointer of leaf l (capture element 4), or 0 when the capture has none
+inline int64_t captured_ptr(PyObject* cap, Py_ssize_t l) {
+  if (PyTuple_GET_SIZE(cap) < 5) return 0;
+  PyObject* b = PyTuple_GET_ITEM(cap, 4);
+  if (!PyBytes_Check(b) || PyBytes_GET_SIZE(b) < 8 * (l + 1)) return 0;
+  return reinterpret_cast<const int64_t*>(PyBytes_AS_STRING(b))[l];
+}
+
 // New reference: the capture tuple, Py_None (not the fast case), or nullptr (Python error).
 PyObject* capture_impl(PyObject* tree, int dev) {
   try {
@@ -927,18 +948,20 @@ PyObject* capture_impl(PyObject* tree, int dev) {
       for (int64_t s : t.sizes()) sig.push_back(s);
     }
     const int64_t tok = structure_token(sig, w);
-    PyObject* out = PyTuple_New(4);
+    PyObject* out = PyTuple_New(5);
     PyObject* a = PyLong_FromLongLong(vs);
     PyObject* b = PyLong_FromLongLong(nbytes);
     PyObject* c = PyLong_FromLongLong(tok);
-    if (!out || !a || !b || !c) {
-      Py_XDECREF(out), Py_XDECREF(a), Py_XDECREF(b), Py_XDECREF(c), Py_DECREF(tup);
+    PyObject* d = ptr_bytes(w.leaves[0].data(), L);
+    if (!out || !a || !b || !c || !d) {
+      Py_XDECREF(out), Py_XDECREF(a), Py_XDECREF(b), Py_XDECREF(c), Py_XDECREF(d), Py_DECREF(tup);
       return nullptr;
     }
     PyTuple_SET_ITEM(out, 0, tup);
     PyTuple_SET_ITEM(out, 1, a);
     PyTuple_SET_ITEM(out, 2, b);
     PyTuple_SET_ITEM(out, 3, c);
+    PyTuple_SET_ITEM(out, 4, d);
     return out;
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
@@ -1028,7 +1051,11 @@ PyObject* append_check(PyObject*, PyObject* args) {
       if (!PyTuple_Check(cap) || PyTuple_GET_SIZE(cap) < 2) Py_RETURN_NONE;
       PyObject* tup = PyTuple_GET_ITEM(cap, 0);
       bool same = PyTuple_GET_SIZE(tup) == L && PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1)) == vs;
-      for (Py_ssize_t l = 0; same && l < L; ++l) same = w.leaves[1][l] == PyTuple_GET_ITEM(tup, l);
+      for (Py_ssize_t l = 0; same && l < L; ++l) {
+        same = w.leaves[1][l] == PyTuple_GET_ITEM(tup, l);
+        const int64_t cp = captured_ptr(cap, l);
+        if (same && cp) same = cp == reinterpret_cast<int64_t>(THPVariable_Unpack(w.leaves[1][l]).data_ptr());
+      }
       if (!same) return PyLong_FromLong(kStale);
       Py_INCREF(cap);
       return cap;
@@ -1041,7 +1068,12 @@ PyObject* append_check(PyObject*, PyObject* args) {
       PyTuple_SET_ITEM(tup, l, w.leaves[1][l]);
       nbytes += 4 * THPVariable_Unpack(w.leaves[1][l]).numel();
     }
-    return Py_BuildValue("(NLL)", tup, static_cast<long long>(vs), static_cast<long long>(nbytes));
+    PyObject* pb = ptr_bytes(w.leaves[1].data(), L);
+    if (!pb) {
+      Py_DECREF(tup);
+      return nullptr;
+    }
+    return Py_BuildValue("(NLLLN)", tup, static_cast<long long>(vs), static_cast<long long>(nbytes), -1LL, pb);
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
@@ -1104,6 +1136,8 @@ PyObject* table_from_caps(PyObject*, PyObject* args) {
         const at::Tensor& t = THPVariable_Unpack(PyTuple_GET_ITEM(tup, l));
         vs += version_of(t);
         out[k * L + l] = reinterpret_cast<int64_t>(t.data_ptr());
+        const int64_t cp = captured_ptr(cap, l);
+        if (cp && cp != out[k * L + l]) return PyLong_FromSsize_t(k);  // storage moved (`.data =`)
       }
       if (vs != PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1))) return PyLong_FromSsize_t(k);
     }
@@ -1191,6 +1225,8 @@ PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const*
         }
         vs += version_of(t);
         ptrs[k * L + l] = reinterpret_cast<int64_t>(t.data_ptr());
+        const int64_t cp = captured_ptr(cap, l);
+        if (cp && cp != ptrs[k * L + l]) return PyLong_FromSsize_t(k);  // storage moved (`.data =`)
       }
       const long long want = PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1));
       if (want == -1 && PyErr_Occurred()) return nullptr;
@@ -1291,7 +1327,11 @@ PyObject* leaf_fold(PyObject*, PyObject* args) {
       PyObject* tup = PyTuple_GET_ITEM(cap, 0);
       long long cv = PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1));
       bool same = PyTuple_GET_SIZE(tup) == static_cast<Py_ssize_t>(w.leaves[k].size()) && cv == vs;
-      for (size_t l = 0; same && l < w.leaves[k].size(); ++l) same = w.leaves[k][l] == PyTuple_GET_ITEM(tup, l);
+      for (size_t l = 0; same && l < w.leaves[k].size(); ++l) {
+        same = w.leaves[k][l] == PyTuple_GET_ITEM(tup, l);
+        const int64_t cp = captured_ptr(cap, static_cast<Py_ssize_t>(l));
+        if (same && cp) same = cp == reinterpret_cast<int64_t>(THPVariable_Unpack(w.leaves[k][l]).data_ptr());
+      }
       if (!same) return Py_BuildValue("(iOOO)", kStale, Py_None, Py_None, Py_None);
     }
     const int L = static_cast<int>(w.leaves[0].size());
@@ -2057,6 +2097,9 @@ PyType_Spec kChainSpec = {"_fjhost.ChainBase", sizeof(ChainObject), 0, kBaseFlag
 PyType_Spec kPSSpec = {"_fjhost.PendingBase", sizeof(PSObject), 0, kBaseFlags, kPSSlots};
 
 struct FastState {
+  PyTypeObject* ticket = nullptr;    // tree_util._Ticket
+  PyTypeObject* norm_view = nullptr;  // tree_util._NormView
+  PyObject* py_l2[2] = {nullptr, nullptr};  // tree_util._tree_l2_squared_py / _tree_l2_norm_py
   PyTypeObject* wt = nullptr;     // tree_util.WeightedTree
   PyTypeObject* ps = nullptr;     // tree_util.PendingSum
   PyTypeObject* chain = nullptr;  // tree_util._Chain
@@ -2209,6 +2252,102 @@ PyObject* fast_tree_add(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyOb
     }
   }
   return PyObject_Vectorcall(g_fast.py_tree_add, args, nargs, kwnames);
+}
+
+
+// fast_install_norms(_Ticket, _NormView, py_tree_l2_squared, py_tree_l2_norm)
+PyObject* fast_install_norms(PyObject*, PyObject* args) {
+  PyObject *tk, *nv, *f0, *f1;
+  if (!PyArg_ParseTuple(args, "O!O!OO", &PyType_Type, &tk, &PyType_Type, &nv, &f0, &f1)) return nullptr;
+  Py_INCREF(tk), Py_INCREF(nv), Py_INCREF(f0), Py_INCREF(f1);
+  Py_XSETREF(g_fast.ticket, reinterpret_cast<PyTypeObject*>(tk));
+  Py_XSETREF(g_fast.norm_view, reinterpret_cast<PyTypeObject*>(nv));
+  Py_XSETREF(g_fast.py_l2[0], f0);
+  Py_XSETREF(g_fast.py_l2[1], f1);
+  Py_RETURN_NONE;
+}
+
+// tree_l2_squared / tree_l2_norm (tree_util.py:105-114) of the delta the running sum just
+// took: a lazy 0-d view into its chain's norm buffer, which the chain's fold fills
+// (tree_util._lazy_norm, built here without a Python frame). The tree must hold exactly the
+// captured leaves of the most recent PendingSum link, unmodified, and the chain's buffer must
+// exist (the Python path allocates it for the chain's first norm). Anything else: the Python
+// function.
+PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, int which) {
+  PyObject* py = g_fast.py_l2[which];
+  if (!py) {
+    PyErr_SetString(PyExc_RuntimeError, "fedjax_amd.tree_util is not installed (fast_install_norms)");
+    return nullptr;
+  }
+  if (nargs == 1 && !kwnames && g_fast.defer && g_fast.last && g_fast.norm_view && g_fast.ticket &&
+      Py_TYPE(args[0]) != g_fast.wt && Py_TYPE(args[0]) != g_fast.ps) {
+    PyObject* no = PyWeakref_GetObject(g_fast.last);
+    if (no && Py_TYPE(no) == g_fast.ps) {
+      auto* node = reinterpret_cast<PSObject*>(no);
+      auto* ch = reinterpret_cast<ChainObject*>(node->chain);
+      if ((!node->value || node->value == Py_None) && node->cap && PyTuple_CheckExact(node->cap) &&
+          PyTuple_GET_SIZE(node->cap) >= 2 && ch && Py_TYPE(ch) == g_fast.chain && ch->buf &&
+          THPVariable_Check(ch->buf)) {
+        Py_INCREF(no);  // (held for the check: the walk below could run Python code)
+        struct Drop {
+          PyObject* o;
+          ~Drop() { Py_DECREF(o); }
+        } drop{no};
+        try {
+          PWalk w;
+          w.K = 1;
+          w.leaves[0].reserve(16);
+          PyObject* tree = args[0];
+          const int rc = pwalk(&tree, w, 0);
+          if (rc < 0) return nullptr;
+          PyObject* tup = PyTuple_GET_ITEM(node->cap, 0);
+          bool same = rc == 0 && PyTuple_Check(tup) &&
+                      static_cast<Py_ssize_t>(w.leaves[0].size()) == PyTuple_GET_SIZE(tup);
+          int64_t vs = 0;
+          for (size_t l = 0; same && l < w.leaves[0].size(); ++l) {
+            same = w.leaves[0][l] == PyTuple_GET_ITEM(tup, l);
+            if (!same) break;
+            const at::Tensor& t = THPVariable_Unpack(w.leaves[0][l]);
+            vs += version_of(t);
+            const int64_t cp = captured_ptr(node->cap, static_cast<Py_ssize_t>(l));
+            if (cp && cp != reinterpret_cast<int64_t>(t.data_ptr())) same = false;
+          }
+          if (same && vs == PyLong_AsLongLong(PyTuple_GET_ITEM(node->cap, 1))) {
+            const at::Tensor& b = THPVariable_Unpack(ch->buf);
+            const int row = which;  // row 0 = squared norms, row 1 = norms
+            if (b.dim() == 2 && node->idx < b.size(1)) {
+              if (!node->ticket || node->ticket == Py_None) {
+                PyObject* t = PyObject_CallOneArg(reinterpret_cast<PyObject*>(g_fast.ticket), no);
+                if (!t) return nullptr;
+                Py_XSETREF(node->ticket, t);
+              }
+              PyObject* v = THPVariable_Wrap(
+                  b.as_strided({}, {}, b.storage_offset() + row * b.stride(0) + node->idx * b.stride(1)),
+                  g_fast.norm_view);
+              if (!v) return nullptr;
+              static PyObject* name = PyUnicode_InternFromString("_ticket");
+              if (PyObject_SetAttr(v, name, node->ticket) != 0) {
+                Py_DECREF(v);
+                return nullptr;
+              }
+              return v;
+            }
+          }
+        } catch (const std::exception& e) {
+          PyErr_SetString(PyExc_RuntimeError, e.what());
+          return nullptr;
+        }
+      }
+    }
+  }
+  return PyObject_Vectorcall(py, args, nargs, kwnames);
+}
+
+PyObject* fast_tree_l2_squared(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
+  return fast_l2(args, nargs, kwnames, 0);
+}
+PyObject* fast_tree_l2_norm(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
+  return fast_l2(args, nargs, kwnames, 1);
 }
 
 // zeros_like(tree) -> tree | None: tree_util.tree_zeros_like (tree_util.py:41-44) for a plain
@@ -2365,6 +2504,17 @@ PyMethodDef kMethods[] = {
     {"mean_triples", mean_triples, METH_O, "tree_mean over (client_id, params, weight) triples (aggregator.py:61-75)"},
     {"pipeline_fracs", pipeline_fracs, METH_O, "chunk ends (fractions of K) of tree_mean's fold-bound pipeline"},
     {"fold_chain", fold_chain, METH_VARARGS, "a PendingSum's deferred fold, its links walked natively"},
+    {"fast_install_norms", fast_install_norms, METH_VARARGS, "register tree_util's lazy norm classes and fallbacks"},
+    {"tree_l2_squared", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_tree_l2_squared)),
+     METH_FASTCALL | METH_KEYWORDS,
+     "tree_l2_squared(pytree)\n--\n\nReturns squared l2 norm of tree (fedjax/core/tree_util.py:105-108), a 0-d "
+     "float32 tensor.\n\nThe delta a deferred running sum just took gets a lazy view its fold fills; anything "
+     "else is\nfedjax_amd.tree_util._tree_l2_squared_py."},
+    {"tree_l2_norm", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_tree_l2_norm)),
+     METH_FASTCALL | METH_KEYWORDS,
+     "tree_l2_norm(pytree)\n--\n\nReturns l2 norm of tree (fedjax/core/tree_util.py:111-114), a 0-d float32 "
+     "tensor.\n\nThe delta a deferred running sum just took gets a lazy view its fold fills; anything else "
+     "is\nfedjax_amd.tree_util._tree_l2_norm_py."},
     {"fast_install", fast_install, METH_VARARGS, "register tree_util's lazy classes and Python fallbacks"},
     {"fast_config", fast_config, METH_VARARGS, "deferred-sum settings (tree_util.set_deferred_sums)"},
     {"set_last", set_last, METH_O, "remember the most recent PendingSum link (weakly)"},

@@ -1514,8 +1514,10 @@ def _l2_fast(pytree_, which: int):
     return None if got is None else got[1 + which]
 
 
-def tree_l2_squared(pytree_: PyTree) -> torch.Tensor:
-    """Returns squared l2 norm of tree (tree_util.py:105-108), a 0-d float32 tensor."""
+def _tree_l2_squared_py(pytree_: PyTree) -> torch.Tensor:
+    """Returns squared l2 norm of tree (tree_util.py:105-108), a 0-d float32 tensor.
+    :func:`tree_l2_squared` is the native fjhost.tree_l2_squared, which returns the lazy
+    view of the delta a deferred sum just took itself and calls this function otherwise."""
     pytree_ = _eager(pytree_)
     got = _l2_fast(pytree_, 0)
     if got is not None:
@@ -1528,8 +1530,9 @@ def tree_l2_squared(pytree_: PyTree) -> torch.Tensor:
     return _l2_rows(rows, take_sqrt=False).reshape(())
 
 
-def tree_l2_norm(pytree_: PyTree) -> torch.Tensor:
-    """Returns l2 norm of tree (tree_util.py:111-114), a 0-d float32 tensor."""
+def _tree_l2_norm_py(pytree_: PyTree) -> torch.Tensor:
+    """Returns l2 norm of tree (tree_util.py:111-114), a 0-d float32 tensor.
+    :func:`tree_l2_norm` is the native fjhost.tree_l2_norm (see _tree_l2_squared_py)."""
     pytree_ = _eager(pytree_)
     got = _l2_fast(pytree_, 1)
     if got is not None:
@@ -1540,6 +1543,13 @@ def tree_l2_norm(pytree_: PyTree) -> torch.Tensor:
     if len({x.dtype for x in rows[0]}) > 1 or rows[0][0].dtype == torch.int32:
         return torch.sqrt(_l2sq_mixed(rows[0]).float())  # jnp.sqrt of an int32 sum is float32
     return _l2_rows(rows, take_sqrt=True).reshape(())
+
+
+# The per-client delta_l2_norm of the running-sum loops (fed_avg.py:142-144), native: the lazy
+# view of the delta the running sum just took, without a Python frame (fjhost.tree_l2_norm).
+_HOST.fast_install_norms(_Ticket, _NormView, _tree_l2_squared_py, _tree_l2_norm_py)
+tree_l2_squared = _HOST.tree_l2_squared
+tree_l2_norm = _HOST.tree_l2_norm
 
 
 def tree_l2_norms(pytrees: Sequence[PyTree]) -> torch.Tensor:

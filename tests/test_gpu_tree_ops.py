@@ -394,6 +394,34 @@ def test_data_writes_bypass_the_deferred_guard_as_documented(cuda, sum_mode):
         assert np.array_equal(bits(tu.tree_inverse_weight(s2, 3.)["a"].cpu().numpy()), bits(old))
 
 
+def test_data_reassignment_is_refused_by_the_deferred_fold(cuda, sum_mode):
+    """``x.data = other`` moves a captured leaf to another storage (its version counter
+    need not change): the capture's data pointers (fjhost capture element 4) make the
+    deferred fold raise instead of summing the other storage; eager mode has already summed
+    the old value, as the reference does. The same for the running sum's base, and for a
+    bf16 storage of the same element count (element-count check only)."""
+    g = torch.Generator().manual_seed(43)
+    h0, h1 = rand_tree({"a": (500,), "b": (7,)}, g), rand_tree({"a": (500,), "b": (7,)}, g)
+    old = ref.tree_inverse_weight(ref.tree_weight(to_np(h0), 3), 3.)
+    for replacement in (lambda: h1["a"].to(cuda), lambda: h1["a"].to(cuda).to(torch.bfloat16)):
+        d = to_dev(h0, cuda)
+        s = tu.tree_add(tu.tree_zeros_like(d), tu.tree_weight(d, 3))
+        d["a"].data = replacement()
+        if sum_mode == "deferred":
+            with pytest.raises(RuntimeError, match="modified"):
+                tu.tree_inverse_weight(s, 3.)
+        else:
+            got = tu.tree_inverse_weight(s, 3.)
+            assert all(np.array_equal(bits(got[k].cpu().numpy()), bits(old[k])) for k in ("a", "b"))
+    if sum_mode == "deferred":
+        d = to_dev(h0, cuda)
+        base = tu.tree_zeros_like(d)
+        s = tu.tree_add(base, tu.tree_weight(d, 3))
+        base["b"].data = torch.ones(7, device=cuda)
+        with pytest.raises(RuntimeError, match="running sum passed to tree_add was modified"):
+            tu.tree_inverse_weight(s, 3.)
+
+
 def test_deferred_chain_budget_is_bounded_by_free_memory(cuda, sum_mode):
     """the automatic per-chain budget is min(4 GiB, free/8); a tiny explicit
     budget folds the older part of the chain early with the same bits."""

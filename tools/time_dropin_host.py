@@ -111,6 +111,27 @@ def main(rounds=30, K=128):
                            "round_sync_ms": med(sync_round), "round_back_to_back_ms": round(b2b, 4),
                            "fold_phases_us": {k: round(v, 2) for k, v in host.host_timers().items()}}
     del s, m
+    # the loop as fedjax/algorithms/fed_avg.py:132-146 writes it: + tree_l2_norm(delta) per client
+    # (the norms read back once after the round, as client_diagnostics are)
+    tn, norm_round = [], []
+    for r in range(rounds + 5):
+        torch.cuda.synchronize()
+        t0 = pc()
+        s = tu.tree_zeros_like(pairs[0][0])
+        norms, c = [], 0.0
+        for t, w in pairs:
+            s = tu.tree_add(s, tu.tree_weight(t, w))
+            u0 = pc()
+            norms.append(tu.tree_l2_norm(t))
+            c += pc() - u0
+        m = tu.tree_inverse_weight(s, W)
+        vals = torch.stack(norms).cpu()  # (one read of the round's norms)
+        torch.cuda.synchronize()
+        if r >= 5:
+            norm_round.append((pc() - t0) * 1e3)
+            tn.append(c / K * 1e6)
+    res["library_loop"]["with_l2_norms"] = {"tree_l2_norm_us": med(tn), "round_sync_ms": med(norm_round)}
+    del s, m, norms, vals
     # ---- synchronous tree_mean / mean_aggregator().apply
     agg = fedjax_amd.aggregators.mean_aggregator()
     triples = [(f"c{k}", t, w) for k, (t, w) in enumerate(pairs)]
