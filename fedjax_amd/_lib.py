@@ -110,6 +110,11 @@ _SIGNATURES = {
     "fjopt_abi_version": (_i32, []),
     "fjopt_adafactor_plan": (_i64, [_vp, _i32, _vp, _vp, _i64, _vp]),
     "fjopt_adafactor_step": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
+    # include/fjalloc.h (opt-in delta-memory segments, fedjax_amd.memory)
+    "fjalloc_alloc": (_vp, [ctypes.c_ssize_t, _i32, _vp]),
+    "fjalloc_free": (None, [_vp, ctypes.c_size_t, _i32, _vp]),
+    "fjalloc_stats": (_i32, [_i32, _vp]),
+    "fjalloc_set_reserve_bytes": (_i32, [_i64]),
 }
 SYMBOLS = tuple(_SIGNATURES)
 

@@ -12,6 +12,7 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); run with -m gpu")
+    config.addinivalue_line("markers", "deferred_only: test_gpu_tree_ops runs it with deferred running sums only")
 
 
 def _build_oracle():

@@ -13,14 +13,15 @@ import torch
 from fedjax_amd import _lib, kernels
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("fjagg.h", "fjcomp.h", "fjcomm.h", "fjtree.h", "fjopt.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("fjagg.h", "fjcomp.h", "fjcomm.h", "fjtree.h", "fjopt.h",
+                                                           "fjalloc.h")]
 
 
 def header_symbols():
     syms = set()
     for h in HEADERS:
         src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
-        syms |= set(re.findall(r"\b(fj(?:agg|comp|comm|tree|opt)_\w+)\s*\(", src))
+        syms |= set(re.findall(r"\b(fj(?:agg|comp|comm|tree|opt|alloc)_\w+)\s*\(", src))
     return syms
 
 
@@ -31,7 +32,7 @@ def test_header_and_binding_agree():
 def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
-    exported = set(re.findall(r"\bT (fj(?:agg|comp|comm|tree|opt)_\w+)", out))
+    exported = set(re.findall(r"\bT (fj(?:agg|comp|comm|tree|opt|alloc)_\w+)", out))
     assert header_symbols() <= exported, header_symbols() - exported
 
 

@@ -22,12 +22,20 @@ from oracle import tree_util_ref as ref
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["deferred", "eager"], autouse=True)
-def sum_mode(request):
+def pytest_generate_tests(metafunc):
     """Every test runs with deferred running sums (PendingSum, the default) and with one
-    fused launch per tree_add (set_deferred_sums(False))."""
-    tu.set_deferred_sums(request.param == "deferred")
-    yield request.param
+    fused launch per tree_add (set_deferred_sums(False)); tests marked deferred_only test
+    the deferred chain itself and run in that mode only."""
+    if "sum_mode" in metafunc.fixturenames:
+        only = metafunc.definition.get_closest_marker("deferred_only") is not None
+        metafunc.parametrize("sum_mode", ["deferred"] if only else ["deferred", "eager"], indirect=True)
+
+
+@pytest.fixture(autouse=True)
+def sum_mode(request):
+    mode = getattr(request, "param", "deferred")
+    tu.set_deferred_sums(mode == "deferred")
+    yield mode
     tu.set_deferred_sums(True)
 
 
@@ -228,12 +236,11 @@ def test_literal_loop_configs1_bitwise_and_host_cost(K, cuda, sum_mode):
     np.testing.assert_allclose(torch.stack(norms).cpu().numpy(), nn.cpu().numpy(), rtol=2e-6)
 
 
+@pytest.mark.deferred_only
 def test_pending_sum_chain_semantics(cuda, sum_mode):
     """PendingSum keeps every intermediate sum valid (s1 stays s0 + x1 after s2 is built),
     folds in bounded chunks under the budget, applies tree_inverse_weight's scale in the
     same launch, and refuses a delta modified in place after its tree_weight."""
-    if sum_mode != "deferred":
-        pytest.skip("deferred mode only")
     g = torch.Generator().manual_seed(11)
     shapes = {"a": (1001,), "b": {"c": (6, 7)}}
     xs = [to_dev(rand_tree(shapes, g), cuda) for _ in range(9)]
@@ -287,13 +294,12 @@ def test_pending_sum_chain_semantics(cuda, sum_mode):
         tu.tree_inverse_weight(s, 5.0)
 
 
+@pytest.mark.deferred_only
 def test_lazy_norms_of_a_deferred_sum(cuda, sum_mode):
     """tree_l2_norm of the delta just added to a deferred sum is a _NormView that the sum's
     fold fills: reading it first runs the fold (any torch function or method), reading it
     after tree_inverse_weight needs nothing more, and once filled the view no longer keeps
     the chain (or its deltas) alive."""
-    if sum_mode != "deferred":
-        pytest.skip("deferred mode only")
     import gc
     import weakref
     g = torch.Generator().manual_seed(12)
@@ -422,11 +428,10 @@ def test_data_reassignment_is_refused_by_the_deferred_fold(cuda, sum_mode):
             tu.tree_inverse_weight(s, 3.)
 
 
+@pytest.mark.deferred_only
 def test_deferred_chain_budget_is_bounded_by_free_memory(cuda, sum_mode):
     """the automatic per-chain budget is min(4 GiB, free/8); a tiny explicit
     budget folds the older part of the chain early with the same bits."""
-    if sum_mode != "deferred":
-        pytest.skip("deferred mode only")
     b = tu._defer_budget(torch.device(cuda))
     free, _ = torch.cuda.mem_get_info()
     assert 64 << 20 <= b <= 4 << 30 and b <= max(64 << 20, free // 4)
@@ -448,13 +453,12 @@ def test_deferred_chain_budget_is_bounded_by_free_memory(cuda, sum_mode):
     assert np.array_equal(bits(got), bits(ref.tree_inverse_weight(want, 45.)["a"]))
 
 
+@pytest.mark.deferred_only
 def test_early_flush_of_the_running_sum(cuda, sum_mode):
     """The deferred chain folds its pending part once it holds flush_bytes in flush_clients
     links (set_deferred_sums): the literal loop with the per-client norm of fed_avg.py:
     137-144 keeps the reference's bits for the mean, and each norm is the same value the
     one-launch chain gives."""
-    if sum_mode != "deferred":
-        pytest.skip("deferred mode only")
     g = torch.Generator().manual_seed(23)
     shapes = {"w": (3000,), "b": {"c": (17,)}}
     K = 23
@@ -489,13 +493,12 @@ def test_early_flush_of_the_running_sum(cuda, sum_mode):
         np.testing.assert_allclose(norms, n64, rtol=2e-6)
 
 
+@pytest.mark.deferred_only
 def test_native_chain_fold_equals_python_path(cuda, sum_mode, monkeypatch):
     """A deferred sum's fold through fjhost.fold_caps (one native call) against the Python
     path (_FOLD_CAPS off): the literal loop's mean and lazy norms bitwise, with early
     flushes (several folds per round), a nested / list / None structure, and the stale
     errors (base and client) raised the same way."""
-    if sum_mode != "deferred":
-        pytest.skip("deferred mode only")
     g = torch.Generator().manual_seed(21)
     shapes = {"z": [(70,), None, ((3,), (5, 2))], "a": {"q": (8,), "p": (1001,)}}
 
