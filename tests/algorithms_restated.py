@@ -1,10 +1,14 @@
-"""Numpy restatement of the client steps of four more FedJAX algorithms whose server
+"""Numpy restatement of the client steps of the other FedJAX algorithms whose server
 side is the running-sum path (test infrastructure, like tests/fedavg_restated.py):
 
 * FedProx            fedjax/algorithms/fed_prox.py:43-151, KAT fed_prox_test.py:36-65
 * Mime               fedjax/algorithms/mime.py:42-211,     KAT mime_test.py:38-63
 * Mime Lite          fedjax/algorithms/mime_lite.py:45-170, KATs mime_lite_test.py:38-66, :92-119
 * AgnosticFedAvg     fedjax/algorithms/agnostic_fed_avg.py:39-311, KAT agnostic_fed_avg_test.py:34-78
+* APFL               fedjax/algorithms/apfl.py:88-231,     KAT apfl_test.py:50-98
+* stateful FedAvg    examples/stateful_fed_avg.py:139-186, KAT stateful_fed_avg_test.py:46-67
+* HypCluster         fedjax/algorithms/hyp_cluster.py:89-301, KATs hyp_cluster_test.py:366-403, :405-472
+  (one running sum per cluster, interleaved)
 
 Client training (the gradients, the client SGD steps, the domain statistics) is NOT on
 the aggregation path; it is restated in float32 numpy, following JAX's reverse-mode
@@ -252,8 +256,105 @@ def agnostic_fed_avg_round(tu, to_leaf, to_numpy, to_weight):
             "betas": {c: metrics[c]["beta"] for c, _, _ in clients}}
 
 
+# ---------------------------------------------------------------------------- APFL
+def apfl_round(tu, to_leaf, to_numpy, to_weight, client_coefficient=0.5):
+    """apfl.py:185-231 with apfl_test.py:28-31's grad_fn (l / sum(batch['x'])), client and
+    server sgd(1.0), batches of 2 (1 epoch, seed 0), client_coefficient 0.5. Each client
+    trains the server track, its own params and the interpolation coefficient
+    (create_train_for_each_client, :88-154); the running sum takes the server track's delta."""
+    from tests.fedavg_restated import CLIENTS, SERVER_PARAMS
+    s0 = np.asarray(SERVER_PARAMS["w"], F)
+    delta_sum = tu.tree_zeros_like({"w": to_leaf(s0)})
+    num_examples_sum = 0.0
+    norms, cparams, coefs = {}, {}, {}
+    for cid, x in CLIENTS:
+        s, c, a = s0.copy(), s0.copy(), 0.5  # client_default_state: params, coefficient (Python float)
+        for idx in shuffle_repeat_batch_indices(len(x), 2, 1, 0):
+            S = np.sum(x[idx], dtype=F)
+            p = (F(a) * c + F(1 - a) * s).astype(F)  # interpolate_params: a * b + (1 - a) * c
+            sg, cg = (s / S).astype(F), (p / S).astype(F)
+            ig = F(np.tensordot((c - s).astype(F), cg, axes=1))  # interpolation_grad_fn
+            s = (s + F(-1.0) * sg).astype(F)
+            c = (c + F(-1.0) * cg).astype(F)
+            a = np.clip(F(F(a) + F(-1.0) * ig), 0, 1)
+        delta = {"w": to_leaf((s0 - s).astype(F))}
+        delta_sum = tu.tree_add(delta_sum, tu.tree_weight(delta, len(x)))
+        num_examples_sum += len(x)
+        norms[cid] = F(to_numpy(tu.tree_l2_norm(delta)))
+        cparams[cid], coefs[cid] = c, np.asarray([a], F)
+    mean = np.asarray(to_numpy(tu.tree_inverse_weight(delta_sum, num_examples_sum)["w"]), F)
+    return {"params": (s0 + F(-1.0) * mean).astype(F), "mean_delta": mean, "norms": norms,
+            "client_params": cparams, "client_coefficients": coefs}
+
+
+# ------------------------------------------------------------- stateful FedAvg example
+def stateful_fed_avg_round(tu, to_leaf, to_numpy, to_weight):
+    """examples/stateful_fed_avg.py:139-186: FedAvg's client update with a per-client step
+    counter (client state; not aggregated) and the same running sum (stateful_fed_avg_test.py
+    :46-67, grad_fn l / sum(batch['x']), batches of 2, 1 epoch, seed 0)."""
+    from tests.fedavg_restated import CLIENTS, SERVER_PARAMS, fed_avg_library_round
+    new, norms = fed_avg_library_round(tu, to_leaf, to_numpy, SERVER_PARAMS, CLIENTS, 2, 1, 0)
+    steps = {cid: len(list(shuffle_repeat_batch_indices(len(x), 2, 1, 0))) for cid, x in CLIENTS}
+    return {"params": np.asarray(new["w"], F), "norms": {k: F(v) for k, v in norms.items()}, "num_steps": steps}
+
+
+# --------------------------------------------------------------------------- HypCluster
+_HC_CLIENTS = [(b"0", np.array([1.1], F)), (b"1", np.array([0.9, 0.9], F)), (b"2", np.array([-1.1], F)),
+               (b"3", np.array([-0.9, -0.9, -0.9], F))]
+
+
+def _hc_delta(p, x, lr=0.5, epochs=5):
+    """ClientDeltaTrainer (hyp_cluster.py:200-210) with models.grad of jnp.square(params - x),
+    sgd(lr), batches of 1 for `epochs` epochs: initial params - final params. (The test's
+    clients repeat one value, so the unseeded shuffle order does not matter.)"""
+    w = F(p)
+    for _ in range(epochs * len(x)):
+        for xi in x[:1]:
+            g = F(F(2) * F(w - xi))  # integer_pow's jvp: 2 * z, times the mean's cotangent 1.0
+            w = F(w + F(F(-lr) * g))
+    return F(F(p) - w)
+
+
+def _hc_expectation(tu, to_leaf, to_numpy, cluster_params, ids, clients):
+    """hyp_cluster.expectation_step (hyp_cluster.py:268-301): one running sum per cluster,
+    the clients' tree_add calls interleaved across the sums; None for a cluster no client
+    chose."""
+    sums = [tu.tree_zeros_like(to_leaf(np.asarray(p, F))) for p in cluster_params]
+    nsum = [0 for _ in cluster_params]
+    for cid, x in clients:
+        cl = ids[cid]
+        d = _hc_delta(cluster_params[cl], x)
+        sums[cl] = tu.tree_add(sums[cl], tu.tree_weight(to_leaf(np.asarray(d, F)), len(x)))
+        nsum[cl] += len(x)
+    return [F(to_numpy(tu.tree_inverse_weight(s, n))) if n > 0 else None for s, n in zip(sums, nsum)]
+
+
+def hyp_cluster_expectation_round(tu, to_leaf, to_numpy, to_weight):
+    """hyp_cluster_test.py:366-403: three clusters [1, -1, 3.14], clients 0, 1, 4 in cluster
+    0 and 2, 3 in cluster 1, none in cluster 2."""
+    clients = _HC_CLIENTS + [(b"4", np.array([-0.1], F))]
+    ids = {b"0": 0, b"1": 0, b"2": 1, b"3": 1, b"4": 0}
+    deltas = _hc_expectation(tu, to_leaf, to_numpy, [1., -1., 3.14], ids, clients)
+    return {"cluster_deltas": deltas[:2], "empty_cluster": deltas[2]}
+
+
+def hyp_cluster_round(tu, to_leaf, to_numpy, to_weight):
+    """hyp_cluster.py:89-128 with hyp_cluster_test.py:405-472's setup: clusters [1, -1], the
+    maximization step's assignment (argmin over clusters of the mean loss (p - x)^2, regularizer
+    0; hyp_cluster.py:224-260), the expectation step's running sums, then sgd(0.25) per cluster."""
+    params = [F(1.), F(-1.)]
+    ids = {}
+    for cid, x in _HC_CLIENTS:
+        losses = [np.mean(np.square((F(p) - x).astype(F)), dtype=F) for p in params]
+        ids[cid] = int(np.argmin(losses))
+    deltas = _hc_expectation(tu, to_leaf, to_numpy, params, ids, _HC_CLIENTS)
+    new = [p if d is None else F(p + F(F(-0.25) * d)) for p, d in zip(params, deltas)]
+    return {"cluster_params": new, "cluster_ids": ids}
+
+
 # The reference's KATs: (name, round fn, {result key: expected}); npt.assert_allclose's
-# default rtol (1e-7) is the reference's tolerance for every value listed.
+# default rtol (1e-7) is the reference's tolerance for every value listed, unless the
+# reference's test gives one: (value, rtol).
 KATS = [
     ("fedjax/algorithms/fed_prox_test.py:62-65", fed_prox_round,
      {"params": -3.77, "norms": {b"cid0": 6.95, b"cid1": 9.}}),
@@ -267,15 +368,37 @@ KATS = [
      {"params": 3.5555556, "norms": {b"cid0": 2.8333335, b"cid1": 7.666667},
       "domain_weights": [0.08702461, 0.18604803, 0.2663479, 0.46057943],
       "domain_window": [[1., 2., 3., 4.], [3., 3., 2., 1.]]}),
+    ("fedjax/algorithms/apfl_test.py:77-98", apfl_round,
+     {"params": [0., 1.5655555, 3.131111], "norms": {b"cid0": 1.4534444262, b"cid1": 0.2484521282},
+      "client_params": {b"cid0": [0., 1.35, 2.7], b"cid1": [0., 1.888889, 3.777778]},
+      "client_coefficients": {b"cid0": [0.5], b"cid1": [0.5]}}),
+    ("examples/stateful_fed_avg_test.py:57-64", stateful_fed_avg_round,
+     {"params": [0., 1.5655555, 3.131111], "norms": {b"cid0": 1.4534444262, b"cid1": 0.2484521282},
+      "num_steps": {b"cid0": 2, b"cid1": 1}}),
+    ("fedjax/algorithms/hyp_cluster_test.py:393-403", hyp_cluster_expectation_round,
+     {"cluster_deltas": [(-0.1 + 0.1 * 2 + 1.1) / 4, ((0.1 - 0.1 * 3) / 4, 1e-6)]}),
+    ("fedjax/algorithms/hyp_cluster_test.py:452-472", hyp_cluster_round,
+     {"cluster_params": [1. - 0.25 * 0.1 / 3, -1. + 0.25 * 0.2 / 4],
+      "cluster_ids": {b"0": 0, b"1": 0, b"2": 1, b"3": 1}}),
 ]
 
 
 def check_kat(name, got, want, rtol=1e-7):
-    """npt.assert_allclose of every listed value at the reference's tolerance."""
+    """npt.assert_allclose of every listed value at the reference's tolerance (an entry
+    (value, rtol) carries the reference test's own rtol)."""
     import numpy.testing as npt
+
+    def close(g, e, msg):
+        e, r = e if isinstance(e, tuple) else (e, rtol)
+        npt.assert_allclose(np.asarray(g, np.float64), e, rtol=r, err_msg=msg)
+
     for key, v in want.items():
         if isinstance(v, dict):
             for cid, e in v.items():
-                npt.assert_allclose(got[key][cid], e, rtol=rtol, err_msg=f"{name} {key} {cid!r}")
+                close(got[key][cid], e, f"{name} {key} {cid!r}")
+        elif isinstance(v, list) and any(isinstance(e, tuple) for e in v):
+            assert len(got[key]) == len(v), (name, key)
+            for i, e in enumerate(v):
+                close(got[key][i], e, f"{name} {key}[{i}]")
         else:
-            npt.assert_allclose(np.asarray(got[key], np.float64), v, rtol=rtol, err_msg=f"{name} {key}")
+            close(got[key], v, f"{name} {key}")

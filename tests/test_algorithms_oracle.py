@@ -1,6 +1,7 @@
 """The running-sum callers other than FedAvg pinned on the CPU: the
-restated rounds of FedProx, Mime, Mime Lite (with and without client delta clipping)
-and AgnosticFedAvg (tests/algorithms_restated.py), aggregated through the oracle
+restated rounds of FedProx, Mime, Mime Lite (with and without client delta clipping),
+AgnosticFedAvg, APFL, the stateful FedAvg example and HypCluster
+(tests/algorithms_restated.py), aggregated through the oracle
 (oracle/tree_util_ref.py), reproduce every value the reference's own tests assert, at
 their tolerance (npt.assert_allclose's default rtol 1e-7)."""
 import numpy as np
