@@ -16,6 +16,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -28,6 +29,7 @@ namespace {
 struct Segment {
   size_t size;
   hipMemGenericAllocationHandle_t handle;
+  bool own_reservation;
 };
 
 struct Arena {
@@ -39,11 +41,27 @@ struct Arena {
   std::multimap<size_t, char*> free_ranges;  // unmapped ranges by size, reused for equal sizes
   std::unordered_map<uintptr_t, Segment> live;
   int64_t mapped_bytes = 0, segments = 0, reuses = 0, failures = 0;
+  int64_t last_error = 0;  // (step << 16) | hipError_t of the last failed request
+  int64_t hinted = 0, hint_missed = 0;  // mode 1: reservations placed at / away from the hint
 };
+
+// record a failed request: which step (1 reserve, 2 create, 3 map, 4 access, 5 range) and the
+// runtime's error code, readable through fjalloc_stats
+inline void* failed(Arena& a, int step, hipError_t e) {
+  ++a.failures;
+  a.last_error = (int64_t(step) << 16) | int64_t(e);
+  return nullptr;
+}
 
 constexpr int kMaxDevices = 64;
 Arena g_arena[kMaxDevices];
 size_t g_reserve_bytes = size_t(512) << 30;  // virtual only: 512 GiB per device
+size_t g_align = size_t(2) << 20;  // segment size / address multiple (>= the runtime's granularity)
+// 1: every segment is its own reservation, requested at the address right after the previous
+// one (so the range stays contiguous while the runtime honours the hint); 0: sub-ranges of ONE
+// reservation. This torch's ROCm 7.0 runtime refuses hipMemSetAccess on the third and later
+// sub-ranges of one reservation (hipErrorInvalidValue; tools/probe_fjalloc.py), hence 1.
+int g_mode = 1;
 
 hipMemAllocationProp prop_for(int device) {
   hipMemAllocationProp p{};
@@ -53,18 +71,22 @@ hipMemAllocationProp prop_for(int device) {
   return p;
 }
 
-bool ensure_reserved(Arena& a, int device) {
-  if (a.base) return true;
+hipError_t ensure_reserved(Arena& a, int device) {
+  if (a.base) return hipSuccess;
   hipMemAllocationProp p = prop_for(device);
-  if (hipMemGetAllocationGranularity(&a.gran, &p, hipMemAllocationGranularityRecommended) != hipSuccess ||
-      a.gran == 0)
-    return false;
+  size_t g = 0;
+  hipError_t e = hipMemGetAllocationGranularity(&g, &p, hipMemAllocationGranularityRecommended);
+  if (e != hipSuccess) return e;
+  if (g == 0) return hipErrorInvalidValue;
+  a.gran = (g_align + g - 1) / g * g;  // a multiple of the runtime's granularity
   void* va = nullptr;
   const size_t want = (g_reserve_bytes + a.gran - 1) / a.gran * a.gran;
-  if (hipMemAddressReserve(&va, want, a.gran, nullptr, 0) != hipSuccess || !va) return false;
+  e = hipMemAddressReserve(&va, want, a.gran, nullptr, 0);
+  if (e != hipSuccess) return e;
+  if (!va) return hipErrorOutOfMemory;
   a.base = static_cast<char*>(va);
   a.reserved = want;
-  return true;
+  return hipSuccess;
 }
 
 }  // namespace
@@ -75,50 +97,61 @@ void* fjalloc_alloc(ssize_t size, int device, void* /*stream*/) {
   if (size <= 0 || device < 0 || device >= kMaxDevices) return nullptr;
   Arena& a = g_arena[device];
   std::lock_guard<std::mutex> lock(a.mu);
-  if (!ensure_reserved(a, device)) {
-    ++a.failures;
-    return nullptr;
+  if (g_mode == 0) {
+    if (hipError_t e = ensure_reserved(a, device)) return failed(a, 1, e);
+  } else if (a.gran == 0) {
+    hipMemAllocationProp p = prop_for(device);
+    size_t g = 0;
+    if (hipError_t e = hipMemGetAllocationGranularity(&g, &p, hipMemAllocationGranularityRecommended))
+      return failed(a, 1, e);
+    a.gran = (g_align + (g ? g : 1) - 1) / (g ? g : 1) * (g ? g : 1);
   }
   const size_t sz = (static_cast<size_t>(size) + a.gran - 1) / a.gran * a.gran;
   char* va = nullptr;
+  bool own = false;
   auto it = a.free_ranges.find(sz);
   if (it != a.free_ranges.end()) {
     va = it->second;
     a.free_ranges.erase(it);
     ++a.reuses;
-  } else {
-    if (a.top + sz > a.reserved) {
-      ++a.failures;
-      return nullptr;
-    }
+  } else if (g_mode == 0) {
+    if (a.top + sz > a.reserved) return failed(a, 5, hipErrorOutOfMemory);
     va = a.base + a.top;
     a.top += sz;
+  } else {
+    void* hint = a.base ? a.base + a.top : nullptr;
+    void* got = nullptr;
+    if (hipError_t e = hipMemAddressReserve(&got, sz, a.gran, hint, 0)) return failed(a, 1, e);
+    va = static_cast<char*>(got);
+    if (!a.base) a.base = va;
+    if (hint && va == hint) ++a.hinted;
+    else if (hint) ++a.hint_missed;
+    if (va >= a.base) a.top = std::max(a.top, static_cast<size_t>(va - a.base) + sz);
+    own = true;
   }
+  auto give_back = [&]() { a.free_ranges.emplace(sz, va); };  // the range stays reserved for a later segment
   hipMemAllocationProp p = prop_for(device);
   hipMemGenericAllocationHandle_t h;
-  if (hipMemCreate(&h, sz, &p, 0) != hipSuccess) {
-    a.free_ranges.emplace(sz, va);
-    ++a.failures;
-    return nullptr;
+  if (hipError_t e = hipMemCreate(&h, sz, &p, 0)) {
+    give_back();
+    return failed(a, 2, e);
   }
-  if (hipMemMap(va, sz, 0, h, 0) != hipSuccess) {
+  if (hipError_t e = hipMemMap(va, sz, 0, h, 0)) {
     hipMemRelease(h);
-    a.free_ranges.emplace(sz, va);
-    ++a.failures;
-    return nullptr;
+    give_back();
+    return failed(a, 3, e);
   }
   hipMemAccessDesc d{};
   d.location.type = hipMemLocationTypeDevice;
   d.location.id = device;
   d.flags = hipMemAccessFlagsProtReadWrite;
-  if (hipMemSetAccess(va, sz, &d, 1) != hipSuccess) {
+  if (hipError_t e = hipMemSetAccess(va, sz, &d, 1)) {
     hipMemUnmap(va, sz);
     hipMemRelease(h);
-    a.free_ranges.emplace(sz, va);
-    ++a.failures;
-    return nullptr;
+    give_back();
+    return failed(a, 4, e);
   }
-  a.live[reinterpret_cast<uintptr_t>(va)] = Segment{sz, h};
+  a.live[reinterpret_cast<uintptr_t>(va)] = Segment{sz, h, own};
   a.mapped_bytes += static_cast<int64_t>(sz);
   ++a.segments;
   return va;
@@ -153,12 +186,17 @@ int fjalloc_stats(int device, int64_t* out) {
   out[5] = static_cast<int64_t>(a.gran);
   out[6] = static_cast<int64_t>(a.top);
   out[7] = reinterpret_cast<int64_t>(a.base);
+  out[8] = a.last_error;
+  out[9] = a.hinted;
+  out[10] = a.hint_missed;
   return 0;
 }
 
-int fjalloc_set_reserve_bytes(int64_t bytes) {
-  if (bytes <= 0) return -1;
-  g_reserve_bytes = static_cast<size_t>(bytes);
+int fjalloc_configure(int64_t reserve_bytes, int64_t align_bytes, int mode) {
+  if (reserve_bytes <= 0 || align_bytes <= 0 || (mode != 0 && mode != 1)) return -1;
+  g_reserve_bytes = static_cast<size_t>(reserve_bytes);
+  g_align = static_cast<size_t>(align_bytes);
+  g_mode = mode;
   return 0;
 }
 

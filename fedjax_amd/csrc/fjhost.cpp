@@ -202,25 +202,11 @@ int collect(PyObject* spec, PyObject* x, std::vector<PyObject*>& objs) {
   return 1;
 }
 
-// Touch the lines a leaf check reads before the checks run: the TensorImpl of every
-// collected leaf, then (once those lines are on their way) every StorageImpl. A client's
-// tensors are scattered over the heap, so the walk of K x L leaves is bound by cache misses;
-// issuing a batch's misses together lets them overlap instead of being paid one by one.
-inline void prefetch_impls(const std::vector<PyObject*>& objs) {
-  for (PyObject* o : objs) {
-    const char* p = reinterpret_cast<const char*>(THPVariable_Unpack(o).unsafeGetTensorImpl());
-    __builtin_prefetch(p);
-    __builtin_prefetch(p + 64);
-    __builtin_prefetch(p + 128);
-    __builtin_prefetch(p + 192);
-  }
-  for (PyObject* o : objs)
-    __builtin_prefetch(THPVariable_Unpack(o).unsafeGetTensorImpl()->storage().unsafeGetStorageImpl());
-}
-
 // Clients trees[k0, k1) against spec: every leaf a strided tensor on cuda:dev (dev < 0: on
 // the host), of dtypes[l] / sizes[l], contiguous; its data pointer goes to rows[k * L + l].
-// Walked in batches of 16 clients (collect, prefetch, check). 0: all match; k + 1: client k
+// Walked in batches of 16 clients (collect the leaf objects, then check them; prefetching the
+// TensorImpl / StorageImpl lines between the two measured no gain, profiles/r04j_pool/host.json).
+// 0: all match; k + 1: client k
 // is the first that does not; -1: a Python error is set.
 int64_t gather_clients(PyObject* spec, PyObject* const* trees, int64_t k0, int64_t k1,
                        const std::vector<at::ScalarType>& dtypes, const std::vector<c10::IntArrayRef>& sizes,
@@ -237,7 +223,6 @@ int64_t gather_clients(PyObject* spec, PyObject* const* trees, int64_t k0, int64
       if (rc < 0) return -1;
       if (rc > 0 || objs.size() - before != L) return k + 1;
     }
-    prefetch_impls(objs);
     for (int64_t k = b0; k < b1; ++k) {
       PyObject* const* row = objs.data() + (k - b0) * L;
       int64_t* out = rows + k * L;
@@ -1181,23 +1166,6 @@ PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const*
     if (static_cast<Py_ssize_t>(w.leaves[0].size()) != L) return PyLong_FromLong(0);
     thread_local std::vector<int64_t> ptrs;
     ptrs.resize(static_cast<size_t>(K * L));
-    {  // the K x L captured tensors' objects, then their TensorImpls and StorageImpls, requested
-       // before the checks below read them (gather_clients' batching, for the chain's captures)
-      thread_local std::vector<PyObject*> objs;
-      objs.clear();
-      for (Py_ssize_t k = 0; k < K; ++k) {
-        PyObject* cap = caps[k];
-        if (!PyTuple_Check(cap) || PyTuple_GET_SIZE(cap) < 2 || !PyTuple_Check(PyTuple_GET_ITEM(cap, 0))) break;
-        PyObject* tup = PyTuple_GET_ITEM(cap, 0);
-        for (Py_ssize_t l = 0; l < PyTuple_GET_SIZE(tup); ++l) {
-          objs.push_back(PyTuple_GET_ITEM(tup, l));
-          __builtin_prefetch(objs.back());
-        }
-      }
-      bool all_tensors = true;
-      for (PyObject* o : objs) all_tensors = all_tensors && THPVariable_Check(o);
-      if (all_tensors) prefetch_impls(objs);
-    }
     std::vector<at::Tensor> row0;
     row0.reserve(L);
     int dev = -1;

@@ -65,11 +65,11 @@ def stats(device: Optional[torch.device] = None) -> dict:
     reused virtual ranges, failed requests, mapping granularity, reserved range."""
     idx = torch.device(device).index if device is not None else None
     idx = torch.cuda.current_device() if idx is None else idx
-    out = np.zeros(8, dtype=np.int64)
+    out = np.zeros(11, dtype=np.int64)
     if _lib.load().fjalloc_stats(idx, out.ctypes.data) != 0:
         raise ValueError(f"fjalloc_stats: bad device {idx}")
     keys = ("mapped_bytes", "live_segments", "segments", "reused_ranges", "failures", "granularity",
-            "bump_offset", "base")
+            "bump_offset", "base", "last_failure", "at_hint", "off_hint")
     return dict(zip(keys, (int(v) for v in out)))
 
 
