@@ -32,6 +32,11 @@ struct Segment {
   bool own_reservation;
 };
 
+struct Chunk {  // mode 2
+  char* base;
+  size_t size, top;
+};
+
 struct Arena {
   std::mutex mu;
   char* base = nullptr;  // reserved virtual range
@@ -40,6 +45,7 @@ struct Arena {
   size_t gran = 0;  // mapping granularity
   std::multimap<size_t, char*> free_ranges;  // unmapped ranges by size, reused for equal sizes
   std::unordered_map<uintptr_t, Segment> live;
+  std::vector<Chunk> chunks;  // mode 2: slices are never returned to the runtime, only reused
   int64_t mapped_bytes = 0, segments = 0, reuses = 0, failures = 0;
   int64_t last_error = 0;  // (step << 16) | hipError_t of the last failed request
   int64_t hinted = 0, hint_missed = 0;  // mode 1: reservations placed at / away from the hint
@@ -57,11 +63,15 @@ constexpr int kMaxDevices = 64;
 Arena g_arena[kMaxDevices];
 size_t g_reserve_bytes = size_t(512) << 30;  // virtual only: 512 GiB per device
 size_t g_align = size_t(2) << 20;  // segment size / address multiple (>= the runtime's granularity)
-// 1: every segment is its own reservation, requested at the address right after the previous
-// one (so the range stays contiguous while the runtime honours the hint); 0: sub-ranges of ONE
-// reservation. This torch's ROCm 7.0 runtime refuses hipMemSetAccess on the third and later
-// sub-ranges of one reservation (hipErrorInvalidValue; tools/probe_fjalloc.py), hence 1.
-int g_mode = 1;
+// 2 (default): segments are slices of large hipMalloc'd chunks (g_chunk_bytes each), so many
+// segments share one allocation and its large translation fragments; 1: every segment is its
+// own VMM reservation + hipMemCreate, requested at the address after the previous one; 0: VMM
+// sub-ranges of ONE reservation. Measured (profiles/r04k_pool/): 1 places segments apart (the
+// runtime ignores the hint) and keeps every (client, leaf)'s translation misses (23,320 per
+// configs[1] fold, as torch's own segments); 0 fails in this torch's ROCm 7.0 runtime
+// (hipMemSetAccess -> hipErrorInvalidValue on later sub-ranges, tools/probe_fjalloc.py).
+int g_mode = 2;
+size_t g_chunk_bytes = size_t(1) << 30;
 
 hipMemAllocationProp prop_for(int device) {
   hipMemAllocationProp p{};
@@ -93,10 +103,47 @@ hipError_t ensure_reserved(Arena& a, int device) {
 
 extern "C" {
 
+void* chunk_alloc(Arena& a, int device, size_t size) {
+  a.gran = g_align;
+  const size_t sz = (size + a.gran - 1) / a.gran * a.gran;
+  char* va = nullptr;
+  auto it = a.free_ranges.find(sz);
+  if (it != a.free_ranges.end()) {
+    va = it->second;
+    a.free_ranges.erase(it);
+    ++a.reuses;
+  } else {
+    for (Chunk& c : a.chunks)
+      if (c.size - c.top >= sz) {
+        va = c.base + c.top;
+        c.top += sz;
+        break;
+      }
+    if (!va) {
+      const size_t csz = std::max(g_chunk_bytes, sz);
+      int prev = -1;
+      hipGetDevice(&prev);
+      hipSetDevice(device);
+      void* p = nullptr;
+      hipError_t e = hipMalloc(&p, csz);
+      if (prev >= 0) hipSetDevice(prev);
+      if (e != hipSuccess || !p) return failed(a, 2, e != hipSuccess ? e : hipErrorOutOfMemory);
+      a.chunks.push_back(Chunk{static_cast<char*>(p), csz, sz});
+      if (!a.base) a.base = static_cast<char*>(p);
+      va = static_cast<char*>(p);
+    }
+  }
+  a.live[reinterpret_cast<uintptr_t>(va)] = Segment{sz, hipMemGenericAllocationHandle_t{}, false};
+  a.mapped_bytes += static_cast<int64_t>(sz);
+  ++a.segments;
+  return va;
+}
+
 void* fjalloc_alloc(ssize_t size, int device, void* /*stream*/) {
   if (size <= 0 || device < 0 || device >= kMaxDevices) return nullptr;
   Arena& a = g_arena[device];
   std::lock_guard<std::mutex> lock(a.mu);
+  if (g_mode == 2) return chunk_alloc(a, device, static_cast<size_t>(size));
   if (g_mode == 0) {
     if (hipError_t e = ensure_reserved(a, device)) return failed(a, 1, e);
   } else if (a.gran == 0) {
@@ -168,8 +215,10 @@ void fjalloc_free(void* ptr, size_t /*size*/, int device, void* stream) {
   if (it == a.live.end()) return;
   const Segment s = it->second;
   a.live.erase(it);
-  hipMemUnmap(ptr, s.size);
-  hipMemRelease(s.handle);
+  if (g_mode != 2) {  // (mode 2 slices stay in their chunk, reused for a segment of the same size)
+    hipMemUnmap(ptr, s.size);
+    hipMemRelease(s.handle);
+  }
   a.free_ranges.emplace(s.size, static_cast<char*>(ptr));
   a.mapped_bytes -= static_cast<int64_t>(s.size);
 }
@@ -193,8 +242,9 @@ int fjalloc_stats(int device, int64_t* out) {
 }
 
 int fjalloc_configure(int64_t reserve_bytes, int64_t align_bytes, int mode) {
-  if (reserve_bytes <= 0 || align_bytes <= 0 || (mode != 0 && mode != 1)) return -1;
+  if (reserve_bytes <= 0 || align_bytes <= 0 || mode < 0 || mode > 2) return -1;
   g_reserve_bytes = static_cast<size_t>(reserve_bytes);
+  g_chunk_bytes = static_cast<size_t>(reserve_bytes);  // mode 2: the chunk size
   g_align = static_cast<size_t>(align_bytes);
   g_mode = mode;
   return 0;

@@ -5,9 +5,8 @@
  * folds whatever jax.Array objects the clients return). Here the caller's deltas are torch
  * allocations, and where they live changes the pytree fold's speed (separate
  * allocations cost compulsory address-translation misses). These entry points are a
- * torch.cuda CUDAPluggableAllocator pair: segments for torch's caching allocator placed one
- * after another in the device's virtual address space (hipMemAddressReserve at the next
- * address), each backed by its own hipMemCreate allocation. fedjax_amd.memory.delta_pool
+ * torch.cuda CUDAPluggableAllocator pair whose segments for torch's caching allocator are
+ * slices of a few large allocations, so the deltas a round allocates share their translations. fedjax_amd.memory.delta_pool
  * wraps them in a torch.cuda.MemPool, used per scope (torch.cuda.use_mem_pool).
  */
 #ifndef FJALLOC_H_
@@ -30,10 +29,11 @@ void fjalloc_free(void* ptr, size_t size, int device, void* stream);
  * 1 reserve, 2 create, 3 map, 4 access, 5 range full), segments reserved at the address
  * hint, segments reserved elsewhere. 0, or -1 for a bad device. */
 int fjalloc_stats(int device, int64_t* out);
-/* Before a device's first allocation: the virtual bytes to reserve for it (mode 0, default
- * 512 GiB), the segment size / address multiple (default 2 MiB, rounded up to the runtime's
- * granularity) and the mode: 1 (default) one reservation per segment at the address after the
- * previous one, 0 sub-ranges of one reservation. 0, or -1 for an invalid value. */
+/* Before a device's first allocation: the mode — 2 (default) segments are 2 MiB-aligned slices
+ * of hipMalloc'd chunks of reserve_bytes (never returned to the runtime, reused for segments of
+ * the same size), 1 one VMM reservation + hipMemCreate per segment, 0 VMM sub-ranges of one
+ * reservation of reserve_bytes — and the segment size / address multiple (default 2 MiB;
+ * rounded up to the runtime's granularity in modes 0 and 1). 0, or -1 for an invalid value. */
 int fjalloc_configure(int64_t reserve_bytes, int64_t align_bytes, int mode);
 
 #ifdef __cplusplus

@@ -37,6 +37,6 @@ if __name__ == "__main__":
     if len(sys.argv) == 4:
         one(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]))
     else:
-        for reserve, align, mode in ((512, 2048, 1), (512, 64, 1), (512, 2048, 0)):
+        for reserve, align, mode in ((1, 2048, 2), (512, 2048, 1), (512, 2048, 0)):
             subprocess.run([sys.executable, os.path.abspath(__file__), str(reserve), str(align), str(mode)],
                            check=False, timeout=120)
