@@ -114,7 +114,7 @@ _SIGNATURES = {
     "fjalloc_alloc": (_vp, [ctypes.c_ssize_t, _i32, _vp]),
     "fjalloc_free": (None, [_vp, ctypes.c_size_t, _i32, _vp]),
     "fjalloc_stats": (_i32, [_i32, _vp]),
-    "fjalloc_configure": (_i32, [_i64, _i64, _i32]),
+    "fjalloc_configure": (_i32, [_i64, _i64, _i32, _i64]),
 }
 SYMBOLS = tuple(_SIGNATURES)
 

@@ -31,6 +31,9 @@ def tmap(f, t):
 
 def main(modes, calls=50, K=128):
     dev = torch.device("cuda:0")
+    if os.environ.get("FJALLOC_STAGGER_KIB") is not None:  # A/B of the segment stagger (fjalloc_configure)
+        from fedjax_amd import _lib
+        assert _lib.load().fjalloc_configure(1 << 30, 64 << 10, 2, int(os.environ["FJALLOC_STAGGER_KIB"]) << 10) == 0
     template = tmap(lambda s: np.zeros(s, np.float32), SHAPES)
     slab = fedjax_amd.ClientDeltaSlab(template, K, device=dev).fill_synthetic(seed=0)
     weights = np.random.RandomState(1).randint(1, 501, size=K).tolist()

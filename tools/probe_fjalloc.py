@@ -16,7 +16,7 @@ def one(reserve_gib, align_kib, mode):
     from fedjax_amd import _lib, memory
     torch.zeros(1, device="cuda")
     lib = _lib.load()
-    assert lib.fjalloc_configure(reserve_gib << 30, align_kib << 10, mode) == 0
+    assert lib.fjalloc_configure(reserve_gib << 30, align_kib << 10, mode, 68 << 10) == 0
     ptrs, steps = [], []
     for mib in (2, 2, 20, 20, 20, 64, 2, 20, 256):
         p = lib.fjalloc_alloc(mib << 20, 0, None)
