@@ -247,8 +247,32 @@ def dropin_surface(dev, calls=20):
     ms = float(np.median(loop)) * 1e3
     res["c1_library_loop_round_ms"] = round(ms, 4)
     res["c1_library_loop_round_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+    # the same clients allocated under the opt-in delta pool (fedjax_amd.memory, include/fjalloc.h):
+    # still one tensor per (client, leaf), placed in shared chunks
+    from fedjax_amd import memory
+    with memory.delta_allocation(dev):
+        pooled = list(zip([tree(k) for k in range(K)], fedavg_weights(K)))
+    for _ in range(5):
+        tu.tree_mean(pooled)
+    torch.cuda.synchronize()
+    t0 = pc()
+    for _ in range(n):
+        tu.tree_mean(pooled)
+    torch.cuda.synchronize()
+    res["c1_delta_pool_tree_mean_back_to_back_ms"] = round((pc() - t0) / n * 1e3, 4)
+    single = []
+    for _ in range(n):
+        torch.cuda.synchronize()
+        t0 = pc()
+        tu.tree_mean(pooled)
+        torch.cuda.synchronize()
+        single.append(pc() - t0)
+    res["c1_delta_pool_tree_mean_sync_call_ms"] = round(float(np.median(single)) * 1e3, 4)
+    res["c1_delta_pool_tree_mean_sync_call_GBs"] = round(K * P * 4 / float(np.median(single)) / 1e9, 1)
+    del pooled
     res["note"] = ("caller-held pytrees, separate allocations; timed after the headline, outside its "
-                   "timed region; GB/s = K*P*4 client-delta bytes per call (library loop: per round)")
+                   "timed region; GB/s = K*P*4 client-delta bytes per call (library loop: per round); "
+                   "c1_delta_pool_*: the same clients allocated under fedjax_amd.memory.delta_allocation()")
     del pairs
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
