@@ -239,7 +239,7 @@ int fjalloc_stats(int device, int64_t* out) {
   out[3] = a.reuses;
   out[4] = a.failures;
   out[5] = static_cast<int64_t>(a.gran);
-  out[6] = static_cast<int64_t>(a.top);
+  out[6] = static_cast<int64_t>(g_mode == 2 ? (a.chunks.empty() ? 0 : a.chunks[0].top) : a.top);  // (mode 2: of the first chunk)
   out[7] = reinterpret_cast<int64_t>(a.base);
   out[8] = a.last_error;
   out[9] = a.hinted;
