@@ -174,6 +174,25 @@ def main(rounds=30, K=128):
             sweep.setdefault(",".join(map(str, fr)) or "0.25 (frac)", []).append(med(walls))
     host.pipeline_fracs([])
     res["tree_mean_sync_sweep_ms"] = sweep
+    # early flushes of the running sum (set_deferred_sums(flush_bytes=, flush_clients=)): the
+    # pending part is folded during the loop, so only the last part's fold follows the loop
+    flush = {}
+    for rep in range(2):
+        for fb, fc in ((1 << 30, 16), (80 << 20, 16), (160 << 20, 16), (320 << 20, 16), (100 << 20, 24)):
+            tu.set_deferred_sums(True, flush_bytes=fb, flush_clients=fc)
+            walls = []
+            for _ in range(2 * rounds):
+                torch.cuda.synchronize()
+                t0 = pc()
+                s = tu.tree_zeros_like(pairs[0][0])
+                for t, w in pairs:
+                    s = tu.tree_add(s, tu.tree_weight(t, w))
+                m = tu.tree_inverse_weight(s, W)
+                torch.cuda.synchronize()
+                walls.append((pc() - t0) * 1e3)
+            flush.setdefault(f"{fb >> 20}MiB/{fc}", []).append(med(walls))
+    tu.set_deferred_sums(True, flush_bytes=1 << 30, flush_clients=16)
+    res["library_round_flush_sweep_ms"] = flush
     print(json.dumps(res), flush=True)
 
 
