@@ -2372,8 +2372,9 @@ PyObject* zeros_like(PyObject*, PyObject* tree) {
 // tree_util._fold_chain for a PendingSum link, walked natively: the unfolded links from the
 // nearest folded ancestor (or the chain's root), the base (the root's tree, or the folded
 // ancestor's value), then fold_caps over [base capture, link captures] with weights
-// [1, n_1 .. n_k]. None (nothing launched) when the run has no captured base or a lazy norm
-// waits on one of its links (the Python path also fills the norms); k: capture k is stale.
+// [1, n_1 .. n_k]; the squared norms of the links a lazy norm view waits on come from the same
+// launch and are written into the chains' norm buffers (tree_util._fill_norms). None (nothing
+// launched) when the run has no captured base; k: capture k is stale.
 PyObject* fold_chain(PyObject*, PyObject* args) {
   PyObject* node;
   double scale, nt_min;
@@ -2391,7 +2392,6 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
       base = p->value;
       break;
     }
-    if (p->ticket && p->ticket != Py_None) Py_RETURN_NONE;  // a lazy norm waits: the Python path
     links.push_back(p);
     if (!p->parent || p->parent == Py_None) {
       base = p->root;
@@ -2416,11 +2416,67 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
     weights[j] = links[j - 1]->weight;
     if (!caps[j] || !weights[j]) Py_RETURN_NONE;
   }
-  Py_INCREF(base);  // (the walk's references are borrowed from the chain, which `node` holds)
-  PyObject* got = fold_caps_impl(base, caps.data(), weights.data(), K, scale, has_scale != 0, nt_min, plan_addr,
-                                 wsum_addr, l2_addr, l2ws_addr, Py_None);
-  Py_DECREF(base);
-  return got;
+  // lazy norms waiting on links of this run (tree_util._NormView tickets): every operand's
+  // squared norm comes from the same launch (fjagg_wsum_l2_ptrs) and is copied into the chains'
+  // norm buffers, as tree_util._fill_norms does
+  static PyObject* node_name = PyUnicode_InternFromString("node");
+  thread_local std::vector<size_t> waiting;
+  waiting.clear();
+  for (size_t j = 0; j < links.size(); ++j) {
+    PyObject* tk = links[j]->ticket;
+    if (!tk || tk == Py_None) continue;
+    PyObject* tn = PyObject_GetAttr(tk, node_name);
+    if (!tn) return nullptr;
+    const bool w = tn != Py_None;
+    Py_DECREF(tn);
+    if (w) waiting.push_back(j);
+  }
+  try {
+    at::Tensor l2;
+    PyObject* l2obj = Py_None;
+    if (!waiting.empty()) {
+      PyObject* t0 = PyTuple_Check(bcap) && PyTuple_GET_SIZE(bcap) > 0 ? PyTuple_GET_ITEM(bcap, 0) : nullptr;
+      if (!t0 || !PyTuple_Check(t0) || PyTuple_GET_SIZE(t0) < 1 || !THPVariable_Check(PyTuple_GET_ITEM(t0, 0)))
+        Py_RETURN_NONE;
+      l2 = at::empty({K}, THPVariable_Unpack(PyTuple_GET_ITEM(t0, 0)).options().dtype(at::kFloat));
+      l2obj = THPVariable_Wrap(l2);
+      if (!l2obj) return nullptr;
+    }
+    Py_INCREF(base);  // (the walk's references are borrowed from the chain, which `node` holds)
+    PyObject* got = fold_caps_impl(base, caps.data(), weights.data(), K, scale, has_scale != 0, nt_min, plan_addr,
+                                   wsum_addr, l2_addr, l2ws_addr, l2obj);
+    Py_DECREF(base);
+    if (l2obj != Py_None) Py_DECREF(l2obj);
+    if (!got || waiting.empty() || !PyTuple_Check(got) || PyLong_AsLong(PyTuple_GET_ITEM(got, 0)) != 0) return got;
+    // runs of consecutive links of one chain: two small launches each (copy, sqrt)
+    for (size_t j = 0; j < links.size();) {
+      PyObject* ch = links[j]->chain;
+      const size_t j0 = j;
+      while (j < links.size() && links[j]->chain == ch &&
+             links[j]->idx == links[j0]->idx + static_cast<long long>(j - j0))
+        ++j;
+      PyObject* buf = ch && Py_TYPE(ch) == g_fast.chain ? reinterpret_cast<ChainObject*>(ch)->buf : nullptr;
+      if (buf && THPVariable_Check(buf)) {
+        const at::Tensor& b = THPVariable_Unpack(buf);
+        const int64_t i0 = links[j0]->idx, n = static_cast<int64_t>(j - j0);
+        const at::Tensor src = l2.narrow(0, 1 + static_cast<int64_t>(j0), n);
+        b.select(0, 0).narrow(0, i0, n).copy_(src);
+        at::Tensor dst = b.select(0, 1).narrow(0, i0, n);
+        at::sqrt_out(dst, src);
+      }
+    }
+    for (size_t j : waiting) {
+      if (PyObject_SetAttr(links[j]->ticket, node_name, Py_None) != 0) {
+        Py_DECREF(got);
+        return nullptr;
+      }
+      Py_CLEAR(links[j]->ticket);
+    }
+    return got;
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
 }
 
 PyObject* image_paths(PyObject*, PyObject*) {
