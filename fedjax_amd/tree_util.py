@@ -671,10 +671,12 @@ _F32_EXACT_INT = 1 << 53
 _DEFER = {"enabled": True, "budget_bytes": None, "max_clients": 4095,
           # fold the pending part early once it holds this much (and >= flush_clients links):
           # that launch runs while the caller's loop goes on, and fewer deltas stay referenced.
-          # A flush costs ~30-50 us of host time, so it pays once the fold it starts early is
-          # long: at configs[1] 256 MiB flushes made a 128-client round slower (0.48 -> 0.54
-          # ms, profiles/r03s_library_loop/); 1 GiB never triggers there
-          "flush_bytes": 1 << 30, "flush_clients": 16}
+          # With the native chain fold a flush costs ~10-25 us of host time (round 3: 30-50 us,
+          # when 256 MiB flushes made a configs[1] round slower); at configs[1] 256 MiB (about
+          # 53 clients per flush) now takes a synchronised round 0.21-0.22 -> 0.17 ms with rounds
+          # back to back unchanged (0.13-0.14 ms; 128 MiB: 0.17 / 0.16 ms, 1 GiB never
+          # flushes there; profiles/r04p_flush/host.json)
+          "flush_bytes": 256 << 20, "flush_clients": 16}
 _AUTO_BUDGET = {}  # device index -> automatic budget in bytes
 
 
@@ -687,7 +689,7 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
     pytree-kernel launch when it is used, at most ``budget_bytes`` of pending deltas or
     ``max_clients`` (<= 4095) clients per launch (an older part of the chain is folded
     first when a limit would be passed, so memory stays bounded). Once the pending part
-    holds >= 1 GiB of deltas in >= 16 clients it is folded at the next ``tree_add``
+    holds >= 256 MiB of deltas in >= 16 clients it is folded at the next ``tree_add``
     (``flush_bytes`` / ``flush_clients``): that launch overlaps the rest of the caller's
     loop, and the deltas it covers are released. Any split gives the same bits. Disabled: every call is
     one fused launch (fjtree_fold_leaves), which also suits loops that update delta
@@ -1147,6 +1149,10 @@ def _tree_add_py(left: PyTree, right: PyTree) -> PyTree:
 # functions above. Per client this is one builtin call each instead of a Python frame, the
 # type tests and a Python object construction.
 _HOST.fast_install(WeightedTree, PendingSum, _Chain, _tree_weight_py, _tree_add_py)
+_HOST.fast_config(_DEFER["enabled"], _DEFER["max_clients"], _DEFER["flush_bytes"], _DEFER["flush_clients"])
+# set_deferred_sums(True, **DEFERRED_SUM_DEFAULTS) restores the defaults
+DEFERRED_SUM_DEFAULTS = {"max_clients": _DEFER["max_clients"], "flush_bytes": _DEFER["flush_bytes"],
+                         "flush_clients": _DEFER["flush_clients"], "budget_bytes": 0}
 tree_weight = _HOST.tree_weight
 tree_add = _HOST.tree_add
 
@@ -1193,7 +1199,9 @@ def _collect_pairs(pairs):
 # when calls run back to back, so it is gated by a host-side estimate: the time the folds
 # this module issued would finish at the 8 TB/s peak; before that the stream is busy with
 # them and is not probed. FJAGG_PIPELINE_FRAC=0 turns the pipeline off (A/B runs).
-_PIPELINE_FRAC = float(os.environ.get("FJAGG_PIPELINE_FRAC", "0.25"))
+# (0.2: profiles/r04p_flush/host.json, sync call 0.115-0.116 ms vs 0.117-0.118 at 0.25 and
+# 0.122 at 0.1, two interleaved sweeps; round 3 picked 0.25 before the walk got faster)
+_PIPELINE_FRAC = float(os.environ.get("FJAGG_PIPELINE_FRAC", "0.2"))
 _PIPELINE_CHUNK = int(os.environ.get("FJAGG_PIPELINE_CHUNK", "512"))
 _PIPELINE_MIN_BYTES = 64 << 20  # below this the first launch is too short to hide the walk
 _WALK_NS_PER_LEAF = 35.0  # native walk + checks per (client, leaf), MI355X host

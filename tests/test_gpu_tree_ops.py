@@ -485,7 +485,7 @@ def test_early_flush_of_the_running_sum(cuda, sum_mode):
         try:
             mean, norms = loop()
         finally:
-            tu.set_deferred_sums(True, flush_bytes=1 << 30, flush_clients=16)
+            tu.set_deferred_sums(True, **tu.DEFERRED_SUM_DEFAULTS)
         for a, b in zip(mean, want):
             assert np.array_equal(bits(a), bits(b)), (fb, fc)
         n64 = [float(np.sqrt(sum(float(np.dot(v.astype(np.float64), v.astype(np.float64)))
@@ -526,7 +526,7 @@ def test_native_chain_fold_equals_python_path(cuda, sum_mode, monkeypatch):
             mean, norms = literal_loop(tu, params, deltas, weights)
             return [x.cpu() for x in pytree.leaves_of(mean)], torch.stack(norms).cpu(), ref.flatten(mean)[1]
         finally:
-            tu.set_deferred_sums(True, flush_bytes=1 << 30, flush_clients=16)
+            tu.set_deferred_sums(True, **tu.DEFERRED_SUM_DEFAULTS)
 
     want, want_n, want_td = run(False, 1 << 30)
     for flush in (1 << 30, 20_000):  # one fold per round / a fold every ~5 clients

@@ -100,7 +100,7 @@ def test_declined_cases_reach_the_python_function(stubs, case):
         got = tu.tree_add(p, wt)
     assert got == "py-tree-add"
     assert len(stubs) == 1 and stubs[0][0] == "tree_add"
-    tu.set_deferred_sums(True, max_clients=4095, flush_bytes=1 << 30, flush_clients=16)
+    tu.set_deferred_sums(True, **tu.DEFERRED_SUM_DEFAULTS)
 
 
 def test_tree_weight_declines_to_python(stubs):
