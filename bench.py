@@ -64,11 +64,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+_LAST_PHASE = ["started"]
+
+
 def phase(rank, name):
     """One stderr line per phase of a rank's run (communicator init, each auto-tune
     candidate, warmup, timed loop, e2e, done), and the rank's current phase in the file a
     spawning parent named in FJ_BENCH_PHASES (spawn_ranks reads them on a timeout to name
     the ranks that had not finished, and where each one stopped)."""
+    _LAST_PHASE[0] = name
     log(f"[bench rank {rank}] {name}")
     d = os.environ.get("FJ_BENCH_PHASES")
     if d:
@@ -300,6 +304,25 @@ def rank_timeout(args) -> float:
     per_rank_s = (K + args.gpus - 1) // args.gpus * P * esize / 0.5e12
     steps = args.warmup + args.steps + 24 * 7 + 6
     return 300.0 + 4.0 * steps * per_rank_s
+
+
+def start_rank_watchdog(rank: int, seconds: float):
+    """Ranks started by an outer launcher (the driver's ``torch.distributed.run``, no
+    spawn_ranks parent to time them): past ``seconds`` without reaching "done" the rank
+    names the phase it is stuck in and exits with status 124, so the launcher tears the
+    job down instead of waiting on a stuck rendezvous or collective. A process exit, not
+    an exec. Returns the timer (cancelled at "done")."""
+    import threading
+
+    def expire():
+        log(f"[bench rank {rank}] watchdog: not done within {seconds:.0f} s, stuck in phase "
+            f"'{_LAST_PHASE[0]}'; exiting with status 124")
+        os._exit(124)
+
+    t = threading.Timer(seconds, expire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 def _rank_phases(d: str, nproc: int):
@@ -594,6 +617,9 @@ def main():
     if world > 1 and args.backend == "nccl" and ngpu < world:
         raise SystemExit(f"--gpus {world} needs {world} visible GPUs for RCCL (found {ngpu}); "
                          f"--backend gloo rehearses on fewer")
+    watchdog = None
+    if world > 1 and "FJ_BENCH_PHASES" not in os.environ:  # (under spawn_ranks the parent times the ranks)
+        watchdog = start_rank_watchdog(rank, args.timeout if args.timeout > 0 else rank_timeout(args))
     dev = torch.device("cuda", local_rank % max(1, ngpu))
     torch.cuda.set_device(dev)
     nshard = world
@@ -855,6 +881,8 @@ def main():
     if sharded:
         dist.destroy_process_group()
     phase(rank, "done")
+    if watchdog is not None:
+        watchdog.cancel()
 
 
 def single_process(args):

@@ -2285,7 +2285,10 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
             const int row = which;  // row 0 = squared norms, row 1 = norms
             if (b.dim() == 2 && node->idx < b.size(1)) {
               if (!node->ticket || node->ticket == Py_None) {
-                PyObject* t = PyObject_CallOneArg(reinterpret_cast<PyObject*>(g_fast.ticket), no);
+                // _Ticket(node) without its Python __init__ frame: allocate, set the slot
+                PyObject* t = g_fast.ticket->tp_alloc(g_fast.ticket, 0);
+                static PyObject* node_name = PyUnicode_InternFromString("node");
+                if (t && PyObject_SetAttr(t, node_name, no) != 0) Py_CLEAR(t);
                 if (!t) return nullptr;
                 Py_XSETREF(node->ticket, t);
               }

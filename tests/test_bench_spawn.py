@@ -138,3 +138,38 @@ def test_rank_timeout_scales_with_the_workload():
     c5 = argparse.Namespace(workload="c5", clients=0, gpus=8, warmup=5, steps=20)
     assert 300 < bench.rank_timeout(a) < 400  # configs[3]: 2.1 GB per rank
     assert bench.rank_timeout(c5) > bench.rank_timeout(a) + 300  # configs[4]: 256 GB per rank
+
+
+def test_rank_watchdog_ends_a_stalled_rank_under_an_outer_launcher(tmp_path):
+    """Under the driver's own torch.distributed.run there is no spawn_ranks parent: each
+    rank's watchdog (bench.start_rank_watchdog) ends a rank that has not reached "done"
+    within the limit with status 124 and names its phase, and the launcher then tears the
+    job down instead of waiting on the stuck rank."""
+    import subprocess
+    import sys
+    import time
+
+    p = tmp_path / "rank.py"
+    p.write_text(textwrap.dedent("""
+        import os, sys, time
+        sys.path.insert(0, %r)
+        import bench
+        r = int(os.environ["RANK"])
+        w = bench.start_rank_watchdog(r, 5.0)
+        bench.phase(r, "init process group (gloo, world 2)")
+        if r == 1:
+            bench.phase(r, "timed loop")
+            time.sleep(600)
+        bench.phase(r, "done")
+        w.cancel()
+    """ % bench.ROOT))
+    env = {k: v for k, v in os.environ.items() if k != "FJ_BENCH_PHASES"}
+    t0 = time.monotonic()
+    proc = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                           "--master-addr=127.0.0.1", f"--master-port={bench._free_port()}", str(p)],
+                          capture_output=True, text=True, timeout=120, env=env)
+    took = time.monotonic() - t0
+    assert proc.returncode != 0
+    assert took < 60, took
+    assert "[bench rank 1] watchdog: not done within 5 s, stuck in phase 'timed loop'" in proc.stderr, proc.stderr
+    assert "[bench rank 0] done" in proc.stderr

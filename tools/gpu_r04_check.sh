@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 check on one GPU box: the GPU test files the round changed, the drop-in host timings
-# (tools/time_dropin_host.py) and the delta-pool placement probe (tools/probe_delta_pool.py).
+# (tools/time_dropin_host.py), the early-flush sweep on a GPU-bound model
+# (tools/time_flush_large.py) and the delta-pool placement probe (tools/probe_delta_pool.py).
 # Every GPU step runs under its own limit; the script stops at the first failing step.
 # usage (repo root, on the box): bash tools/gpu_r04_check.sh TAG
 set -u
@@ -14,6 +15,8 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_
 rc=$?; tail -3 "$O/tests.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/time_dropin_host.py > "$O/host.json" 2> "$O/host.err" || exit $?
 cat "$O/host.json"
+timeout -k 10 300 python tools/time_flush_large.py > "$O/flush_large.json" 2> "$O/flush_large.err" || exit $?
+cat "$O/flush_large.json"
 timeout -k 10 300 python tools/probe_delta_pool.py > "$O/pool.jsonl" 2> "$O/pool.err" || exit $?
 cat "$O/pool.jsonl"
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$O/pool_trace" -o run --output-format csv -- \

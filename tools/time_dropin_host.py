@@ -178,7 +178,7 @@ def main(rounds=30, K=128):
     # pending part is folded during the loop, so only the last part's fold follows the loop
     flush = {}
     for rep in range(2):
-        for fb, fc in ((1 << 30, 16), (128 << 20, 16), (192 << 20, 16), (256 << 20, 16), (384 << 20, 16)):
+        for fb, fc in ((1 << 30, 16), (128 << 20, 16), (256 << 20, 16), (256 << 20, 48), (384 << 20, 16)):
             tu.set_deferred_sums(True, flush_bytes=fb, flush_clients=fc)
             walls = []
             for _ in range(2 * rounds):
@@ -200,7 +200,7 @@ def main(rounds=30, K=128):
             torch.cuda.synchronize()
             b2b = (pc() - t0) / rounds * 1e3
             flush.setdefault(f"{fb >> 20}MiB/{fc}", []).append([med(walls), round(b2b, 4)])
-    tu.set_deferred_sums(True, flush_bytes=1 << 30, flush_clients=16)
+    tu.set_deferred_sums(True, **tu.DEFERRED_SUM_DEFAULTS)
     res["library_round_flush_sweep_ms"] = flush  # [synchronised round, rounds back to back]
     print(json.dumps(res), flush=True)
 
