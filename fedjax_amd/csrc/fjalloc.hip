@@ -5,13 +5,15 @@
 // fold (k_ptrs) walks all K client rows from every CU, and rows that live in separately
 // hipMalloc'd segments cost compulsory address-translation misses (23 K UTCL1
 // misses per configs[1] launch against 5 when the same bytes are views of one allocation,
-// 94.6 vs 87.6 us). This allocator gives torch's caching allocator its segments from ONE
-// reserved virtual range per device, each segment backed by its own physical allocation
-// (hipMemCreate) mapped at a granularity-aligned address (hipMemMap), so the deltas a round
-// allocates sit next to each other in one address range. It is plugged in per scope through
-// torch.cuda.MemPool(CUDAPluggableAllocator(libfjagg.so, "fjalloc_alloc", "fjalloc_free"))
-// (fedjax_amd.memory.delta_pool); the caching allocator still splits and caches blocks
-// inside the segments. Nothing else in the library uses it.
+// 94.6 vs 87.6 us). This allocator gives torch's caching allocator its segments as slices of a
+// few large hipMalloc'd chunks (1 GiB by default), each slice staggered from the previous one,
+// so the deltas a round allocates share a few large mappings (mode 2, the default; modes 1 and
+// 0 are the VMM designs that were measured and kept for comparison, see g_mode). It is plugged
+// in per scope through torch.cuda.MemPool(CUDAPluggableAllocator(libfjagg.so, "fjalloc_alloc",
+// "fjalloc_free")) (fedjax_amd.memory.delta_pool); the caching allocator still splits and
+// caches blocks inside the segments. A chunk goes back to the runtime when its last slice is
+// freed (torch frees a pool's segments when the pool is released). Nothing else in the library
+// uses it.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -35,6 +37,7 @@ struct Segment {
 struct Chunk {  // mode 2
   char* base;
   size_t size, top;
+  int64_t live;  // slices in use
 };
 
 struct Arena {
@@ -45,7 +48,8 @@ struct Arena {
   size_t gran = 0;  // mapping granularity
   std::multimap<size_t, char*> free_ranges;  // unmapped ranges by size, reused for equal sizes
   std::unordered_map<uintptr_t, Segment> live;
-  std::vector<Chunk> chunks;  // mode 2: slices are never returned to the runtime, only reused
+  std::vector<Chunk> chunks;  // mode 2: a freed slice is reused for a segment of its size; an
+                              // empty chunk is returned to the runtime
   int64_t mapped_bytes = 0, segments = 0, reuses = 0, failures = 0;
   int64_t last_error = 0;  // (step << 16) | hipError_t of the last failed request
   int64_t hinted = 0, hint_missed = 0;  // mode 1: reservations placed at / away from the hint
@@ -104,9 +108,33 @@ hipError_t ensure_reserved(Arena& a, int device) {
   return hipSuccess;
 }
 
-}  // namespace
+// mode 2: the chunk holding address p, or nullptr
+Chunk* chunk_of(Arena& a, const char* p) {
+  for (Chunk& c : a.chunks)
+    if (p >= c.base && p < c.base + c.size) return &c;
+  return nullptr;
+}
 
-extern "C" {
+// mode 2: slice p of `size` bytes is free again. Its range is kept for a later segment of the
+// same size; when it was its chunk's last live slice, the chunk (and the free ranges in it)
+// goes back to the runtime.
+void chunk_free(Arena& a, int device, char* p, size_t size) {
+  Chunk* c = chunk_of(a, p);
+  if (!c) return;
+  if (--c->live > 0) {
+    a.free_ranges.emplace(size, p);
+    return;
+  }
+  for (auto it = a.free_ranges.begin(); it != a.free_ranges.end();)
+    it = (it->second >= c->base && it->second < c->base + c->size) ? a.free_ranges.erase(it) : std::next(it);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(device);
+  (void)hipFree(c->base);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  a.chunks.erase(a.chunks.begin() + (c - a.chunks.data()));
+  a.base = a.chunks.empty() ? nullptr : a.chunks[0].base;
+}
 
 void* chunk_alloc(Arena& a, int device, size_t size) {
   a.gran = g_align;
@@ -118,24 +146,26 @@ void* chunk_alloc(Arena& a, int device, size_t size) {
     va = it->second;
     a.free_ranges.erase(it);
     ++a.reuses;
+    if (Chunk* c = chunk_of(a, va)) ++c->live;
   } else {
     for (Chunk& c : a.chunks)
       if (c.size - c.top >= sz + pad) {
         va = c.base + c.top + pad;
         c.top += pad + sz;
+        ++c.live;
         break;
       }
     if (!va) {
       const size_t csz = std::max(g_chunk_bytes, sz);
       int prev = -1;
-      hipGetDevice(&prev);
-      hipSetDevice(device);
+      (void)hipGetDevice(&prev);
+      (void)hipSetDevice(device);
       void* p = nullptr;
       hipError_t e = hipMalloc(&p, csz);
-      if (prev >= 0) hipSetDevice(prev);
+      if (prev >= 0) (void)hipSetDevice(prev);
       if (e != hipSuccess || !p) return failed(a, 2, e != hipSuccess ? e : hipErrorOutOfMemory);
-      a.chunks.push_back(Chunk{static_cast<char*>(p), csz, sz});
-      if (!a.base) a.base = static_cast<char*>(p);
+      a.chunks.push_back(Chunk{static_cast<char*>(p), csz, sz, 1});
+      if (a.chunks.size() == 1) a.base = static_cast<char*>(p);
       va = static_cast<char*>(p);
     }
   }
@@ -144,6 +174,10 @@ void* chunk_alloc(Arena& a, int device, size_t size) {
   ++a.segments;
   return va;
 }
+
+}  // namespace
+
+extern "C" {
 
 void* fjalloc_alloc(ssize_t size, int device, void* /*stream*/) {
   if (size <= 0 || device < 0 || device >= kMaxDevices) return nullptr;
@@ -190,7 +224,7 @@ void* fjalloc_alloc(ssize_t size, int device, void* /*stream*/) {
     return failed(a, 2, e);
   }
   if (hipError_t e = hipMemMap(va, sz, 0, h, 0)) {
-    hipMemRelease(h);
+    (void)hipMemRelease(h);
     give_back();
     return failed(a, 3, e);
   }
@@ -199,8 +233,8 @@ void* fjalloc_alloc(ssize_t size, int device, void* /*stream*/) {
   d.location.id = device;
   d.flags = hipMemAccessFlagsProtReadWrite;
   if (hipError_t e = hipMemSetAccess(va, sz, &d, 1)) {
-    hipMemUnmap(va, sz);
-    hipMemRelease(h);
+    (void)hipMemUnmap(va, sz);
+    (void)hipMemRelease(h);
     give_back();
     return failed(a, 4, e);
   }
@@ -215,18 +249,20 @@ void fjalloc_free(void* ptr, size_t /*size*/, int device, void* stream) {
   Arena& a = g_arena[device];
   // torch's caching allocator releases a segment only when none of its blocks is in use
   // (empty_cache, or an out-of-memory retry); wait for work queued on the segment's stream
-  hipStreamSynchronize(static_cast<hipStream_t>(stream));
+  (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
   std::lock_guard<std::mutex> lock(a.mu);
   auto it = a.live.find(reinterpret_cast<uintptr_t>(ptr));
   if (it == a.live.end()) return;
   const Segment s = it->second;
   a.live.erase(it);
-  if (g_mode != 2) {  // (mode 2 slices stay in their chunk, reused for a segment of the same size)
-    hipMemUnmap(ptr, s.size);
-    hipMemRelease(s.handle);
-  }
-  a.free_ranges.emplace(s.size, static_cast<char*>(ptr));
   a.mapped_bytes -= static_cast<int64_t>(s.size);
+  if (g_mode == 2) {
+    chunk_free(a, device, static_cast<char*>(ptr), s.size);
+    return;
+  }
+  (void)hipMemUnmap(ptr, s.size);
+  (void)hipMemRelease(s.handle);
+  a.free_ranges.emplace(s.size, static_cast<char*>(ptr));
 }
 
 int fjalloc_stats(int device, int64_t* out) {

@@ -61,10 +61,24 @@ def delta_allocation(device: Optional[torch.device] = None):
         yield pool
 
 
+def release(device: Optional[torch.device] = None) -> None:
+    """Drop the process's delta pool for ``device``: once no tensor allocated from it is
+    alive, torch frees its segments and fjalloc returns the emptied chunks to the runtime
+    (a later :func:`delta_pool` starts a new pool). Call it outside ``delta_allocation``."""
+    idx = torch.device(device).index if device is not None else None
+    idx = torch.cuda.current_device() if idx is None else idx
+    pool = _POOLS.pop(idx, None)
+    if pool is not None:
+        del pool
+        torch.cuda.synchronize(idx)
+        torch.cuda.empty_cache()
+
+
 def stats(device: Optional[torch.device] = None) -> dict:
-    """fjalloc's counters for ``device`` (include/fjalloc.h ``fjalloc_stats``): mapped bytes,
-    live segments, segments created, reused ranges, failed requests, granularity, first
-    chunk's top, base address, last failure, placement hints."""
+    """fjalloc's counters for ``device`` (include/fjalloc.h ``fjalloc_stats``): bytes in live
+    segments, live segments, segments created, reused ranges, failed requests, granularity,
+    first chunk's top and base address (``bump_offset``, ``base``), last failure, placement
+    hints."""
     idx = torch.device(device).index if device is not None else None
     idx = torch.cuda.current_device() if idx is None else idx
     out = np.zeros(11, dtype=np.int64)
@@ -75,4 +89,4 @@ def stats(device: Optional[torch.device] = None) -> dict:
     return dict(zip(keys, (int(v) for v in out)))
 
 
-__all__ = ["delta_pool", "delta_allocation", "stats"]
+__all__ = ["delta_pool", "delta_allocation", "release", "stats"]

@@ -1,6 +1,6 @@
 """fedjax_amd.memory (include/fjalloc.h): client deltas allocated under the fjalloc-backed
-pool fold to the same bits as default allocations, and the pool's segments come from one
-reserved virtual range (the caller-side placement of DESIGN.md §3)."""
+pool fold to the same bits as default allocations, the pool's segments are slices of its
+chunks (the caller-side placement of DESIGN.md §3), and a released pool gives its chunks back."""
 import numpy as np
 import pytest
 import torch
@@ -22,7 +22,7 @@ def test_delta_pool_allocations_fold_bitwise(cuda):
     st = memory.stats(cuda)
     assert st["live_segments"] >= 1 and st["failures"] == 0
     lo, hi = st["base"], st["base"] + st["bump_offset"]
-    assert all(lo <= x.data_ptr() < hi for c in pooled for x in c)  # inside the reserved range
+    assert all(lo <= x.data_ptr() < hi for c in pooled for x in c)  # inside the first chunk
     assert not any(lo <= x.data_ptr() < hi for c in plain for x in c)
     a = tu.tree_mean(list(zip(pooled, weights)))
     b = tu.tree_mean(list(zip(plain, weights)))
@@ -32,3 +32,29 @@ def test_delta_pool_allocations_fold_bitwise(cuda):
         assert np.array_equal(y.cpu().numpy().view(np.uint32), z.view(np.uint32))
     del pooled
     torch.cuda.synchronize()
+
+
+def test_released_pool_returns_its_chunks_and_a_new_pool_works(cuda):
+    """Segments over one chunk (1 GiB) spill into a second; releasing the pool after its
+    tensors are gone frees every segment and returns both chunks; a new pool then
+    allocates and folds correctly."""
+    memory.release(cuda)  # (whatever earlier tests left)
+    free0 = torch.cuda.mem_get_info(cuda)[0]
+    with memory.delta_allocation(cuda):
+        big = [torch.full((100 << 20,), float(k + 1), device=cuda) for k in range(4)]  # 4 x 400 MiB
+    st = memory.stats(cuda)
+    assert st["live_segments"] >= 4 and st["failures"] == 0 and st["mapped_bytes"] >= 4 * (400 << 20)
+    assert [float(x[-1]) for x in big] == [1.0, 2.0, 3.0, 4.0]
+    del big
+    memory.release(cuda)
+    st = memory.stats(cuda)
+    assert st["live_segments"] == 0 and st["mapped_bytes"] == 0, st
+    assert torch.cuda.mem_get_info(cuda)[0] >= free0 - (64 << 20)  # the chunks went back
+    host = [[torch.full((3000,), 0.5 * (k + 1))] for k in range(5)]
+    with memory.delta_allocation(cuda):
+        pooled = [[x.to(cuda) for x in c] for c in host]
+    got = tu.tree_mean([(c, k + 1) for k, c in enumerate(pooled)])
+    want = ref.tree_mean([([x.numpy() for x in c], k + 1) for k, c in enumerate(host)])
+    assert np.array_equal(got[0].cpu().numpy().view(np.uint32), want[0].view(np.uint32))
+    del pooled, got
+    memory.release(cuda)
