@@ -669,14 +669,15 @@ _F32_EXACT_INT = 1 << 53
 # budget_bytes None = automatic: min(4 GiB, 1/8 of the device's free memory when the
 # process first defers a sum on it), see _defer_budget
 _DEFER = {"enabled": True, "budget_bytes": None, "max_clients": 4095,
-          # fold the pending part early once it holds this much (and >= flush_clients links):
-          # that launch runs while the caller's loop goes on, and fewer deltas stay referenced.
-          # With the native chain fold a flush costs ~10-25 us of host time (round 3: 30-50 us,
-          # when 256 MiB flushes made a configs[1] round slower); at configs[1] 256 MiB (about
-          # 53 clients per flush) now takes a synchronised round 0.21-0.22 -> 0.17 ms with rounds
-          # back to back unchanged (0.13-0.14 ms; 128 MiB: 0.17 / 0.16 ms, 1 GiB never
-          # flushes there; profiles/r04p_flush/host.json)
-          "flush_bytes": 256 << 20, "flush_clients": 16}
+          # fold the pending part early once it holds this much in >= flush_clients links: that
+          # launch runs while the caller's loop goes on, and fewer deltas stay referenced. With
+          # the native chain fold a flush costs ~10-25 us of host time; at configs[1] (about 4.8
+          # MB per client) a flush at 256 MiB takes a synchronised round 0.21 -> 0.17 ms with
+          # rounds back to back unchanged (profiles/r04p_flush/host.json). Each flush also reads
+          # and writes the running sum once more: where the GPU bounds the loop (configs[2]'s
+          # 16 MiB clients) a flush every 16 clients costs 17 % (2.60 -> 3.08 ms per round), one
+          # every >= 64 clients ~1.5 % (profiles/r04q_check/flush_large.json) — hence 64
+          "flush_bytes": 256 << 20, "flush_clients": 64}
 _AUTO_BUDGET = {}  # device index -> automatic budget in bytes
 
 
@@ -689,7 +690,7 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
     pytree-kernel launch when it is used, at most ``budget_bytes`` of pending deltas or
     ``max_clients`` (<= 4095) clients per launch (an older part of the chain is folded
     first when a limit would be passed, so memory stays bounded). Once the pending part
-    holds >= 256 MiB of deltas in >= 16 clients it is folded at the next ``tree_add``
+    holds >= 256 MiB of deltas in >= 64 clients it is folded at the next ``tree_add``
     (``flush_bytes`` / ``flush_clients``): that launch overlaps the rest of the caller's
     loop, and the deltas it covers are released. Any split gives the same bits. Disabled: every call is
     one fused launch (fjtree_fold_leaves), which also suits loops that update delta
@@ -827,7 +828,10 @@ class PendingSum(_HOST.PendingBase):
         live = parent is not None and parent._value is None
         self._n = 1 + (parent._n if live else 0)
         self._bytes = cap[2] + (parent._bytes if live else 0)
-        if live and parent._chain.tip is parent:
+        if parent is not None and parent._chain.tip is parent and (
+                live or (parent._chain.buf is not None and parent._idx + 1 < parent._chain.buf.shape[1])):
+            # (a parent folded early — an early flush, or a bounded chain — keeps its chain when
+            # the chain's norm buffer has room: the next lazy norm needs no new buffer)
             self._chain, self._idx = parent._chain, parent._idx + 1
         else:
             self._chain, self._idx = _Chain(), 0

@@ -466,10 +466,13 @@ def test_early_flush_of_the_running_sum(cuda, sum_mode):
     ws = [int(v) for v in np.random.RandomState(4).randint(1, 50, size=K)]
 
     def loop():
-        s, norms = tu.tree_zeros_like(xs[0]), []
+        s, norms, chains = tu.tree_zeros_like(xs[0]), [], set()
         for x, w in zip(xs, ws):
             s = tu.tree_add(s, tu.tree_weight(x, w))
             norms.append(tu.tree_l2_norm(x))
+            chains.add(id(s._chain))
+        # an early flush keeps the run's chain (its norm buffer serves the next links)
+        assert len(chains) == 1
         mean = tu.tree_inverse_weight(s, float(sum(ws)))
         return leaves_np(mean), [float(n) for n in norms]
 

@@ -132,6 +132,26 @@ def main(rounds=30, K=128):
             tn.append(c / K * 1e6)
     res["library_loop"]["with_l2_norms"] = {"tree_l2_norm_us": med(tn), "round_sync_ms": med(norm_round)}
     del s, m, norms, vals
+    nsweep = {}
+    for rep in range(2):
+        for fb in (1 << 30, 256 << 20):
+            tu.set_deferred_sums(True, flush_bytes=fb)
+            walls = []
+            for r in range(rounds):
+                torch.cuda.synchronize()
+                t0 = pc()
+                s, norms = tu.tree_zeros_like(pairs[0][0]), []
+                for t, w in pairs:
+                    s = tu.tree_add(s, tu.tree_weight(t, w))
+                    norms.append(tu.tree_l2_norm(t))
+                m = tu.tree_inverse_weight(s, W)
+                vals = torch.stack(norms).cpu()
+                torch.cuda.synchronize()
+                walls.append((pc() - t0) * 1e3)
+            nsweep.setdefault(f"{fb >> 20}MiB", []).append(med(walls))
+    tu.set_deferred_sums(True, **tu.DEFERRED_SUM_DEFAULTS)
+    res["library_loop"]["with_l2_norms"]["flush_sweep_round_sync_ms"] = nsweep
+    del s, m, norms, vals
     # ---- synchronous tree_mean / mean_aggregator().apply
     agg = fedjax_amd.aggregators.mean_aggregator()
     triples = [(f"c{k}", t, w) for k, (t, w) in enumerate(pairs)]
@@ -178,7 +198,7 @@ def main(rounds=30, K=128):
     # pending part is folded during the loop, so only the last part's fold follows the loop
     flush = {}
     for rep in range(2):
-        for fb, fc in ((1 << 30, 16), (128 << 20, 16), (256 << 20, 16), (256 << 20, 48), (384 << 20, 16)):
+        for fb, fc in ((1 << 30, 16), (128 << 20, 16), (256 << 20, 16), (256 << 20, 48), (256 << 20, 64)):
             tu.set_deferred_sums(True, flush_bytes=fb, flush_clients=fc)
             walls = []
             for _ in range(2 * rounds):
