@@ -2075,7 +2075,7 @@ struct FastState {
   PyObject* py_tree_add = nullptr;
   // tree_util.set_deferred_sums
   bool defer = true;
-  long long max_clients = 4095, flush_bytes = 1LL << 30, flush_clients = 16;
+  long long max_clients = 4095, flush_bytes = 256LL << 20, flush_clients = 64;  // (set by fast_config)
   PyObject* last = nullptr;  // weak reference to the most recent PendingSum link
 };
 FastState g_fast;

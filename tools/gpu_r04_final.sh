@@ -1,7 +1,8 @@
 #!/bin/bash
 # Evidence run on one GPU box: full GPU suite (-rs: skip reasons), smoke, the default bench
-# line, the bare N=2 launcher (gloo exchange, both ranks on the box's GPU, e2e leg), and the
-# rocprofv3 kernel-trace summary of the bench. Each step has its own limit; the script stops
+# line, the FETCH/WRITE traffic passes of this build (bench.py --measure-traffic), the bare
+# N=2 launcher (gloo exchange, both ranks on the box's GPU, e2e leg), and the rocprofv3
+# kernel-trace summary of the bench. Each step has its own limit; the script stops
 # at the first failing step (test failures included).
 # usage (repo root, on the box): bash tools/gpu_r04_final.sh TAG
 set -u
@@ -16,6 +17,9 @@ timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > "$O/smoke
 tail -1 "$O/smoke.log"
 timeout -k 10 600 python bench.py > "$O/bench.json" 2> "$O/bench.err" || exit $?
 cat "$O/bench.json"
+timeout -k 10 900 python bench.py --measure-traffic --traffic-out "$O/traffic_c3.json" --no-cpu-baseline --no-dropin \
+  > "$O/bench_traffic.json" 2> "$O/bench_traffic.err" || exit $?
+cat "$O/bench_traffic.json"
 timeout -k 10 600 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 > "$O/bench_n2_gloo.json" \
   2> "$O/bench_n2_gloo.err" || exit $?
 cat "$O/bench_n2_gloo.json"
