@@ -2461,7 +2461,9 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
       PyObject* buf = ch && Py_TYPE(ch) == g_fast.chain ? reinterpret_cast<ChainObject*>(ch)->buf : nullptr;
       if (buf && THPVariable_Check(buf)) {
         const at::Tensor& b = THPVariable_Unpack(buf);
-        const int64_t i0 = links[j0]->idx, n = static_cast<int64_t>(j - j0);
+        // (links past the buffer's end — a chain continued across folds — have no views)
+        const int64_t i0 = links[j0]->idx, n = std::min<int64_t>(static_cast<int64_t>(j - j0), b.size(1) - i0);
+        if (n <= 0) continue;
         const at::Tensor src = l2.narrow(0, 1 + static_cast<int64_t>(j0), n);
         b.select(0, 0).narrow(0, i0, n).copy_(src);
         at::Tensor dst = b.select(0, 1).narrow(0, i0, n);

@@ -967,9 +967,12 @@ def _fill_norms(links, waiting, l2sq):
         while j < len(links) and links[j]._chain is ch and links[j]._idx == links[j0]._idx + (j - j0):
             j += 1
         if ch.buf is not None:
-            i0, i1 = links[j0]._idx, links[j0]._idx + (j - j0)
-            ch.buf[0, i0:i1].copy_(l2sq[1 + j0:1 + j])
-            torch.sqrt(l2sq[1 + j0:1 + j], out=ch.buf[1, i0:i1])
+            # (links past the buffer's end — a chain continued across folds — have no views)
+            i0 = links[j0]._idx
+            n = min(j - j0, ch.buf.shape[1] - i0)
+            if n > 0:
+                ch.buf[0, i0:i0 + n].copy_(l2sq[1 + j0:1 + j0 + n])
+                torch.sqrt(l2sq[1 + j0:1 + j0 + n], out=ch.buf[1, i0:i0 + n])
     for n in waiting:
         n._ticket.node = None
         n._ticket = None

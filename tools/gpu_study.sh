@@ -14,6 +14,8 @@
 #   karg          FJAGG_HOST_TABLES: parity tests, tree_mean wall at configs[1], bench c2 / c3 / N=8 shard
 #                 rehearsal with kernel-argument weights vs uploaded weights, kernel trace of the
 #                 tree_mean loop                                       (profiles/r02r_*)
+#   delta_pool    fjalloc modes, k_ptrs per segment stagger with UTCL1 / TCC tag-stall counters
+#                                                                      (profiles/r04m_delta_pool)
 # Every GPU step runs under its own time limit; the script stops at the first failure.
 set -u
 STUDY=${1:?study name}
@@ -162,6 +164,22 @@ case "$STUDY" in
       done
     done
     grep -H . $O/time_*.jsonl
+    ;;
+  delta_pool)
+    # fjalloc placement (DESIGN §3 "Caller-side placement", profiles/r04m_delta_pool): k_ptrs on
+    # default / pooled / slab-view leaves per segment stagger (FJALLOC_STAGGER_KIB), kernel trace +
+    # UTCL1 and TCC tag-stall counters, and the allocator modes (tools/probe_fjalloc.py)
+    timeout -k 10 300 python tools/probe_fjalloc.py > $O/fjalloc.jsonl 2> $O/fjalloc.err || die fjalloc
+    for st in ${STAGGERS:-0 4 68 260}; do
+      FJALLOC_STAGGER_KIB=$st timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $O/s$st/trace -o run \
+        --output-format csv -- python tools/probe_delta_pool.py clones,pool,views 20 > $O/s$st.log 2>&1 || die "trace $st"
+      python tools/pool_table.py $O/s$st/trace $O/s$st/trace $O/s$st/table.json || die "table $st"
+      rm -f $O/s$st/trace/run_kernel_trace.csv
+    done
+    FJALLOC_STAGGER_KIB=68 timeout -s KILL 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCC_TAG_STALL_sum \
+      -d $O/s68/pmc -o run --output-format csv -- python tools/probe_delta_pool.py clones,pool,views 10 \
+      > $O/s68_pmc.log 2>&1 || die pmc
+    python tools/pool_table.py $O/s68/trace $O/s68/pmc $O/s68/table_pmc.json
     ;;
   *) echo "unknown study $STUDY"; exit 2 ;;
 esac
