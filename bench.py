@@ -777,8 +777,22 @@ def main():
                         continue  # P too small for that many aligned buckets
                     engine, collective, buckets = eng, col, b
                     phase(rank, f"auto-tune candidate {eng}/{col}/{fd.bucket_name(b)}")
-                    wall(2)
-                    tune[(eng, col, b)] = wall(5) / 5 * 1e3
+                    # a candidate that raises on every rank (e.g. an RCCL error from the
+                    # library's own communicator) is dropped and the others still run; the
+                    # ranks agree on that over the process group before going on
+                    ok, t = 1.0, float("inf")
+                    try:
+                        wall(2)
+                        t = wall(5) / 5 * 1e3
+                    except Exception as e:  # noqa: BLE001
+                        ok = 0.0
+                        log(f"[bench rank {rank}] auto-tune candidate {eng}/{col}/{fd.bucket_name(b)} failed: {e}")
+                    flag = torch.tensor([ok], dtype=torch.float32, device=dev)
+                    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+                    if float(flag.item()) == 1.0:
+                        tune[(eng, col, b)] = t
+        if not tune:
+            raise SystemExit("every exchange candidate failed (see the auto-tune lines above)")
         engine, collective, buckets = min(tune, key=tune.get)
         tune = {f"{e}/{c}/{fd.bucket_name(b)}": t for (e, c, b), t in tune.items()}
         log(f"exchange auto-tune (ms/step, max over ranks): {tune} -> "
