@@ -15,6 +15,8 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_
 rc=$?; tail -3 "$O/tests.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/time_dropin_host.py > "$O/host.json" 2> "$O/host.err" || exit $?
 cat "$O/host.json"
+timeout -k 10 300 python tools/time_norms_loop.py > "$O/norms_loop.json" 2> "$O/norms_loop.err" || exit $?
+cat "$O/norms_loop.json"
 timeout -k 10 300 python tools/time_flush_large.py > "$O/flush_large.json" 2> "$O/flush_large.err" || exit $?
 cat "$O/flush_large.json"
 timeout -k 10 300 python tools/probe_delta_pool.py > "$O/pool.jsonl" 2> "$O/pool.err" || exit $?
