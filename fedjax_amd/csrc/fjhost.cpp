@@ -1065,6 +1065,15 @@ PyObject* append_check(PyObject*, PyObject* args) {
   }
 }
 
+// A 0-d tensor over element `offset` of b's storage: its own TensorImpl on b's storage (no
+// dispatcher round trip, unlike as_strided; not an autograd view of b, which needs none here).
+at::Tensor scalar_at(const at::Tensor& b, int64_t offset) {
+  at::Tensor v = at::detail::make_tensor<c10::TensorImpl>(c10::Storage(b.storage()), b.key_set(), b.dtype());
+  v.unsafeGetTensorImpl()->set_storage_offset(offset);
+  v.unsafeGetTensorImpl()->set_sizes_contiguous({});
+  return v;
+}
+
 // norm_view(buf, row, index, type) -> 0-d tensor of `type` (a torch.Tensor subclass) viewing
 // buf[row, index]: the lazy l2-norm values of deferred sums (tree_util._NormView).
 PyObject* norm_view(PyObject*, PyObject* args) {
@@ -1081,8 +1090,7 @@ PyObject* norm_view(PyObject*, PyObject* args) {
       PyErr_SetString(PyExc_IndexError, "norm_view: index out of range");
       return nullptr;
     }
-    // one view op (b[row, index]) instead of two selects
-    return THPVariable_Wrap(b.as_strided({}, {}, b.storage_offset() + row * b.stride(0) + index * b.stride(1)),
+    return THPVariable_Wrap(scalar_at(b, b.storage_offset() + row * b.stride(0) + index * b.stride(1)),
                             reinterpret_cast<PyTypeObject*>(type));
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
@@ -2293,8 +2301,7 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
                 Py_XSETREF(node->ticket, t);
               }
               PyObject* v = THPVariable_Wrap(
-                  b.as_strided({}, {}, b.storage_offset() + row * b.stride(0) + node->idx * b.stride(1)),
-                  g_fast.norm_view);
+                  scalar_at(b, b.storage_offset() + row * b.stride(0) + node->idx * b.stride(1)), g_fast.norm_view);
               if (!v) return nullptr;
               static PyObject* name = PyUnicode_InternFromString("_ticket");
               if (PyObject_SetAttr(v, name, node->ticket) != 0) {
