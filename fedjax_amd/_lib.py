@@ -106,6 +106,7 @@ _SIGNATURES = {
     "fjtree_abi_version": (_i32, []),
     "fjtree_workspace_bytes": (_i64, [_vp]),
     "fjtree_fold_leaves": (_i32, [_vp, _vp]),
+    "fjtree_norms_fill": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     # include/fjopt.h
     "fjopt_abi_version": (_i32, []),
     "fjopt_adafactor_plan": (_i64, [_vp, _i32, _vp, _vp, _i64, _vp]),

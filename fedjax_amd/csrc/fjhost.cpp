@@ -2076,6 +2076,7 @@ struct FastState {
   PyTypeObject* ticket = nullptr;    // tree_util._Ticket
   PyTypeObject* norm_view = nullptr;  // tree_util._NormView
   PyObject* py_l2[2] = {nullptr, nullptr};  // tree_util._tree_l2_squared_py / _tree_l2_norm_py
+  PyObject* py_fold_ticket = nullptr;        // tree_util._fold_ticket (flush_views)
   PyTypeObject* wt = nullptr;     // tree_util.WeightedTree
   PyTypeObject* ps = nullptr;     // tree_util.PendingSum
   PyTypeObject* chain = nullptr;  // tree_util._Chain
@@ -2231,15 +2232,82 @@ PyObject* fast_tree_add(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyOb
 }
 
 
-// fast_install_norms(_Ticket, _NormView, py_tree_l2_squared, py_tree_l2_norm)
+// fast_install_norms(_Ticket, _NormView, py_tree_l2_squared, py_tree_l2_norm[, py_fold_ticket])
 PyObject* fast_install_norms(PyObject*, PyObject* args) {
-  PyObject *tk, *nv, *f0, *f1;
-  if (!PyArg_ParseTuple(args, "O!O!OO", &PyType_Type, &tk, &PyType_Type, &nv, &f0, &f1)) return nullptr;
-  Py_INCREF(tk), Py_INCREF(nv), Py_INCREF(f0), Py_INCREF(f1);
+  PyObject *tk, *nv, *f0, *f1, *ft = Py_None;
+  if (!PyArg_ParseTuple(args, "O!O!OO|O", &PyType_Type, &tk, &PyType_Type, &nv, &f0, &f1, &ft)) return nullptr;
+  Py_INCREF(tk), Py_INCREF(nv), Py_INCREF(f0), Py_INCREF(f1), Py_INCREF(ft);
   Py_XSETREF(g_fast.ticket, reinterpret_cast<PyTypeObject*>(tk));
   Py_XSETREF(g_fast.norm_view, reinterpret_cast<PyTypeObject*>(nv));
   Py_XSETREF(g_fast.py_l2[0], f0);
   Py_XSETREF(g_fast.py_l2[1], f1);
+  Py_XSETREF(g_fast.py_fold_ticket, ft);
+  Py_RETURN_NONE;
+}
+
+// flush_views(obj): tree_util._flush_views natively — every lazy norm view (tree_util._NormView)
+// in obj (nested lists / tuples / dict values) whose ticket still names an unfolded link gets
+// its chain folded (py_fold_ticket(ticket)), so no torch function reads its buffer early.
+// Views already filled cost a dict lookup each.
+PyObject* flush_views(PyObject*, PyObject* arg) {
+  if (!g_fast.norm_view || !g_fast.py_fold_ticket || g_fast.py_fold_ticket == Py_None) {
+    PyErr_SetString(PyExc_RuntimeError, "fedjax_amd.tree_util is not installed (fast_install_norms)");
+    return nullptr;
+  }
+  static PyObject* tk_name = PyUnicode_InternFromString("_ticket");
+  static PyObject* node_name = PyUnicode_InternFromString("node");
+  std::vector<std::pair<PyObject*, int>> st;  // (not shared: a fold may run Python code that calls back)
+  Py_INCREF(arg);  // (every stacked object is held: folding runs Python code)
+  st.emplace_back(arg, 0);
+  struct Held {
+    std::vector<std::pair<PyObject*, int>>& v;
+    ~Held() {
+      for (auto& e : v) Py_DECREF(e.first);
+      v.clear();
+    }
+  } held{st};
+  while (!st.empty()) {
+    PyObject* x = st.back().first;
+    const int depth = st.back().second;
+    st.pop_back();
+    struct Drop {
+      PyObject* o;
+      ~Drop() { Py_DECREF(o); }
+    } drop{x};
+    PyTypeObject* t = Py_TYPE(x);
+    if (t == g_fast.norm_view) {
+      PyObject** dp = _PyObject_GetDictPtr(x);
+      if (!dp || !*dp) continue;
+      PyObject* tk = PyDict_GetItemWithError(*dp, tk_name);  // borrowed
+      if (!tk) {
+        if (PyErr_Occurred()) return nullptr;
+        continue;
+      }
+      if (tk == Py_None) continue;
+      PyObject* node = PyObject_GetAttr(tk, node_name);
+      if (!node) return nullptr;
+      const bool live = node != Py_None;
+      Py_DECREF(node);
+      if (live) {
+        PyObject* r = PyObject_CallOneArg(g_fast.py_fold_ticket, tk);
+        if (!r) return nullptr;
+        Py_DECREF(r);
+      }
+    } else if (depth < 64 && (t == &PyList_Type || t == &PyTuple_Type)) {
+      for (Py_ssize_t i = Py_SIZE(x) - 1; i >= 0; --i) {
+        PyObject* c = t == &PyList_Type ? PyList_GET_ITEM(x, i) : PyTuple_GET_ITEM(x, i);
+        Py_INCREF(c);
+        st.emplace_back(c, depth + 1);
+      }
+    } else if (depth < 64 && t == &PyDict_Type) {
+      Py_ssize_t pos = 0;
+      PyObject *k, *v;
+      while (PyDict_Next(x, &pos, &k, &v)) {
+        Py_INCREF(v);
+        st.emplace_back(v, depth + 1);
+      }
+    }
+  }
   Py_RETURN_NONE;
 }
 
@@ -2389,9 +2457,9 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
   PyObject* node;
   double scale, nt_min;
   int has_scale;
-  unsigned long long plan_addr, wsum_addr, l2_addr, l2ws_addr;
-  if (!PyArg_ParseTuple(args, "OdpdKKKK", &node, &scale, &has_scale, &nt_min, &plan_addr, &wsum_addr, &l2_addr,
-                        &l2ws_addr))
+  unsigned long long plan_addr, wsum_addr, l2_addr, l2ws_addr, fill_addr = 0;
+  if (!PyArg_ParseTuple(args, "OdpdKKKK|K", &node, &scale, &has_scale, &nt_min, &plan_addr, &wsum_addr, &l2_addr,
+                        &l2ws_addr, &fill_addr))
     return nullptr;
   if (!g_fast.ps || Py_TYPE(node) != g_fast.ps) Py_RETURN_NONE;
   thread_local std::vector<PSObject*> links;
@@ -2458,7 +2526,10 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
     Py_DECREF(base);
     if (l2obj != Py_None) Py_DECREF(l2obj);
     if (!got || waiting.empty() || !PyTuple_Check(got) || PyLong_AsLong(PyTuple_GET_ITEM(got, 0)) != 0) return got;
-    // runs of consecutive links of one chain: two small launches each (copy, sqrt)
+    // runs of consecutive links of one chain: one fjtree_norms_fill launch each (or, without
+    // its address, a copy and a sqrt)
+    typedef int (*FillFn)(const float*, float*, float*, int64_t, void*);
+    auto fill = reinterpret_cast<FillFn>(fill_addr);
     for (size_t j = 0; j < links.size();) {
       PyObject* ch = links[j]->chain;
       const size_t j0 = j;
@@ -2471,6 +2542,18 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
         // (links past the buffer's end — a chain continued across folds — have no views)
         const int64_t i0 = links[j0]->idx, n = std::min<int64_t>(static_cast<int64_t>(j - j0), b.size(1) - i0);
         if (n <= 0) continue;
+        if (fill && b.is_contiguous() && b.scalar_type() == at::kFloat && b.is_cuda() &&
+            b.get_device() == l2.get_device()) {
+          float* row0 = b.data_ptr<float>() + i0;
+          const hipStream_t s = c10::hip::getCurrentHIPStream(l2.get_device()).stream();
+          const int rc = fill(l2.data_ptr<float>() + 1 + j0, row0, row0 + b.size(1), n, s);
+          if (rc != 0) {
+            Py_DECREF(got);
+            PyErr_Format(PyExc_RuntimeError, "fjtree_norms_fill failed (%d)", rc);
+            return nullptr;
+          }
+          continue;
+        }
         const at::Tensor src = l2.narrow(0, 1 + static_cast<int64_t>(j0), n);
         b.select(0, 0).narrow(0, i0, n).copy_(src);
         at::Tensor dst = b.select(0, 1).narrow(0, i0, n);
@@ -2540,6 +2623,7 @@ PyMethodDef kMethods[] = {
     {"mean_triples", mean_triples, METH_O, "tree_mean over (client_id, params, weight) triples (aggregator.py:61-75)"},
     {"pipeline_fracs", pipeline_fracs, METH_O, "chunk ends (fractions of K) of tree_mean's fold-bound pipeline"},
     {"fold_chain", fold_chain, METH_VARARGS, "a PendingSum's deferred fold, its links walked natively"},
+    {"flush_views", flush_views, METH_O, "fold the chains lazy norm views in an object still wait on"},
     {"fast_install_norms", fast_install_norms, METH_VARARGS, "register tree_util's lazy norm classes and fallbacks"},
     {"tree_l2_squared", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_tree_l2_squared)),
      METH_FASTCALL | METH_KEYWORDS,

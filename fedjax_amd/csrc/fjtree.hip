@@ -236,11 +236,35 @@ int launch(const Args& a, hipStream_t s) {
   return e == hipSuccess ? FJAGG_OK : fail(FJAGG_EHIP, "k_leaves: %s", hipGetErrorString(e));
 }
 
+// The lazy norms' fill (fjtree_norms_fill): sq[i] = l2sq[i], nrm[i] = sqrt(l2sq[i]), the square
+// root correctly rounded (IEEE binary32, as jnp.sqrt on XLA:CPU; tree_util.py:112-114).
+__global__ void k_norms_fill(const float* __restrict__ l2sq, float* __restrict__ sq, float* __restrict__ nrm,
+                             int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const float v = l2sq[i];
+    sq[i] = v;
+    nrm[i] = __fsqrt_rn(v);
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
 int fjtree_abi_version(void) { return FJTREE_ABI_VERSION; }
+
+int fjtree_norms_fill(const float* l2sq, float* sq_out, float* norm_out, int64_t n, void* stream) {
+  fjagg_g_err[0] = 0;
+  if (n < 0 || n > (int64_t(1) << 30)) return fail(FJAGG_EINVAL, "norms_fill: n = %lld", (long long)n);
+  if (n == 0) return FJAGG_OK;
+  if (!l2sq || !sq_out || !norm_out) return fail(FJAGG_EINVAL, "norms_fill: null pointer");
+  const unsigned blocks = static_cast<unsigned>((n + kThreads - 1) / kThreads);
+  hipLaunchKernelGGL(k_norms_fill, dim3(blocks), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream), l2sq,
+                     sq_out, norm_out, n);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? FJAGG_OK : fail(FJAGG_EHIP, "k_norms_fill: %s", hipGetErrorString(e));
+}
 
 int64_t fjtree_workspace_bytes(const fjtree_leaves* t) {
   if (!t || !(t->flags & FJTREE_NORM) || t->L < 1 || t->L > FJTREE_MAX_LEAVES) return 0;

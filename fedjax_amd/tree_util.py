@@ -314,12 +314,16 @@ def _fold(rows, weights, *, scale=None,
 _ENTRY_ADDRS = None  # (plan_leaves, wsum_ptrs, wsum_l2_ptrs, l2 workspace bytes) addresses for fjhost.fold_table
 
 
+_FILL_ADDR = 0  # fjtree_norms_fill, for fjhost.fold_chain's lazy-norm fill
+
+
 def _native_fold_addrs() -> None:
-    global _ENTRY_ADDRS
+    global _ENTRY_ADDRS, _FILL_ADDR
     lib = _lib.load()
     _ENTRY_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
                          for f in ("fjagg_ptrs_plan_leaves", "fjagg_wsum_ptrs", "fjagg_wsum_l2_ptrs",
                                    "fjagg_wsum_l2_ptrs_workspace_bytes"))
+    _FILL_ADDR = ctypes.cast(lib.fjtree_norms_fill, ctypes.c_void_p).value
     _mean_config()
 
 
@@ -763,19 +767,26 @@ class _NormView(torch.Tensor):
 
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):
-        _flush_views(args)
+        _HOST.flush_views(args)
         if kwargs:
-            _flush_views(kwargs)
+            _HOST.flush_views(kwargs)
         with torch._C.DisableTorchFunctionSubclass():
             return func(*args, **(kwargs or {}))
 
     def __format__(self, spec):
-        _flush_views(self)
+        _HOST.flush_views(self)
         with torch._C.DisableTorchFunctionSubclass():
             return self.item().__format__(spec) if self.dim() == 0 else torch.Tensor.__format__(self, spec)
 
 
+def _fold_ticket(ticket) -> None:
+    """Fold the chain a waiting lazy norm's ticket names (fjhost.flush_views calls this)."""
+    if ticket.node is not None:
+        ticket.node._chain.tip.materialize()  # folds every pending link of the chain
+
+
 def _flush_views(x) -> None:
+    """The Python statement of fjhost.flush_views (which the views use)."""
     t = type(x)
     if t is _NormView:
         ticket = x.__dict__.get("_ticket")
@@ -881,7 +892,7 @@ def _fold_pending(node: "PendingSum", scale):
         if _ENTRY_ADDRS is None:
             _native_fold_addrs()
         got = _HOST.fold_chain(node, float(np.float32(scale)) if scale is not None else 1.0, scale is not None,
-                               float(NONTEMPORAL_MIN_BYTES), *_ENTRY_ADDRS)
+                               float(NONTEMPORAL_MIN_BYTES), *_ENTRY_ADDRS, _FILL_ADDR)
         if type(got) is int:
             _stale_chain(got)
         if got is not None:
@@ -970,9 +981,11 @@ def _fill_norms(links, waiting, l2sq):
             # (links past the buffer's end — a chain continued across folds — have no views)
             i0 = links[j0]._idx
             n = min(j - j0, ch.buf.shape[1] - i0)
-            if n > 0:
-                ch.buf[0, i0:i0 + n].copy_(l2sq[1 + j0:1 + j0 + n])
-                torch.sqrt(l2sq[1 + j0:1 + j0 + n], out=ch.buf[1, i0:i0 + n])
+            if n > 0:  # buf[0, i] = l2sq, buf[1, i] = sqrt(l2sq), one launch (include/fjtree.h)
+                src, cols = l2sq[1 + j0:1 + j0 + n], ch.buf.shape[1]
+                _lib.check(_lib.load().fjtree_norms_fill(
+                    src.data_ptr(), ch.buf.data_ptr() + 4 * i0, ch.buf.data_ptr() + 4 * (cols + i0), n,
+                    torch.cuda.current_stream(src.device).cuda_stream), "fjtree_norms_fill")
     for n in waiting:
         n._ticket.node = None
         n._ticket = None
@@ -1562,7 +1575,7 @@ def _tree_l2_norm_py(pytree_: PyTree) -> torch.Tensor:
 
 # The per-client delta_l2_norm of the running-sum loops (fed_avg.py:142-144), native: the lazy
 # view of the delta the running sum just took, without a Python frame (fjhost.tree_l2_norm).
-_HOST.fast_install_norms(_Ticket, _NormView, _tree_l2_squared_py, _tree_l2_norm_py)
+_HOST.fast_install_norms(_Ticket, _NormView, _tree_l2_squared_py, _tree_l2_norm_py, _fold_ticket)
 tree_l2_squared = _HOST.tree_l2_squared
 tree_l2_norm = _HOST.tree_l2_norm
 

@@ -88,6 +88,13 @@ int fjtree_abi_version(void);
 int64_t fjtree_workspace_bytes(const fjtree_leaves* t);
 /* One launch on `stream`; t is read during the call only. */
 int fjtree_fold_leaves(const fjtree_leaves* t, void* stream);
+/* The deferred running sum's lazy norms (fedjax_amd.tree_util): for i < n,
+ * sq_out[i] = l2sq[i] and norm_out[i] = sqrt(l2sq[i]) (correctly rounded), one launch on
+ * `stream`. Replaces, for the per-client tree_l2_squared / tree_l2_norm of the deltas a fold
+ * covered (fedjax/core/tree_util.py:105-114, called at fedjax/algorithms/fed_avg.py:142-144),
+ * the copy and the sqrt the fold's squared norms would otherwise take as two launches.
+ * Device pointers, float32; n <= 2^30. */
+int fjtree_norms_fill(const float* l2sq, float* sq_out, float* norm_out, int64_t n, void* stream);
 
 #ifdef __cplusplus
 }

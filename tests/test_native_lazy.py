@@ -124,3 +124,34 @@ def test_chains_are_freed():
     gc.collect()  # node -> chain -> tip -> node is a cycle: the collector frees it
     assert wr_root() is None and wr_tip() is None
     assert H.last() is None
+
+
+def test_flush_views_folds_only_waiting_chains():
+    """fjhost.flush_views (what every torch function on a lazy norm view runs first) folds
+    the chain of a view whose ticket still names a link, walks nested lists / tuples / dict
+    values, and leaves filled views (ticket node None) and other objects alone."""
+    buf = torch.arange(8, dtype=torch.float32).view(2, 4)
+    folded = []
+
+    class Tip:
+        def materialize(self):
+            folded.append(1)
+            t1.node = None  # (a fold clears the tickets it fills)
+
+    class Chain:
+        tip = Tip()
+
+    class Node:
+        _chain = Chain()
+
+    t1, t2 = tu._Ticket(Node()), tu._Ticket(None)
+    v1, v2, v3 = (H.norm_view(buf, 1, i, tu._NormView) for i in range(3))
+    v1._ticket, v2._ticket = t1, t2  # v3: no ticket at all
+    H.flush_views([v3, (1, {"a": [v2]}), "x"])
+    assert folded == []
+    H.flush_views({"k": [(v2, v1)], "j": v3})
+    assert folded == [1]
+    H.flush_views([v1, v1])  # filled now: no second fold
+    assert folded == [1]
+    with torch._C.DisableTorchFunctionSubclass():
+        assert float(v1) == 4.0  # buf[1, 0]: a view of the chain buffer

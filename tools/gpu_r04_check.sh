@@ -11,7 +11,7 @@ mkdir -p "$O"
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_tree_ops.py tests/test_gpu_fuzz.py \
   tests/test_gpu_host_tables.py tests/test_gpu_parity.py tests/test_gpu_algorithms.py tests/test_gpu_inference_tensors.py \
-  tests/test_gpu_memory.py -q -rfs -x --timeout 300 --timeout-method thread -p no:cacheprovider > "$O/tests.log" 2>&1
+  tests/test_gpu_memory.py tests/test_gpu_running_sum_fuzz.py -q -rfs -x --timeout 300 --timeout-method thread -p no:cacheprovider > "$O/tests.log" 2>&1
 rc=$?; tail -3 "$O/tests.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/time_dropin_host.py > "$O/host.json" 2> "$O/host.err" || exit $?
 cat "$O/host.json"
