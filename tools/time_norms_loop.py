@@ -4,6 +4,7 @@
   norms      + tree_l2_norm(x) per client, the views left unread
   read       + one torch.stack(norms).cpu() after the round (as bench tools read them)
   read_each  + float(v) for every view after the round
+  *_1g       the same without the early flush (flush_bytes 1 GiB)
 and the host time of each phase. Prints one JSON line. usage: python tools/time_norms_loop.py [rounds]"""
 import json
 import os
@@ -39,7 +40,8 @@ def main(rounds=30, K=128):
     pc = time.perf_counter
     res = {}
     for rep in range(2):
-        for mode in ("plain", "norms", "read", "read_each"):
+        for mode in ("plain", "norms", "read", "read_each", "norms_1g", "read_1g"):
+            tu.set_deferred_sums(True, flush_bytes=(1 << 30) if mode.endswith("_1g") else tu.DEFERRED_SUM_DEFAULTS["flush_bytes"])
             walls, loop_us, fold_us, read_us = [], [], [], []
             for r in range(rounds + 3):
                 torch.cuda.synchronize()
@@ -52,7 +54,7 @@ def main(rounds=30, K=128):
                 t1 = pc()
                 m = tu.tree_inverse_weight(s, W)
                 t2 = pc()
-                if mode == "read":
+                if mode.startswith("read") and mode != "read_each":
                     torch.stack(norms).cpu()
                 elif mode == "read_each":
                     [float(v) for v in norms]
@@ -68,6 +70,7 @@ def main(rounds=30, K=128):
             res.setdefault(mode, []).append({"round_sync_ms": med(walls), "loop_us": med(loop_us),
                                              "fold_call_us": med(fold_us), "read_us": med(read_us)})
             del s, m, norms
+    tu.set_deferred_sums(True, **tu.DEFERRED_SUM_DEFAULTS)
     print(json.dumps(res), flush=True)
 
 
