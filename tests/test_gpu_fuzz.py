@@ -29,6 +29,8 @@ default NaN is positive, x86's negative; the reference gives whichever its backe
 """
 import math
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -41,7 +43,9 @@ pytestmark = pytest.mark.gpu
 
 SIZES = [0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 63, 64, 65, 255, 256, 257, 1023, 1024, 1025,
          4095, 4096, 4097, 8191, 12289, 65537]
-NCASES = 200
+# FJ_FUZZ_CASES / FJ_FUZZ_SEED0: a longer campaign over other seeds (the suite runs the defaults)
+NCASES = int(os.environ.get("FJ_FUZZ_CASES", "200"))
+SEED0 = int(os.environ.get("FJ_FUZZ_SEED0", "1000"))
 
 
 def _shape(rs, n):
@@ -239,7 +243,7 @@ def _same(got, want, what):
 @pytest.mark.filterwarnings("ignore::RuntimeWarning")  # inf - inf in the oracle's numpy
 @pytest.mark.parametrize("seed", range(NCASES))
 def test_random_case_matches_oracle(cuda, seed, monkeypatch):
-    c = _case(1000 + seed)
+    c = _case(SEED0 + seed)
     trees = _place(c, cuda)
     np_trees = [_realize(c["struct"], leaves) for leaves in c["host"]]
     ws, K = c["ws"], c["K"]
