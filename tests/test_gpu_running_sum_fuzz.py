@@ -5,7 +5,7 @@ The library algorithms build their sums one client at a time (fedjax/algorithms/
 here draws a pytree structure (nested dict / list / tuple / None nodes, float32 leaves of
 random shapes, empty ones included), 1-3 running sums, a client order, Python int or float
 weights, and per client the calls a caller may make around its tree_add: tree_l2_norm /
-tree_l2_squared of the delta, an unweighted tree_add, reading a sum mid-round. The deferred
+tree_l2_squared of the delta, an unweighted tree_add, reading a sum or a norm mid-round. The deferred
 chain's limits (max_clients, early-flush thresholds) are drawn too, so the chains split at
 random places; each case also runs with deferral off. Every sum, mid-round read and final
 tree_inverse_weight must be bitwise the oracle's op sequence (oracle/tree_util_ref.py,
@@ -111,7 +111,7 @@ def test_random_running_sum_program(cuda, mode, seed):
         tu.set_deferred_sums(True, max_clients=int(rs.choice([2, 3, 7, 4095])),
                              flush_bytes=int(rs.choice([1, 4096, 256 << 20])),
                              flush_clients=int(rs.choice([1, 2, 5, 64])))
-    K, S = int(rs.randint(1, 41)), int(rs.randint(1, 4))
+    K, S = int(rs.randint(1, 41)) if rs.rand() < 0.9 else int(rs.randint(41, 300)), int(rs.randint(1, 4))
     hosts = [_build(spec, lambda s: ((torch.rand(s, generator=g) * 2 - 1) * 0.1)) for _ in range(K)]
     deltas = [_tmap(lambda x: x.to(cuda), h) for h in hosts]
     host_np = [_tmap(lambda x: x.numpy(), h) for h in hosts]
@@ -143,6 +143,9 @@ def test_random_running_sum_program(cuda, mode, seed):
             want_norms.append(_norm64(host_np[k]) ** 2)
         if rs.rand() < 0.06:  # a caller reading the sum mid-round
             assert _bits_equal(sums[j], want[j]), (seed, k, "mid-round read")
+        if norms and rs.rand() < 0.05:  # ... or one of the norms so far (folds the chain it waits on)
+            i = int(rs.randint(0, len(norms)))
+            np.testing.assert_allclose(float(norms[i]), want_norms[i], rtol=2e-6, atol=1e-30)
     for j in range(S):
         if not used[j]:
             continue
