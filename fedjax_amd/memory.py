@@ -64,7 +64,9 @@ def delta_allocation(device: Optional[torch.device] = None):
 def release(device: Optional[torch.device] = None) -> None:
     """Drop the process's delta pool for ``device``: once no tensor allocated from it is
     alive, torch frees its segments and fjalloc returns the emptied chunks to the runtime
-    (a later :func:`delta_pool` starts a new pool). Call it outside ``delta_allocation``."""
+    (a later :func:`delta_pool` starts a new pool). Call it outside ``delta_allocation``.
+    It also empties torch's own cache (``torch.cuda.empty_cache``), which is what hands a
+    released pool's segments back."""
     idx = torch.device(device).index if device is not None else None
     idx = torch.cuda.current_device() if idx is None else idx
     pool = _POOLS.pop(idx, None)
