@@ -32,6 +32,7 @@ struct Segment {
   size_t size;
   hipMemGenericAllocationHandle_t handle;
   bool own_reservation;
+  bool chunk_slice;  // mode 2: a slice of a chunk (freed by chunk_free whatever g_mode is then)
 };
 
 struct Chunk {  // mode 2
@@ -169,7 +170,7 @@ void* chunk_alloc(Arena& a, int device, size_t size) {
       va = static_cast<char*>(p);
     }
   }
-  a.live[reinterpret_cast<uintptr_t>(va)] = Segment{sz, hipMemGenericAllocationHandle_t{}, false};
+  a.live[reinterpret_cast<uintptr_t>(va)] = Segment{sz, hipMemGenericAllocationHandle_t{}, false, true};
   a.mapped_bytes += static_cast<int64_t>(sz);
   ++a.segments;
   return va;
@@ -238,7 +239,7 @@ void* fjalloc_alloc(ssize_t size, int device, void* /*stream*/) {
     give_back();
     return failed(a, 4, e);
   }
-  a.live[reinterpret_cast<uintptr_t>(va)] = Segment{sz, h, own};
+  a.live[reinterpret_cast<uintptr_t>(va)] = Segment{sz, h, own, false};
   a.mapped_bytes += static_cast<int64_t>(sz);
   ++a.segments;
   return va;
@@ -256,7 +257,7 @@ void fjalloc_free(void* ptr, size_t /*size*/, int device, void* stream) {
   const Segment s = it->second;
   a.live.erase(it);
   a.mapped_bytes -= static_cast<int64_t>(s.size);
-  if (g_mode == 2) {
+  if (s.chunk_slice) {
     chunk_free(a, device, static_cast<char*>(ptr), s.size);
     return;
   }
@@ -286,6 +287,10 @@ int fjalloc_stats(int device, int64_t* out) {
 int fjalloc_configure(int64_t reserve_bytes, int64_t align_bytes, int mode, int64_t stagger_bytes) {
   if (reserve_bytes <= 0 || align_bytes <= 0 || mode < 0 || mode > 2 || stagger_bytes < 0 || stagger_bytes % 256)
     return -1;
+  for (Arena& a : g_arena) {  // the layout is fixed once any device has a segment
+    std::lock_guard<std::mutex> lock(a.mu);
+    if (a.segments > 0) return -1;
+  }
   g_stagger = static_cast<size_t>(stagger_bytes);
   g_reserve_bytes = static_cast<size_t>(reserve_bytes);
   g_chunk_bytes = static_cast<size_t>(reserve_bytes);  // mode 2: the chunk size

@@ -29,7 +29,7 @@ void fjalloc_free(void* ptr, size_t size, int device, void* stream);
  * 1 reserve, 2 create, 3 map, 4 access, 5 range full), segments reserved at the address
  * hint, segments reserved elsewhere. 0, or -1 for a bad device. */
 int fjalloc_stats(int device, int64_t* out);
-/* Before a device's first allocation: the mode — 2 (default) segments are slices of
+/* Before the first allocation on any device (-1 afterwards): the mode — 2 (default) segments are slices of
  * hipMalloc'd chunks of reserve_bytes (default 1 GiB; never returned to the runtime, reused for
  * segments of the same size), segment n starting (n mod 31) x stagger_bytes (default 68 KiB)
  * after the previous one; 1 one VMM reservation + hipMemCreate per segment; 0 VMM sub-ranges of

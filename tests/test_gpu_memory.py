@@ -21,6 +21,8 @@ def test_delta_pool_allocations_fold_bitwise(cuda):
     plain = [[x.to(cuda) for x in c] for c in host]
     st = memory.stats(cuda)
     assert st["live_segments"] >= 1 and st["failures"] == 0
+    from fedjax_amd import _lib
+    assert _lib.load().fjalloc_configure(1 << 30, 64 << 10, 2, 68 << 10) == -1  # layout fixed once allocating
     lo, hi = st["base"], st["base"] + st["bump_offset"]
     assert all(lo <= x.data_ptr() < hi for c in pooled for x in c)  # inside the first chunk
     assert not any(lo <= x.data_ptr() < hi for c in plain for x in c)
