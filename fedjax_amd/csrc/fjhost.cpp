@@ -2421,7 +2421,13 @@ PyObject* zeros_like(PyObject*, PyObject* tree) {
       offs[l + 1] = offs[l] + (t.numel() + 63) / 64 * 64;
     }
     const at::Tensor& t0 = THPVariable_Unpack(w.leaves[0][0]);
-    at::Tensor flat = at::zeros({std::max<int64_t>(offs[L], 1)}, t0.options());
+    // zeroed by one hipMemsetAsync on the current stream (at::zeros would add a dispatched fill)
+    at::Tensor flat = at::empty({std::max<int64_t>(offs[L], 1)}, t0.options());
+    const hipStream_t zs = c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(dev)).stream();
+    if (hipMemsetAsync(flat.data_ptr(), 0, static_cast<size_t>(flat.numel()) * 4, zs) != hipSuccess) {
+      PyErr_SetString(PyExc_RuntimeError, "tree_zeros_like: hipMemsetAsync failed");
+      return nullptr;
+    }
     std::vector<PyObject*> wrapped(L, nullptr);
     struct Drop {
       std::vector<PyObject*>& v;
