@@ -13,6 +13,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_tree_ops.py tests/test_gpu_
   --timeout-method thread -p no:cacheprovider > "$O/tests.log" 2>&1
 rc=$?; tail -3 "$O/tests.log"; [ $rc -eq 0 ] || exit $rc
 for v in new old; do
+  mkdir -p "$O/$v"
   if [ $v = old ]; then export FJAGG_LIB=$FJAGG_LIB_OLD; fi
   timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d "$O/$v/loop" -o run --output-format csv -- \
     python tools/time_norms_loop.py 10 > "$O/$v/loop.json" 2> "$O/$v/loop.err" || exit $?
