@@ -50,18 +50,12 @@ namespace {
 // Per-client sum of squares accumulated during the fold (fjagg_wsum_l2_dense):
 // each lane sums the squares of its units of client k, the wave reduces that with
 // a fixed xor butterfly and lane 0 adds it to its wave's LDS slot [wave][k].
-// take() / finish(k, q) split end_client so fold() can run a group's butterflies after the
-// next group's loads are issued (the same additions in the same order: the bits do not change).
 struct NoNorm {
-  static constexpr bool kOn = false;
   template <class T, int V>
   __device__ __forceinline__ void add(const T (&)[V], bool) {}
   __device__ __forceinline__ void end_client(int64_t) {}
-  __device__ __forceinline__ float take() { return 0.f; }
-  __device__ __forceinline__ void finish(int64_t, float) {}
 };
 struct LdsNorm {
-  static constexpr bool kOn = true;
   float* slot;  // this wave's K floats in LDS
   float q;
   template <class T, int V>
@@ -71,17 +65,13 @@ struct LdsNorm {
     for (int i = 0; i < V; ++i) s = __fadd_rn(s, __fmul_rn((float)t[i], (float)t[i]));
     q = __fadd_rn(q, valid ? s : 0.f);
   }
-  __device__ __forceinline__ float take() {
-    const float v = q;
-    q = 0.f;
-    return v;
-  }
-  __device__ __forceinline__ void finish(int64_t k, float v) {
+  __device__ __forceinline__ void end_client(int64_t k) {
+    float v = q;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o, 64));
     if ((threadIdx.x & 63) == 0) slot[k] = __fadd_rn(slot[k], v);
+    q = 0.f;
   }
-  __device__ __forceinline__ void end_client(int64_t k) { finish(k, take()); }
 };
 
 // ----------------------------------------------------------------- epilogues
@@ -207,10 +197,6 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
   const uint8_t* nxt[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) nxt[u] = row(k + u < K ? k + u : K - 1);
-  // fused norms: each client's lane sums wait here until the next group's loads are issued,
-  // so the cross-lane reductions overlap those loads instead of holding them back
-  float pend[U];
-  int64_t kp = -1;
   for (; k + U <= K; k += U) {
     Raw v[U][E];
 #pragma unroll
@@ -223,13 +209,6 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
     for (int u = 0; u < U; ++u) {
       const int64_t kn = k + U + u;
       nxt[u] = row(kn < K ? kn : K - 1);
-    }
-    if constexpr (NORM::kOn) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (kp >= 0) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) nrm.finish(kp + u, pend[u]);
-      }
     }
     // BURST (default): every load of the group is issued before the first is consumed
     // (E*U in flight per lane); otherwise the scheduler interleaves loads and folds. Burst
@@ -247,14 +226,7 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(acc[j][i], ACC::mul(t[i], wk));
       }
-      pend[u] = nrm.take();
-    }
-    kp = k;
-  }
-  if constexpr (NORM::kOn) {
-    if (kp >= 0) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) nrm.finish(kp + u, pend[u]);
+      nrm.end_client(k + u);
     }
   }
   for (; k < K; ++k) {
