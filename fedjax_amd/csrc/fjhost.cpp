@@ -2276,13 +2276,19 @@ PyObject* flush_views(PyObject*, PyObject* arg) {
     } drop{x};
     PyTypeObject* t = Py_TYPE(x);
     if (t == g_fast.norm_view) {
-      PyObject** dp = _PyObject_GetDictPtr(x);
-      if (!dp || !*dp) continue;
-      PyObject* tk = PyDict_GetItemWithError(*dp, tk_name);  // borrowed
+      PyObject* dict = PyObject_GenericGetDict(x, nullptr);  // (new reference; public API)
+      if (!dict) return nullptr;
+      PyObject* tk = PyDict_GetItemWithError(dict, tk_name);  // borrowed from dict
+      Py_XINCREF(tk);
+      Py_DECREF(dict);
       if (!tk) {
         if (PyErr_Occurred()) return nullptr;
         continue;
       }
+      struct DropTk {
+        PyObject* o;
+        ~DropTk() { Py_DECREF(o); }
+      } drop_tk{tk};
       if (tk == Py_None) continue;
       PyObject* node = PyObject_GetAttr(tk, node_name);
       if (!node) return nullptr;
