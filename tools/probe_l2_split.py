@@ -16,7 +16,7 @@ import torch
 from fedjax_amd import _lib, kernels
 
 SHAPES = [(32,), (3, 3, 1, 32), (64,), (3, 3, 32, 64), (128,), (9216, 128), (62,), (128, 62)]
-F32, SCALE = 0, 1
+F32, SCALE, NONTEMPORAL = 0, 1, 4  # fjagg.h (tree_mean passes NONTEMPORAL for jobs >= 256 MiB)
 
 
 def split(blocks, s):
@@ -57,6 +57,19 @@ def main(calls=50, K=128):
     w = torch.tensor(np.random.RandomState(1).randint(1, 501, size=K), dtype=torch.float32, device=dev)
     l2 = torch.empty(K, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # the same clients through tree_mean (plan image in the kernel arguments), same box
+    from fedjax_amd import tree_util as tu
+    pairs = list(zip(leaves, w.cpu().numpy().astype(int).tolist()))
+    for _ in range(5):
+        tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(calls):
+        tu.tree_mean(pairs)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    print(json.dumps({"tree_mean_karg_us_per_call": round(e0.elapsed_time(e1) / calls * 1e3, 2)}), flush=True)
     ref_out, ref_l2 = None, None
     for s in (1, 2, 3, 4):
         blocks = split(base, s)
@@ -68,9 +81,9 @@ def main(calls=50, K=128):
             def go():
                 if name == "plain":
                     return lib.fjagg_wsum_ptrs(F32, F32, F32, img.data_ptr(), L, K, n, w.data_ptr(),
-                                               ctypes.c_float(1e-3), SCALE, ctypes.c_void_p(stream.cuda_stream))
+                                               ctypes.c_float(1e-3), SCALE | NONTEMPORAL, ctypes.c_void_p(stream.cuda_stream))
                 return lib.fjagg_wsum_l2_ptrs(F32, F32, F32, img.data_ptr(), L, K, n, w.data_ptr(),
-                                              ctypes.c_float(1e-3), l2.data_ptr(), SCALE, ws.data_ptr(), ws.numel(),
+                                              ctypes.c_float(1e-3), l2.data_ptr(), SCALE | NONTEMPORAL, ws.data_ptr(), ws.numel(),
                                               ctypes.c_void_p(stream.cuda_stream))
             for _ in range(5):
                 _lib.check(go(), name)
