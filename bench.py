@@ -97,6 +97,112 @@ def _cgroup_cpus():
         return None
 
 
+def _oracle():
+    """The oracle's C restatement (oracle/fold_ref.c through tests/coracle.py). TEST
+    INFRASTRUCTURE: loaded only by the cpu_baseline leg (the reported CPU baseline) and by
+    check_result (the checker of the timed output, after the timed region); the measured
+    path never touches it."""
+    from tests import coracle as co
+
+    lib_path = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(lib_path):
+        import __graft_entry__
+        __graft_entry__.build()
+    return co.load(lib_path)
+
+
+def check_cols(P, n=2000, edges=(), seed=0):
+    """Columns the check compares: n random ones, both ends of the row, and both sides of
+    every bucket edge of the exchange (fd.bucket_edges)."""
+    rs = np.random.RandomState(seed)
+    extra = [0, 1, 2, 3, P - 4, P - 3, P - 2, P - 1]
+    for e in edges:
+        extra += [e - 1, e, e + 1]
+    c = np.concatenate([rs.randint(0, P, n), np.asarray(extra, dtype=np.int64)])
+    return np.unique(c[(c >= 0) & (c < P)]).astype(np.int64)
+
+
+def _bf16_bits(a):
+    """float32 -> bfloat16 bits (RNE; finite inputs), as the kernels' f32_to_bf16."""
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def _ulps(a, b):
+    """Distance in float32 ulps (ordered bit patterns)."""
+    def ordered(x):
+        i = np.ascontiguousarray(x, dtype=np.float32).view(np.int32).astype(np.int64)
+        return np.where(i < 0, -(i & 0x7FFFFFFF), i)
+    return np.abs(ordered(a) - ordered(b))
+
+
+def check_result(y, *, K, P, k0, k1, weights, W, dtype, seed=0, exact=True, nranks=1, edges=(),
+                 reference_bf16=False, f32_mean=None):
+    """Checks the timed run's result against the oracle, after the timed region (VERDICT r4
+    next #1): the synthetic deltas are a counter hash of (client, column), so the host
+    regenerates exactly the ~2,000 sampled columns it compares (oracle_synth_cols_f32) and
+    folds them with the oracle's restatement of tree_util.py:76-96 (oracle_wsum_f32).
+
+    * ``exact``: ``y`` (the mean, or at a rehearsal rank 0's scaled partial over clients
+      k0..k1) must be bitwise the oracle's sequential fold — f32 out, bf16 out (the fold's
+      one RNE rounding), or with ``reference_bf16`` the reference's bf16 op sequence;
+    * otherwise (N > 1 ranks, rank 0 after the exchange): the f32 mean over all K clients
+      within SURVEY §8(c)'s bound with the N-way combine's extra roundings,
+      |y - y_ref| <= (K+N+2) 2^-24 r sum_k |w_k x_k| + 2^-24 |y_ref|, with
+      max-abs and max-ulp reported; for bf16 deltas (configs[4]) ``y`` is the bf16 mean and
+      ``f32_mean`` the f32 mean before the cast: the cast is checked bitwise, and the bf16
+      mean against the f64 oracle within 2^-8 |y64| + that bound.
+    Returns (status, detail): status "bitwise", "within_tolerance" or "FAILED"."""
+    o = _oracle()
+    cols = check_cols(P, edges=edges)
+    ct = torch.from_numpy(cols).to(y.device)
+    bf16 = dtype == torch.bfloat16
+    got = y.index_select(0, ct)
+    got = (got.view(torch.int16).cpu().numpy().view(np.uint16) if y.dtype == torch.bfloat16
+           else got.cpu().numpy())
+    kc = (k1 - k0) if exact else K
+    x = o.synth_cols_f32(kc, cols, seed=seed, k0=k0 if exact else 0, bf16=bf16)
+    w = np.float32(weights[k0:k1] if exact else weights)
+    r = np.float32(1.0 / W) if W > 0 else np.float32(0.0)
+    detail = {"columns": int(cols.size), "clients": int(kc),
+              "oracle": "oracle/fold_ref.c (sequential fold, tree_util.py:76-96) on host-regenerated columns"}
+    if exact:
+        if reference_bf16:
+            xu = (x.view(np.uint32) >> 16).astype(np.uint16)
+            want = o.wsum_bf16_refsem(xu, w, r)
+        else:
+            want = o.wsum_f32(x, w, scale=r)
+            if y.dtype == torch.bfloat16:
+                want = _bf16_bits(want)
+        bad = int(np.count_nonzero(got.view(np.uint16 if want.dtype == np.uint16 else np.uint32)
+                                   != want.view(np.uint16 if want.dtype == np.uint16 else np.uint32)))
+        detail["compare"] = "bitwise"
+        detail["mismatches"] = bad
+        return ("bitwise" if bad == 0 else "FAILED"), detail
+    want = o.wsum_f32(x, w, scale=r)
+    grow = (K + nranks + 2) / (K + 2)
+    bound = o.bound_f32(x, w, r, want) * grow
+    ym = got if f32_mean is None else f32_mean.index_select(0, ct).cpu().numpy()
+    err = np.abs(ym.astype(np.float64) - want.astype(np.float64))
+    ok = bool(np.all(err <= bound))
+    detail.update({"compare": f"f32 mean within the (K+N+2) sequential-sum bound, N={nranks}",
+                   "max_abs": float(err.max()), "max_ulp": int(_ulps(ym, want).max()),
+                   "max_err_over_bound": float((err / np.maximum(bound, 1e-300)).max()),
+                   "bitwise_columns": int(np.count_nonzero(ym.view(np.uint32) == want.view(np.uint32)))})
+    if f32_mean is not None:  # bf16 deltas: the cast of the f32 mean, and the bf16 mean vs f64
+        cast_ok = bool(np.array_equal(got, _bf16_bits(ym)))
+        xu = (x.view(np.uint32) >> 16).astype(np.uint16)
+        y64 = o.wsum_bf16_f64(xu, w.astype(np.float64), float(r))
+        fb = (K + nranks + 3) * 2.0 ** -24 * float(r) * np.abs(x.astype(np.float64) * w[:, None]).sum(0) \
+            + 2.0 ** -24 * np.abs(y64)
+        yb = (got.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+        b_ok = bool(np.all(np.abs(yb - y64) <= 2.0 ** -8 * np.abs(y64) + fb))
+        detail.update({"bf16_cast_bitwise": cast_ok, "bf16_mean_within_f64_bound": b_ok,
+                       "bf16_max_abs_vs_f64": float(np.abs(yb - y64).max())})
+        ok = ok and cast_ok and b_ok
+    return ("within_tolerance" if ok else "FAILED"), detail
+
+
 def cpu_baseline(K, seconds=6.0):
     """Reference op sequence (per client: fresh w*x buffer, in-place add; final
     scale) on the host, bounded sample, timed at 1 thread, at the cgroup's CPU
@@ -104,13 +210,7 @@ def cpu_baseline(K, seconds=6.0):
     §8(d)). ``value`` / ``cores`` are the fastest of those runs (on a box whose cgroup
     quota is below its visible cores, the quota's thread count beats all cores);
     ``sweep`` holds every run."""
-    from tests import coracle as co
-
-    lib_path = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
-    if not os.path.exists(lib_path):
-        import __graft_entry__
-        __graft_entry__.build()
-    o = co.load(lib_path)
+    o = _oracle()
     Ps = 1 << 18  # sample: all K clients x 262,144 params (1 GiB for K = 1024)
     x = o.synth_f32(K, Ps, seed=0)
     w = np.float32(fedavg_weights(K))
@@ -235,22 +335,32 @@ def dropin_surface(dev, calls=20):
     res["c1_mean_aggregator_apply_sync_call_GBs"] = round(K * P * 4 / ms / 1e6, 1)
     del triples
     # the library algorithms' running sum (fedjax/algorithms/fed_avg.py:132-146): one
-    # synchronous round of tree_add(s, tree_weight(delta, n)) x K + tree_inverse_weight
+    # synchronous round of tree_add(s, tree_weight(delta, n)) x K + tree_inverse_weight,
+    # (a) as fed_avg.py:132-146 writes it, with the per-client delta_l2_norm kept in
+    # client_diagnostics (:142-144), and (b) without the norm (the aggregation alone)
     W = float(sum(w for _, w in pairs))
-    loop = []
-    for _ in range(calls):
-        torch.cuda.synchronize()
-        t0 = pc()
-        s = tu.tree_zeros_like(pairs[0][0])
-        for t, w in pairs:
-            s = tu.tree_add(s, tu.tree_weight(t, w))
-        mean = tu.tree_inverse_weight(s, W)
-        torch.cuda.synchronize()
-        loop.append(pc() - t0)
-    del s, mean
-    ms = float(np.median(loop)) * 1e3
-    res["c1_library_loop_round_ms"] = round(ms, 4)
-    res["c1_library_loop_round_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+    for with_norms in (True, False):
+        loop = []
+        for _ in range(calls):
+            torch.cuda.synchronize()
+            t0 = pc()
+            s, client_diagnostics = tu.tree_zeros_like(pairs[0][0]), {}
+            for cid, (t, w) in enumerate(pairs):
+                s = tu.tree_add(s, tu.tree_weight(t, w))
+                if with_norms:
+                    client_diagnostics[cid] = {"delta_l2_norm": tu.tree_l2_norm(t)}
+            mean = tu.tree_inverse_weight(s, W)
+            torch.cuda.synchronize()
+            loop.append(pc() - t0)
+        ms = float(np.median(loop)) * 1e3
+        key = "c1_library_loop_with_norms_round" if with_norms else "c1_library_loop_without_norms_round"
+        res[key + "_ms"] = round(ms, 4)
+        res[key + "_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+        if with_norms:  # the kept norms hold the values (outside the timing): vs one batched launch
+            got = torch.stack([client_diagnostics[c]["delta_l2_norm"] for c in range(K)])
+            ref = tu.tree_l2_norms([t for t, _ in pairs])
+            res["c1_library_loop_norms_max_rel_diff"] = float(((got - ref).abs() / ref).max())
+        del s, mean, client_diagnostics
     # the same clients allocated under the opt-in delta pool (fedjax_amd.memory, include/fjalloc.h):
     # still one tensor per (client, leaf), placed in shared chunks
     from fedjax_amd import memory
@@ -276,21 +386,13 @@ def dropin_surface(dev, calls=20):
     del pooled
     res["note"] = ("caller-held pytrees, separate allocations; timed after the headline, outside its "
                    "timed region; GB/s = K*P*4 client-delta bytes per call (library loop: per round); "
+                   "c1_library_loop_with_norms: fed_avg.py:132-146 as written (tree_l2_norm per client into "
+                   "client_diagnostics), c1_library_loop_without_norms: the same loop without the norm; "
                    "c1_delta_pool_*: the same clients allocated under fedjax_amd.memory.delta_allocation()")
     del pairs
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return res
-
-
-def _free_port() -> int:
-    import socket
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def rank_timeout(args) -> float:
@@ -357,9 +459,12 @@ def spawn_ranks(nproc: int, argv, script: str = None, timeout: float = None) -> 
     import subprocess
     import tempfile
 
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script or os.path.abspath(__file__),
-           *argv]
+    # --standalone: the launcher's c10d rendezvous binds its TCP store on port 0 and keeps it,
+    # and the ranks join through that store (TORCHELASTIC_USE_AGENT_STORE). Until round 4 a
+    # port found by binding 0 and closing the socket was passed as --master-port; another
+    # process could take it in between (the intermittent rc=1 of test_spawn_forwards_rank0_json).
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--local-addr=127.0.0.1", script or os.path.abspath(__file__), *argv]
     fd, json_path = tempfile.mkstemp(prefix="fj_bench_", suffix=".json")
     os.close(fd)
     phase_dir = tempfile.mkdtemp(prefix="fj_bench_phases_")
@@ -392,7 +497,8 @@ def spawn_ranks(nproc: int, argv, script: str = None, timeout: float = None) -> 
         os.unlink(json_path)
         shutil.rmtree(phase_dir, ignore_errors=True)
     if proc.returncode != 0:
-        log(f"rank launcher exited with status {proc.returncode}")
+        log(f"bench: spawn_ranks returns {proc.returncode}: the rank launcher exited with that status "
+            f"(a rank failed; its stderr is above)")
         return proc.returncode
     if filed:  # rank 0's line from its own file: nothing else can be interleaved into it
         lines = [filed]
@@ -407,7 +513,8 @@ def spawn_ranks(nproc: int, argv, script: str = None, timeout: float = None) -> 
                 except ValueError:
                     pass
     if len(lines) != 1:
-        log(f"expected one JSON line from rank 0, got {len(lines)}")
+        log(f"bench: spawn_ranks returns 1: expected one JSON line from rank 0, got {len(lines)} "
+            f"(rank 0's file {'was empty' if not filed else 'held a line'}; stdout {len(out)} bytes)")
         return 1
     sys.stdout.write(lines[0] + "\n")
     sys.stdout.flush()
@@ -473,6 +580,8 @@ def measure_traffic(workload, dst=None):
 
 # host RAM one rank may pin for its shard in the e2e leg (a configs[4] shard is 256 GB)
 E2E_MAX_PINNED_BYTES = 64 << 30
+# N = 1 default e2e sample: the first 256 clients of the slab (4.3 GB at configs[2]); --e2e: all
+E2E_SAMPLE_CLIENTS = 256
 
 
 def host_resident_rate(x, w_local, sharded_step, out, scale, nt, dev, rank, sharded, job_bytes, reps=3):
@@ -481,7 +590,9 @@ def host_resident_rate(x, w_local, sharded_step, out, scale, nt, dev, rank, shar
     then the fold — at N>1 the whole sharded step, fold + RCCL reduce — and the mean comes
     back to the host (D2H on rank 0). Rate = all clients' bytes / the max-over-ranks wall
     time of ``reps`` such rounds. Every rank decides together whether its shard fits the
-    pinned budget (one all_reduce), so either all ranks run the leg or none does."""
+    pinned budget (one all_reduce), so either all ranks run the leg or none does. At N = 1
+    ``x`` may be the first clients of the slab only (a sub-sample: the rate is PCIe-bound
+    and does not depend on the client count; ``job_bytes`` are that sample's bytes)."""
     from fedjax_amd import kernels
 
     nbytes = x.shape[0] * x.shape[1] * x.element_size()
@@ -490,7 +601,7 @@ def host_resident_rate(x, w_local, sharded_step, out, scale, nt, dev, rank, shar
     if ok:
         try:
             xh = torch.empty(x.shape, dtype=x.dtype).pin_memory()
-            xh.copy_(x.cpu())
+            xh.copy_(x)  # D2H straight into the pinned buffer
         except RuntimeError as e:  # pinned allocation refused: skip the leg on every rank
             log(f"[bench rank {rank}] e2e: pinned host buffer of {nbytes / 2**30:.1f} GiB refused ({e})")
             ok, xh = False, None
@@ -503,7 +614,7 @@ def host_resident_rate(x, w_local, sharded_step, out, scale, nt, dev, rank, shar
                 "e2e_note": f"skipped: a rank's shard ({nbytes / 2**30:.1f} GiB) exceeds the "
                             f"{E2E_MAX_PINNED_BYTES >> 30} GiB pinned-host budget or was refused"}
     yh = torch.empty(out.shape, dtype=out.dtype).pin_memory()
-    wd = torch.from_numpy(np.float32(w_local)).to(dev)
+    wd = torch.from_numpy(np.float32(w_local[:x.shape[0]])).to(dev)
 
     def one():
         x.copy_(xh, non_blocking=True)
@@ -554,8 +665,11 @@ def main():
                     help="skip the drop-in surface sub-record (mean_aggregator().apply / tree_mean over "
                          "caller-held pytrees, timed after the headline)")
     ap.add_argument("--e2e", action="store_true",
-                    help="N=1: also time host-resident deltas (H2D + fold + D2H); on by default at N>1")
-    ap.add_argument("--no-e2e", action="store_true", help="N>1: skip the host-resident end-to-end leg")
+                    help="N=1: time host-resident deltas (H2D + fold + D2H) over ALL the clients (default: "
+                         f"the first {E2E_SAMPLE_CLIENTS} clients' deltas, a stated sub-sample)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-resident end-to-end leg")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the check of the timed result against the oracle (sampled columns)")
     ap.add_argument("--measure-traffic", action="store_true",
                     help="N=1: run the FETCH_SIZE / WRITE_SIZE rocprofv3 passes from this run (child processes) "
                          "and report their HBM bytes as roofline.traffic (default: profiles/traffic_<workload>.json "
@@ -626,16 +740,14 @@ def main():
     if args.rehearse_shard > 1:
         if world != 1:
             raise SystemExit("--rehearse-shard runs as a single process")
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
         nshard = args.rehearse_shard
     sharded = nshard > 1
     if sharded:
         phase(rank, f"init process group ({args.backend}, world {world})")
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-        else:
-            dist.init_process_group(args.backend, rank=rank, world_size=world)
+        kw = {"device_id": dev} if args.backend == "nccl" else {}
+        if world == 1:  # the one-GPU rehearsal: its own store, bound on port 0 and held (no port race)
+            kw["store"] = dist.TCPStore("127.0.0.1", 0, 1, True)
+        dist.init_process_group(args.backend, rank=rank, world_size=world, **kw)
 
     import fedjax_amd  # noqa: F401
     from fedjax_amd import distributed as fd, kernels, tree_util as tu
@@ -824,11 +936,31 @@ def main():
     mean_kernel_s = float(np.mean(kernel_ms)) / 1e3
     achieved = bytes_per_launch / mean_kernel_s / 1e9
 
+    # the timed result against the oracle (rank 0, after the timed region)
+    check, check_detail = None, None
+    if rank == 0 and not args.no_check:
+        if args.server != "none":
+            check_detail = {"skipped": "the fused server step writes params, not the mean"}
+        else:
+            phase(rank, "check the result against the oracle (sampled columns)")
+            exact = nshard != world or not sharded  # one fold, or rank 0's share in a rehearsal
+            edges = [p0 for p0, _ in fd.bucket_edges(P, buckets)[1:]] if sharded else []
+            check, check_detail = check_result(
+                final if (final is not None and not exact) else out, K=K, P=P, k0=k0, k1=k1, weights=weights,
+                W=W, dtype=dtype, exact=exact, nranks=nshard, edges=edges, reference_bf16=args.reference_bf16,
+                f32_mean=out if (final is not None and not exact) else None)
+            check_detail["wall_s"] = round(time.perf_counter() - t1, 2)
+            log(f"[bench rank 0] check: {check} {check_detail}")
+
     e2e = None
-    if (args.e2e or (sharded and not args.no_e2e)) and args.server == "none" and not args.with_norms:
+    if not args.no_e2e and args.server == "none" and not args.with_norms:
         phase(rank, "e2e: host-resident deltas (pinned H2D + fold [+ reduce] + D2H)")
-        e2e = host_resident_rate(x, w_local, step if sharded else None, out, scale, nt, dev, rank, sharded,
-                                 K * P * esize if nshard == world else Kl * P * esize)
+        ns = Kl if (sharded or args.e2e) else min(Kl, E2E_SAMPLE_CLIENTS)
+        e2e = host_resident_rate(x[:ns], w_local, step if sharded else None, out, scale, nt, dev, rank, sharded,
+                                 K * P * esize if nshard == world else ns * P * esize)
+        if not sharded:
+            e2e["e2e_sample"] = (f"the first {ns} of the {Kl} clients ({ns * P * esize / 1e9:.2f} GB)"
+                                 if ns < Kl else f"all {Kl} clients ({ns * P * esize / 1e9:.2f} GB)")
 
     traffic = (None, None)
     if rank == 0 and not sharded and not args.with_norms and args.server == "none" and not args.variant \
@@ -879,6 +1011,8 @@ def main():
                          "bytes_per_launch": bytes_per_launch,
                          "mean_launch_ms": round(mean_kernel_s * 1e3, 4)},
         }
+        res["check"] = check
+        res["check_detail"] = check_detail
         if e2e is not None:
             res.update(e2e)
         if nshard != world:
@@ -897,6 +1031,9 @@ def main():
     phase(rank, "done")
     if watchdog is not None:
         watchdog.cancel()
+    if check == "FAILED":
+        log("bench: the timed result does NOT match the oracle (check_detail in the JSON line)")
+        raise SystemExit(3)
 
 
 def single_process(args):
@@ -950,6 +1087,11 @@ def single_process(args):
     sync()
     elapsed = time.perf_counter() - t0
     comm.close()
+    check, check_detail = None, None
+    if not args.no_check:  # device 0's mean over all K clients vs the oracle, after the timed region
+        check, check_detail = check_result(outs[0], K=K, P=P, k0=0, k1=K, weights=weights, W=W, dtype=dtype,
+                                           exact=False, nranks=N,
+                                           edges=[p0 for p0, _ in fd.bucket_edges(P, buckets)[1:]])
     res = {"metric": METRIC, "value": round(K * P * esize * args.steps / elapsed / 1e9, 2), "unit": "GB/s",
            "n_gpus": N, "ranks": 1, "rccl_ranks": N, "launcher": "single process (fjcomm_init_all)",
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -959,8 +1101,11 @@ def single_process(args):
            "config": {"workload": desc, "clients": K, "params": P,
                       "parallelism": f"client-sharded x{N}, one process, grouped RCCL "
                                      f"{'all_reduce' if args.all_ranks else 'reduce'}",
-                      "buckets": fd.bucket_name(buckets)}}
+                      "buckets": fd.bucket_name(buckets)},
+           "check": check, "check_detail": check_detail}
     emit_json(json_fd, res)
+    if check == "FAILED":
+        raise SystemExit(3)
 
 
 if __name__ == "__main__":

@@ -47,32 +47,92 @@ __attribute__((visibility("hidden"))) thread_local char fjagg_g_err[512] = "";
 namespace {
 
 // ------------------------------------------------------------- fused l2 hooks
-// Per-client sum of squares accumulated during the fold (fjagg_wsum_l2_dense):
-// each lane sums the squares of its units of client k, the wave reduces that with
-// a fixed xor butterfly and lane 0 adds it to its wave's LDS slot [wave][k].
+// Per-client sum of squares accumulated during the fold (fjagg_wsum_l2_*). The
+// reference's norm is an XLA reduction (tree_util.py:105-114) whose order is not
+// pinned, so this one is free to pick the cheapest fixed order (deterministic; the
+// tests bound it against an f64 norm):
+//   * each lane accumulates its units' squares of client k with packed FMAs into a
+//     float2 (lanes of invalid units load zeros, fold() points them past the row);
+//   * a group of N clients is reduced across the wave together, in registers, with
+//     no LDS round trip: v_permlane32_swap halves the lanes and pairs clients
+//     (q0 | q2), v_permlane16_swap pairs the rows (one client per 16-lane row), and
+//     four DPP row rotations finish each row's sum (row c holds client c);
+//   * lane 16c adds client k+c's total to its wave's LDS slot [wave][k+c].
+// The plain fold instantiates NoNorm: nothing of this is emitted.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float swap32_sum(float a, float b) {  // [a.lo+a.hi | b.lo+b.hi]
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __fadd_rn(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+// rows r0..r3 of 16 lanes: [a.r0+a.r1, b.r0+b.r1, a.r2+a.r3, b.r2+b.r3]
+__device__ __forceinline__ float swap16_sum(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __fadd_rn(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {  // v + v[DPP CTRL]
+  return __fadd_rn(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false)));
+}
+__device__ __forceinline__ float row16_sum(float v) {  // every lane: the sum of its 16-lane row
+  v = dpp_add<0x128>(v);  // row_ror:8
+  v = dpp_add<0x124>(v);  // row_ror:4
+  v = dpp_add<0x122>(v);  // row_ror:2
+  return dpp_add<0x121>(v);  // row_ror:1
+}
+
 struct NoNorm {
-  template <class T, int V>
-  __device__ __forceinline__ void add(const T (&)[V], bool) {}
-  __device__ __forceinline__ void end_client(int64_t) {}
+  static constexpr bool kOn = false;
+  template <int N>
+  __device__ __forceinline__ void commit(const f32x2 (&)[N], int64_t) {}
 };
 struct LdsNorm {
+  static constexpr bool kOn = true;
   float* slot;  // this wave's K floats in LDS
-  float q;
-  template <class T, int V>
-  __device__ __forceinline__ void add(const T (&t)[V], bool valid) {
-    float s = 0.f;
+  // clients k .. k+N-1 (N = 1, 2, 4 or 8): lane partials -> the wave's LDS slots
+  template <int N>
+  __device__ __forceinline__ void commit(const f32x2 (&q2)[N], int64_t k) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (N == 8) {
+      const f32x2 a[4] = {q2[0], q2[1], q2[2], q2[3]}, b[4] = {q2[4], q2[5], q2[6], q2[7]};
+      commit<4>(a, k);
+      commit<4>(b, k + 4);
+    } else {
+      float q[N];
 #pragma unroll
-    for (int i = 0; i < V; ++i) s = __fadd_rn(s, __fmul_rn((float)t[i], (float)t[i]));
-    q = __fadd_rn(q, valid ? s : 0.f);
-  }
-  __device__ __forceinline__ void end_client(int64_t k) {
-    float v = q;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o, 64));
-    if ((threadIdx.x & 63) == 0) slot[k] = __fadd_rn(slot[k], v);
-    q = 0.f;
+      for (int i = 0; i < N; ++i) q[i] = __fadd_rn(q2[i].x, q2[i].y);
+      float v;
+      if constexpr (N == 4) {
+        v = row16_sum(swap16_sum(swap32_sum(q[0], q[2]), swap32_sum(q[1], q[3])));  // row c: client c
+      } else if constexpr (N == 2) {
+        const float h = swap32_sum(q[0], q[1]);  // lanes 0-31: client 0, 32-63: client 1
+        v = row16_sum(swap16_sum(h, h));          // rows 0, 1: client 0; rows 2, 3: client 1
+      } else {
+        const float h = swap32_sum(q[0], q[0]);
+        v = row16_sum(swap16_sum(h, h));  // every row: the client
+      }
+      constexpr int kStep = 64 / N;  // lane holding client c: c * kStep
+      if ((lane & (kStep - 1)) == 0) {
+        float* s = slot + k + lane / kStep;
+        *s = __fadd_rn(*s, v);
+      }
+    }
   }
 };
+
+// a lane's squares of one unit into its client's packed accumulator
+template <class T, int V>
+__device__ __forceinline__ void sq_acc(const T (&t)[V], f32x2& q) {
+  if constexpr (V == 1) {
+    q.x = __builtin_fmaf((float)t[0], (float)t[0], q.x);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; i += 2) {
+      const f32x2 p = {(float)t[i], (float)t[i + 1]};
+      q = __builtin_elementwise_fma(p, p, q);
+    }
+  }
+}
 
 // ----------------------------------------------------------------- epilogues
 // PlainEpi: the fold's result goes to the output (tree_mean). OptEpi: the mean
@@ -163,22 +223,30 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
   auto outp = [&](int j) { return obase + (size_t)(off[j] / IB) * OB; };
   using T = typename ACC::T;
   using Raw = typename Unit<IN, V>::Raw;
+  // With norms, loads of an invalid unit (a lane past its range) point past every row
+  // descriptor's range, so they read zeros without touching memory: the unit's store is
+  // skipped, and the squares need no masking. outp() keeps the caller's in-bounds offset.
+  // (The plain fold keeps the caller's clamped offsets: its code is unchanged.)
+  uint32_t loff[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) loff[j] = (!NORM::kOn || valid[j]) ? off[j] : 0x80000000u;
   T acc[E][V];
   {  // client 0: s_0 = t_0 (tree_util.py:89-91) or out + t_0 (running sum)
     const auto r = row_rsrc(row(0), row_bytes);
     Raw v[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) v[j] = load_unit<IN, V, NT>(r, off[j]);
+    for (int j = 0; j < E; ++j) v[j] = load_unit<IN, V, NT>(r, loff[j]);
     const T w0 = ACC::weight(w[0]);
+    f32x2 q[1] = {{0.f, 0.f}};
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       T t[V];
       decode<IN, ACC, V>(v[j], t);
-      nrm.add(t, valid[j]);
+      if constexpr (NORM::kOn) sq_acc<T, V>(t, q[0]);
 #pragma unroll
       for (int i = 0; i < V; ++i) acc[j][i] = ACC::mul(t[i], w0);
     }
-    nrm.end_client(0);
+    nrm.template commit<1>(q, 0);
     if (accumulate) {
 #pragma unroll
       for (int j = 0; j < E; ++j) {
@@ -203,7 +271,7 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
     for (int u = 0; u < U; ++u) {
       const auto r = row_rsrc(nxt[u], row_bytes);
 #pragma unroll
-      for (int j = 0; j < E; ++j) v[u][j] = load_unit<IN, V, NT>(r, off[j]);
+      for (int j = 0; j < E; ++j) v[u][j] = load_unit<IN, V, NT>(r, loff[j]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -215,6 +283,9 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
     // is faster with one workgroup per CU, interleaved with two or more full tiles per CU
     // (k_dense picks per launch, launch_dense_v).
     if constexpr (BURST) __builtin_amdgcn_sched_barrier(0);
+    f32x2 q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) q[u] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const T wk = ACC::weight(w[k + u]);
@@ -222,25 +293,26 @@ __device__ __forceinline__ void fold(RowFn row, uint32_t row_bytes, int64_t K,
       for (int j = 0; j < E; ++j) {
         T t[V];
         decode<IN, ACC, V>(v[u][j], t);
-        nrm.add(t, valid[j]);
+        if constexpr (NORM::kOn) sq_acc<T, V>(t, q[u]);
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(acc[j][i], ACC::mul(t[i], wk));
       }
-      nrm.end_client(k + u);
     }
+    nrm.template commit<U>(q, k);
   }
   for (; k < K; ++k) {
     const auto r = row_rsrc(row(k), row_bytes);
     const T wk = ACC::weight(w[k]);
+    f32x2 q[1] = {{0.f, 0.f}};
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       T t[V];
-      decode<IN, ACC, V>(load_unit<IN, V, NT>(r, off[j]), t);
-      nrm.add(t, valid[j]);
+      decode<IN, ACC, V>(load_unit<IN, V, NT>(r, loff[j]), t);
+      if constexpr (NORM::kOn) sq_acc<T, V>(t, q[0]);
 #pragma unroll
       for (int i = 0; i < V; ++i) acc[j][i] = ACC::add(acc[j][i], ACC::mul(t[i], wk));
     }
-    nrm.end_client(k);
+    nrm.template commit<1>(q, k);
   }
 #pragma unroll
   for (int j = 0; j < E; ++j) {
@@ -328,7 +400,7 @@ __global__ __launch_bounds__(kThreads) void k_dense_l2(
   const int tid = threadIdx.x;
   for (int64_t i = tid; i < (kThreads / 64) * K; i += kThreads) l2lds[i] = 0.f;
   __syncthreads();
-  LdsNorm nrm{l2lds + (tid >> 6) * K, 0.f};
+  LdsNorm nrm{l2lds + (tid >> 6) * K};
   auto row = [=](int64_t k) { return x + k * ld_bytes; };
   const uint32_t row_bytes = (uint32_t)((nunits * V + tail_n) * IB);
   int64_t b = blockIdx.x;
@@ -523,7 +595,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   if constexpr (L2) {
     for (int64_t i = tid; i < (kThreads / 64) * K; i += kThreads) l2lds[i] = 0.f;
     __syncthreads();
-    nrm = LdsNorm{l2lds + (tid >> 6) * K, 0.f};
+    nrm = LdsNorm{l2lds + (tid >> 6) * K};
   }
   if (tail) {
     const bool active = tid < n - nunits * V;

@@ -62,6 +62,18 @@ void oracle_fill_synth_bf16(uint16_t* x, int64_t ld, int64_t K, int64_t P, int64
     for (int64_t p = 0; p < P; ++p)
       x[k * ld + p] = f32_to_bf16(fj_synth(seed, (uint64_t)(k0 + k), (uint64_t)p, amp));
 }
+/* The same generator restricted to n sampled columns cols[] of clients k0..k0+K-1:
+ * x[k * n + i] = synth(k0 + k, cols[i]); bf16 != 0 rounds each value to bf16 (RNE) and
+ * returns it widened back to f32 (the value a bf16 slab holds). Lets a checker regenerate
+ * exactly the columns it compares without the whole K x P slab. */
+void oracle_synth_cols_f32(float* x, int64_t K, int64_t k0, const int64_t* cols, int64_t n,
+                           uint64_t seed, float amp, int bf16) {
+  for (int64_t k = 0; k < K; ++k)
+    for (int64_t i = 0; i < n; ++i) {
+      float v = fj_synth(seed, (uint64_t)(k0 + k), (uint64_t)cols[i], amp);
+      x[k * n + i] = bf16 ? bf16_to_f32(f32_to_bf16(v)) : v;
+    }
+}
 
 /* ---- single-pass restatement (same bits as the reference op sequence) ----
  * y[p] = fl(fold_k(fl(x_k[p]*w_k)) * scale); init: s_0 = t_0 (tree_util.py:89-91),

@@ -20,7 +20,17 @@ class COracle:
         lib.oracle_wsum_bound_f32.argtypes = [_f32p, _i64, _i64, _i64, _f32p, _f32, _f32p, _f64p]
         lib.oracle_tree_mean_refseq_f32.argtypes = [_f32p, _i64, _i64, _i64, _f32p, _f32, _f32p, _int]
         lib.oracle_tree_mean_refseq_f32.restype = _int
+        lib.oracle_synth_cols_f32.argtypes = [_f32p, _i64, _i64, np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS"),
+                                              _i64, _u64, _f32, _int]
         self.lib = lib
+
+    def synth_cols_f32(self, K, cols, seed=0, amp=0.01, k0=0, bf16=False):
+        """Clients k0..k0+K-1 of the synthetic slab at columns ``cols`` only: [K, len(cols)]
+        float32 (bf16: the bf16-rounded values, widened)."""
+        cols = np.ascontiguousarray(cols, dtype=np.int64)
+        x = np.empty((K, cols.size), np.float32)
+        self.lib.oracle_synth_cols_f32(x, K, k0, cols, cols.size, seed, amp, int(bool(bf16)))
+        return x
 
     def synth_f32(self, K, P, seed=0, amp=0.01, k0=0):
         x = np.empty((K, P), np.float32)

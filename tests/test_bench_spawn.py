@@ -40,8 +40,9 @@ def rank_script(tmp_path):
 @pytest.mark.parametrize("n", [2, 3])
 def test_spawn_forwards_rank0_json(rank_script, capfd, n):
     rc = bench.spawn_ranks(n, ["-1"], script=rank_script, timeout=180)
-    out = capfd.readouterr().out
-    assert rc == 0
+    cap = capfd.readouterr()
+    out = cap.out
+    assert rc == 0, cap.err  # spawn_ranks names the branch that returned non-zero on stderr
     lines = [ln for ln in out.splitlines() if ln.strip()]
     assert len(lines) == 1, out
     d = json.loads(lines[0])
@@ -165,8 +166,8 @@ def test_rank_watchdog_ends_a_stalled_rank_under_an_outer_launcher(tmp_path):
     """ % bench.ROOT))
     env = {k: v for k, v in os.environ.items() if k != "FJ_BENCH_PHASES"}
     t0 = time.monotonic()
-    proc = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                           "--master-addr=127.0.0.1", f"--master-port={bench._free_port()}", str(p)],
+    proc = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--nnodes=1",
+                           "--nproc-per-node=2", "--local-addr=127.0.0.1", str(p)],
                           capture_output=True, text=True, timeout=120, env=env)
     took = time.monotonic() - t0
     assert proc.returncode != 0

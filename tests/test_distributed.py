@@ -5,9 +5,6 @@ the sharding, bucketing, W handling and reduce/all_reduce logic of
 fedjax_amd.distributed run without a GPU; the GPU test runs the same function
 with the HIP kernel.
 """
-import os
-import socket
-
 import numpy as np
 import pytest
 import torch
@@ -15,16 +12,9 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import tree_util_ref as ref
+from tests.rendezvous import HeldStore, init_group
 
 K, P = 24, 5000
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _oracle_partial(x, w, scale, out):
@@ -33,9 +23,7 @@ def _oracle_partial(x, w, scale, out):
 
 
 def _worker(rank, world, port, all_ranks, buckets, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_group("gloo", rank, world, port)
     try:
         from fedjax_amd import distributed as fd
         weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
@@ -57,7 +45,8 @@ def _worker(rank, world, port, all_ranks, buckets, q):
 def test_sharded_mean_world2_gloo(all_ranks, buckets, coracle):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = HeldStore(2)
+    port = store.port
     procs = [ctx.Process(target=_worker, args=(r, 2, port, all_ranks, buckets, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -80,9 +69,7 @@ def test_sharded_mean_world2_gloo(all_ranks, buckets, coracle):
 
 
 def _worker_ragged(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_group("gloo", rank, world, port)
     try:
         from fedjax_amd import distributed as fd
         Kr = 7
@@ -100,7 +87,8 @@ def _worker_ragged(rank, world, port, q):
 def test_ragged_shards_world3_gloo():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = HeldStore(3)
+    port = store.port
     procs = [ctx.Process(target=_worker_ragged, args=(r, 3, port, q)) for r in range(3)]
     for p in procs:
         p.start()
@@ -117,9 +105,7 @@ def test_ragged_shards_world3_gloo():
 
 
 def _worker_empty(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_group("gloo", rank, world, port)
     try:
         from fedjax_amd import distributed as fd
         tmpl = {"w": torch.zeros(3, 2), "b": torch.zeros(2)}
@@ -135,7 +121,8 @@ def test_sharded_tree_mean_without_clients_world3_gloo():
     """ranks without clients must reach the same collectives (no hang)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = HeldStore(3)
+    port = store.port
     procs = [ctx.Process(target=_worker_empty, args=(r, 3, port, q)) for r in range(3)]
     for p in procs:
         p.start()
@@ -147,9 +134,7 @@ def test_sharded_tree_mean_without_clients_world3_gloo():
 
 
 def _worker_bad(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_group("gloo", rank, world, port)
     try:
         from fedjax_amd import distributed as fd
         tmpl = {"w": torch.zeros(3, 2), "b": torch.zeros(2)}
@@ -170,7 +155,8 @@ def test_sharded_tree_mean_local_failure_raises_on_every_rank_gloo():
     every rank raises (that rank its own error, the others a ValueError naming it)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = HeldStore(2)
+    port = store.port
     procs = [ctx.Process(target=_worker_bad, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -189,7 +175,8 @@ def test_sharded_mean_1_to_8_ranks_gloo(world, coracle):
     is bitwise the single fold; G ranks stay within the G-partial bound of DESIGN.md §4."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = HeldStore(world)
+    port = store.port
     procs = [ctx.Process(target=_worker, args=(r, world, port, True, 2, q)) for r in range(world)]
     for p in procs:
         p.start()

@@ -3,8 +3,6 @@
 Both ranks share the box's single GPU, so the exchange uses gloo (RCCL refuses
 two ranks on one device); the RCCL path itself runs in bench.py --gpus N.
 """
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -13,24 +11,15 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import tree_util_ref as ref
+from tests.rendezvous import HeldStore, init_group, init_world1  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 K, P = 48, 70001
 P2 = (1 << 20) + 3  # host-weight runs: buckets too wide for the narrow kernel (which takes device weights)
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _worker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_group("gloo", rank, world, port)
     try:
         import fedjax_amd
         from fedjax_amd import distributed as fd, kernels
@@ -61,7 +50,8 @@ def _worker(rank, world, port, q):
 def test_sharded_mean_world2_on_gpu(cuda, coracle):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _port()
+    store = HeldStore(2)
+    port = store.port
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -91,11 +81,9 @@ def test_sharded_mean_world2_on_gpu(cuda, coracle):
 
 def _native_worker(port, q):
     """World-1 RCCL communicator: the native fold+reduce pipeline of include/fjcomm.h."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    init_world1("nccl", device_id=dev)
     try:
         from fedjax_amd import distributed as fd, kernels
         weights = [int(v) for v in ref.fedavg_weights(K, seed=3)]
@@ -154,7 +142,7 @@ def _native_worker(port, q):
 def test_native_rccl_pipeline_world1(cuda, coracle):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_native_worker, args=(_port(), q))
+    p = ctx.Process(target=_native_worker, args=(None, q))
     p.start()
     res, yb, y0, errs = q.get(timeout=300)
     p.join(timeout=60)

@@ -14,8 +14,6 @@ columns: the synthetic deltas are a counter hash of (client, column), so the hos
 regenerates exactly the columns it checks. Float32 is bitwise; bf16 is within the
 DESIGN.md §4 bound against the f64 oracle.
 """
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -23,6 +21,7 @@ import torch
 
 from fedjax_amd import kernels, pytree, tree_util as tu
 from oracle import tree_util_ref as ref
+from tests.rendezvous import HeldStore, init_group, init_world1  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 U = 2.0 ** -24
@@ -108,21 +107,11 @@ def test_configs2_tree_mean_1024_separate_tensors(cuda):
     _free()
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _configs3_rank0_worker(port, q):
     import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    init_world1("nccl", device_id=dev)
     try:
         from fedjax_amd import distributed as fd
         K, P, N = 1024, 4 * 1024 * 1024, 8
@@ -155,7 +144,7 @@ def test_configs3_rank0_share_native_pipeline(cuda):
     _free()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_configs3_rank0_worker, args=(_port(), q))
+    p = ctx.Process(target=_configs3_rank0_worker, args=(None, q))
     p.start()
     k0, k1, W, cols, outs = q.get(timeout=300)
     p.join(timeout=60)
@@ -182,11 +171,9 @@ def _configs4_rank0_worker(port, q):
     """configs[4], rank 0 of 8: the step bench.py --workload c5 times per rank (bench.py
     step(): sharded_weighted_mean -> f32 partial, then the bf16 cast of the mean)."""
     import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    init_world1("nccl", device_id=dev)
     try:
         from fedjax_amd import distributed as fd
         K, P, N = 8192, 125_000_000, 8
@@ -234,7 +221,7 @@ def test_configs4_rank0_share_native_pipeline(cuda):
     _free()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_configs4_rank0_worker, args=(_port(), q))
+    p = ctx.Process(target=_configs4_rank0_worker, args=(None, q))
     p.start()
     status, payload = q.get(timeout=600)
     p.join(timeout=120)

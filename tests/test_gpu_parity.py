@@ -458,16 +458,27 @@ def synth_cols(K, cols, seed, amp=0.01):
     return np.float32(amp) * u
 
 
+@pytest.mark.parametrize("weights", ["device", "kernel_args"])
 @pytest.mark.parametrize("K,P", [(128, 1206590), (1024, 4 * 1024 * 1024), (40, 700001), (128, 524288)])
-def test_full_size_configs(K, P, cuda):
+def test_full_size_configs(K, P, weights, cuda):
     """BASELINE configs 2 and 3 at full size: sampled columns bitwise vs the oracle,
-    weight-scaling invariance (2w gives the identical bits) over every element."""
+    weight-scaling invariance (2w gives the identical bits) over every element.
+
+    ``kernel_args``: host weights, which travel in the launch's kernel arguments
+    (FJAGG_HOST_TABLES, the k_dense<..., WK=1024> instance bench.py times at configs[2]);
+    the test asserts that the launch took that route rather than an upload."""
     x = torch.empty(K, P, dtype=torch.float32, device=cuda)
     kernels.fill_synth(x, seed=0)
     wi = [int(v) for v in ref.fedavg_weights(K)]
     r = ref.mean_scale(wi)
-    w = torch.tensor(np.float32(wi), device=cuda)
-    y = kernels.weighted_sum_dense(x, w, scale=float(r), nontemporal=True)
+    if weights == "device":
+        w = torch.tensor(np.float32(wi), device=cuda)
+        y = kernels.weighted_sum_dense(x, w, scale=float(r), nontemporal=True)
+    else:
+        before = dict(kernels.HOST_WEIGHT_PATHS)
+        y = kernels.weighted_sum_dense(x, np.float32(wi), scale=float(r), nontemporal=True)
+        assert kernels.HOST_WEIGHT_PATHS["kernel_args"] == before["kernel_args"] + 1
+        assert kernels.HOST_WEIGHT_PATHS["uploaded"] == before["uploaded"]
     rs = np.random.RandomState(0)
     cols = np.unique(np.concatenate([rs.randint(0, P, 2000), [0, 1, 2, 3, P - 4, P - 3, P - 2, P - 1]]))
     xs = synth_cols(K, cols, 0)
