@@ -957,7 +957,7 @@ def main():
         phase(rank, "e2e: host-resident deltas (pinned H2D + fold [+ reduce] + D2H)")
         ns = Kl if (sharded or args.e2e) else min(Kl, E2E_SAMPLE_CLIENTS)
         e2e = host_resident_rate(x[:ns], w_local, step if sharded else None, out, scale, nt, dev, rank, sharded,
-                                 K * P * esize if nshard == world else ns * P * esize)
+                                 K * P * esize if (sharded and nshard == world) else ns * P * esize)
         if not sharded:
             e2e["e2e_sample"] = (f"the first {ns} of the {Kl} clients ({ns * P * esize / 1e9:.2f} GB)"
                                  if ns < Kl else f"all {Kl} clients ({ns * P * esize / 1e9:.2f} GB)")

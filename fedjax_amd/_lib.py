@@ -213,23 +213,53 @@ def load() -> ctypes.CDLL:
 
 HOST_PATH = os.path.join(_HERE, "_build", "_fjhost.so")
 _host = None
+_REBUILD = "rebuild it with `python -c 'import __graft_entry__ as g; g.build()'` from the repo root"
+
+
+def torch_stamp() -> str:
+    """The torch build _fjhost.so must be compiled against: version, git revision, HIP
+    version and C++ ABI flag (fjhost.cpp uses torch's TensorImpl / THPVariable layout)."""
+    import sys
+
+    ver = getattr(torch, "version", None)
+    return (f"torch {torch.__version__} git {getattr(ver, 'git_version', '?')} hip {getattr(ver, 'hip', None)} "
+            f"cxx11abi {int(torch._C._GLIBCXX_USE_CXX11_ABI)} py {sys.version_info[0]}.{sys.version_info[1]}")
+
+
+def host_stamp_path(path: str = None) -> str:
+    """The stamp file build() writes beside _fjhost.so (read before the library is loaded)."""
+    return (path or HOST_PATH) + ".torch"
 
 
 def host():
     """The native host helper ``_fjhost`` (fedjax_amd/csrc/fjhost.cpp: pytree walk and
-    pointer table, weight packing; no device work). Raises FjaggError if missing."""
+    pointer table, weight packing; no device work). Raises FjaggError if it is missing or
+    was built against another torch: its stamp file (checked before the library is loaded,
+    since a mismatched build can fail inside dlopen or misread torch's objects) and the
+    TORCH_STAMP compiled into it must both equal :func:`torch_stamp`."""
     global _host
     if _host is None:
         import importlib.machinery
         import importlib.util
 
         if not os.path.exists(HOST_PATH):
-            raise FjaggError(f"{HOST_PATH} is missing: build it with "
-                             "`python -c 'import __graft_entry__ as g; g.build()'` from the repo root")
+            raise FjaggError(f"{HOST_PATH} is missing: {_REBUILD}")
+        want = torch_stamp()
+        try:
+            with open(host_stamp_path()) as f:
+                built = f.read().strip()
+        except OSError:
+            built = None
+        if built != want:
+            raise FjaggError(f"{HOST_PATH} was built against [{built or 'no stamp file'}], this process runs "
+                             f"[{want}]: {_REBUILD}")
         loader = importlib.machinery.ExtensionFileLoader("_fjhost", HOST_PATH)
         spec = importlib.util.spec_from_file_location("_fjhost", HOST_PATH, loader=loader)
         mod = importlib.util.module_from_spec(spec)
         loader.exec_module(mod)
+        if getattr(mod, "TORCH_STAMP", None) != want:
+            raise FjaggError(f"{HOST_PATH} was compiled against [{getattr(mod, 'TORCH_STAMP', None)}], this "
+                             f"process runs [{want}] (its stamp file says otherwise): {_REBUILD}")
         _host = mod
     return _host
 

@@ -46,7 +46,10 @@ class MeanAggregatorState:
 
 
 def mean_aggregator() -> Aggregator:
-    """Builds (weighted) mean aggregator."""
+    """Builds (weighted) mean aggregator.
+
+    ``apply`` returns ``tree_util.tree_mean``'s result: its float32 leaves may be slices of
+    one allocation (see tree_mean), so one kept leaf holds the whole mean's memory."""
 
     def init():
         return MeanAggregatorState()

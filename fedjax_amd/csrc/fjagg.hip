@@ -444,9 +444,12 @@ __global__ __launch_bounds__(kThreads) void k_dense_l2(
 }
 
 // out[k] = sum over b of ws[b*K + k]. Workgroup = 64 clients x 16 waves: wave w sums
-// partials b = w, w+16, ... (coalesced 256-B rows, 4 loads in flight), then the 16
-// wave sums are added in wave order: deterministic, latency cost ~nb/64 loads.
-constexpr int kCombineWaves = 16;
+// partials b = w, w+16, ... in that order (coalesced 256-B rows), then the 16 wave sums
+// are added in wave order: deterministic. The kernel runs after the fold, on a few
+// workgroups, so it is latency-bound: each lane issues a batch of 16 loads before it adds
+// any (one memory round trip per 256 partials per client; the fold's ~256 workgroups are
+// one batch).
+constexpr int kCombineWaves = 16, kCombineBatch = 16;
 __global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* __restrict__ ws,
                                                                    int64_t nb, int64_t K,
                                                                    float* __restrict__ out) {
@@ -455,13 +458,17 @@ __global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* 
   const int64_t k = (int64_t)blockIdx.x * 64 + lane;
   float s = 0.f;
   if (k < K) {
-    int64_t b = wv;
-    for (; b + 3 * kCombineWaves < nb; b += 4 * kCombineWaves) {
-      const float a0 = ws[b * K + k], a1 = ws[(b + kCombineWaves) * K + k];
-      const float a2 = ws[(b + 2 * kCombineWaves) * K + k], a3 = ws[(b + 3 * kCombineWaves) * K + k];
-      s = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(s, a0), a1), a2), a3);
+    for (int64_t b0 = wv; b0 < nb; b0 += (int64_t)kCombineWaves * kCombineBatch) {
+      float a[kCombineBatch];
+#pragma unroll
+      for (int i = 0; i < kCombineBatch; ++i) {
+        const int64_t b = b0 + (int64_t)i * kCombineWaves;
+        a[i] = b < nb ? ws[b * K + k] : 0.f;
+      }
+      // partials are sums of squares (>= +0), so adding the +0 of an absent one keeps s
+#pragma unroll
+      for (int i = 0; i < kCombineBatch; ++i) s = __fadd_rn(s, a[i]);
     }
-    for (; b < nb; b += kCombineWaves) s = __fadd_rn(s, ws[b * K + k]);
   }
   part[wv][lane] = s;
   __syncthreads();

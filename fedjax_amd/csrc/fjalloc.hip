@@ -11,9 +11,10 @@
 // 0 are the VMM designs that were measured and kept for comparison, see g_mode). It is plugged
 // in per scope through torch.cuda.MemPool(CUDAPluggableAllocator(libfjagg.so, "fjalloc_alloc",
 // "fjalloc_free")) (fedjax_amd.memory.delta_pool); the caching allocator still splits and
-// caches blocks inside the segments. A chunk goes back to the runtime when its last slice is
-// freed (torch frees a pool's segments when the pool is released). Nothing else in the library
-// uses it.
+// caches blocks inside the segments. A freed slice's range is coalesced with free neighbours
+// and reused best-fit for any later segment that fits (or returned to the chunk's bump tail); a
+// chunk goes back to the runtime when its last slice is freed (torch frees a pool's segments
+// when the pool is released). Nothing else in the library uses it.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -21,6 +22,7 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -33,6 +35,7 @@ struct Segment {
   hipMemGenericAllocationHandle_t handle;
   bool own_reservation;
   bool chunk_slice;  // mode 2: a slice of a chunk (freed by chunk_free whatever g_mode is then)
+  size_t pad = 0;    // mode 2: stagger bytes in front of the slice, owned by it (freed with it)
 };
 
 struct Chunk {  // mode 2
@@ -47,10 +50,13 @@ struct Arena {
   size_t reserved = 0;
   size_t top = 0;   // bump offset
   size_t gran = 0;  // mapping granularity
-  std::multimap<size_t, char*> free_ranges;  // unmapped ranges by size, reused for equal sizes
+  std::multimap<size_t, char*> free_ranges;  // modes 0, 1: unmapped ranges by size, reused for equal sizes
   std::unordered_map<uintptr_t, Segment> live;
-  std::vector<Chunk> chunks;  // mode 2: a freed slice is reused for a segment of its size; an
-                              // empty chunk is returned to the runtime
+  std::vector<Chunk> chunks;  // mode 2; an empty chunk is returned to the runtime
+  // mode 2: free ranges inside the chunks by address (start -> bytes), coalesced with their
+  // free neighbours in the same chunk; a range that reaches its chunk's bump offset is
+  // given back to the bump tail instead
+  std::map<char*, size_t> chunk_free_ranges;
   int64_t mapped_bytes = 0, segments = 0, reuses = 0, failures = 0;
   int64_t last_error = 0;  // (step << 16) | hipError_t of the last failed request
   int64_t hinted = 0, hint_missed = 0;  // mode 1: reservations placed at / away from the hint
@@ -82,6 +88,9 @@ size_t g_chunk_bytes = size_t(1) << 30;
 // not all share their address residue modulo 2 MiB: rows with equal residues contend for the
 // same L2 tags (one allocation with 2 MiB-aligned rows, 91.7 vs 87.6 us).
 size_t g_stagger = size_t(68) << 10;
+// The layout globals above are written by fjalloc_configure under an exclusive lock and read
+// by fjalloc_alloc under a shared one, so no allocation sees a half-applied configuration.
+std::shared_mutex g_config_mu;
 
 hipMemAllocationProp prop_for(int device) {
   hipMemAllocationProp p{};
@@ -116,18 +125,41 @@ Chunk* chunk_of(Arena& a, const char* p) {
   return nullptr;
 }
 
-// mode 2: slice p of `size` bytes is free again. Its range is kept for a later segment of the
-// same size; when it was its chunk's last live slice, the chunk (and the free ranges in it)
-// goes back to the runtime.
-void chunk_free(Arena& a, int device, char* p, size_t size) {
+// mode 2: the range [p, p + size) of chunk c is free again: merged with free neighbours of the
+// same chunk, and returned to the bump tail when it reaches the chunk's bump offset.
+void chunk_release_range(Arena& a, Chunk& c, char* p, size_t size) {
+  auto next = a.chunk_free_ranges.lower_bound(p);
+  if (next != a.chunk_free_ranges.end() && next->first == p + size && next->first < c.base + c.size) {
+    size += next->second;
+    next = a.chunk_free_ranges.erase(next);
+  }
+  if (next != a.chunk_free_ranges.begin()) {
+    auto prev = std::prev(next);
+    if (prev->first >= c.base && prev->first + prev->second == p) {
+      p = prev->first;
+      size += prev->second;
+      a.chunk_free_ranges.erase(prev);
+    }
+  }
+  if (p + size == c.base + c.top) {
+    c.top = static_cast<size_t>(p - c.base);
+  } else {
+    a.chunk_free_ranges.emplace(p, size);
+  }
+}
+
+// mode 2: slice p of `size` bytes (and its `pad` stagger bytes in front) is free again: its
+// range goes back to the chunk (chunk_release_range); when it was the chunk's last live slice,
+// the chunk (and the free ranges in it) goes back to the runtime.
+void chunk_free(Arena& a, int device, char* p, size_t size, size_t pad) {
   Chunk* c = chunk_of(a, p);
   if (!c) return;
   if (--c->live > 0) {
-    a.free_ranges.emplace(size, p);
+    chunk_release_range(a, *c, p - pad, size + pad);
     return;
   }
-  for (auto it = a.free_ranges.begin(); it != a.free_ranges.end();)
-    it = (it->second >= c->base && it->second < c->base + c->size) ? a.free_ranges.erase(it) : std::next(it);
+  for (auto it = a.chunk_free_ranges.begin(); it != a.chunk_free_ranges.end();)
+    it = (it->first >= c->base && it->first < c->base + c->size) ? a.chunk_free_ranges.erase(it) : std::next(it);
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(device);
@@ -137,15 +169,24 @@ void chunk_free(Arena& a, int device, char* p, size_t size) {
   a.base = a.chunks.empty() ? nullptr : a.chunks[0].base;
 }
 
+// mode 2: a slice of >= size bytes: the best-fitting free range of any chunk (split, the rest
+// stays free), else the bump tail of a chunk with room (staggered), else a new chunk — so a
+// request that fits in freed space never needs a new hipMalloc (torch's out-of-memory retry
+// frees its cached segments and asks again).
 void* chunk_alloc(Arena& a, int device, size_t size) {
   a.gran = g_align;
   const size_t sz = (size + a.gran - 1) / a.gran * a.gran;
-  const size_t pad = (static_cast<size_t>(a.segments) % 31) * g_stagger;
+  size_t pad = (static_cast<size_t>(a.segments) % 31) * g_stagger;
   char* va = nullptr;
-  auto it = a.free_ranges.find(sz);
-  if (it != a.free_ranges.end()) {
-    va = it->second;
-    a.free_ranges.erase(it);
+  auto best = a.chunk_free_ranges.end();
+  for (auto it = a.chunk_free_ranges.begin(); it != a.chunk_free_ranges.end(); ++it)
+    if (it->second >= sz && (best == a.chunk_free_ranges.end() || it->second < best->second)) best = it;
+  if (best != a.chunk_free_ranges.end()) {
+    va = best->first;
+    const size_t rest = best->second - sz;
+    a.chunk_free_ranges.erase(best);
+    if (rest > 0) a.chunk_free_ranges.emplace(va + sz, rest);
+    pad = 0;
     ++a.reuses;
     if (Chunk* c = chunk_of(a, va)) ++c->live;
   } else {
@@ -168,9 +209,10 @@ void* chunk_alloc(Arena& a, int device, size_t size) {
       a.chunks.push_back(Chunk{static_cast<char*>(p), csz, sz, 1});
       if (a.chunks.size() == 1) a.base = static_cast<char*>(p);
       va = static_cast<char*>(p);
+      pad = 0;
     }
   }
-  a.live[reinterpret_cast<uintptr_t>(va)] = Segment{sz, hipMemGenericAllocationHandle_t{}, false, true};
+  a.live[reinterpret_cast<uintptr_t>(va)] = Segment{sz, hipMemGenericAllocationHandle_t{}, false, true, pad};
   a.mapped_bytes += static_cast<int64_t>(sz);
   ++a.segments;
   return va;
@@ -183,6 +225,7 @@ extern "C" {
 void* fjalloc_alloc(ssize_t size, int device, void* /*stream*/) {
   if (size <= 0 || device < 0 || device >= kMaxDevices) return nullptr;
   Arena& a = g_arena[device];
+  std::shared_lock<std::shared_mutex> config(g_config_mu);
   std::lock_guard<std::mutex> lock(a.mu);
   if (g_mode == 2) return chunk_alloc(a, device, static_cast<size_t>(size));
   if (g_mode == 0) {
@@ -258,7 +301,7 @@ void fjalloc_free(void* ptr, size_t /*size*/, int device, void* stream) {
   a.live.erase(it);
   a.mapped_bytes -= static_cast<int64_t>(s.size);
   if (s.chunk_slice) {
-    chunk_free(a, device, static_cast<char*>(ptr), s.size);
+    chunk_free(a, device, static_cast<char*>(ptr), s.size, s.pad);
     return;
   }
   (void)hipMemUnmap(ptr, s.size);
@@ -281,12 +324,17 @@ int fjalloc_stats(int device, int64_t* out) {
   out[8] = a.last_error;
   out[9] = a.hinted;
   out[10] = a.hint_missed;
+  out[11] = static_cast<int64_t>(a.chunks.size());
+  int64_t fr = 0;
+  for (const auto& r : a.chunk_free_ranges) fr += static_cast<int64_t>(r.second);
+  out[12] = fr;
   return 0;
 }
 
 int fjalloc_configure(int64_t reserve_bytes, int64_t align_bytes, int mode, int64_t stagger_bytes) {
   if (reserve_bytes <= 0 || align_bytes <= 0 || mode < 0 || mode > 2 || stagger_bytes < 0 || stagger_bytes % 256)
     return -1;
+  std::unique_lock<std::shared_mutex> config(g_config_mu);  // no allocation runs meanwhile
   for (Arena& a : g_arena) {  // the layout is fixed once any device has a segment
     std::lock_guard<std::mutex> lock(a.mu);
     if (a.segments > 0) return -1;

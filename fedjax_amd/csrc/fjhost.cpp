@@ -384,6 +384,8 @@ constexpr int kF32 = 0, kScale = 1, kAccumulate = 2, kNontemporal = 4;  // fjagg
 // Fresh output leaves shaped like row0: ONE allocation, each leaf its own tensor (own
 // TensorImpl and version counter) over a 256-byte aligned slice — one allocator call instead
 // of one per leaf on the path to the first launch. A single leaf is a plain allocation.
+// The leaves share that storage: one live leaf keeps the whole result's bytes allocated, and
+// torch.save of one leaf writes them all (tree_mean's and mean_aggregator's docstrings say so).
 void carve_outputs(const std::vector<at::Tensor>& row0, std::vector<at::Tensor>& outs) {
   const size_t L = row0.size();
   if (L == 1) {
@@ -392,7 +394,8 @@ void carve_outputs(const std::vector<at::Tensor>& row0, std::vector<at::Tensor>&
   }
   thread_local std::vector<int64_t> offs;
   offs.assign(L + 1, 0);
-  for (size_t l = 0; l < L; ++l) offs[l + 1] = offs[l] + (row0[l].numel() + 63) / 64 * 64;
+  const int64_t q = std::max<int64_t>(1, 256 / static_cast<int64_t>(row0[0].element_size()));  // 256 B in elements
+  for (size_t l = 0; l < L; ++l) offs[l + 1] = offs[l] + (row0[l].numel() + q - 1) / q * q;
   at::Tensor flat = at::empty({std::max<int64_t>(offs[L], 1)}, row0[0].options());
   for (size_t l = 0; l < L; ++l) {
     at::Tensor t = at::detail::make_tensor<c10::TensorImpl>(c10::Storage(flat.storage()), flat.key_set(),
@@ -614,6 +617,8 @@ struct PWalk {
   std::vector<PyObject*> leaves[FJTREE_MAX_OPERANDS];  // borrowed, flatten order
   std::vector<PyObject*> keys;                         // owned sorted key lists, pre-order
   std::vector<int64_t>* sig = nullptr;  // optional: operand 0's structure (kinds, lengths, key objects)
+  std::vector<PyObject*>* dicts = nullptr;  // optional: operand 0's dict nodes, pre-order (borrowed)
+  bool seq_nodes = false;                   // operand 0 has a list / tuple node
   ~PWalk() {
     for (PyObject* k : keys) Py_DECREF(k);
   }
@@ -710,6 +715,7 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
     PyObject* keys = sorted_keys(x0, &unorderable);
     if (!keys) return unorderable ? 1 : -1;  // unorderable keys: the Python path decides
     w.keys.push_back(keys);
+    if (w.dicts) w.dicts->push_back(x0);
     if (w.sig) {
       w.sig->push_back(kDict);
       w.sig->push_back(n);
@@ -730,6 +736,7 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
   }
   const bool is_list = PyList_CheckExact(x0), is_tuple = PyTuple_CheckExact(x0);
   if (!is_list && !is_tuple) return 1;
+  w.seq_nodes = true;
   const Py_ssize_t n = Py_SIZE(x0);
   for (int k = 1; k < K; ++k)
     if (Py_TYPE(xs[k]) != Py_TYPE(x0) || Py_SIZE(xs[k]) != n) return 1;
@@ -898,14 +905,61 @@ inline int64_t captured_ptr(PyObject* cap, Py_ssize_t l) {
   return reinterpret_cast<const int64_t*>(PyBytes_AS_STRING(b))[l];
 }
 
+// Capture element 5: the tree's dict nodes in pre-order as int64 pairs (address, CPython
+// dict version tag), bytes — or None when the tree is not dicts over leaves (a list / tuple
+// node, or a leaf at the root). A dict's version tag (PEP 509) changes with every mutation
+// and is never reused, so while the root is the same object and every tag is unchanged,
+// walking the tree again would give the captured leaves: tree_l2_norm of the delta just
+// added checks that instead of re-walking (same_tree). Visiting in pre-order means a dict is
+// dereferenced only after its parent — which still holds it — was found unchanged.
+PyObject* dict_tags(const PWalk& w, PyObject* root) {
+#if PY_VERSION_HEX < 0x030C0000
+  if (!w.dicts || w.seq_nodes || w.dicts->empty() || (*w.dicts)[0] != root) Py_RETURN_NONE;
+  const size_t n = w.dicts->size();
+  PyObject* b = PyBytes_FromStringAndSize(nullptr, static_cast<Py_ssize_t>(16 * n));
+  if (!b) return nullptr;
+  auto* p = reinterpret_cast<int64_t*>(PyBytes_AS_STRING(b));
+  for (size_t i = 0; i < n; ++i) {
+    PyObject* d = (*w.dicts)[i];
+    p[2 * i] = reinterpret_cast<int64_t>(d);
+    p[2 * i + 1] = static_cast<int64_t>(reinterpret_cast<PyDictObject*>(d)->ma_version_tag);
+  }
+  return b;
+#else
+  (void)w, (void)root;
+  Py_RETURN_NONE;
+#endif
+}
+
+// tree is the captured tree, unchanged (capture element 5): true, or false = not known.
+bool same_tree(PyObject* tree, PyObject* cap) {
+#if PY_VERSION_HEX < 0x030C0000
+  if (PyTuple_GET_SIZE(cap) < 6) return false;
+  PyObject* b = PyTuple_GET_ITEM(cap, 5);
+  if (!PyBytes_CheckExact(b) || PyBytes_GET_SIZE(b) < 16) return false;
+  const auto* p = reinterpret_cast<const int64_t*>(PyBytes_AS_STRING(b));
+  const Py_ssize_t n = PyBytes_GET_SIZE(b) / 16;
+  if (p[0] != reinterpret_cast<int64_t>(tree) || !PyDict_CheckExact(tree)) return false;
+  for (Py_ssize_t i = 0; i < n; ++i)
+    if (static_cast<int64_t>(reinterpret_cast<PyDictObject*>(p[2 * i])->ma_version_tag) != p[2 * i + 1]) return false;
+  return true;
+#else
+  (void)tree, (void)cap;
+  return false;
+#endif
+}
+
 // New reference: the capture tuple, Py_None (not the fast case), or nullptr (Python error).
 PyObject* capture_impl(PyObject* tree, int dev) {
   try {
     thread_local std::vector<int64_t> sig;
+    thread_local std::vector<PyObject*> dicts;
     sig.clear();
+    dicts.clear();
     PWalk w;
     w.K = 1;
     w.sig = &sig;
+    w.dicts = &dicts;
     w.leaves[0].reserve(16);
     int rc = pwalk(&tree, w, 0);
     if (rc < 0) return nullptr;
@@ -933,13 +987,14 @@ PyObject* capture_impl(PyObject* tree, int dev) {
       for (int64_t s : t.sizes()) sig.push_back(s);
     }
     const int64_t tok = structure_token(sig, w);
-    PyObject* out = PyTuple_New(5);
+    PyObject* out = PyTuple_New(6);
     PyObject* a = PyLong_FromLongLong(vs);
     PyObject* b = PyLong_FromLongLong(nbytes);
     PyObject* c = PyLong_FromLongLong(tok);
     PyObject* d = ptr_bytes(w.leaves[0].data(), L);
-    if (!out || !a || !b || !c || !d) {
-      Py_XDECREF(out), Py_XDECREF(a), Py_XDECREF(b), Py_XDECREF(c), Py_XDECREF(d), Py_DECREF(tup);
+    PyObject* e = dict_tags(w, tree);
+    if (!out || !a || !b || !c || !d || !e) {
+      Py_XDECREF(out), Py_XDECREF(a), Py_XDECREF(b), Py_XDECREF(c), Py_XDECREF(d), Py_XDECREF(e), Py_DECREF(tup);
       return nullptr;
     }
     PyTuple_SET_ITEM(out, 0, tup);
@@ -947,6 +1002,7 @@ PyObject* capture_impl(PyObject* tree, int dev) {
     PyTuple_SET_ITEM(out, 2, b);
     PyTuple_SET_ITEM(out, 3, c);
     PyTuple_SET_ITEM(out, 4, d);
+    PyTuple_SET_ITEM(out, 5, e);
     return out;
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
@@ -1682,6 +1738,16 @@ PyObject* mean_config(PyObject*, PyObject* args) {
   Py_RETURN_NONE;
 }
 
+// busy_until([t]) -> t: the time (time.perf_counter() seconds) before which the folds this
+// process issued cannot have finished, at peak bandwidth — ONE estimate for the builtin
+// tree_mean and tree_util's Python paths (tree_util._BUSY_UNTIL reads and writes it here).
+PyObject* busy_until(PyObject*, PyObject* args) {
+  double t = -1.0;
+  if (!PyArg_ParseTuple(args, "|d", &t)) return nullptr;
+  if (t >= 0.0) g_mean.busy_until = t;
+  return PyFloat_FromDouble(g_mean.busy_until);
+}
+
 PyObject* mean_fast(PyObject* arg, bool triples) {
   const double now = now_s();
   PyObject* got = mean_pairs_impl(arg, triples, g_mean.frac > 0.0 && now >= g_mean.busy_until, g_mean.frac,
@@ -1925,6 +1991,7 @@ struct ChainObject {
   PyObject* tip;
   PyObject* buf;
   PyObject* budget;
+  PyObject* views;  // list: pre-made (norm view, ticket) pairs of buf's row 1 by link index, or NULL
 };
 
 struct PSObject {
@@ -1950,6 +2017,7 @@ PyMemberDef kWTMembers[] = {FJ_OBJ_MEMBER(WTObject, tree), FJ_OBJ_MEMBER(WTObjec
 PyMemberDef kChainMembers[] = {{const_cast<char*>("tip"), T_OBJECT, offsetof(ChainObject, tip), 0, nullptr},
                                {const_cast<char*>("buf"), T_OBJECT, offsetof(ChainObject, buf), 0, nullptr},
                                {const_cast<char*>("budget"), T_OBJECT, offsetof(ChainObject, budget), 0, nullptr},
+                               {const_cast<char*>("views"), T_OBJECT, offsetof(ChainObject, views), 0, nullptr},
                                {nullptr}};
 PyMemberDef kPSMembers[] = {FJ_OBJ_MEMBER(PSObject, root),   FJ_OBJ_MEMBER(PSObject, parent),
                             FJ_OBJ_MEMBER(PSObject, cap),    FJ_OBJ_MEMBER(PSObject, weight),
@@ -1993,6 +2061,7 @@ int chain_traverse(PyObject* o, visitproc visit, void* arg) {
   Py_VISIT(x->tip);
   Py_VISIT(x->buf);
   Py_VISIT(x->budget);
+  Py_VISIT(x->views);
   return 0;
 }
 int chain_clear(PyObject* o) {
@@ -2000,6 +2069,7 @@ int chain_clear(PyObject* o) {
   Py_CLEAR(x->tip);
   Py_CLEAR(x->buf);
   Py_CLEAR(x->budget);
+  Py_CLEAR(x->views);
   return 0;
 }
 void chain_dealloc(PyObject* o) {
@@ -2086,6 +2156,15 @@ struct FastState {
   bool defer = true;
   long long max_clients = 4095, flush_bytes = 256LL << 20, flush_clients = 64;  // (set by fast_config)
   PyObject* last = nullptr;  // weak reference to the most recent PendingSum link
+  // Lazy-norm pool: a norm buffer [2, max_clients + 1] and a list of pre-made (view of
+  // buf[1, i], ticket) pairs for i < the norms the last round asked for. Creating a 0-d
+  // tensor subclass object costs ~0.3 us of host time, on the critical path of the library
+  // loop (one tree_l2_norm per client, fed_avg.py:142-144); the pool is built right after a
+  // round's final fold is launched (fold_chain with the 1/W scale), while the GPU folds, and
+  // the next chain that takes a norm takes the pool as its buffer (fast_l2).
+  PyObject* pool_buf = nullptr;
+  PyObject* pool_views = nullptr;
+  long long pool_want = 0;  // norms (row 1) the current round's chains asked for: the next pool's size
 };
 FastState g_fast;
 
@@ -2317,12 +2396,22 @@ PyObject* flush_views(PyObject*, PyObject* arg) {
   Py_RETURN_NONE;
 }
 
+// A new _Ticket naming `node` (tree_util._Ticket, without its Python __init__ frame).
+PyObject* new_ticket(PyObject* node) {
+  static PyObject* node_name = PyUnicode_InternFromString("node");
+  PyObject* t = g_fast.ticket->tp_alloc(g_fast.ticket, 0);
+  if (t && PyObject_SetAttr(t, node_name, node) != 0) Py_CLEAR(t);
+  return t;
+}
+
 // tree_l2_squared / tree_l2_norm (tree_util.py:105-114) of the delta the running sum just
 // took: a lazy 0-d view into its chain's norm buffer, which the chain's fold fills
 // (tree_util._lazy_norm, built here without a Python frame). The tree must hold exactly the
-// captured leaves of the most recent PendingSum link, unmodified, and the chain's buffer must
-// exist (the Python path allocates it for the chain's first norm). Anything else: the Python
-// function.
+// captured leaves of the most recent PendingSum link, unmodified — known without a walk when
+// it is the captured dict tree with every dict version tag unchanged (same_tree) — and the
+// chain must have a norm buffer: its own, or the pool's (FastState), which a chain without
+// one takes for its first norm; the pool's views and tickets are handed out by link index.
+// Anything else: the Python function.
 PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, int which) {
   PyObject* py = g_fast.py_l2[which];
   if (!py) {
@@ -2336,53 +2425,91 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
       auto* node = reinterpret_cast<PSObject*>(no);
       auto* ch = reinterpret_cast<ChainObject*>(node->chain);
       if ((!node->value || node->value == Py_None) && node->cap && PyTuple_CheckExact(node->cap) &&
-          PyTuple_GET_SIZE(node->cap) >= 2 && ch && Py_TYPE(ch) == g_fast.chain && ch->buf &&
-          THPVariable_Check(ch->buf)) {
+          PyTuple_GET_SIZE(node->cap) >= 2 && ch && Py_TYPE(ch) == g_fast.chain) {
         Py_INCREF(no);  // (held for the check: the walk below could run Python code)
         struct Drop {
           PyObject* o;
           ~Drop() { Py_DECREF(o); }
         } drop{no};
         try {
-          PWalk w;
-          w.K = 1;
-          w.leaves[0].reserve(16);
-          PyObject* tree = args[0];
-          const int rc = pwalk(&tree, w, 0);
-          if (rc < 0) return nullptr;
           PyObject* tup = PyTuple_GET_ITEM(node->cap, 0);
-          bool same = rc == 0 && PyTuple_Check(tup) &&
-                      static_cast<Py_ssize_t>(w.leaves[0].size()) == PyTuple_GET_SIZE(tup);
+          bool same = PyTuple_Check(tup) && PyTuple_GET_SIZE(tup) > 0;
+          if (same && !same_tree(args[0], node->cap)) {
+            PWalk w;
+            w.K = 1;
+            w.leaves[0].reserve(16);
+            PyObject* tree = args[0];
+            const int rc = pwalk(&tree, w, 0);
+            if (rc < 0) return nullptr;
+            same = rc == 0 && static_cast<Py_ssize_t>(w.leaves[0].size()) == PyTuple_GET_SIZE(tup);
+            for (size_t l = 0; same && l < w.leaves[0].size(); ++l) same = w.leaves[0][l] == PyTuple_GET_ITEM(tup, l);
+          }
           int64_t vs = 0;
-          for (size_t l = 0; same && l < w.leaves[0].size(); ++l) {
-            same = w.leaves[0][l] == PyTuple_GET_ITEM(tup, l);
-            if (!same) break;
-            const at::Tensor& t = THPVariable_Unpack(w.leaves[0][l]);
+          for (Py_ssize_t l = 0; same && l < PyTuple_GET_SIZE(tup); ++l) {
+            const at::Tensor& t = THPVariable_Unpack(PyTuple_GET_ITEM(tup, l));
             vs += version_of(t);
-            const int64_t cp = captured_ptr(node->cap, static_cast<Py_ssize_t>(l));
+            const int64_t cp = captured_ptr(node->cap, l);
             if (cp && cp != reinterpret_cast<int64_t>(t.data_ptr())) same = false;
           }
           if (same && vs == PyLong_AsLongLong(PyTuple_GET_ITEM(node->cap, 1))) {
-            const at::Tensor& b = THPVariable_Unpack(ch->buf);
-            const int row = which;  // row 0 = squared norms, row 1 = norms
-            if (b.dim() == 2 && node->idx < b.size(1)) {
-              if (!node->ticket || node->ticket == Py_None) {
-                // _Ticket(node) without its Python __init__ frame: allocate, set the slot
-                PyObject* t = g_fast.ticket->tp_alloc(g_fast.ticket, 0);
+            if ((!ch->buf || ch->buf == Py_None) && which == 1 && g_fast.pool_buf && g_fast.pool_views) {
+              // the chain's first norm: take the pool as the chain's buffer and views (same device,
+              // the current chain size)
+              const at::Tensor& pb = THPVariable_Unpack(g_fast.pool_buf);
+              const at::Tensor& t0 = THPVariable_Unpack(PyTuple_GET_ITEM(tup, 0));
+              if (pb.get_device() == t0.get_device() && pb.dim() == 2 && pb.size(1) == g_fast.max_clients + 1) {
+                Py_XSETREF(ch->buf, g_fast.pool_buf);
+                Py_XSETREF(ch->views, g_fast.pool_views);
+                g_fast.pool_buf = g_fast.pool_views = nullptr;
+              }
+            }
+            PyObject* buf = ch->buf;
+            if (buf && THPVariable_Check(buf)) {
+              const at::Tensor& b = THPVariable_Unpack(buf);
+              const int row = which;  // row 0 = squared norms, row 1 = norms
+              if (b.dim() == 2 && node->idx < b.size(1)) {
+                if (which == 1 && node->idx + 1 > g_fast.pool_want) g_fast.pool_want = node->idx + 1;
+                PyObject* pair = nullptr;  // a pool (view, ticket) for this link, if one is left
+                if (which == 1 && (!node->ticket || node->ticket == Py_None) && ch->views &&
+                    PyList_CheckExact(ch->views) && node->idx < PyList_GET_SIZE(ch->views)) {
+                  pair = PyList_GET_ITEM(ch->views, node->idx);
+                  if (pair != Py_None && PyTuple_CheckExact(pair) && PyTuple_GET_SIZE(pair) == 2) {
+                    Py_INCREF(pair);
+                    Py_INCREF(Py_None);
+                    PyList_SET_ITEM(ch->views, node->idx, Py_None);  // handed out once
+                  } else {
+                    pair = nullptr;
+                  }
+                }
                 static PyObject* node_name = PyUnicode_InternFromString("node");
-                if (t && PyObject_SetAttr(t, node_name, no) != 0) Py_CLEAR(t);
-                if (!t) return nullptr;
-                Py_XSETREF(node->ticket, t);
+                static PyObject* name = PyUnicode_InternFromString("_ticket");
+                if (pair) {
+                  struct DropPair {
+                    PyObject* o;
+                    ~DropPair() { Py_DECREF(o); }
+                  } drop_pair{pair};
+                  PyObject* v = PyTuple_GET_ITEM(pair, 0);
+                  PyObject* t = PyTuple_GET_ITEM(pair, 1);
+                  if (PyObject_SetAttr(t, node_name, no) != 0) return nullptr;
+                  Py_INCREF(t);
+                  Py_XSETREF(node->ticket, t);
+                  Py_INCREF(v);
+                  return v;  // (its _ticket was set to t when the pool was built)
+                }
+                if (!node->ticket || node->ticket == Py_None) {
+                  PyObject* t = new_ticket(no);
+                  if (!t) return nullptr;
+                  Py_XSETREF(node->ticket, t);
+                }
+                PyObject* v = THPVariable_Wrap(
+                    scalar_at(b, b.storage_offset() + row * b.stride(0) + node->idx * b.stride(1)), g_fast.norm_view);
+                if (!v) return nullptr;
+                if (PyObject_SetAttr(v, name, node->ticket) != 0) {
+                  Py_DECREF(v);
+                  return nullptr;
+                }
+                return v;
               }
-              PyObject* v = THPVariable_Wrap(
-                  scalar_at(b, b.storage_offset() + row * b.stride(0) + node->idx * b.stride(1)), g_fast.norm_view);
-              if (!v) return nullptr;
-              static PyObject* name = PyUnicode_InternFromString("_ticket");
-              if (PyObject_SetAttr(v, name, node->ticket) != 0) {
-                Py_DECREF(v);
-                return nullptr;
-              }
-              return v;
             }
           }
         } catch (const std::exception& e) {
@@ -2393,6 +2520,63 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
     }
   }
   return PyObject_Vectorcall(py, args, nargs, kwnames);
+}
+
+// Builds the lazy-norm pool (FastState) for the next round: a fresh norm buffer on device dev
+// and g_fast.pool_want (view of buf[1, i], ticket) pairs, each view's _ticket set to its
+// ticket (ticket.node None until fast_l2 hands the pair out). 0, or -1 with a Python error.
+int refill_pool(c10::DeviceIndex dev) {
+  const long long m = std::min<long long>(g_fast.pool_want, g_fast.max_clients + 1);
+  g_fast.pool_want = 0;
+  if (m <= 0 || !g_fast.norm_view || !g_fast.ticket) return 0;
+  if (g_fast.pool_buf) {  // an unused pool: kept if a chain on this device could still take it
+    const at::Tensor& pb = THPVariable_Unpack(g_fast.pool_buf);
+    if (pb.get_device() == dev && pb.size(1) == g_fast.max_clients + 1 && g_fast.pool_views &&
+        PyList_GET_SIZE(g_fast.pool_views) >= m)
+      return 0;
+    Py_CLEAR(g_fast.pool_buf);
+    Py_CLEAR(g_fast.pool_views);
+  }
+  static PyObject* name = PyUnicode_InternFromString("_ticket");
+  at::Tensor b = at::empty({2, g_fast.max_clients + 1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
+  PyObject* views = PyList_New(m);
+  if (!views) return -1;
+  for (long long i = 0; i < m; ++i) {
+    PyObject* v = THPVariable_Wrap(scalar_at(b, b.size(1) + i), g_fast.norm_view);
+    PyObject* t = v ? new_ticket(Py_None) : nullptr;
+    if (!t || PyObject_SetAttr(v, name, t) != 0) {
+      Py_XDECREF(v), Py_XDECREF(t), Py_DECREF(views);
+      return -1;
+    }
+    PyObject* pair = PyTuple_Pack(2, v, t);
+    Py_DECREF(v), Py_DECREF(t);
+    if (!pair) {
+      Py_DECREF(views);
+      return -1;
+    }
+    PyList_SET_ITEM(views, i, pair);
+  }
+  g_fast.pool_buf = THPVariable_Wrap(b);
+  if (!g_fast.pool_buf) {
+    Py_DECREF(views);
+    return -1;
+  }
+  g_fast.pool_views = views;
+  return 0;
+}
+
+// drop_pool(): forget the lazy-norm pool (tests; tree_util.set_deferred_sums)
+PyObject* drop_pool(PyObject*, PyObject*) {
+  Py_CLEAR(g_fast.pool_buf);
+  Py_CLEAR(g_fast.pool_views);
+  g_fast.pool_want = 0;
+  Py_RETURN_NONE;
+}
+
+// pool_info() -> (pool views ready, pool_want)
+PyObject* pool_info(PyObject*, PyObject*) {
+  return Py_BuildValue("(nL)", g_fast.pool_views ? PyList_GET_SIZE(g_fast.pool_views) : Py_ssize_t(0),
+                       g_fast.pool_want);
 }
 
 PyObject* fast_tree_l2_squared(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
@@ -2579,6 +2763,12 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
       }
       Py_CLEAR(links[j]->ticket);
     }
+    // the round's final fold (tree_inverse_weight: the 1/W scale) is in flight: build the next
+    // round's lazy-norm pool while the GPU folds
+    if (has_scale && refill_pool(l2.get_device()) != 0) {
+      Py_DECREF(got);
+      return nullptr;
+    }
     return got;
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
@@ -2631,12 +2821,17 @@ PyMethodDef kMethods[] = {
      "tree_mean(pytrees_and_weights)\n--\n\nReturns (weighted) mean of input trees and weights "
      "(fedjax/core/tree_util.py:76-96).\n\nA resident list / tuple of (float32 device pytree, Python-number weight) "
      "pairs is folded by one native call\n(the pytree kernel, pipelined with the walk on an idle GPU); every other "
-     "input is\nfedjax_amd.tree_util._tree_mean_py's (one-shot iterables stream in chunks)."},
+     "input is\nfedjax_amd.tree_util._tree_mean_py's (one-shot iterables stream in chunks).\n\nThe result's "
+     "float32 leaves are slices of one allocation (each its own tensor and\nversion counter): one live leaf keeps "
+     "all of them allocated, and torch.save of one\nleaf writes every leaf's bytes (clone a leaf to keep it alone)."},
     {"mean_triples", mean_triples, METH_O, "tree_mean over (client_id, params, weight) triples (aggregator.py:61-75)"},
     {"pipeline_fracs", pipeline_fracs, METH_O, "chunk ends (fractions of K) of tree_mean's fold-bound pipeline"},
+    {"busy_until", busy_until, METH_VARARGS, "the shared estimate of when this process's folds finish ([set])"},
     {"fold_chain", fold_chain, METH_VARARGS, "a PendingSum's deferred fold, its links walked natively"},
     {"flush_views", flush_views, METH_O, "fold the chains lazy norm views in an object still wait on"},
     {"fast_install_norms", fast_install_norms, METH_VARARGS, "register tree_util's lazy norm classes and fallbacks"},
+    {"drop_pool", drop_pool, METH_NOARGS, "forget the lazy-norm pool"},
+    {"pool_info", pool_info, METH_NOARGS, "(pool views ready, norms asked for since the last refill)"},
     {"tree_l2_squared", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_tree_l2_squared)),
      METH_FASTCALL | METH_KEYWORDS,
      "tree_l2_squared(pytree)\n--\n\nReturns squared l2 norm of tree (fedjax/core/tree_util.py:105-108), a 0-d "
@@ -2669,9 +2864,21 @@ PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_fjhost", "native host side of th
 
 }  // namespace
 
+// The torch this extension was compiled against (fedjax_amd._lib.torch_stamp(), passed by
+// __graft_entry__.build()): fjhost reaches into torch's TensorImpl / THPVariable layout, so
+// _lib.host() refuses to use it under any other torch (a layout mismatch would not fail
+// loudly by itself).
+#ifndef FJHOST_TORCH_STAMP
+#define FJHOST_TORCH_STAMP "unstamped"
+#endif
+
 PyMODINIT_FUNC PyInit__fjhost(void) {
   PyObject* m = PyModule_Create(&kModule);
   if (!m) return nullptr;
+  if (PyModule_AddStringConstant(m, "TORCH_STAMP", FJHOST_TORCH_STAMP) != 0) {
+    Py_DECREF(m);
+    return nullptr;
+  }
   const std::pair<const char*, PyType_Spec*> types[] = {
       {"WeightedBase", &kWTSpec}, {"ChainBase", &kChainSpec}, {"PendingBase", &kPSSpec}};
   for (const auto& t : types) {

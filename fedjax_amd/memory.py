@@ -80,14 +80,14 @@ def stats(device: Optional[torch.device] = None) -> dict:
     """fjalloc's counters for ``device`` (include/fjalloc.h ``fjalloc_stats``): bytes in live
     segments, live segments, segments created, reused ranges, failed requests, granularity,
     first chunk's top and base address (``bump_offset``, ``base``), last failure, placement
-    hints."""
+    hints, chunks and the free bytes inside them."""
     idx = torch.device(device).index if device is not None else None
     idx = torch.cuda.current_device() if idx is None else idx
-    out = np.zeros(11, dtype=np.int64)
+    out = np.zeros(13, dtype=np.int64)
     if _lib.load().fjalloc_stats(idx, out.ctypes.data) != 0:
         raise ValueError(f"fjalloc_stats: bad device {idx}")
     keys = ("mapped_bytes", "live_segments", "segments", "reused_ranges", "failures", "granularity",
-            "bump_offset", "base", "last_failure", "at_hint", "off_hint")
+            "bump_offset", "base", "last_failure", "at_hint", "off_hint", "chunks", "free_bytes")
     return dict(zip(keys, (int(v) for v in out)))
 
 

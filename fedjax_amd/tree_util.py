@@ -327,6 +327,15 @@ def _native_fold_addrs() -> None:
     _mean_config()
 
 
+def set_nontemporal_min_bytes(nbytes: int) -> None:
+    """Folds whose client deltas total at least ``nbytes`` use non-temporal loads (default
+    256 MiB, the Infinity Cache's size: :data:`NONTEMPORAL_MIN_BYTES`). Sets the module value
+    and the builtin tree_mean's copy of it together."""
+    global NONTEMPORAL_MIN_BYTES
+    NONTEMPORAL_MIN_BYTES = int(nbytes)
+    _mean_config()
+
+
 def _mean_config() -> None:
     """Configure the builtin tree_mean (fjhost.tree_mean / mean_triples): the same settings
     _native_mean passes, the library's entry points once loaded (until then the builtin
@@ -723,6 +732,7 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
     if flush_clients is not None:
         _DEFER["flush_clients"] = max(1, int(flush_clients))
     _HOST.fast_config(_DEFER["enabled"], _DEFER["max_clients"], _DEFER["flush_bytes"], _DEFER["flush_clients"])
+    _HOST.drop_pool()  # (the lazy-norm pool's buffer is sized by max_clients)
 
 
 def _defer_budget(device: torch.device) -> int:
@@ -1226,7 +1236,21 @@ _PIPELINE_CHUNK = int(os.environ.get("FJAGG_PIPELINE_CHUNK", "512"))
 _PIPELINE_MIN_BYTES = 64 << 20  # below this the first launch is too short to hide the walk
 _WALK_NS_PER_LEAF = 35.0  # native walk + checks per (client, leaf), MI355X host
 _PEAK_BYTES_PER_S = 8.0e12
-_BUSY_UNTIL = [0.0]  # perf_counter() time before which this module's issued folds cannot have finished
+class _BusyUntil:
+    """perf_counter() time before which this module's issued folds cannot have finished:
+    the builtin tree_mean's own estimate (fjhost.busy_until), so the native and the Python
+    paths keep ONE (``_BUSY_UNTIL[0]`` reads it, ``_BUSY_UNTIL[0] = t`` sets it)."""
+
+    __slots__ = ()
+
+    def __getitem__(self, i):
+        return _HOST.busy_until()
+
+    def __setitem__(self, i, t):
+        _HOST.busy_until(float(t))
+
+
+_BUSY_UNTIL = _BusyUntil()
 
 
 # The whole call in one native function (fjhost.mean_pairs) for the common case — plain
@@ -1347,6 +1371,11 @@ def _tree_mean_py(pytrees_and_weights: Iterable[Tuple[PyTree, float]]) -> PyTree
     scale fused into the last chunk's launch. Like the reference, which holds one client
     at a time, a generator of host-resident or freshly produced deltas therefore never
     needs all K deltas on the GPU at once; below the budget it is still one launch.
+
+    Storage: the native path's float32 result leaves are slices of one allocation (each its
+    own tensor and version counter, 256-byte aligned): one live leaf keeps every leaf's bytes
+    allocated, and ``torch.save`` of one leaf writes them all — ``clone()`` a leaf to keep it
+    on its own.
     """
     if type(pytrees_and_weights) is not list and type(pytrees_and_weights) is not tuple:
         return _tree_mean_stream(iter(pytrees_and_weights))

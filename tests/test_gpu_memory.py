@@ -60,3 +60,36 @@ def test_released_pool_returns_its_chunks_and_a_new_pool_works(cuda):
     assert np.array_equal(got[0].cpu().numpy().view(np.uint32), want[0].view(np.uint32))
     del pooled, got
     memory.release(cuda)
+
+
+def test_freed_neighbours_coalesce_and_take_a_larger_segment(cuda):
+    """ADVICE r4 (fjalloc mode 2): freed slices are merged with their free neighbours and
+    reused best-fit, so a segment that fits only in freed space (a torch out-of-memory retry
+    after freeing its cache) needs no new hipMalloc; the bump tail takes back a freed range at
+    its end; an emptied chunk still goes back to the runtime."""
+    from fedjax_amd import _lib
+    lib = _lib.load()
+    memory.release(cuda)
+    dev = cuda.index if cuda.index is not None else 0
+    MiB = 1 << 20
+    st0 = memory.stats(cuda)
+    a = lib.fjalloc_alloc(100 * MiB, dev, None)
+    b = lib.fjalloc_alloc(200 * MiB, dev, None)
+    c = lib.fjalloc_alloc(700 * MiB, dev, None)  # a 1 GiB chunk now has < 290 MiB of bump tail
+    assert a and b and c
+    st1 = memory.stats(cuda)
+    assert st1["failures"] == st0["failures"]
+    lib.fjalloc_free(a, 0, dev, None)
+    lib.fjalloc_free(b, 0, dev, None)
+    st2 = memory.stats(cuda)
+    assert st2["free_bytes"] >= st1["free_bytes"] + 300 * MiB  # a and b (with b's stagger bytes)
+    d = lib.fjalloc_alloc(290 * MiB, dev, None)  # only the merged a+b range holds it
+    st3 = memory.stats(cuda)
+    assert d and st3["chunks"] == st1["chunks"] and st3["reused_ranges"] == st2["reused_ranges"] + 1
+    if st0["chunks"] == 0:  # a, b, c shared one fresh chunk: d starts where a's range did
+        assert a - 31 * (68 << 10) <= d <= a
+    lib.fjalloc_free(d, 0, dev, None)
+    lib.fjalloc_free(c, 0, dev, None)
+    st4 = memory.stats(cuda)
+    assert st4["chunks"] == st0["chunks"] and st4["live_segments"] == st0["live_segments"]
+    assert st4["failures"] == st0["failures"]

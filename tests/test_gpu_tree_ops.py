@@ -347,6 +347,51 @@ def test_lazy_norms_of_a_deferred_sum(cuda, sum_mode):
     assert type(tu.tree_l2_norm(xs[0])) is not tu._NormView
 
 
+@pytest.mark.deferred_only
+def test_lazy_norm_pool_across_rounds(cuda, sum_mode):
+    """The library loop's per-client tree_l2_norm takes pre-made views (fjhost's lazy-norm pool,
+    built while each round's final fold runs) and recognises the captured dict tree by its dict
+    version tags instead of re-walking it. Over rounds of growing size (more clients than the
+    pool holds), with a mid-round read, every norm equals the float64 norm, every mean is the
+    oracle's bits, and the pool is refilled to the round's size; a delta dict changed after its
+    tree_weight gets the norm of its new contents, eagerly."""
+    H = tu._HOST
+    H.drop_pool()
+    g = torch.Generator().manual_seed(41)
+    shapes = {"a": (5000,), "b": {"c": (33, 3)}}
+    xs = [to_dev(rand_tree(shapes, g), cuda) for _ in range(16)]
+
+    def f64norm(t):
+        x = np.concatenate([v.astype(np.float64) for v in leaves_np(t)])
+        return np.sqrt((x * x).sum())
+    for rnd, K in enumerate((6, 9, 12, 12)):
+        s, norms = tu.tree_zeros_like(xs[0]), []
+        for k in range(K):
+            s = tu.tree_add(s, tu.tree_weight(xs[k], k + 1))
+            norms.append(tu.tree_l2_norm(xs[k]))
+            if rnd == 2 and k == 3:
+                np.testing.assert_allclose(float(norms[1]), f64norm(xs[1]), rtol=2e-6)  # folds links 0..3
+        assert all(type(v) is tu._NormView for v in norms)
+        W = float(sum(range(1, K + 1)))
+        mean = tu.tree_inverse_weight(s, W)
+        assert H.pool_info()[0] == K  # the next round's views, made while this fold ran
+        np.testing.assert_allclose([float(v) for v in norms], [f64norm(x) for x in xs[:K]], rtol=2e-6)
+        want = tmap(lambda s_: np.zeros(s_, np.float32), shapes)
+        for k in range(K):
+            want = ref.tree_add(want, ref.tree_weight(to_np(xs[k]), k + 1))
+        want = ref.tree_inverse_weight(want, W)
+        for a, b in zip(leaves_np(mean), pytree.leaves_of(want)):
+            assert np.array_equal(bits(a), bits(b.reshape(-1)))
+    t = {"a": xs[0]["a"].clone(), "b": {"c": xs[0]["b"]["c"].clone()}}
+    s = tu.tree_add(tu.tree_zeros_like(t), tu.tree_weight(t, 1))
+    t["b"] = {"c": xs[1]["b"]["c"]}  # a new inner dict: the root's version tag moved
+    v = tu.tree_l2_norm(t)
+    assert type(v) is not tu._NormView
+    np.testing.assert_allclose(float(v), f64norm({"a": xs[0]["a"], "b": {"c": xs[1]["b"]["c"]}}), rtol=2e-6)
+    tu.tree_inverse_weight(s, 1.0)
+    H.drop_pool()
+
+
 def test_norm_combine_orders_give_the_same_bits(cuda):
     """The per-call fused norm with its workgroup partials handed off by the gfx950
     write-through + drain form (default) and by release/acquire atomics (FJTREE_ORDERED,
