@@ -2163,8 +2163,15 @@ struct FastState {
   // round's final fold is launched (fold_chain with the 1/W scale), while the GPU folds, and
   // the next chain that takes a norm takes the pool as its buffer (fast_l2).
   PyObject* pool_buf = nullptr;
-  PyObject* pool_views = nullptr;
+  PyObject* pool_views = nullptr;  // the pairs still to hand out (items become None)
+  PyObject* pool_all = nullptr;    // every pair of the pool, in order (never modified)
+  // pools a chain took: (buf, all pairs). Once the caller has dropped every view of one and
+  // nothing else holds its buffer, the next refill reuses it whole (no new objects).
+  std::vector<std::pair<PyObject*, PyObject*>> retired;
+  PyObject* d_view_ticket = nullptr;  // _NormView._ticket and _Ticket.node slot descriptors
+  PyObject* d_ticket_node = nullptr;
   long long pool_want = 0;  // norms (row 1) the current round's chains asked for: the next pool's size
+  double refill_us = 0.0;   // host time of the last refill (pool_info)
 };
 FastState g_fast;
 
@@ -2321,8 +2328,22 @@ PyObject* fast_install_norms(PyObject*, PyObject* args) {
   Py_XSETREF(g_fast.py_l2[0], f0);
   Py_XSETREF(g_fast.py_l2[1], f1);
   Py_XSETREF(g_fast.py_fold_ticket, ft);
+  // the slots' descriptors, so setting / reading them skips the attribute lookup
+  PyObject* dv = PyObject_GetAttrString(nv, "_ticket");
+  PyObject* dn = dv ? PyObject_GetAttrString(tk, "node") : nullptr;
+  if (!dv || !dn || !Py_TYPE(dv)->tp_descr_set || !Py_TYPE(dn)->tp_descr_set || !Py_TYPE(dv)->tp_descr_get) {
+    Py_XDECREF(dv), Py_XDECREF(dn);
+    PyErr_Clear();
+    PyErr_SetString(PyExc_TypeError, "fast_install_norms: _NormView._ticket and _Ticket.node must be __slots__");
+    return nullptr;
+  }
+  Py_XSETREF(g_fast.d_view_ticket, dv);
+  Py_XSETREF(g_fast.d_ticket_node, dn);
   Py_RETURN_NONE;
 }
+
+// obj.<slot> = v through the slot's descriptor (0, or -1 with a Python error)
+inline int slot_set(PyObject* descr, PyObject* obj, PyObject* v) { return Py_TYPE(descr)->tp_descr_set(descr, obj, v); }
 
 // flush_views(obj): tree_util._flush_views natively — every lazy norm view (tree_util._NormView)
 // in obj (nested lists / tuples / dict values) whose ticket still names an unfolded link gets
@@ -2333,7 +2354,6 @@ PyObject* flush_views(PyObject*, PyObject* arg) {
     PyErr_SetString(PyExc_RuntimeError, "fedjax_amd.tree_util is not installed (fast_install_norms)");
     return nullptr;
   }
-  static PyObject* tk_name = PyUnicode_InternFromString("_ticket");
   static PyObject* node_name = PyUnicode_InternFromString("node");
   std::vector<std::pair<PyObject*, int>> st;  // (not shared: a fold may run Python code that calls back)
   Py_INCREF(arg);  // (every stacked object is held: folding runs Python code)
@@ -2355,13 +2375,11 @@ PyObject* flush_views(PyObject*, PyObject* arg) {
     } drop{x};
     PyTypeObject* t = Py_TYPE(x);
     if (t == g_fast.norm_view) {
-      PyObject* dict = PyObject_GenericGetDict(x, nullptr);  // (new reference; public API)
-      if (!dict) return nullptr;
-      PyObject* tk = PyDict_GetItemWithError(dict, tk_name);  // borrowed from dict
-      Py_XINCREF(tk);
-      Py_DECREF(dict);
-      if (!tk) {
-        if (PyErr_Occurred()) return nullptr;
+      PyObject* tk = Py_TYPE(g_fast.d_view_ticket)->tp_descr_get(g_fast.d_view_ticket, x,
+                                                                  reinterpret_cast<PyObject*>(t));
+      if (!tk) {  // the slot was never set: no ticket
+        if (!PyErr_ExceptionMatches(PyExc_AttributeError)) return nullptr;
+        PyErr_Clear();
         continue;
       }
       struct DropTk {
@@ -2396,11 +2414,12 @@ PyObject* flush_views(PyObject*, PyObject* arg) {
   Py_RETURN_NONE;
 }
 
+void retire_pool(PyObject* buf, PyObject* all);
+
 // A new _Ticket naming `node` (tree_util._Ticket, without its Python __init__ frame).
 PyObject* new_ticket(PyObject* node) {
-  static PyObject* node_name = PyUnicode_InternFromString("node");
   PyObject* t = g_fast.ticket->tp_alloc(g_fast.ticket, 0);
-  if (t && PyObject_SetAttr(t, node_name, node) != 0) Py_CLEAR(t);
+  if (t && slot_set(g_fast.d_ticket_node, t, node) != 0) Py_CLEAR(t);
   return t;
 }
 
@@ -2458,8 +2477,10 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
               const at::Tensor& pb = THPVariable_Unpack(g_fast.pool_buf);
               const at::Tensor& t0 = THPVariable_Unpack(PyTuple_GET_ITEM(tup, 0));
               if (pb.get_device() == t0.get_device() && pb.dim() == 2 && pb.size(1) == g_fast.max_clients + 1) {
+                retire_pool(g_fast.pool_buf, g_fast.pool_all);
                 Py_XSETREF(ch->buf, g_fast.pool_buf);
                 Py_XSETREF(ch->views, g_fast.pool_views);
+                Py_CLEAR(g_fast.pool_all);
                 g_fast.pool_buf = g_fast.pool_views = nullptr;
               }
             }
@@ -2481,8 +2502,6 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
                     pair = nullptr;
                   }
                 }
-                static PyObject* node_name = PyUnicode_InternFromString("node");
-                static PyObject* name = PyUnicode_InternFromString("_ticket");
                 if (pair) {
                   struct DropPair {
                     PyObject* o;
@@ -2490,7 +2509,7 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
                   } drop_pair{pair};
                   PyObject* v = PyTuple_GET_ITEM(pair, 0);
                   PyObject* t = PyTuple_GET_ITEM(pair, 1);
-                  if (PyObject_SetAttr(t, node_name, no) != 0) return nullptr;
+                  if (slot_set(g_fast.d_ticket_node, t, no) != 0) return nullptr;
                   Py_INCREF(t);
                   Py_XSETREF(node->ticket, t);
                   Py_INCREF(v);
@@ -2504,7 +2523,7 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
                 PyObject* v = THPVariable_Wrap(
                     scalar_at(b, b.storage_offset() + row * b.stride(0) + node->idx * b.stride(1)), g_fast.norm_view);
                 if (!v) return nullptr;
-                if (PyObject_SetAttr(v, name, node->ticket) != 0) {
+                if (slot_set(g_fast.d_view_ticket, v, node->ticket) != 0) {
                   Py_DECREF(v);
                   return nullptr;
                 }
@@ -2522,29 +2541,83 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
   return PyObject_Vectorcall(py, args, nargs, kwnames);
 }
 
-// Builds the lazy-norm pool (FastState) for the next round: a fresh norm buffer on device dev
-// and g_fast.pool_want (view of buf[1, i], ticket) pairs, each view's _ticket set to its
+void clear_pool() {
+  Py_CLEAR(g_fast.pool_buf);
+  Py_CLEAR(g_fast.pool_views);
+  Py_CLEAR(g_fast.pool_all);
+}
+
+// a chain took (buf, all): keep them (new references) for reuse, at most 4 (the oldest goes)
+void retire_pool(PyObject* buf, PyObject* all) {
+  if (!buf || !all) return;
+  Py_INCREF(buf);
+  Py_INCREF(all);
+  g_fast.retired.emplace_back(buf, all);
+  if (g_fast.retired.size() > 4) {
+    Py_DECREF(g_fast.retired.front().first);
+    Py_DECREF(g_fast.retired.front().second);
+    g_fast.retired.erase(g_fast.retired.begin());
+  }
+}
+
+// A retired pool is reusable when nothing but the pool itself references it: the buffer
+// object and every pair, view and ticket are held only by the pool (the caller dropped the
+// views, the chain is gone) and the buffer's storage has no alias outside the pool's own
+// tensors — so writing new norms into it cannot change a value anybody can still read.
+bool reusable(PyObject* buf, PyObject* all, c10::DeviceIndex dev, long long m) {
+  if (Py_REFCNT(buf) != 1 || !THPVariable_Check(buf) || !PyList_CheckExact(all) || PyList_GET_SIZE(all) < m)
+    return false;
+  const at::Tensor& b = THPVariable_Unpack(buf);
+  if (b.get_device() != dev || b.dim() != 2 || b.size(1) != g_fast.max_clients + 1 || b.use_count() != 1 ||
+      static_cast<long long>(b.storage().use_count()) != PyList_GET_SIZE(all) + 1)
+    return false;
+  for (Py_ssize_t i = 0; i < PyList_GET_SIZE(all); ++i) {
+    PyObject* pair = PyList_GET_ITEM(all, i);
+    if (Py_REFCNT(pair) != 1) return false;
+    PyObject* v = PyTuple_GET_ITEM(pair, 0);
+    PyObject* t = PyTuple_GET_ITEM(pair, 1);
+    if (Py_REFCNT(v) != 1 || THPVariable_Unpack(v).use_count() != 1 || Py_REFCNT(t) != 2) return false;
+  }
+  return true;
+}
+
+// Builds the lazy-norm pool (FastState) for the next round: a retired pool nobody references
+// any more, reused whole (every ticket's node reset to None), or a fresh norm buffer on device
+// dev and g_fast.pool_want (view of buf[1, i], ticket) pairs, each view's _ticket set to its
 // ticket (ticket.node None until fast_l2 hands the pair out). 0, or -1 with a Python error.
 int refill_pool(c10::DeviceIndex dev) {
+  Stamp clock;
   const long long m = std::min<long long>(g_fast.pool_want, g_fast.max_clients + 1);
   g_fast.pool_want = 0;
-  if (m <= 0 || !g_fast.norm_view || !g_fast.ticket) return 0;
+  if (m <= 0 || !g_fast.norm_view || !g_fast.ticket || !g_fast.d_view_ticket) return 0;
   if (g_fast.pool_buf) {  // an unused pool: kept if a chain on this device could still take it
     const at::Tensor& pb = THPVariable_Unpack(g_fast.pool_buf);
     if (pb.get_device() == dev && pb.size(1) == g_fast.max_clients + 1 && g_fast.pool_views &&
         PyList_GET_SIZE(g_fast.pool_views) >= m)
       return 0;
-    Py_CLEAR(g_fast.pool_buf);
-    Py_CLEAR(g_fast.pool_views);
+    clear_pool();
   }
-  static PyObject* name = PyUnicode_InternFromString("_ticket");
+  for (size_t r = 0; r < g_fast.retired.size(); ++r) {
+    auto [buf, all] = g_fast.retired[r];
+    if (!reusable(buf, all, dev, m)) continue;
+    for (Py_ssize_t i = 0; i < PyList_GET_SIZE(all); ++i)
+      if (slot_set(g_fast.d_ticket_node, PyTuple_GET_ITEM(PyList_GET_ITEM(all, i), 1), Py_None) != 0) return -1;
+    PyObject* views = PyList_GetSlice(all, 0, PyList_GET_SIZE(all));
+    if (!views) return -1;
+    g_fast.retired.erase(g_fast.retired.begin() + static_cast<std::ptrdiff_t>(r));
+    g_fast.pool_buf = buf;  // (the retired entry's references move to the pool)
+    g_fast.pool_all = all;
+    g_fast.pool_views = views;
+    g_fast.refill_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - clock.t).count();
+    return 0;
+  }
   at::Tensor b = at::empty({2, g_fast.max_clients + 1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
   PyObject* views = PyList_New(m);
   if (!views) return -1;
   for (long long i = 0; i < m; ++i) {
     PyObject* v = THPVariable_Wrap(scalar_at(b, b.size(1) + i), g_fast.norm_view);
     PyObject* t = v ? new_ticket(Py_None) : nullptr;
-    if (!t || PyObject_SetAttr(v, name, t) != 0) {
+    if (!t || slot_set(g_fast.d_view_ticket, v, t) != 0) {
       Py_XDECREF(v), Py_XDECREF(t), Py_DECREF(views);
       return -1;
     }
@@ -2557,26 +2630,33 @@ int refill_pool(c10::DeviceIndex dev) {
     PyList_SET_ITEM(views, i, pair);
   }
   g_fast.pool_buf = THPVariable_Wrap(b);
-  if (!g_fast.pool_buf) {
+  g_fast.pool_views = g_fast.pool_buf ? PyList_GetSlice(views, 0, m) : nullptr;
+  if (!g_fast.pool_buf || !g_fast.pool_views) {
     Py_DECREF(views);
+    clear_pool();
     return -1;
   }
-  g_fast.pool_views = views;
+  g_fast.pool_all = views;
+  g_fast.refill_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - clock.t).count();
   return 0;
 }
 
 // drop_pool(): forget the lazy-norm pool (tests; tree_util.set_deferred_sums)
 PyObject* drop_pool(PyObject*, PyObject*) {
-  Py_CLEAR(g_fast.pool_buf);
-  Py_CLEAR(g_fast.pool_views);
+  clear_pool();
+  for (auto& e : g_fast.retired) {
+    Py_DECREF(e.first);
+    Py_DECREF(e.second);
+  }
+  g_fast.retired.clear();
   g_fast.pool_want = 0;
   Py_RETURN_NONE;
 }
 
-// pool_info() -> (pool views ready, pool_want)
+// pool_info() -> (pool views ready, pool_want, host us of the last refill, retired pools)
 PyObject* pool_info(PyObject*, PyObject*) {
-  return Py_BuildValue("(nL)", g_fast.pool_views ? PyList_GET_SIZE(g_fast.pool_views) : Py_ssize_t(0),
-                       g_fast.pool_want);
+  return Py_BuildValue("(nLdn)", g_fast.pool_views ? PyList_GET_SIZE(g_fast.pool_views) : Py_ssize_t(0),
+                       g_fast.pool_want, g_fast.refill_us, static_cast<Py_ssize_t>(g_fast.retired.size()));
 }
 
 PyObject* fast_tree_l2_squared(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
@@ -2699,7 +2779,9 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
   for (size_t j = 0; j < links.size(); ++j) {
     PyObject* tk = links[j]->ticket;
     if (!tk || tk == Py_None) continue;
-    PyObject* tn = PyObject_GetAttr(tk, node_name);
+    PyObject* tn = (Py_TYPE(tk) == g_fast.ticket && g_fast.d_ticket_node)
+                       ? Py_TYPE(g_fast.d_ticket_node)->tp_descr_get(g_fast.d_ticket_node, tk, nullptr)
+                       : PyObject_GetAttr(tk, node_name);
     if (!tn) return nullptr;
     const bool w = tn != Py_None;
     Py_DECREF(tn);
@@ -2757,17 +2839,28 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
       }
     }
     for (size_t j : waiting) {
-      if (PyObject_SetAttr(links[j]->ticket, node_name, Py_None) != 0) {
+      PyObject* tk = links[j]->ticket;
+      if ((Py_TYPE(tk) == g_fast.ticket && g_fast.d_ticket_node ? slot_set(g_fast.d_ticket_node, tk, Py_None)
+                                                                 : PyObject_SetAttr(tk, node_name, Py_None)) != 0) {
         Py_DECREF(got);
         return nullptr;
       }
       Py_CLEAR(links[j]->ticket);
     }
-    // the round's final fold (tree_inverse_weight: the 1/W scale) is in flight: build the next
-    // round's lazy-norm pool while the GPU folds
-    if (has_scale && refill_pool(l2.get_device()) != 0) {
-      Py_DECREF(got);
-      return nullptr;
+    // the round's final fold (tree_inverse_weight: the 1/W scale) is in flight: the chain, now
+    // folded to its tip, lets go of its norm buffer (its views hold their own references; a sum
+    // continued from here starts a new chain), and the next round's lazy-norm pool is built
+    // while the GPU folds
+    if (has_scale) {
+      auto* ch = reinterpret_cast<ChainObject*>(links.back()->chain);
+      if (ch && Py_TYPE(ch) == g_fast.chain && ch->tip == node) {
+        Py_CLEAR(ch->buf);
+        Py_CLEAR(ch->views);
+      }
+      if (refill_pool(l2.get_device()) != 0) {
+        Py_DECREF(got);
+        return nullptr;
+      }
     }
     return got;
   } catch (const std::exception& e) {

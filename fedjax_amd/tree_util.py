@@ -775,6 +775,8 @@ class _NormView(torch.Tensor):
     arithmetic) first runs that fold if it has not run, then computes on plain tensors —
     so no read can see the buffer before the value is there."""
 
+    __slots__ = ("_ticket",)  # (no per-view __dict__: fjhost sets the slot through its descriptor)
+
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):
         _HOST.flush_views(args)
@@ -799,7 +801,7 @@ def _flush_views(x) -> None:
     """The Python statement of fjhost.flush_views (which the views use)."""
     t = type(x)
     if t is _NormView:
-        ticket = x.__dict__.get("_ticket")
+        ticket = getattr(x, "_ticket", None)
         if ticket is not None and ticket.node is not None:
             ticket.node._chain.tip.materialize()  # folds every pending link of the chain
     elif t is list or t is tuple:

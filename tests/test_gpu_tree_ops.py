@@ -359,29 +359,38 @@ def test_lazy_norm_pool_across_rounds(cuda, sum_mode):
     H.drop_pool()
     g = torch.Generator().manual_seed(41)
     shapes = {"a": (5000,), "b": {"c": (33, 3)}}
-    xs = [to_dev(rand_tree(shapes, g), cuda) for _ in range(16)]
+    xs = [to_dev(rand_tree(shapes, g), cuda) for _ in range(20)]
 
     def f64norm(t):
         x = np.concatenate([v.astype(np.float64) for v in leaves_np(t)])
         return np.sqrt((x * x).sum())
-    for rnd, K in enumerate((6, 9, 12, 12)):
+    kept = alias = None
+    for rnd, K in enumerate((6, 9, 12, 12, 12, 12)):
         s, norms = tu.tree_zeros_like(xs[0]), []
         for k in range(K):
-            s = tu.tree_add(s, tu.tree_weight(xs[k], k + 1))
-            norms.append(tu.tree_l2_norm(xs[k]))
+            s = tu.tree_add(s, tu.tree_weight(xs[rnd + k], k + 1))
+            norms.append(tu.tree_l2_norm(xs[rnd + k]))
             if rnd == 2 and k == 3:
-                np.testing.assert_allclose(float(norms[1]), f64norm(xs[1]), rtol=2e-6)  # folds links 0..3
+                np.testing.assert_allclose(float(norms[1]), f64norm(xs[rnd + 1]), rtol=2e-6)  # folds links 0..3
         assert all(type(v) is tu._NormView for v in norms)
         W = float(sum(range(1, K + 1)))
         mean = tu.tree_inverse_weight(s, W)
         assert H.pool_info()[0] == K  # the next round's views, made while this fold ran
-        np.testing.assert_allclose([float(v) for v in norms], [f64norm(x) for x in xs[:K]], rtol=2e-6)
+        np.testing.assert_allclose([float(v) for v in norms], [f64norm(x) for x in xs[rnd:rnd + K]], rtol=2e-6)
         want = tmap(lambda s_: np.zeros(s_, np.float32), shapes)
         for k in range(K):
-            want = ref.tree_add(want, ref.tree_weight(to_np(xs[k]), k + 1))
+            want = ref.tree_add(want, ref.tree_weight(to_np(xs[rnd + k]), k + 1))
         want = ref.tree_inverse_weight(want, W)
         for a, b in zip(leaves_np(mean), pytree.leaves_of(want)):
             assert np.array_equal(bits(a), bits(b.reshape(-1)))
+        if rnd == 0:
+            kept = norms  # round 0's views stay referenced: their pool is never reused
+        if rnd == 1:
+            alias = norms[2].view(1)  # a plain tensor on round 1's norm buffer: that pool is never reused
+        assert H.pool_info()[3] <= 4
+    # later rounds reused pools nobody held (rounds 2, 3, ...), never these
+    np.testing.assert_allclose([float(v) for v in kept], [f64norm(x) for x in xs[:6]], rtol=2e-6)
+    np.testing.assert_allclose(float(alias[0]), f64norm(xs[3]), rtol=2e-6)  # round 1, client 2
     t = {"a": xs[0]["a"].clone(), "b": {"c": xs[0]["b"]["c"].clone()}}
     s = tu.tree_add(tu.tree_zeros_like(t), tu.tree_weight(t, 1))
     t["b"] = {"c": xs[1]["b"]["c"]}  # a new inner dict: the root's version tag moved

@@ -40,7 +40,11 @@ def main(reps=40, K=128):
     buf = torch.empty((2, 257), dtype=torch.float32, device=dev)
     res = {}
 
+    phases = {}
+
     def loop(norm):
+        torch.cuda.synchronize()
+        tz = pc()
         s, norms = tu.tree_zeros_like(pairs[0][0]), []
         t0 = pc()
         for t, w in pairs:
@@ -49,7 +53,12 @@ def main(reps=40, K=128):
                 norms.append(tu.tree_l2_norm(t))
         t1 = pc()
         m = tu.tree_inverse_weight(s, W)
+        t2 = pc()
         torch.cuda.synchronize()
+        t3 = pc()
+        key = "norms" if norm else "plain"
+        phases.setdefault(key, []).append((t0 - tz, t1 - t0, t2 - t1, t3 - t2, t3 - tz,
+                                           host.pool_info()[2] if norm else 0.0))
         del m, norms
         return (t1 - t0) / K * 1e6
 
@@ -80,6 +89,11 @@ def main(reps=40, K=128):
         vals = [fn() for _ in range(reps)]
         res[name + "_us_per_client"] = round(float(np.median(vals)), 3)
     res["norm_call_us_per_client"] = round(res["loop_norms_us_per_client"] - res["loop_plain_us_per_client"], 3)
+    for key, rows in phases.items():  # median host microseconds of each phase of a synchronised round
+        a = np.median(np.array(rows[3:]), axis=0) * 1e6
+        res[f"round_{key}_us"] = {"zeros": round(a[0], 1), "loop": round(a[1], 1), "final_call": round(a[2], 1),
+                                  "sync_wait": round(a[3], 1), "total": round(a[4], 1),
+                                  "pool_refill_in_final_call": round(a[5] / 1e6, 1)}
     print(json.dumps(res), flush=True)
 
 
