@@ -361,11 +361,21 @@ def dropin_surface(dev, calls=20):
             ref = tu.tree_l2_norms([t for t, _ in pairs])
             res["c1_library_loop_norms_max_rel_diff"] = float(((got - ref).abs() / ref).max())
         del s, mean, client_diagnostics
-    # the same clients allocated under the opt-in delta pool (fedjax_amd.memory, include/fjalloc.h):
-    # still one tensor per (client, leaf), placed in shared chunks
-    from fedjax_amd import memory
-    with memory.delta_allocation(dev):
-        pooled = list(zip([tree(k) for k in range(K)], fedavg_weights(K)))
+    # the same clients as fedjax_amd produces them under the process-wide switch
+    # memory.set_default(True): host deltas copied to the device leaf by leaf
+    # (memory.to_device), from the delta pool (include/fjalloc.h) — still one tensor per
+    # (client, leaf), placed in shared chunks
+    from fedjax_amd import memory, pytree
+    host_trees = []
+    for t, _ in pairs:
+        lv, td = pytree.flatten(t)
+        host_trees.append(pytree.unflatten(td, [x.cpu().pin_memory() for x in lv]))
+    memory.set_default(True)
+    try:
+        pooled = list(zip([memory.to_device(t, dev) for t in host_trees], fedavg_weights(K)))
+    finally:
+        memory.set_default(False)
+    del host_trees
     for _ in range(5):
         tu.tree_mean(pooled)
     torch.cuda.synchronize()
@@ -373,7 +383,7 @@ def dropin_surface(dev, calls=20):
     for _ in range(n):
         tu.tree_mean(pooled)
     torch.cuda.synchronize()
-    res["c1_delta_pool_tree_mean_back_to_back_ms"] = round((pc() - t0) / n * 1e3, 4)
+    res["c1_default_pool_tree_mean_back_to_back_ms"] = round((pc() - t0) / n * 1e3, 4)
     single = []
     for _ in range(n):
         torch.cuda.synchronize()
@@ -381,14 +391,20 @@ def dropin_surface(dev, calls=20):
         tu.tree_mean(pooled)
         torch.cuda.synchronize()
         single.append(pc() - t0)
-    res["c1_delta_pool_tree_mean_sync_call_ms"] = round(float(np.median(single)) * 1e3, 4)
-    res["c1_delta_pool_tree_mean_sync_call_GBs"] = round(K * P * 4 / float(np.median(single)) / 1e9, 1)
+    res["c1_default_pool_tree_mean_sync_call_ms"] = round(float(np.median(single)) * 1e3, 4)
+    res["c1_default_pool_tree_mean_sync_call_GBs"] = round(K * P * 4 / float(np.median(single)) / 1e9, 1)
+    got = tu.tree_mean(pooled)  # the same bits as the default allocations' mean
+    ref = tu.tree_mean(pairs)
+    res["c1_default_pool_bitwise"] = all(torch.equal(a.view(torch.int32), b.view(torch.int32)) for a, b in
+                                         zip(pytree.leaves_of(got), pytree.leaves_of(ref)))
+    del got, ref
     del pooled
     res["note"] = ("caller-held pytrees, separate allocations; timed after the headline, outside its "
                    "timed region; GB/s = K*P*4 client-delta bytes per call (library loop: per round); "
                    "c1_library_loop_with_norms: fed_avg.py:132-146 as written (tree_l2_norm per client into "
                    "client_diagnostics), c1_library_loop_without_norms: the same loop without the norm; "
-                   "c1_delta_pool_*: the same clients allocated under fedjax_amd.memory.delta_allocation()")
+                   "c1_default_pool_*: the same clients produced by fedjax_amd.memory.to_device under "
+                   "fedjax_amd.memory.set_default(True) (the delta pool)")
     del pairs
     torch.cuda.synchronize()
     torch.cuda.empty_cache()

@@ -2172,6 +2172,7 @@ struct FastState {
   PyObject* d_ticket_node = nullptr;
   long long pool_want = 0;  // norms (row 1) the current round's chains asked for: the next pool's size
   double refill_us = 0.0;   // host time of the last refill (pool_info)
+  long long pool_reuses = 0, pool_builds = 0;
 };
 FastState g_fast;
 
@@ -2495,9 +2496,10 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
                     PyList_CheckExact(ch->views) && node->idx < PyList_GET_SIZE(ch->views)) {
                   pair = PyList_GET_ITEM(ch->views, node->idx);
                   if (pair != Py_None && PyTuple_CheckExact(pair) && PyTuple_GET_SIZE(pair) == 2) {
-                    Py_INCREF(pair);
+                    // handed out once: the list's reference moves to this call (PyList_SET_ITEM
+                    // does not release the item it overwrites)
                     Py_INCREF(Py_None);
-                    PyList_SET_ITEM(ch->views, node->idx, Py_None);  // handed out once
+                    PyList_SET_ITEM(ch->views, node->idx, Py_None);
                   } else {
                     pair = nullptr;
                   }
@@ -2608,6 +2610,7 @@ int refill_pool(c10::DeviceIndex dev) {
     g_fast.pool_buf = buf;  // (the retired entry's references move to the pool)
     g_fast.pool_all = all;
     g_fast.pool_views = views;
+    ++g_fast.pool_reuses;
     g_fast.refill_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - clock.t).count();
     return 0;
   }
@@ -2637,6 +2640,7 @@ int refill_pool(c10::DeviceIndex dev) {
     return -1;
   }
   g_fast.pool_all = views;
+  ++g_fast.pool_builds;
   g_fast.refill_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - clock.t).count();
   return 0;
 }
@@ -2653,10 +2657,12 @@ PyObject* drop_pool(PyObject*, PyObject*) {
   Py_RETURN_NONE;
 }
 
-// pool_info() -> (pool views ready, pool_want, host us of the last refill, retired pools)
+// pool_info() -> (pool views ready, pool_want, host us of the last refill, retired pools,
+//                 refills that reused a retired pool, refills that built one)
 PyObject* pool_info(PyObject*, PyObject*) {
-  return Py_BuildValue("(nLdn)", g_fast.pool_views ? PyList_GET_SIZE(g_fast.pool_views) : Py_ssize_t(0),
-                       g_fast.pool_want, g_fast.refill_us, static_cast<Py_ssize_t>(g_fast.retired.size()));
+  return Py_BuildValue("(nLdnLL)", g_fast.pool_views ? PyList_GET_SIZE(g_fast.pool_views) : Py_ssize_t(0),
+                       g_fast.pool_want, g_fast.refill_us, static_cast<Py_ssize_t>(g_fast.retired.size()),
+                       g_fast.pool_reuses, g_fast.pool_builds);
 }
 
 PyObject* fast_tree_l2_squared(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {

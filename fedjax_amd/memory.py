@@ -61,6 +61,48 @@ def delta_allocation(device: Optional[torch.device] = None):
         yield pool
 
 
+# set_default: the process-wide switch for the deltas fedjax_amd itself produces
+_DEFAULT = {"on": False}
+
+
+def set_default(enabled: bool = True) -> None:
+    """Process-wide switch: while on, the client deltas fedjax_amd itself
+    produces are allocated from :func:`delta_pool` — device copies of host deltas
+    (:func:`to_device`), client-delta slabs (:class:`~fedjax_amd.slab.ClientDeltaSlab`, the rows
+    :class:`~fedjax_amd.ingest.DeltaIngestor` fills) and the materialised results of
+    ``tree_weight`` — so callers get the pooled placement without changing their code.
+    Results are the same bits either way; off by default (the pool keeps 1 GiB chunks)."""
+    _DEFAULT["on"] = bool(enabled)
+
+
+def default_enabled() -> bool:
+    return _DEFAULT["on"]
+
+
+def producing(device) -> "contextlib.AbstractContextManager":
+    """The scope fedjax_amd allocates the client deltas it produces on ``device`` in:
+    :func:`delta_allocation` under :func:`set_default`, else a no-op."""
+    dev = torch.device(device) if device is not None else None
+    if not _DEFAULT["on"] or dev is None or dev.type != "cuda":
+        return contextlib.nullcontext()
+    return delta_allocation(dev)
+
+
+def to_device(tree, device: Optional[torch.device] = None):
+    """A client's delta pytree (torch tensors or numpy arrays, any container this package
+    flattens) copied to ``device`` leaf by leaf — each leaf its own tensor, as a client's
+    training output is — from :func:`delta_pool` under :func:`set_default`. The copies are
+    asynchronous on the current stream (pinned sources) like ``Tensor.to``."""
+    from fedjax_amd import pytree
+
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    leaves, td = pytree.flatten(tree)
+    with producing(dev):
+        out = [(torch.from_numpy(np.ascontiguousarray(x)) if isinstance(x, np.ndarray) else x).to(dev)
+               for x in leaves]
+    return pytree.unflatten(td, out)
+
+
 def release(device: Optional[torch.device] = None) -> None:
     """Drop the process's delta pool for ``device``: once no tensor allocated from it is
     alive, torch frees its segments and fjalloc returns the emptied chunks to the runtime
@@ -91,4 +133,5 @@ def stats(device: Optional[torch.device] = None) -> dict:
     return dict(zip(keys, (int(v) for v in out)))
 
 
-__all__ = ["delta_pool", "delta_allocation", "release", "stats"]
+__all__ = ["delta_pool", "delta_allocation", "release", "stats", "set_default", "default_enabled", "producing",
+           "to_device"]

@@ -44,7 +44,10 @@ class ClientDeltaSlab:
         self.device = device if device is not None else tree_util._default_device()
         vw = 16 // torch.empty((), dtype=dtype).element_size()
         self.row_stride = max(vw, (self.num_params + vw - 1) // vw * vw)
-        self.storage = torch.empty(self.num_clients, self.row_stride, dtype=dtype, device=self.device)
+        from fedjax_amd import memory
+
+        with memory.producing(self.device):  # the delta pool under memory.set_default(True)
+            self.storage = torch.empty(self.num_clients, self.row_stride, dtype=dtype, device=self.device)
         if self.row_stride > self.num_params:
             self.storage[:, self.num_params:].zero_()
 

@@ -647,7 +647,9 @@ class WeightedTree(_HOST.WeightedBase):
 
     def materialize(self) -> PyTree:
         if self._value is None:
-            got = _leaf_fold([self._tree], [self._weight], [self._cap])
+            from fedjax_amd import memory
+            with memory.producing(self._cap[0][0].device if memory.default_enabled() else None):
+                got = _leaf_fold([self._tree], [self._weight], [self._cap])
             if got is None:
                 raise RuntimeError("the pytree passed to tree_weight changed structure before use")
             self._value = got[0]

@@ -93,3 +93,42 @@ def test_freed_neighbours_coalesce_and_take_a_larger_segment(cuda):
     st4 = memory.stats(cuda)
     assert st4["chunks"] == st0["chunks"] and st4["live_segments"] == st0["live_segments"]
     assert st4["failures"] == st0["failures"]
+
+
+def test_set_default_pools_the_deltas_fedjax_amd_produces(cuda):
+    """under memory.set_default(True) the deltas fedjax_amd produces — host
+    deltas copied by memory.to_device, ClientDeltaSlab storage (DeltaIngestor's rows) and a
+    materialised tree_weight — come from the delta pool's chunks; the fold gives the same bits;
+    switched off, allocations are torch's own again."""
+    import fedjax_amd
+    memory.release(cuda)
+    g = torch.Generator().manual_seed(8)
+    host = [{"a": torch.rand(5000, generator=g) - 0.5, "b": [torch.rand(33, 3, generator=g) - 0.5]}
+            for _ in range(6)]
+    weights = [3, 1, 4, 1, 5, 9]
+
+    def in_pool(ptr):  # inside the first chunk (these few KB all fit in it)
+        st = memory.stats(cuda)
+        return st["chunks"] > 0 and st["base"] <= ptr < st["base"] + (1 << 30)
+    memory.set_default(True)
+    try:
+        pooled = [memory.to_device(t, cuda) for t in host]
+        slab = fedjax_amd.ClientDeltaSlab(host[0], 4, device=cuda)
+        wt = tu.tree_weight(pooled[0], 2).materialize()  # (a deferred WeightedTree, made concrete here)
+    finally:
+        memory.set_default(False)
+    assert not memory.default_enabled()
+    assert all(in_pool(x.data_ptr()) for c in pooled for x in [c["a"], c["b"][0]])
+    assert in_pool(slab.storage.data_ptr())
+    assert in_pool(wt["a"].data_ptr())
+    plain = [memory.to_device(t, cuda) for t in host]
+    assert not in_pool(plain[0]["a"].data_ptr())
+    a = tu.tree_mean(list(zip(pooled, weights)))
+    b = tu.tree_mean(list(zip(plain, weights)))
+    want = ref.tree_mean([({"a": t["a"].numpy(), "b": [t["b"][0].numpy()]}, w) for t, w in zip(host, weights)])
+    for x, y, z in zip([a["a"], a["b"][0]], [b["a"], b["b"][0]], [want["a"], want["b"][0]]):
+        assert np.array_equal(x.cpu().numpy().view(np.uint32), z.view(np.uint32))
+        assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+    del pooled, slab, wt, a
+    torch.cuda.synchronize()
+    memory.release(cuda)

@@ -388,7 +388,7 @@ def test_lazy_norm_pool_across_rounds(cuda, sum_mode):
         if rnd == 1:
             alias = norms[2].view(1)  # a plain tensor on round 1's norm buffer: that pool is never reused
         assert H.pool_info()[3] <= 4
-    # later rounds reused pools nobody held (rounds 2, 3, ...), never these
+    assert H.pool_info()[4] >= 1  # later rounds reused pools nobody held (rounds 2, 3, ...), never these
     np.testing.assert_allclose([float(v) for v in kept], [f64norm(x) for x in xs[:6]], rtol=2e-6)
     np.testing.assert_allclose(float(alias[0]), f64norm(xs[3]), rtol=2e-6)  # round 1, client 2
     t = {"a": xs[0]["a"].clone(), "b": {"c": xs[0]["b"]["c"].clone()}}

@@ -94,6 +94,8 @@ def main(reps=40, K=128):
         res[f"round_{key}_us"] = {"zeros": round(a[0], 1), "loop": round(a[1], 1), "final_call": round(a[2], 1),
                                   "sync_wait": round(a[3], 1), "total": round(a[4], 1),
                                   "pool_refill_in_final_call": round(a[5] / 1e6, 1)}
+    info = host.pool_info()
+    res["pool"] = {"refills_reusing_a_pool": info[4], "refills_building_one": info[5], "retired": info[3]}
     print(json.dumps(res), flush=True)
 
 
