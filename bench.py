@@ -339,28 +339,33 @@ def dropin_surface(dev, calls=20):
     # (a) as fed_avg.py:132-146 writes it, with the per-client delta_l2_norm kept in
     # client_diagnostics (:142-144), and (b) without the norm (the aggregation alone)
     W = float(sum(w for _, w in pairs))
-    for with_norms in (True, False):
-        loop = []
-        for _ in range(calls):
-            torch.cuda.synchronize()
-            t0 = pc()
-            s, client_diagnostics = tu.tree_zeros_like(pairs[0][0]), {}
-            for cid, (t, w) in enumerate(pairs):
-                s = tu.tree_add(s, tu.tree_weight(t, w))
-                if with_norms:
-                    client_diagnostics[cid] = {"delta_l2_norm": tu.tree_l2_norm(t)}
-            mean = tu.tree_inverse_weight(s, W)
-            torch.cuda.synchronize()
-            loop.append(pc() - t0)
-        ms = float(np.median(loop)) * 1e3
-        key = "c1_library_loop_with_norms_round" if with_norms else "c1_library_loop_without_norms_round"
-        res[key + "_ms"] = round(ms, 4)
-        res[key + "_GBs"] = round(K * P * 4 / ms / 1e6, 1)
-        if with_norms:  # the kept norms hold the values (outside the timing): vs one batched launch
+    import gc
+    gc.collect()
+    loops = {True: [], False: []}
+    for i in range(2 * (calls + 2)):  # rounds with and without the norms alternate (box drift hits both)
+        with_norms = i % 2 == 0
+        torch.cuda.synchronize()
+        t0 = pc()
+        s, client_diagnostics = tu.tree_zeros_like(pairs[0][0]), {}
+        for cid, (t, w) in enumerate(pairs):
+            s = tu.tree_add(s, tu.tree_weight(t, w))
+            if with_norms:
+                client_diagnostics[cid] = {"delta_l2_norm": tu.tree_l2_norm(t)}
+        mean = tu.tree_inverse_weight(s, W)
+        torch.cuda.synchronize()
+        if i >= 4:
+            loops[with_norms].append(pc() - t0)
+        if with_norms and i == 2 * (calls + 2) - 2:  # the kept norms hold the values: vs one batched launch
             got = torch.stack([client_diagnostics[c]["delta_l2_norm"] for c in range(K)])
             ref = tu.tree_l2_norms([t for t, _ in pairs])
             res["c1_library_loop_norms_max_rel_diff"] = float(((got - ref).abs() / ref).max())
-        del s, mean, client_diagnostics
+            del got, ref
+    del s, mean, client_diagnostics
+    for with_norms in (True, False):
+        ms = float(np.median(loops[with_norms])) * 1e3
+        key = "c1_library_loop_with_norms_round" if with_norms else "c1_library_loop_without_norms_round"
+        res[key + "_ms"] = round(ms, 4)
+        res[key + "_GBs"] = round(K * P * 4 / ms / 1e6, 1)
     # the same clients as fedjax_amd produces them under the process-wide switch
     # memory.set_default(True): host deltas copied to the device leaf by leaf
     # (memory.to_device), from the delta pool (include/fjalloc.h) — still one tensor per

@@ -62,6 +62,8 @@ _SIGNATURES = {
     "fjagg_karg_image_words": (_i64, [_i64, _i32, _i64]),
     "fjagg_wsum_l2_ptrs_workspace_bytes": (_i64, [_i64, _i64]),
     "fjagg_wsum_l2_ptrs": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _vp, _i32, _vp, _i64, _vp]),
+    "fjagg_wsum_l2_ptrs_rows": (_i32, [_i32, _i32, _i32, _vp, _i32, _i64, _i64, _vp, _f32, _vp, _vp, _i64, _i32, _vp,
+                                       _i64, _vp]),
     "fjagg_server_update_dense": (_i32, [_i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "fjagg_server_update_ptrs": (_i32, [_i32, _vp, _i32, _i64, _i64, _vp, _f32, _vp, _vp, _i32, _vp]),
     "fjagg_wsum_l2_workspace_bytes": (_i64, [_i64, _i64]),

@@ -449,10 +449,18 @@ __global__ __launch_bounds__(kThreads) void k_dense_l2(
 // workgroups, so it is latency-bound: each lane issues a batch of 16 loads before it adds
 // any (one memory round trip per 256 partials per client; the fold's ~256 workgroups are
 // one batch).
+// Where the combined norms go: operand k >= first gets its squared norm in sq[k - first] and,
+// when nrm is set, its correctly rounded square root in nrm[k - first] (IEEE binary32 sqrt, as
+// jnp.sqrt: tree_util.py:111-114). fjagg_wsum_l2_*: {l2sq, nullptr, 0}; fjagg_wsum_l2_ptrs_rows:
+// a deferred running sum's two norm rows, skipping operand 0 (its base).
+struct L2Out {
+  float* sq;
+  float* nrm;
+  int64_t first;
+};
 constexpr int kCombineWaves = 16, kCombineBatch = 16;
 __global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* __restrict__ ws,
-                                                                   int64_t nb, int64_t K,
-                                                                   float* __restrict__ out) {
+                                                                   int64_t nb, int64_t K, L2Out out) {
   __shared__ float part[kCombineWaves][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t k = (int64_t)blockIdx.x * 64 + lane;
@@ -472,12 +480,18 @@ __global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* 
   }
   part[wv][lane] = s;
   __syncthreads();
-  if (wv == 0 && k < K) {
+  if (wv == 0 && k < K && k >= out.first) {
     float t = part[0][lane];
 #pragma unroll
     for (int i = 1; i < kCombineWaves; ++i) t = __fadd_rn(t, part[i][lane]);
-    out[k] = t;
+    if (out.sq) out.sq[k - out.first] = t;
+    if (out.nrm) out.nrm[k - out.first] = __fsqrt_rn(t);
   }
+}
+
+int launch_l2_combine(const float* ws, int64_t nb, int64_t K, L2Out out, hipStream_t s) {
+  hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s, ws, nb, K, out);
+  return check_launch("k_l2_combine");
 }
 
 // Exact fold of the slab + the server optimizer step in the epilogue (no mean
@@ -1378,7 +1392,7 @@ int dense_exact_chunked(int in, int acc, int out, const uint8_t* x, int64_t ld_b
 
 template <int IN, class ACC, int OUT, int V>
 int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w,
-                  float scale, int do_scale, int accumulate, float* ws, float* l2, hipStream_t s) {
+                  float scale, int do_scale, int accumulate, float* ws, L2Out l2, hipStream_t s) {
   const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
   if constexpr (std::is_same<ACC, AccF>::value) {
     if (ws) {  // fused per-client squared l2 norms: block partials, then ordered combine
@@ -1390,9 +1404,7 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true>), dim3((unsigned)nblk), dim3(kThreads), smem,
                            s, img, L, K, wt, scale, do_scale, accumulate, ws, KargWords<1>{});
       if (int rc = check_launch("k_ptrs (l2)")) return rc;
-      hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s,
-                         ws, nblk, K, l2);
-      return check_launch("k_l2_combine");
+      return launch_l2_combine(ws, nblk, K, l2, s);
     }
   }
   // fold schedule as for the dense path (launch_dense_v): interleaved once the plan has
@@ -1432,7 +1444,7 @@ int launch_ptrs_narrow(bool nt, const int64_t* img, int L, int64_t K, int64_t nb
 
 template <int IN, class ACC, int OUT>
 int launch_ptrs_io(bool vec, bool nt, const int64_t* img, int L, int64_t K, int64_t nblk,
-                   const void* w, float scale, int do_scale, int accumulate, float* ws, float* l2,
+                   const void* w, float scale, int do_scale, int accumulate, float* ws, L2Out l2,
                    hipStream_t s) {
   if (vec)
     return launch_ptrs_t<IN, ACC, OUT, vec_width<IN>()>(nt, img, L, K, nblk, w, scale, do_scale,
@@ -1457,9 +1469,7 @@ int launch_dense_l2_t(const DenseArgs& a, float* ws, int64_t ws_floats, float* l
                      a.accumulate, a.out, S, ws);
   int rc = check_launch("k_dense_l2");
   if (rc) return rc;
-  hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((a.K + 63) / 64)), dim3(64 * kCombineWaves), 0, s,
-                     ws, grid, a.K, l2);
-  return check_launch("k_l2_combine");
+  return launch_l2_combine(ws, grid, a.K, L2Out{l2, nullptr, 0}, s);
 }
 
 template <int IN, int OUT>
@@ -1678,7 +1688,7 @@ namespace {
 extern "C++" {
 template <int NW>
 int launch_ptrs_karg_n(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w, float scale,
-                       int ds, int ac, float* ws, float* l2, hipStream_t s) {
+                       int ds, int ac, float* ws, L2Out l2, hipStream_t s) {
   constexpr int IN = FJAGG_F32, OUT = FJAGG_F32, V = 4;
   using ACC = AccF;
   KargWords<NW> ki;
@@ -1696,9 +1706,7 @@ int launch_ptrs_karg_n(bool nt, const int64_t* img, int L, int64_t K, int64_t nb
       hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true, true, NW>), grid, block, smem, s, nullptr, L,
                          K, nullptr, scale, ds, ac, ws, ki);
     if (int rc = check_launch("k_ptrs (l2, kernel-argument image)")) return rc;
-    hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s, ws, nblk, K,
-                       l2);
-    return check_launch("k_l2_combine");
+    return launch_l2_combine(ws, nblk, K, l2, s);
   }
   // the schedule rule of launch_ptrs_t
   const bool burst = nblk < 2 * (int64_t)residency(reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true>)).cus;
@@ -1719,7 +1727,7 @@ int launch_ptrs_karg_n(bool nt, const int64_t* img, int L, int64_t K, int64_t nb
 }  // extern "C++"
 
 int launch_ptrs_karg(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w, float scale,
-                     int ds, int ac, float* ws, float* l2, hipStream_t s) {
+                     int ds, int ac, float* ws, L2Out l2, hipStream_t s) {
   const int64_t words = fjagg_karg_image_words(K, L, nblk);
   if (words <= 1024) return launch_ptrs_karg_n<1024>(nt, img, L, K, nblk, w, scale, ds, ac, ws, l2, s);
   if (words <= 2048) return launch_ptrs_karg_n<2048>(nt, img, L, K, nblk, w, scale, ds, ac, ws, l2, s);
@@ -1728,7 +1736,7 @@ int launch_ptrs_karg(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk
 
 int wsum_ptrs_impl(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,
                    int64_t K, int64_t nblk, const void* w_dev, float scale, int flags, float* ws,
-                   float* l2, void* stream) {
+                   L2Out l2, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const bool vec = !(flags & FJAGG_UNALIGNED);
   const bool nt = (flags & FJAGG_NONTEMPORAL) != 0;
@@ -1794,7 +1802,7 @@ int fjagg_wsum_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* i
   if (nblk < 0 || nblk > 0x7fffffff || !image_dev || !w_dev || L < 1)
     return fail(FJAGG_EINVAL, "bad plan (nblk=%lld, L=%d)", (long long)nblk, L);
   return wsum_ptrs_impl(in_dtype, acc_dtype, out_dtype, image_dev, L, K, nblk, w_dev, scale, flags,
-                        nullptr, nullptr, stream);
+                        nullptr, L2Out{nullptr, nullptr, 0}, stream);
 }
 
 }  // extern "C"
@@ -1851,10 +1859,37 @@ int64_t fjagg_wsum_l2_ptrs_workspace_bytes(int64_t K, int64_t nblk) {
   return (K < 1 || nblk < 1) ? 0 : K * nblk * 4;
 }
 
+namespace {
+int wsum_l2_ptrs_checked(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L, int64_t K,
+                         int64_t nblk, const void* w_dev, float scale, L2Out out, int flags, void* ws_dev,
+                         int64_t ws_bytes, void* stream);
+}  // namespace
+
 int fjagg_wsum_l2_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,
                        int64_t K, int64_t nblk, const void* w_dev, float scale, float* l2sq_dev,
                        int flags, void* ws_dev, int64_t ws_bytes, void* stream) {
   g_err[0] = 0;
+  if (!l2sq_dev) return fail(FJAGG_EINVAL, "null pointer argument");
+  return wsum_l2_ptrs_checked(in_dtype, acc_dtype, out_dtype, image_dev, L, K, nblk, w_dev, scale,
+                              L2Out{l2sq_dev, nullptr, 0}, flags, ws_dev, ws_bytes, stream);
+}
+
+int fjagg_wsum_l2_ptrs_rows(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L,
+                            int64_t K, int64_t nblk, const void* w_dev, float scale, float* sq_dev,
+                            float* norm_dev, int64_t first, int flags, void* ws_dev, int64_t ws_bytes,
+                            void* stream) {
+  g_err[0] = 0;
+  if (!sq_dev && !norm_dev) return fail(FJAGG_EINVAL, "null pointer argument");
+  if (first < 0 || first > K) return fail(FJAGG_EINVAL, "first = %lld outside [0, K]", (long long)first);
+  return wsum_l2_ptrs_checked(in_dtype, acc_dtype, out_dtype, image_dev, L, K, nblk, w_dev, scale,
+                              L2Out{sq_dev, norm_dev, first}, flags, ws_dev, ws_bytes, stream);
+}
+
+}  // extern "C"
+namespace {
+int wsum_l2_ptrs_checked(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L, int64_t K,
+                         int64_t nblk, const void* w_dev, float scale, L2Out out, int flags, void* ws_dev,
+                         int64_t ws_bytes, void* stream) {
   int rc = validate_common(in_dtype, acc_dtype, out_dtype, K, flags, scale);
   if (rc) return rc;
   if (acc_dtype != FJAGG_F32 || in_dtype == FJAGG_I32)
@@ -1863,13 +1898,15 @@ int fjagg_wsum_l2_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t
     return fail(FJAGG_EUNSUPPORTED, "fused l2 norms support K <= %lld", (long long)kL2MaxClients);
   if (nblk < 1 || nblk > 0x7fffffff || !image_dev || !w_dev || L < 1)
     return fail(FJAGG_EINVAL, "bad plan (nblk=%lld, L=%d)", (long long)nblk, L);
-  if (!l2sq_dev || !ws_dev) return fail(FJAGG_EINVAL, "null pointer argument");
+  if (!ws_dev) return fail(FJAGG_EINVAL, "null pointer argument");
   if (ws_bytes < fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk))
     return fail(FJAGG_EINVAL, "l2 workspace too small (need %lld bytes)",
                 (long long)fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk));
   return wsum_ptrs_impl(in_dtype, acc_dtype, out_dtype, image_dev, L, K, nblk, w_dev, scale, flags,
-                        reinterpret_cast<float*>(ws_dev), l2sq_dev, stream);
+                        reinterpret_cast<float*>(ws_dev), out, stream);
 }
+}  // namespace
+extern "C" {
 
 int fjagg_server_update_dense(int in_dtype, const void* x_dev, int64_t ld, int64_t K, int64_t P,
                               const float* w_dev, float scale, const fjagg_server_opt* opt,

@@ -379,6 +379,15 @@ typedef int (*WsumFn)(int, int, int, const int64_t*, int, int64_t, int64_t, cons
 typedef int64_t (*L2WsFn)(int64_t, int64_t);
 typedef int (*WsumL2Fn)(int, int, int, const int64_t*, int, int64_t, int64_t, const void*, float, float*, int, void*,
                         int64_t, void*);
+// fjagg_wsum_l2_ptrs_rows: the norms straight into a chain's two norm rows (operands >= first)
+typedef int (*WsumL2RowsFn)(int, int, int, const int64_t*, int, int64_t, int64_t, const void*, float, float*, float*,
+                            int64_t, int, void*, int64_t, void*);
+struct L2Rows {
+  WsumL2RowsFn fn;
+  float* sq;
+  float* nrm;
+  int64_t first;
+};
 constexpr int kF32 = 0, kScale = 1, kAccumulate = 2, kNontemporal = 4;  // fjagg.h enums
 
 // Fresh output leaves shaped like row0: ONE allocation, each leaf its own tensor (own
@@ -414,9 +423,9 @@ void carve_outputs(const std::vector<at::Tensor>& row0, std::vector<at::Tensor>&
 int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K, const float* wf, double scale,
               bool has_scale, double nt_min_bytes, int dev, unsigned long long stream, PlanFn plan, WsumFn wsum,
               std::vector<at::Tensor>& outs, bool accumulate, WsumL2Fn l2fn, L2WsFn l2ws, float* l2p, int* rc,
-              Stamp& st) {
+              Stamp& st, const L2Rows* rows = nullptr) {
   const int64_t L = static_cast<int64_t>(row0.size());
-  const bool with_l2 = l2p != nullptr;
+  const bool with_l2 = l2p != nullptr || rows != nullptr;
   if (L < 1 || K < 1 || (accumulate && outs.empty())) return 1;
   // fast case only: float32 leaves (fold type and output type are then float32 for any
   // weights). A leaf with a client pointer off 16 bytes walks element units (per-leaf
@@ -504,6 +513,9 @@ int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K,
     ws = at::empty({need > 4 ? need : 4}, outs[0].options().dtype(at::kByte));
   }
   auto launch = [&](const int64_t* image, const int64_t* w, int fl) {
+    if (rows)
+      return rows->fn(kF32, kF32, kF32, image, static_cast<int>(L), K, nblk, w, static_cast<float>(scale), rows->sq,
+                      rows->nrm, rows->first, fl, ws.data_ptr(), ws.numel(), reinterpret_cast<void*>(stream));
     if (with_l2)
       return l2fn(kF32, kF32, kF32, image, static_cast<int>(L), K, nblk, w, static_cast<float>(scale), l2p, fl,
                   ws.data_ptr(), ws.numel(), reinterpret_cast<void*>(stream));
@@ -1208,7 +1220,8 @@ PyObject* table_from_caps(PyObject*, PyObject* args) {
 //     case (nothing launched).
 PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const* weights, Py_ssize_t K, double scale,
                          bool has_scale, double nt_min, unsigned long long plan_addr, unsigned long long wsum_addr,
-                         unsigned long long l2_addr, unsigned long long l2ws_addr, PyObject* l2sq) {
+                         unsigned long long l2_addr, unsigned long long l2ws_addr, PyObject* l2sq,
+                         const L2Rows* rows = nullptr) {
   if (K < 1) Py_RETURN_NONE;
   Stamp st;
   ++g_timer_calls;
@@ -1279,8 +1292,8 @@ PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const*
     int rc = 0;
     if (fold_core(row0, ptrs.data(), K, wf.data(), scale, has_scale, nt_min, dev, stream,
                   reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs, false,
-                  l2p ? reinterpret_cast<WsumL2Fn>(l2_addr) : nullptr, l2p ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr,
-                  l2p, &rc, st) != 0)
+                  l2p ? reinterpret_cast<WsumL2Fn>(l2_addr) : nullptr,
+                  (l2p || rows) ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr, l2p, &rc, st, rows) != 0)
       Py_RETURN_NONE;
     if (rc != 0) return Py_BuildValue("(iO)", rc, Py_None);
     std::vector<PyObject*> wrapped(L);
@@ -2739,9 +2752,9 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
   PyObject* node;
   double scale, nt_min;
   int has_scale;
-  unsigned long long plan_addr, wsum_addr, l2_addr, l2ws_addr, fill_addr = 0;
-  if (!PyArg_ParseTuple(args, "OdpdKKKK|K", &node, &scale, &has_scale, &nt_min, &plan_addr, &wsum_addr, &l2_addr,
-                        &l2ws_addr, &fill_addr))
+  unsigned long long plan_addr, wsum_addr, l2_addr, l2ws_addr, fill_addr = 0, rows_addr = 0;
+  if (!PyArg_ParseTuple(args, "OdpdKKKK|KK", &node, &scale, &has_scale, &nt_min, &plan_addr, &wsum_addr, &l2_addr,
+                        &l2ws_addr, &fill_addr, &rows_addr))
     return nullptr;
   if (!g_fast.ps || Py_TYPE(node) != g_fast.ps) Py_RETURN_NONE;
   thread_local std::vector<PSObject*> links;
@@ -2794,9 +2807,33 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
     if (w) waiting.push_back(j);
   }
   try {
+    // the common case: the run is consecutive links of ONE chain whose norm buffer covers them —
+    // the fold's norm combine writes the buffer's two rows itself (fjagg_wsum_l2_ptrs_rows,
+    // operand 0, the base, skipped): no l2 tensor and no fill launch
+    L2Rows rows{};
+    bool use_rows = false;
+    c10::DeviceIndex rows_dev = -1;
+    if (!waiting.empty() && rows_addr) {
+      PyObject* ch0 = links[0]->chain;
+      bool one = ch0 && Py_TYPE(ch0) == g_fast.chain;
+      for (size_t j = 1; one && j < links.size(); ++j)
+        one = links[j]->chain == ch0 && links[j]->idx == links[0]->idx + static_cast<long long>(j);
+      PyObject* buf = one ? reinterpret_cast<ChainObject*>(ch0)->buf : nullptr;
+      if (buf && THPVariable_Check(buf)) {
+        const at::Tensor& b = THPVariable_Unpack(buf);
+        const int64_t i0 = links[0]->idx, n = static_cast<int64_t>(links.size());
+        if (b.dim() == 2 && b.size(0) == 2 && b.is_contiguous() && b.scalar_type() == at::kFloat && b.is_cuda() &&
+            i0 >= 0 && i0 + n <= b.size(1)) {
+          float* row0 = b.data_ptr<float>() + i0;
+          rows = L2Rows{reinterpret_cast<WsumL2RowsFn>(rows_addr), row0, row0 + b.size(1), 1};
+          use_rows = true;
+          rows_dev = b.get_device();
+        }
+      }
+    }
     at::Tensor l2;
     PyObject* l2obj = Py_None;
-    if (!waiting.empty()) {
+    if (!waiting.empty() && !use_rows) {
       PyObject* t0 = PyTuple_Check(bcap) && PyTuple_GET_SIZE(bcap) > 0 ? PyTuple_GET_ITEM(bcap, 0) : nullptr;
       if (!t0 || !PyTuple_Check(t0) || PyTuple_GET_SIZE(t0) < 1 || !THPVariable_Check(PyTuple_GET_ITEM(t0, 0)))
         Py_RETURN_NONE;
@@ -2806,7 +2843,7 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
     }
     Py_INCREF(base);  // (the walk's references are borrowed from the chain, which `node` holds)
     PyObject* got = fold_caps_impl(base, caps.data(), weights.data(), K, scale, has_scale != 0, nt_min, plan_addr,
-                                   wsum_addr, l2_addr, l2ws_addr, l2obj);
+                                   wsum_addr, l2_addr, l2ws_addr, l2obj, use_rows ? &rows : nullptr);
     Py_DECREF(base);
     if (l2obj != Py_None) Py_DECREF(l2obj);
     if (!got || waiting.empty() || !PyTuple_Check(got) || PyLong_AsLong(PyTuple_GET_ITEM(got, 0)) != 0) return got;
@@ -2814,7 +2851,7 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
     // its address, a copy and a sqrt)
     typedef int (*FillFn)(const float*, float*, float*, int64_t, void*);
     auto fill = reinterpret_cast<FillFn>(fill_addr);
-    for (size_t j = 0; j < links.size();) {
+    for (size_t j = use_rows ? links.size() : 0; j < links.size();) {
       PyObject* ch = links[j]->chain;
       const size_t j0 = j;
       while (j < links.size() && links[j]->chain == ch &&
@@ -2863,7 +2900,7 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
         Py_CLEAR(ch->buf);
         Py_CLEAR(ch->views);
       }
-      if (refill_pool(l2.get_device()) != 0) {
+      if (refill_pool(use_rows ? rows_dev : l2.get_device()) != 0) {
         Py_DECREF(got);
         return nullptr;
       }

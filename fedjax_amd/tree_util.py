@@ -315,15 +315,17 @@ _ENTRY_ADDRS = None  # (plan_leaves, wsum_ptrs, wsum_l2_ptrs, l2 workspace bytes
 
 
 _FILL_ADDR = 0  # fjtree_norms_fill, for fjhost.fold_chain's lazy-norm fill
+_ROWS_ADDR = 0  # fjagg_wsum_l2_ptrs_rows: fjhost.fold_chain's norms straight into a chain's norm rows
 
 
 def _native_fold_addrs() -> None:
-    global _ENTRY_ADDRS, _FILL_ADDR
+    global _ENTRY_ADDRS, _FILL_ADDR, _ROWS_ADDR
     lib = _lib.load()
     _ENTRY_ADDRS = tuple(ctypes.cast(getattr(lib, f), ctypes.c_void_p).value
                          for f in ("fjagg_ptrs_plan_leaves", "fjagg_wsum_ptrs", "fjagg_wsum_l2_ptrs",
                                    "fjagg_wsum_l2_ptrs_workspace_bytes"))
     _FILL_ADDR = ctypes.cast(lib.fjtree_norms_fill, ctypes.c_void_p).value
+    _ROWS_ADDR = ctypes.cast(lib.fjagg_wsum_l2_ptrs_rows, ctypes.c_void_p).value
     _mean_config()
 
 
@@ -906,7 +908,7 @@ def _fold_pending(node: "PendingSum", scale):
         if _ENTRY_ADDRS is None:
             _native_fold_addrs()
         got = _HOST.fold_chain(node, float(np.float32(scale)) if scale is not None else 1.0, scale is not None,
-                               float(NONTEMPORAL_MIN_BYTES), *_ENTRY_ADDRS, _FILL_ADDR)
+                               float(NONTEMPORAL_MIN_BYTES), *_ENTRY_ADDRS, _FILL_ADDR, _ROWS_ADDR)
         if type(got) is int:
             _stale_chain(got)
         if got is not None:

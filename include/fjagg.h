@@ -171,9 +171,11 @@ int64_t fjagg_karg_image_words(int64_t K, int L, int64_t nblk);
  * fjagg_wsum_ptrs fused with every client's squared L2 norm over ALL L leaves, in the
  * same pass (same plan image and nblk as fjagg_wsum_ptrs; the outputs are bitwise
  * the fjagg_wsum_ptrs ones). l2sq_dev[k] = sum over leaves and elements of x^2 in f32,
- * fixed order: lane partial -> wave xor-butterfly -> LDS per wave -> workgroup
- * partials ws[b*K + k] added in workgroup order. Float inputs, float fold, K <= 4096;
- * ws_dev of fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk) bytes.
+ * fixed order: per lane a packed-FMA sum of its units' squares -> the wave's lanes by
+ * v_permlane32_swap / v_permlane16_swap and DPP row rotations (groups of clients at once)
+ * -> LDS per wave -> workgroup partials ws[b*K + k] added in workgroup order (XLA's own
+ * reduction order is not pinned; the tests bound it against an f64 norm). Float inputs,
+ * float fold, K <= 4096; ws_dev of fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk) bytes.
  * Replaces the per-client tree_l2_norm(delta) of examples/fed_avg.py:79-81
  * (tree_util.py:105-114) next to the tree_mean of the same deltas (:82).
  */
@@ -181,6 +183,18 @@ int64_t fjagg_wsum_l2_ptrs_workspace_bytes(int64_t K, int64_t nblk);
 int fjagg_wsum_l2_ptrs(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev,
                        int L, int64_t K, int64_t nblk, const void* w_dev, float scale,
                        float* l2sq_dev, int flags, void* ws_dev, int64_t ws_bytes, void* stream);
+/*
+ * fjagg_wsum_l2_ptrs writing the norms where a deferred running sum's lazy norm views read
+ * them: operand k >= first gets its squared norm in sq_dev[k - first] and its correctly
+ * rounded square root in norm_dev[k - first] (either may be NULL, not both); operands below
+ * `first` are not written. The per-client delta_l2_norm of the library loop
+ * (fedjax/algorithms/fed_avg.py:142-144, tree_util.py:111-114) straight from the fold's norm
+ * combine, without a separate fill launch. 0 <= first <= K.
+ */
+int fjagg_wsum_l2_ptrs_rows(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev,
+                            int L, int64_t K, int64_t nblk, const void* w_dev, float scale,
+                            float* sq_dev, float* norm_dev, int64_t first, int flags, void* ws_dev,
+                            int64_t ws_bytes, void* stream);
 
 /*
  * fjagg_wsum_dense (exact mode) fused with the per-client squared L2 norms of the

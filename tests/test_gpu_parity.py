@@ -1044,6 +1044,60 @@ def test_native_fold_table_is_used_and_declines(cuda):
     assert torch.equal(m["a"], tu.tree_mean(zip([{"a": base[k, 1:].clone()} for k in range(5)], w))["a"])
 
 
+@pytest.mark.parametrize("karg", [False, True])
+def test_wsum_l2_ptrs_rows_writes_the_norm_rows(karg, cuda):
+    """fjagg_wsum_l2_ptrs_rows (the deferred running sum's lazy-norm rows, include/fjagg.h):
+    the mean is bitwise fjagg_wsum_ptrs'; operand k >= first gets fjagg_wsum_l2_ptrs' squared
+    norm (bitwise) in sq[k - first] and its correctly rounded sqrt in nrm[k - first]; nothing
+    below `first`, nor past the K - first written entries, is touched. With the plan image in
+    device memory and in the kernel arguments (FJAGG_HOST_TABLES)."""
+    import ctypes
+    lib = _lib.load()
+    shapes = [(37,), (3, 3, 4), (1000,), (61, 13)]
+    K, L = 7, len(shapes)
+    g = torch.Generator().manual_seed(3)
+    leaves = [[(torch.rand(s, generator=g) - 0.5).to(cuda) for s in shapes] for _ in range(K)]
+    n = np.array([int(np.prod(s)) for s in shapes], dtype=np.int64)
+    outs = [torch.empty(int(v), device=cuda) for v in n]
+    nb = lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, None, 0)
+    blocks = np.empty(2 * nb, dtype=np.int64)
+    lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, blocks.ctypes.data, nb)
+    img = np.concatenate([np.array([[x.data_ptr() for x in r] for r in leaves], dtype=np.int64).ravel(),
+                          np.array([o.data_ptr() for o in outs], dtype=np.int64), n, blocks])
+    wh = np.float32([3, 1, 4, 1, 5, 9, 2])
+    flags = _lib.SCALE | (_lib.HOST_TABLES if karg else 0)
+    if karg:
+        img_p, w_p = img.ctypes.data, wh.ctypes.data
+    else:
+        img_d, w_d = torch.from_numpy(img).to(cuda), torch.from_numpy(wh).to(cuda)
+        img_p, w_p = img_d.data_ptr(), w_d.data_ptr()
+    ws = torch.empty(max(4, lib.fjagg_wsum_l2_ptrs_workspace_bytes(K, nb)), dtype=torch.uint8, device=cuda)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(lib.fjagg_wsum_ptrs(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p, ctypes.c_float(0.04), flags, s),
+               "wsum")
+    mean0 = torch.cat([o.clone() for o in outs])
+    l2 = torch.empty(K, device=cuda)
+    _lib.check(lib.fjagg_wsum_l2_ptrs(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p, ctypes.c_float(0.04),
+                                      l2.data_ptr(), flags, ws.data_ptr(), ws.numel(), s), "l2")
+    for first in (0, 1, 3):
+        rows = torch.full((2, K + 2), -7.0, device=cuda)
+        _lib.check(lib.fjagg_wsum_l2_ptrs_rows(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p,
+                                               ctypes.c_float(0.04), rows.data_ptr(), rows.data_ptr() + 4 * (K + 2),
+                                               first, flags, ws.data_ptr(), ws.numel(), s), "rows")
+        torch.cuda.synchronize()
+        assert torch.equal(torch.cat(outs).view(torch.int32), mean0.view(torch.int32))
+        m = K - first
+        assert torch.equal(rows[0, :m].view(torch.int32), l2[first:].view(torch.int32))
+        want_sqrt = np.sqrt(l2[first:].cpu().numpy())  # IEEE binary32 sqrt, correctly rounded
+        assert np.array_equal(rows[1, :m].cpu().numpy().view(np.uint32), want_sqrt.view(np.uint32))
+        assert bool((rows[:, m:] == -7.0).all())
+    want = np.array([sum(float((x.double() ** 2).sum()) for x in r) for r in leaves])
+    npt.assert_allclose(l2.double().cpu().numpy(), want, rtol=2e-6)
+    bad = lib.fjagg_wsum_l2_ptrs_rows(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p, ctypes.c_float(1.0),
+                                      None, None, 0, flags, ws.data_ptr(), ws.numel(), s)
+    assert bad == -1 and b"null pointer" in lib.fjagg_last_error()  # FJAGG_EINVAL
+
+
 def test_native_fold_table_fused_l2(cuda):
     """fjhost.fold_table with l2sq launches fjagg_wsum_l2_ptrs: the mean and norms are
     bitwise those of the Python fused path, for aligned and misaligned leaves."""
