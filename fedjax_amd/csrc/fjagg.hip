@@ -485,7 +485,7 @@ __global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* 
 #pragma unroll
     for (int i = 1; i < kCombineWaves; ++i) t = __fadd_rn(t, part[i][lane]);
     if (out.sq) out.sq[k - out.first] = t;
-    if (out.nrm) out.nrm[k - out.first] = __fsqrt_rn(t);
+    if (out.nrm) out.nrm[k - out.first] = sqrt_rn(t);  // (__fsqrt_rn measured 1 ulp off on gfx950)
   }
 }
 
@@ -984,7 +984,7 @@ __global__ void k_l2sq_groups(const float* __restrict__ ws, int64_t nb, int64_t 
   if (g >= G) return;
   float s = 0.f;
   for (int64_t i = 0; i < rows_per_group * nb; ++i) s = __fadd_rn(s, ws[g * rows_per_group * nb + i]);
-  out[g] = take_sqrt ? __fsqrt_rn(s) : s;
+  out[g] = take_sqrt ? sqrt_rn(s) : s;  // correctly rounded, via f64
 }
 
 // Synthetic deltas (tests/bench only): bit-identical to oracle/fold_ref.c.

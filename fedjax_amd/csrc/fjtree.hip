@@ -244,7 +244,7 @@ __global__ void k_norms_fill(const float* __restrict__ l2sq, float* __restrict__
   if (i < n) {
     const float v = l2sq[i];
     sq[i] = v;
-    nrm[i] = __fsqrt_rn(v);
+    nrm[i] = (float)sqrt((double)v);  // correctly rounded (p = 53 >= 2*24 + 2); __fsqrt_rn is 1 ulp off at times
   }
 }
 

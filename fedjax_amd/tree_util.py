@@ -1491,7 +1491,7 @@ def tree_mean_with_l2_norms(pytrees_and_weights: Iterable[Tuple[PyTree, float]])
             and 0 < len(pytrees_and_weights) <= _L2_MAX_CLIENTS):
         got = _native_mean(pytrees_and_weights, with_l2=True)
         if got is not None:
-            return got[0], torch.sqrt(got[1])
+            return got[0], _sqrt_rn(got[1])
     trees, weights, sum_weight = _collect_pairs(pytrees_and_weights)
     if not trees:
         return None, None
@@ -1509,7 +1509,17 @@ def tree_mean_with_l2_norms(pytrees_and_weights: Iterable[Tuple[PyTree, float]])
         return pytree.unflatten(td, outs), tree_l2_norms(trees)
     l2sq = torch.empty(len(trees), dtype=torch.float32, device=rows[0][0].device)
     outs = _fold(rows, weights, scale=_inverse(sum_weight), validated=True, l2sq=l2sq)
-    return pytree.unflatten(td, outs), torch.sqrt(l2sq)
+    return pytree.unflatten(td, outs), _sqrt_rn(l2sq)
+
+
+def _sqrt_rn(l2sq: torch.Tensor) -> torch.Tensor:
+    """Correctly rounded float32 square roots of a device vector (jnp.sqrt of the reference's
+    tree_l2_norm, tree_util.py:111-114): one fjtree_norms_fill launch (its f64 route; the
+    single-precision device sqrt can be 1 ulp off)."""
+    out = torch.empty_like(l2sq)
+    _lib.check(_lib.load().fjtree_norms_fill(l2sq.data_ptr(), l2sq.data_ptr(), out.data_ptr(), l2sq.numel(),
+                                             torch.cuda.current_stream(l2sq.device).cuda_stream), "fjtree_norms_fill")
+    return out
 
 
 _L2_MAX_CLIENTS = 4096  # fjagg_wsum_l2_ptrs (kL2MaxClients in fjagg.hip)
