@@ -2276,6 +2276,18 @@ PyObject* fast_tree_weight(PyObject*, PyObject* const* args, Py_ssize_t nargs, P
   return PyObject_Vectorcall(g_fast.py_tree_weight, args, nargs, kwnames);
 }
 
+// Should the pending run ending at p be folded before the next link is appended (an early
+// flush)? (a) it holds >= flush_bytes in >= flush_clients links; or (b) the chain was folded
+// before (an earlier flush), the run holds half of both, and the folds this process issued
+// have finished by the busy estimate: the GPU would otherwise idle while the host walks the rest
+// of the round, and the round's last fold — the part that runs after the loop — gets shorter.
+// tree_util._flush_due states the same rule.
+inline bool flush_due(const PSObject* p) {
+  if (p->bytes >= g_fast.flush_bytes && p->n >= g_fast.flush_clients) return true;
+  return p->idx + 1 > p->n && 2 * p->n >= g_fast.flush_clients && 2 * p->bytes >= g_fast.flush_bytes &&
+         now_s() >= g_mean.busy_until;
+}
+
 // tree_add(left, right): tree_util.tree_add (tree_util.py:47-50). The fast case is the
 // running sum's append, s = tree_add(s, tree_weight(x, n)) with s a live PendingSum at the
 // tip of its chain, the capture's structure token equal to the sum's, and no chain limit
@@ -2298,8 +2310,7 @@ PyObject* fast_tree_add(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyOb
       const long long nb = PyLong_AsLongLong(PyTuple_GET_ITEM(r->cap, 2));
       const long long budget = PyLong_AsLongLong(ch->budget);
       if (PyErr_Occurred()) return nullptr;
-      if (tok == p->tok && p->n + 1 <= g_fast.max_clients && p->bytes + nb <= budget &&
-          !(p->bytes >= g_fast.flush_bytes && p->n >= g_fast.flush_clients)) {
+      if (tok == p->tok && p->n + 1 <= g_fast.max_clients && p->bytes + nb <= budget && !flush_due(p)) {
         auto* q = reinterpret_cast<PSObject*>(g_fast.ps->tp_alloc(g_fast.ps, 0));
         if (!q) return nullptr;
         Py_INCREF(p);
@@ -2476,15 +2487,21 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
             if (rc < 0) return nullptr;
             same = rc == 0 && static_cast<Py_ssize_t>(w.leaves[0].size()) == PyTuple_GET_SIZE(tup);
             for (size_t l = 0; same && l < w.leaves[0].size(); ++l) same = w.leaves[0][l] == PyTuple_GET_ITEM(tup, l);
+            // the captured leaf objects, unmodified since tree_weight (version and storage)
+            int64_t vs = 0;
+            for (Py_ssize_t l = 0; same && l < PyTuple_GET_SIZE(tup); ++l) {
+              const at::Tensor& t = THPVariable_Unpack(PyTuple_GET_ITEM(tup, l));
+              vs += version_of(t);
+              const int64_t cp = captured_ptr(node->cap, l);
+              if (cp && cp != reinterpret_cast<int64_t>(t.data_ptr())) same = false;
+            }
+            same = same && vs == PyLong_AsLongLong(PyTuple_GET_ITEM(node->cap, 1));
           }
-          int64_t vs = 0;
-          for (Py_ssize_t l = 0; same && l < PyTuple_GET_SIZE(tup); ++l) {
-            const at::Tensor& t = THPVariable_Unpack(PyTuple_GET_ITEM(tup, l));
-            vs += version_of(t);
-            const int64_t cp = captured_ptr(node->cap, l);
-            if (cp && cp != reinterpret_cast<int64_t>(t.data_ptr())) same = false;
-          }
-          if (same && vs == PyLong_AsLongLong(PyTuple_GET_ITEM(node->cap, 1))) {
+          // (the captured tree itself, unchanged dicts: its leaves' versions and storages are not
+          // re-read here — the chain's fold checks every captured leaf before it launches and
+          // raises for one modified since tree_weight, so a view is either filled from the
+          // values tree_weight saw or never filled)
+          if (same) {
             if ((!ch->buf || ch->buf == Py_None) && which == 1 && g_fast.pool_buf && g_fast.pool_views) {
               // the chain's first norm: take the pool as the chain's buffer and views (same device,
               // the current chain size)
@@ -2844,6 +2861,12 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
     Py_INCREF(base);  // (the walk's references are borrowed from the chain, which `node` holds)
     PyObject* got = fold_caps_impl(base, caps.data(), weights.data(), K, scale, has_scale != 0, nt_min, plan_addr,
                                    wsum_addr, l2_addr, l2ws_addr, l2obj, use_rows ? &rows : nullptr);
+    if (got && PyTuple_Check(got)) {  // launched: this fold's bytes extend the busy estimate
+      const double now = now_s();
+      const auto* tip = reinterpret_cast<PSObject*>(node);
+      const double bytes = static_cast<double>(tip->bytes) * (1.0 + 1.0 / std::max<long long>(1, tip->n));
+      g_mean.busy_until = std::max(now, g_mean.busy_until) + bytes / g_mean.peak;
+    }
     Py_DECREF(base);
     if (l2obj != Py_None) Py_DECREF(l2obj);
     if (!got || waiting.empty() || !PyTuple_Check(got) || PyLong_AsLong(PyTuple_GET_ITEM(got, 0)) != 0) return got;

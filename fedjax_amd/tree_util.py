@@ -1062,13 +1062,24 @@ def _defer(sum_side, item, item_weight, item_cap):
         budget = parent._chain.budget
         if budget is None:
             budget = parent._chain.budget = _defer_budget(cap[0][0].device)
-        if (parent._n + 1 > _DEFER["max_clients"] or parent._bytes + cap[2] > budget or
-                (parent._bytes >= _DEFER["flush_bytes"] and parent._n >= _DEFER["flush_clients"])):
+        if parent._n + 1 > _DEFER["max_clients"] or parent._bytes + cap[2] > budget or _flush_due(parent):
             parent.materialize()  # bound the chain: fold what is pending, continue from it
             bcap = host.capture(parent._value, -1)
     node = PendingSum(root, parent, cap, item_weight, ref, bcap, tok)
     host.set_last(node)
     return node
+
+
+def _flush_due(p: "PendingSum") -> bool:
+    """An early flush of the pending run ending at ``p`` before the next link (fjhost's
+    flush_due): it holds flush_bytes in flush_clients links, or — when its chain was folded
+    before — half of both while the folds this process issued have finished by the busy
+    estimate (the GPU would idle while the host walks on; the round's last fold gets shorter)."""
+    fb, fc = _DEFER["flush_bytes"], _DEFER["flush_clients"]
+    if p._bytes >= fb and p._n >= fc:
+        return True
+    return (p._idx + 1 > p._n and 2 * p._n >= fc and 2 * p._bytes >= fb
+            and time.perf_counter() >= _BUSY_UNTIL[0])
 
 
 def _tree_weight_py(pytree_: PyTree, weight: float) -> PyTree:

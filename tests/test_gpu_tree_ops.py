@@ -398,6 +398,14 @@ def test_lazy_norm_pool_across_rounds(cuda, sum_mode):
     assert type(v) is not tu._NormView
     np.testing.assert_allclose(float(v), f64norm({"a": xs[0]["a"], "b": {"c": xs[1]["b"]["c"]}}), rtol=2e-6)
     tu.tree_inverse_weight(s, 1.0)
+    # the same dict with a leaf updated in place after tree_weight: the view is lazy, and the
+    # chain's fold refuses the modified capture when the view is read (no stale value is filled)
+    t = {"a": xs[0]["a"].clone(), "b": {"c": xs[0]["b"]["c"].clone()}}
+    s = tu.tree_add(tu.tree_zeros_like(t), tu.tree_weight(t, 1))
+    t["a"].add_(1.0)
+    v = tu.tree_l2_norm(t)
+    with pytest.raises(RuntimeError, match="modified"):
+        float(v)
     H.drop_pool()
 
 
