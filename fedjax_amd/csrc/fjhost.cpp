@@ -2168,6 +2168,7 @@ struct FastState {
   // tree_util.set_deferred_sums
   bool defer = true;
   long long max_clients = 4095, flush_bytes = 256LL << 20, flush_clients = 64;  // (set by fast_config)
+  bool idle_flush = true;
   PyObject* last = nullptr;  // weak reference to the most recent PendingSum link
   // Lazy-norm pool: a norm buffer [2, max_clients + 1] and a list of pre-made (view of
   // buf[1, i], ticket) pairs for i < the norms the last round asked for. Creating a 0-d
@@ -2209,10 +2210,11 @@ PyObject* fast_install(PyObject*, PyObject* args) {
 
 // fast_config(enabled, max_clients, flush_bytes, flush_clients): tree_util.set_deferred_sums
 PyObject* fast_config(PyObject*, PyObject* args) {
-  int en;
+  int en, idle = 1;
   long long mc, fb, fc;
-  if (!PyArg_ParseTuple(args, "pLLL", &en, &mc, &fb, &fc)) return nullptr;
+  if (!PyArg_ParseTuple(args, "pLLL|p", &en, &mc, &fb, &fc, &idle)) return nullptr;
   g_fast.defer = en != 0;
+  g_fast.idle_flush = idle != 0;
   g_fast.max_clients = mc;
   g_fast.flush_bytes = fb;
   g_fast.flush_clients = fc;
@@ -2284,8 +2286,8 @@ PyObject* fast_tree_weight(PyObject*, PyObject* const* args, Py_ssize_t nargs, P
 // tree_util._flush_due states the same rule.
 inline bool flush_due(const PSObject* p) {
   if (p->bytes >= g_fast.flush_bytes && p->n >= g_fast.flush_clients) return true;
-  return p->idx + 1 > p->n && 2 * p->n >= g_fast.flush_clients && 2 * p->bytes >= g_fast.flush_bytes &&
-         now_s() >= g_mean.busy_until;
+  return g_fast.idle_flush && p->idx + 1 > p->n && 2 * p->n >= g_fast.flush_clients &&
+         2 * p->bytes >= g_fast.flush_bytes && now_s() >= g_mean.busy_until;
 }
 
 // tree_add(left, right): tree_util.tree_add (tree_util.py:47-50). The fast case is the
