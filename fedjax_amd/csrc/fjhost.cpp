@@ -2168,7 +2168,6 @@ struct FastState {
   // tree_util.set_deferred_sums
   bool defer = true;
   long long max_clients = 4095, flush_bytes = 256LL << 20, flush_clients = 64;  // (set by fast_config)
-  bool idle_flush = true;
   PyObject* last = nullptr;  // weak reference to the most recent PendingSum link
   // Lazy-norm pool: a norm buffer [2, max_clients + 1] and a list of pre-made (view of
   // buf[1, i], ticket) pairs for i < the norms the last round asked for. Creating a 0-d
@@ -2210,11 +2209,10 @@ PyObject* fast_install(PyObject*, PyObject* args) {
 
 // fast_config(enabled, max_clients, flush_bytes, flush_clients): tree_util.set_deferred_sums
 PyObject* fast_config(PyObject*, PyObject* args) {
-  int en, idle = 1;
+  int en;
   long long mc, fb, fc;
-  if (!PyArg_ParseTuple(args, "pLLL|p", &en, &mc, &fb, &fc, &idle)) return nullptr;
+  if (!PyArg_ParseTuple(args, "pLLL", &en, &mc, &fb, &fc)) return nullptr;
   g_fast.defer = en != 0;
-  g_fast.idle_flush = idle != 0;
   g_fast.max_clients = mc;
   g_fast.flush_bytes = fb;
   g_fast.flush_clients = fc;
@@ -2279,16 +2277,9 @@ PyObject* fast_tree_weight(PyObject*, PyObject* const* args, Py_ssize_t nargs, P
 }
 
 // Should the pending run ending at p be folded before the next link is appended (an early
-// flush)? (a) it holds >= flush_bytes in >= flush_clients links; or (b) the chain was folded
-// before (an earlier flush), the run holds half of both, and the folds this process issued
-// have finished by the busy estimate: the GPU would otherwise idle while the host walks the rest
-// of the round, and the round's last fold — the part that runs after the loop — gets shorter.
-// tree_util._flush_due states the same rule.
-inline bool flush_due(const PSObject* p) {
-  if (p->bytes >= g_fast.flush_bytes && p->n >= g_fast.flush_clients) return true;
-  return g_fast.idle_flush && p->idx + 1 > p->n && 2 * p->n >= g_fast.flush_clients &&
-         2 * p->bytes >= g_fast.flush_bytes && now_s() >= g_mean.busy_until;
-}
+// flush)? It holds >= flush_bytes in >= flush_clients links. tree_util._flush_due states the
+// same rule.
+inline bool flush_due(const PSObject* p) { return p->bytes >= g_fast.flush_bytes && p->n >= g_fast.flush_clients; }
 
 // tree_add(left, right): tree_util.tree_add (tree_util.py:47-50). The fast case is the
 // running sum's append, s = tree_add(s, tree_weight(x, n)) with s a live PendingSum at the

@@ -694,15 +694,13 @@ _DEFER = {"enabled": True, "budget_bytes": None, "max_clients": 4095,
           # and writes the running sum once more: where the GPU bounds the loop (configs[2]'s
           # 16 MiB clients) a flush every 16 clients costs 17 % (2.60 -> 3.08 ms per round), one
           # every >= 64 clients ~1.5 % (profiles/r04q_check/flush_large.json) — hence 64
-          "flush_bytes": 256 << 20, "flush_clients": 64,
-          # a second early flush at half the thresholds while the GPU is idle (round 5, _flush_due)
-          "idle_flush": True}
+          "flush_bytes": 256 << 20, "flush_clients": 64}
 _AUTO_BUDGET = {}  # device index -> automatic budget in bytes
 
 
 def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = None,
                       max_clients: Optional[int] = None, flush_bytes: Optional[int] = None,
-                      flush_clients: Optional[int] = None, idle_flush: Optional[bool] = None) -> None:
+                      flush_clients: Optional[int] = None) -> None:
     """Configure how ``tree_add(s, tree_weight(x, n))`` runs.
 
     Enabled (default): the sum is deferred (:class:`PendingSum`) and folded by ONE
@@ -737,10 +735,7 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
         _DEFER["flush_bytes"] = max(0, int(flush_bytes))
     if flush_clients is not None:
         _DEFER["flush_clients"] = max(1, int(flush_clients))
-    if idle_flush is not None:
-        _DEFER["idle_flush"] = bool(idle_flush)
-    _HOST.fast_config(_DEFER["enabled"], _DEFER["max_clients"], _DEFER["flush_bytes"], _DEFER["flush_clients"],
-                      _DEFER["idle_flush"])
+    _HOST.fast_config(_DEFER["enabled"], _DEFER["max_clients"], _DEFER["flush_bytes"], _DEFER["flush_clients"])
     _HOST.drop_pool()  # (the lazy-norm pool's buffer is sized by max_clients)
 
 
@@ -1077,14 +1072,10 @@ def _defer(sum_side, item, item_weight, item_cap):
 
 def _flush_due(p: "PendingSum") -> bool:
     """An early flush of the pending run ending at ``p`` before the next link (fjhost's
-    flush_due): it holds flush_bytes in flush_clients links, or — when its chain was folded
-    before — half of both while the folds this process issued have finished by the busy
-    estimate (the GPU would idle while the host walks on; the round's last fold gets shorter)."""
-    fb, fc = _DEFER["flush_bytes"], _DEFER["flush_clients"]
-    if p._bytes >= fb and p._n >= fc:
-        return True
-    return (_DEFER["idle_flush"] and p._idx + 1 > p._n and 2 * p._n >= fc and 2 * p._bytes >= fb
-            and time.perf_counter() >= _BUSY_UNTIL[0])
+    flush_due): it holds flush_bytes in flush_clients links. (A second flush at half the
+    thresholds while the GPU is idle was measured and dropped in round 5: synchronised
+    configs[1] rounds 0.218 -> 0.266 ms with norms, profiles/r05_norm_loop/k_ab_idle_flush.jsonl.)"""
+    return p._bytes >= _DEFER["flush_bytes"] and p._n >= _DEFER["flush_clients"]
 
 
 def _tree_weight_py(pytree_: PyTree, weight: float) -> PyTree:
@@ -1201,11 +1192,10 @@ def _tree_add_py(left: PyTree, right: PyTree) -> PyTree:
 # functions above. Per client this is one builtin call each instead of a Python frame, the
 # type tests and a Python object construction.
 _HOST.fast_install(WeightedTree, PendingSum, _Chain, _tree_weight_py, _tree_add_py)
-_HOST.fast_config(_DEFER["enabled"], _DEFER["max_clients"], _DEFER["flush_bytes"], _DEFER["flush_clients"],
-                  _DEFER["idle_flush"])
+_HOST.fast_config(_DEFER["enabled"], _DEFER["max_clients"], _DEFER["flush_bytes"], _DEFER["flush_clients"])
 # set_deferred_sums(True, **DEFERRED_SUM_DEFAULTS) restores the defaults
 DEFERRED_SUM_DEFAULTS = {"max_clients": _DEFER["max_clients"], "flush_bytes": _DEFER["flush_bytes"],
-                         "flush_clients": _DEFER["flush_clients"], "budget_bytes": 0, "idle_flush": True}
+                         "flush_clients": _DEFER["flush_clients"], "budget_bytes": 0}
 tree_weight = _HOST.tree_weight
 tree_add = _HOST.tree_add
 
