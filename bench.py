@@ -239,6 +239,22 @@ def cpu_baseline(K, seconds=6.0):
                       + (f" (cgroup quota: {share} CPUs)" if share else "")}
 
 
+def _back_to_back_ms(call, n, batches=5):
+    """Milliseconds per call of `call` issued back to back: the median over `batches` batches of
+    n // batches calls, each bracketed by a device synchronize (one host stall — a garbage
+    collection, a pinned-memory release — then moves one batch, not the figure)."""
+    per = max(1, n // batches)
+    vals = []
+    for _ in range(batches):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(per):
+            call()
+        torch.cuda.synchronize()
+        vals.append((time.perf_counter() - t0) / per * 1e3)
+    return float(np.median(vals))
+
+
 def dropin_surface(dev, calls=20):
     """The drop-in surface itself, timed in the same run as the headline but outside its
     timed region: what examples/fed_avg.py:82 (tree_mean) and
@@ -304,11 +320,7 @@ def dropin_surface(dev, calls=20):
         tu.tree_mean(pairs)
     torch.cuda.synchronize()
     n = 5 * calls
-    t0 = pc()
-    for _ in range(n):
-        tu.tree_mean(pairs)
-    torch.cuda.synchronize()
-    ms = (pc() - t0) / n * 1e3
+    ms = _back_to_back_ms(lambda: tu.tree_mean(pairs), n)
     res["c1_tree_mean_back_to_back_ms"] = round(ms, 4)
     res["c1_tree_mean_back_to_back_GBs"] = round(K * P * 4 / ms / 1e6, 1)
     single = []
@@ -384,11 +396,7 @@ def dropin_surface(dev, calls=20):
     for _ in range(5):
         tu.tree_mean(pooled)
     torch.cuda.synchronize()
-    t0 = pc()
-    for _ in range(n):
-        tu.tree_mean(pooled)
-    torch.cuda.synchronize()
-    res["c1_default_pool_tree_mean_back_to_back_ms"] = round((pc() - t0) / n * 1e3, 4)
+    res["c1_default_pool_tree_mean_back_to_back_ms"] = round(_back_to_back_ms(lambda: tu.tree_mean(pooled), n), 4)
     single = []
     for _ in range(n):
         torch.cuda.synchronize()
@@ -800,8 +808,6 @@ def main():
     scale = float(np.float32(tu._inverse(W)))
     stream = torch.cuda.current_stream(dev)
     l2sq = torch.empty(Kl, dtype=torch.float32, device=dev) if args.with_norms else None
-    l2ws = torch.empty(max(4, int(kernels._lib.load().fjagg_wsum_l2_workspace_bytes(Kl, P))),
-                       dtype=torch.uint8, device=dev) if args.with_norms else None
     kernel_ms = []
 
     def fold(xs, wd, o, events):
@@ -809,8 +815,7 @@ def main():
             e0, e1 = kernels.Event(), kernels.Event()
             e0.record(stream)
         if args.with_norms:
-            kernels.weighted_sum_l2_dense(xs, wd, scale=scale, out=o, l2sq=l2sq, nontemporal=nt,
-                                          workspace=l2ws)
+            kernels.weighted_sum_l2_dense(xs, wd, scale=scale, out=o, l2sq=l2sq, nontemporal=nt)
         else:
             kernels.weighted_sum_dense(xs, wd, scale=scale, out=o, nontemporal=nt, variant=args.variant,
                                        reference_bf16=args.reference_bf16)

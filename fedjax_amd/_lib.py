@@ -30,6 +30,7 @@ LIB_PATH = os.environ.get("FJAGG_LIB", os.path.join(_HERE, "_build", "libfjagg.s
 F32, BF16, I32 = 0, 1, 2
 # enum fjagg_flags
 SCALE, ACCUMULATE, NONTEMPORAL, UNALIGNED, UNBALANCED, NARROW, HOST_TABLES = 1, 2, 4, 8, 16, 32, 64
+ZEROED_WS = 128  # fused-norm calls: the workspace's 16-byte completion counter is zero (fjagg.h)
 KARG_MAX_WEIGHTS, KARG_MAX_WORDS = 1024, 3584
 # enum fjagg_mode
 MODE_EXACT, MODE_SPLIT = 0, 1

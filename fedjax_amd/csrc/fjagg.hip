@@ -387,14 +387,118 @@ __global__ __launch_bounds__(kThreads, MINW) void k_dense(
   }
 }
 
+// Where the combined norms go: operand k >= first gets its squared norm in sq[k - first] and,
+// when nrm is set, its correctly rounded square root in nrm[k - first] (IEEE binary32 sqrt, as
+// jnp.sqrt: tree_util.py:111-114). fjagg_wsum_l2_*: {l2sq, nullptr, 0}; fjagg_wsum_l2_ptrs_rows:
+// a deferred running sum's two norm rows, skipping operand 0 (its base). done: the completion
+// counter of a FJAGG_ZEROED_WS workspace when the fold's last workgroup combines (combine_last),
+// nullptr when k_l2_combine does.
+struct L2Out {
+  float* sq;
+  float* nrm;
+  int64_t first;
+  unsigned* done;
+};
+constexpr int kCombineWaves = 16, kCombineBatch = 16;
+// The last-workgroup combine serves K <= kFusedCombineMax: partial rows padded to K4 =
+// round_up(K, 4) floats (float4 columns: 16 x K4/4 column sums over 256 lanes, at most two
+// per lane; the pad columns are summed and never written). Above that one workgroup would
+// issue too many dependent loads and k_l2_combine's wider grid wins.
+constexpr int64_t kFusedCombineMax = 128;
+__host__ __device__ __forceinline__ int64_t round4(int64_t K) { return (K + 3) & ~(int64_t)3; }
+
+__device__ __forceinline__ void write_norm(const L2Out& out, int64_t k, float t) {
+  if (k < out.first) return;
+  if (out.sq) out.sq[k - out.first] = t;
+  if (out.nrm) out.nrm[k - out.first] = sqrt_rn(t);  // (__fsqrt_rn measured 1 ulp off on gfx950)
+}
+
+// The completion hand-off of a fused-norm fold whose last workgroup combines (the counter form
+// of the HIP guide's inter-workgroup recipe, no fences): every workgroup stores its partial row
+// write-through (sc1, 4 B per lane), every storing wave drains its stores, the workgroup
+// barrier, then ONE lane adds 1 to the agent-scope counter; the workgroup whose add returns
+// nb - 1 is last, and reads every row with sc1 loads only (they bypass this CU's L1, so no
+// acquire is needed), adds them and re-arms the counter at 0. Placement-independent for one
+// workgroup per CU, which the launchers ensure (grid <= CUs). lds: 16 x K4 floats + the flag.
+// The sum order is k_l2_combine's exactly (column wv of 16 adds partials b = wv, wv+16, ... in
+// order from +0, then the 16 column sums in wv order): bitwise the two-launch norms.
+__device__ __forceinline__ void combine_last(const float* __restrict__ ws, int64_t K, const L2Out& out,
+                                             float* lds) {
+  const int tid = threadIdx.x;
+  const int64_t nb = gridDim.x, K4 = round4(K), q = K4 / 4;
+  unsigned* last = reinterpret_cast<unsigned*>(lds + kCombineWaves * K4);  // in the one dynamic LDS array
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 partials are out
+  __syncthreads();
+  if (tid == 0)
+    *last = __hip_atomic_fetch_add(out.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nb - 1);
+  __syncthreads();
+  if (!*last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below)
+  const auto r = row_rsrc(reinterpret_cast<const uint8_t*>(ws), row_range(nb * K4 * 4));
+  for (int64_t p = tid; p < kCombineWaves * q; p += kThreads) {
+    const int64_t wv = p / q, c = p - wv * q;
+    float4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t b0 = wv; b0 < nb; b0 += (int64_t)kCombineWaves * kCombineBatch) {
+      u32x4 a[kCombineBatch];
+#pragma unroll
+      for (int i = 0; i < kCombineBatch; ++i) {  // rows past nb lie past the range: zeros
+        const int64_t b = b0 + (int64_t)i * kCombineWaves;
+        a[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)((b * q + c) * 16), 0, 16);  // aux 16 = sc1
+      }
+#pragma unroll
+      for (int i = 0; i < kCombineBatch; ++i) {
+        s.x = __fadd_rn(s.x, __uint_as_float(a[i][0]));
+        s.y = __fadd_rn(s.y, __uint_as_float(a[i][1]));
+        s.z = __fadd_rn(s.z, __uint_as_float(a[i][2]));
+        s.w = __fadd_rn(s.w, __uint_as_float(a[i][3]));
+      }
+    }
+    reinterpret_cast<float4*>(lds + wv * K4)[c] = s;
+  }
+  __syncthreads();
+  for (int64_t k = tid; k < K; k += kThreads) {
+    float t = lds[k];
+#pragma unroll
+    for (int i = 1; i < kCombineWaves; ++i) t = __fadd_rn(t, lds[i * K4 + k]);
+    write_norm(out, k, t);
+  }
+  if (tid == 0) __hip_atomic_store(out.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A fused-norm workgroup's epilogue: its (kThreads/64) wave rows of LDS norms -> the partial
+// row ws[b*ld + k] (ld = K; with a completion counter ld = round4(K), sc1 stores, then the
+// last-workgroup combine).
+__device__ __forceinline__ void l2_epilogue(float* l2lds, float* __restrict__ ws, int64_t K, const L2Out& out) {
+  __syncthreads();
+  if (out.done) {
+    const int64_t ld = round4(K);
+    for (int64_t k = threadIdx.x; k < K; k += kThreads) {
+      float t = l2lds[k];
+#pragma unroll
+      for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, l2lds[i * K + k]);
+      __hip_atomic_store(reinterpret_cast<unsigned*>(ws) + (int64_t)blockIdx.x * ld + k, __float_as_uint(t),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through (sc1)
+    }
+    combine_last(ws, K, out, l2lds);  // (its first barrier also ends the reads of l2lds above)
+    return;
+  }
+  for (int64_t k = threadIdx.x; k < K; k += kThreads) {
+    float t = l2lds[k];
+#pragma unroll
+    for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, l2lds[i * K + k]);
+    ws[(int64_t)blockIdx.x * K + k] = t;
+  }
+}
+
 // k_dense + per-client squared norms (exact mode, float fold). Dynamic LDS holds
-// (kThreads/64) x K floats; block b writes its per-client partials to ws[b*K + k]
-// and k_l2_combine adds the gridDim.x partials of each client in block order.
+// (kThreads/64) x K floats (16 x K with a completion counter); block b writes its
+// per-client partials to ws[b*K + k], added in block order by the last workgroup
+// (combine_last) or by k_l2_combine.
 template <int IN, int OUT, int V, int E, int U, bool NT>
 __global__ __launch_bounds__(kThreads) void k_dense_l2(
     const uint8_t* __restrict__ x, int64_t ld_bytes, int64_t K, int64_t nunits, int tail_n,
     const float* __restrict__ w, float scale, int do_scale, int accumulate,
-    uint8_t* __restrict__ out, int64_t S, float* __restrict__ ws) {
+    uint8_t* __restrict__ out, int64_t S, float* __restrict__ ws, const L2Out l2out) {
   extern __shared__ __attribute__((aligned(16))) float l2lds[];
   constexpr int IB = Elem<IN>::B;
   const int tid = threadIdx.x;
@@ -434,13 +538,7 @@ __global__ __launch_bounds__(kThreads) void k_dense_l2(
                                        scale, accumulate != 0, nrm);
     }
   }
-  __syncthreads();
-  for (int64_t k = tid; k < K; k += kThreads) {
-    float t = l2lds[k];
-#pragma unroll
-    for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, l2lds[i * K + k]);
-    ws[(int64_t)blockIdx.x * K + k] = t;
-  }
+  l2_epilogue(l2lds, ws, K, l2out);
 }
 
 // out[k] = sum over b of ws[b*K + k]. Workgroup = 64 clients x 16 waves: wave w sums
@@ -448,17 +546,7 @@ __global__ __launch_bounds__(kThreads) void k_dense_l2(
 // are added in wave order: deterministic. The kernel runs after the fold, on a few
 // workgroups, so it is latency-bound: each lane issues a batch of 16 loads before it adds
 // any (one memory round trip per 256 partials per client; the fold's ~256 workgroups are
-// one batch).
-// Where the combined norms go: operand k >= first gets its squared norm in sq[k - first] and,
-// when nrm is set, its correctly rounded square root in nrm[k - first] (IEEE binary32 sqrt, as
-// jnp.sqrt: tree_util.py:111-114). fjagg_wsum_l2_*: {l2sq, nullptr, 0}; fjagg_wsum_l2_ptrs_rows:
-// a deferred running sum's two norm rows, skipping operand 0 (its base).
-struct L2Out {
-  float* sq;
-  float* nrm;
-  int64_t first;
-};
-constexpr int kCombineWaves = 16, kCombineBatch = 16;
+// one batch). Output as L2Out says (its done is unused here).
 __global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* __restrict__ ws,
                                                                    int64_t nb, int64_t K, L2Out out) {
   __shared__ float part[kCombineWaves][64];
@@ -480,18 +568,24 @@ __global__ __launch_bounds__(64 * kCombineWaves) void k_l2_combine(const float* 
   }
   part[wv][lane] = s;
   __syncthreads();
-  if (wv == 0 && k < K && k >= out.first) {
+  if (wv == 0 && k < K) {
     float t = part[0][lane];
 #pragma unroll
     for (int i = 1; i < kCombineWaves; ++i) t = __fadd_rn(t, part[i][lane]);
-    if (out.sq) out.sq[k - out.first] = t;
-    if (out.nrm) out.nrm[k - out.first] = sqrt_rn(t);  // (__fsqrt_rn measured 1 ulp off on gfx950)
+    write_norm(out, k, t);
   }
 }
 
+// after a fused-norm fold: nothing when its last workgroup combined (out.done), else k_l2_combine
 int launch_l2_combine(const float* ws, int64_t nb, int64_t K, L2Out out, hipStream_t s) {
+  if (out.done) return FJAGG_OK;
   hipLaunchKernelGGL(k_l2_combine, dim3((unsigned)((K + 63) / 64)), dim3(64 * kCombineWaves), 0, s, ws, nb, K, out);
   return check_launch("k_l2_combine");
+}
+
+// dynamic LDS of a fused-norm fold: the wave rows, or combine_last's 16 columns
+inline size_t l2_smem(int64_t K, const L2Out& out) {
+  return out.done ? (size_t)(kCombineWaves * round4(K) + 4) * sizeof(float) : (size_t)(kThreads / 64) * K * sizeof(float);
 }
 
 // Exact fold of the slab + the server optimizer step in the epilogue (no mean
@@ -582,7 +676,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
                                                    int64_t K,
                                                    const typename ACC::T* __restrict__ w_p,
                                                    float scale, int do_scale, int accumulate,
-                                                   float* __restrict__ ws,
+                                                   float* __restrict__ ws, const L2Out l2out,
                                                    const KargWords<(IW > 0 ? IW : 1)> ki) {
   constexpr int IB = Elem<IN>::B;
   const int tid = threadIdx.x;
@@ -631,15 +725,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   } else {
     walk_units<IN, ACC, OUT, V, NT, BURST>(row, row_bytes, K, 0, u1 - u0, ob, w, dsc, scale, acm, nrm, PlainEpi());
   }
-  if constexpr (L2) {
-    __syncthreads();
-    for (int64_t k = tid; k < K; k += kThreads) {
-      float t = l2lds[k];
-#pragma unroll
-      for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, l2lds[i * K + k]);
-      ws[bid * K + k] = t;
-    }
-  }
+  if constexpr (L2) l2_epilogue(l2lds, ws, K, l2out);
 }
 
 // Pytree path + server optimizer step in the epilogue (fjagg_server_update_ptrs): the
@@ -1396,13 +1482,14 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
   const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
   if constexpr (std::is_same<ACC, AccF>::value) {
     if (ws) {  // fused per-client squared l2 norms: block partials, then ordered combine
-      const size_t smem = (size_t)(kThreads / 64) * K * sizeof(float);
+      if (nblk > cu_count()) l2.done = nullptr;  // combine_last's hand-off: one workgroup per CU
+      const size_t smem = l2_smem(K, l2);
       if (nt)
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true>), dim3((unsigned)nblk), dim3(kThreads), smem, s,
-                           img, L, K, wt, scale, do_scale, accumulate, ws, KargWords<1>{});
+                           img, L, K, wt, scale, do_scale, accumulate, ws, l2, KargWords<1>{});
       else
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true>), dim3((unsigned)nblk), dim3(kThreads), smem,
-                           s, img, L, K, wt, scale, do_scale, accumulate, ws, KargWords<1>{});
+                           s, img, L, K, wt, scale, do_scale, accumulate, ws, l2, KargWords<1>{});
       if (int rc = check_launch("k_ptrs (l2)")) return rc;
       return launch_l2_combine(ws, nblk, K, l2, s);
     }
@@ -1412,16 +1499,16 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
   const bool burst = nblk < 2 * (int64_t)residency(reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true>)).cus;
   if (nt && burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr, KargWords<1>{});
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, L2Out{}, KargWords<1>{});
   else if (nt)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr, KargWords<1>{});
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, L2Out{}, KargWords<1>{});
   else if (burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr, KargWords<1>{});
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, L2Out{}, KargWords<1>{});
   else
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, false>), dim3((unsigned)nblk), dim3(kThreads), 0, s,
-                       img, L, K, wt, scale, do_scale, accumulate, nullptr, KargWords<1>{});
+                       img, L, K, wt, scale, do_scale, accumulate, nullptr, L2Out{}, KargWords<1>{});
   return check_launch("k_ptrs");
 }
 
@@ -1453,28 +1540,32 @@ int launch_ptrs_io(bool vec, bool nt, const int64_t* img, int L, int64_t K, int6
 }
 
 template <int IN, int OUT, int V, int E, int U, bool NT>
-int launch_dense_l2_t(const DenseArgs& a, float* ws, int64_t ws_floats, float* l2, hipStream_t s) {
+int launch_dense_l2_t(const DenseArgs& a, float* ws, int64_t ws_floats, L2Out l2, hipStream_t s) {
   auto kern = k_dense_l2<IN, OUT, V, E, U, NT>;
-  const size_t smem = (size_t)(kThreads / 64) * a.K * sizeof(float);
+  size_t smem = l2_smem(a.K, l2);
   int64_t S = (int64_t)kThreads * E, nblk = 0;
   balanced_grid(residency(reinterpret_cast<const void*>(kern), smem), a.nunits, (int64_t)kThreads * E,
                 1, &S, &nblk);
   if (a.nunits == 0) nblk = 0;
   const int64_t grid = nblk + (a.tail_n > 0 ? 1 : 0);
-  if (grid * a.K > ws_floats)
+  if (l2.done && grid > cu_count()) {  // combine_last's hand-off: one workgroup per CU
+    l2.done = nullptr;
+    smem = l2_smem(a.K, l2);
+  }
+  if (grid * (l2.done ? round4(a.K) : a.K) > ws_floats)
     return fail(FJAGG_EINVAL, "l2 workspace too small (%lld workgroups x %lld clients)",
                 (long long)grid, (long long)a.K);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), smem, s, a.x, a.ld_bytes, a.K,
                      a.nunits, a.tail_n, reinterpret_cast<const float*>(a.w), a.scale, a.do_scale,
-                     a.accumulate, a.out, S, ws);
+                     a.accumulate, a.out, S, ws, l2);
   int rc = check_launch("k_dense_l2");
   if (rc) return rc;
-  return launch_l2_combine(ws, grid, a.K, L2Out{l2, nullptr, 0}, s);
+  return launch_l2_combine(ws, grid, a.K, l2, s);
 }
 
 template <int IN, int OUT>
 int launch_dense_l2_io(bool vec, bool nt, int variant, const DenseArgs& a, float* ws,
-                       int64_t ws_floats, float* l2, hipStream_t s) {
+                       int64_t ws_floats, L2Out l2, hipStream_t s) {
   constexpr int VW = vec_width<IN>();
   if (!vec)
     return nt ? launch_dense_l2_t<IN, OUT, 1, 1, 8, true>(a, ws, ws_floats, l2, s)
@@ -1513,7 +1604,8 @@ int launch_dense_opt_io(bool vec, bool nt, int variant, const DenseArgs& a, cons
             : launch_dense_opt_t<IN, VW, 1, 8, false>(a, epi, s);
 }
 
-constexpr int64_t kL2MaxClients = 4096;  // (kThreads/64) x K floats of LDS <= 64 KiB
+constexpr int64_t kL2MaxClients = 4096;
+constexpr int64_t kL2Header = 16;  // fused-norm workspaces: the FJAGG_ZEROED_WS completion counter  // (kThreads/64) x K floats of LDS <= 64 KiB
 
 }  // namespace
 
@@ -1698,13 +1790,14 @@ int launch_ptrs_karg_n(bool nt, const int64_t* img, int L, int64_t K, int64_t nb
   std::memcpy(ki.w + nimg, w, sizeof(float) * (size_t)K);
   const dim3 grid((unsigned)nblk), block(kThreads);
   if (ws) {
-    const size_t smem = (size_t)(kThreads / 64) * K * sizeof(float);
+    if (nblk > cu_count()) l2.done = nullptr;  // combine_last's hand-off: one workgroup per CU
+    const size_t smem = l2_smem(K, l2);
     if (nt)
       hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true, true, NW>), grid, block, smem, s, nullptr, L,
-                         K, nullptr, scale, ds, ac, ws, ki);
+                         K, nullptr, scale, ds, ac, ws, l2, ki);
     else
       hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, true, true, NW>), grid, block, smem, s, nullptr, L,
-                         K, nullptr, scale, ds, ac, ws, ki);
+                         K, nullptr, scale, ds, ac, ws, l2, ki);
     if (int rc = check_launch("k_ptrs (l2, kernel-argument image)")) return rc;
     return launch_l2_combine(ws, nblk, K, l2, s);
   }
@@ -1712,16 +1805,16 @@ int launch_ptrs_karg_n(bool nt, const int64_t* img, int L, int64_t K, int64_t nb
   const bool burst = nblk < 2 * (int64_t)residency(reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true>)).cus;
   if (nt && burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, true, NW>), grid, block, 0, s, nullptr, L, K,
-                       nullptr, scale, ds, ac, nullptr, ki);
+                       nullptr, scale, ds, ac, nullptr, L2Out{}, ki);
   else if (nt)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, false, false, NW>), grid, block, 0, s, nullptr, L, K,
-                       nullptr, scale, ds, ac, nullptr, ki);
+                       nullptr, scale, ds, ac, nullptr, L2Out{}, ki);
   else if (burst)
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, true, NW>), grid, block, 0, s, nullptr, L, K,
-                       nullptr, scale, ds, ac, nullptr, ki);
+                       nullptr, scale, ds, ac, nullptr, L2Out{}, ki);
   else
     hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, false, false, false, NW>), grid, block, 0, s, nullptr, L, K,
-                       nullptr, scale, ds, ac, nullptr, ki);
+                       nullptr, scale, ds, ac, nullptr, L2Out{}, ki);
   return check_launch("k_ptrs (kernel-argument image)");
 }
 }  // extern "C++"
@@ -1856,10 +1949,22 @@ int fjagg_server_update_ptrs(int in_dtype, const int64_t* image_dev, int L, int6
 }
 
 int64_t fjagg_wsum_l2_ptrs_workspace_bytes(int64_t K, int64_t nblk) {
-  return (K < 1 || nblk < 1) ? 0 : K * nblk * 4;
+  return (K < 1 || nblk < 1) ? 0 : kL2Header + round4(K) * nblk * 4;
 }
 
 namespace {
+// The norm partials of a fused-norm call and where its combine runs: with FJAGG_ZEROED_WS the
+// workspace's first kL2Header bytes are the completion counter (zero between calls) and the
+// partials follow; the fold's last workgroup combines when K fits combine_last.
+L2Out l2_layout(L2Out out, void* ws_dev, int64_t K, int flags, float** ws) {
+  *ws = reinterpret_cast<float*>(ws_dev);
+  if (!(flags & FJAGG_ZEROED_WS)) return out;
+  *ws += kL2Header / 4;
+  if (K <= kFusedCombineMax && reinterpret_cast<uintptr_t>(ws_dev) % 16 == 0)
+    out.done = reinterpret_cast<unsigned*>(ws_dev);
+  return out;
+}
+
 int wsum_l2_ptrs_checked(int in_dtype, int acc_dtype, int out_dtype, const int64_t* image_dev, int L, int64_t K,
                          int64_t nblk, const void* w_dev, float scale, L2Out out, int flags, void* ws_dev,
                          int64_t ws_bytes, void* stream);
@@ -1902,8 +2007,10 @@ int wsum_l2_ptrs_checked(int in_dtype, int acc_dtype, int out_dtype, const int64
   if (ws_bytes < fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk))
     return fail(FJAGG_EINVAL, "l2 workspace too small (need %lld bytes)",
                 (long long)fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk));
-  return wsum_ptrs_impl(in_dtype, acc_dtype, out_dtype, image_dev, L, K, nblk, w_dev, scale, flags,
-                        reinterpret_cast<float*>(ws_dev), out, stream);
+  float* ws = nullptr;
+  out = l2_layout(out, ws_dev, K, flags, &ws);
+  return wsum_ptrs_impl(in_dtype, acc_dtype, out_dtype, image_dev, L, K, nblk, w_dev, scale, flags, ws, out,
+                        stream);
 }
 }  // namespace
 extern "C" {
@@ -1955,7 +2062,7 @@ int64_t fjagg_wsum_l2_workspace_bytes(int64_t K, int64_t P) {
     cus = 256;
   (void)hipGetLastError();
   const int64_t max_blocks = (int64_t)cus * (2048 / kThreads) + 1;  // resident cap + tail block
-  return max_blocks * K * 4;
+  return kL2Header + max_blocks * round4(K) * 4;
 }
 
 int fjagg_wsum_l2_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_dev, int64_t ld,
@@ -1996,14 +2103,15 @@ int fjagg_wsum_l2_dense(int in_dtype, int acc_dtype, int out_dtype, const void* 
   const int variant = pick_variant(a.nunits, K);
   const bool nt = (flags & FJAGG_NONTEMPORAL) != 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  float* ws = reinterpret_cast<float*>(ws_dev);
-  const int64_t wsf = ws_bytes / 4;
+  float* ws = nullptr;
+  const L2Out l2 = l2_layout(L2Out{l2sq_dev, nullptr, 0, nullptr}, ws_dev, K, flags, &ws);
+  const int64_t wsf = (ws_bytes - (flags & FJAGG_ZEROED_WS ? kL2Header : 0)) / 4;
   if (in_dtype == FJAGG_F32 && out_dtype == FJAGG_F32)
-    return launch_dense_l2_io<FJAGG_F32, FJAGG_F32>(vec, nt, variant, a, ws, wsf, l2sq_dev, s);
+    return launch_dense_l2_io<FJAGG_F32, FJAGG_F32>(vec, nt, variant, a, ws, wsf, l2, s);
   if (in_dtype == FJAGG_BF16 && out_dtype == FJAGG_BF16)
-    return launch_dense_l2_io<FJAGG_BF16, FJAGG_BF16>(vec, nt, variant, a, ws, wsf, l2sq_dev, s);
+    return launch_dense_l2_io<FJAGG_BF16, FJAGG_BF16>(vec, nt, variant, a, ws, wsf, l2, s);
   if (in_dtype == FJAGG_BF16 && out_dtype == FJAGG_F32)
-    return launch_dense_l2_io<FJAGG_BF16, FJAGG_F32>(vec, nt, variant, a, ws, wsf, l2sq_dev, s);
+    return launch_dense_l2_io<FJAGG_BF16, FJAGG_F32>(vec, nt, variant, a, ws, wsf, l2, s);
   return fail(FJAGG_EUNSUPPORTED, "fused l2 norms: unsupported dtype combination");
 }
 

@@ -420,6 +420,23 @@ void carve_outputs(const std::vector<at::Tensor>& row0, std::vector<at::Tensor>&
 // else the destinations (float32, contiguous, row0's shapes and device). Returns 0 with the
 // library status in *rc (launched), 1 when the case does not hold (nothing launched).
 // Throws on torch errors.
+// The fused-norm workspace of (device, stream): FJAGG_ZEROED_WS layout, its 16-byte completion
+// counter zeroed once on the stream when the buffer is (re)allocated and left zero by every
+// launch, so the fold's last workgroup adds the norm partials (no combine launch, fjagg.h).
+// Launches on one stream are ordered, so they share it; a grown buffer's predecessor goes
+// back to torch's stream-ordered allocator.
+at::Tensor l2_workspace(int dev, unsigned long long stream, int64_t need) {
+  static auto* m = new std::unordered_map<uint64_t, at::Tensor>();
+  at::Tensor& ws = (*m)[static_cast<uint64_t>(stream) ^ (static_cast<uint64_t>(dev) << 56)];
+  if (!ws.defined() || ws.numel() < need) {
+    ws = at::empty({std::max<int64_t>(need * 2, 4096)},
+                   at::TensorOptions().dtype(at::kByte).device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)));
+    if (hipMemsetAsync(ws.data_ptr(), 0, 16, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+      throw std::runtime_error("fused-norm workspace: hipMemsetAsync failed");
+  }
+  return ws;
+}
+
 int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K, const float* wf, double scale,
               bool has_scale, double nt_min_bytes, int dev, unsigned long long stream, PlanFn plan, WsumFn wsum,
               std::vector<at::Tensor>& outs, bool accumulate, WsumL2Fn l2fn, L2WsFn l2ws, float* l2p, int* rc,
@@ -505,12 +522,12 @@ int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K,
   };
   const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
   const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0) |
-                    (narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0);
-  at::Tensor ws;  // fused l2 norms: per-workgroup partials, from torch's allocator (stream-ordered)
+                    (narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0) | (with_l2 ? FJAGG_ZEROED_WS : 0);
+  at::Tensor ws;  // fused l2 norms: counter header + per-workgroup partials (l2_workspace)
   if (with_l2) {
     const int64_t need = l2ws(K, nblk);
     if (need < 0) return 1;
-    ws = at::empty({need > 4 ? need : 4}, outs[0].options().dtype(at::kByte));
+    ws = l2_workspace(dev, stream, need);
   }
   auto launch = [&](const int64_t* image, const int64_t* w, int fl) {
     if (rows)

@@ -178,16 +178,33 @@ def weighted_sum_l2_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[f
         l2sq = torch.empty(K, dtype=torch.float32, device=x.device)
     dev = _require_device(x, w, out, l2sq)
     need = int(_lib.load().fjagg_wsum_l2_workspace_bytes(K, P))
-    if workspace is None or workspace.numel() * workspace.element_size() < need:
-        workspace = torch.empty(max(need, 4), dtype=torch.uint8, device=dev)
     flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
     flags |= _lib.NONTEMPORAL if nontemporal else 0
+    if workspace is None:  # the stream's zeroed-counter workspace: the fold's last workgroup combines
+        workspace = _l2_workspace(dev, need)
+        flags |= _lib.ZEROED_WS
+    elif workspace.numel() * workspace.element_size() < need:  # (a caller's workspace: two launches)
+        workspace = torch.empty(max(need, 4), dtype=torch.uint8, device=dev)
     ld = x.stride(0) if K > 1 else P
     _lib.call("fjagg_wsum_l2_dense", dtype_code(x.dtype), _lib.F32, dtype_code(out.dtype), x.data_ptr(),
               ld, K, P, w.data_ptr(), float(scale if scale is not None else 1.0), out.data_ptr(),
               l2sq.data_ptr(), flags, workspace.data_ptr(), workspace.numel() * workspace.element_size(),
               _stream_handle(dev))
     return out, l2sq
+
+
+_L2_WS = {}  # (device index, stream handle) -> fused-norm workspace, counter header zero
+
+
+def _l2_workspace(dev: torch.device, need: int) -> torch.Tensor:
+    """The FJAGG_ZEROED_WS workspace of ``dev``'s current stream (fjagg.h): zeroed when it is
+    (re)allocated; every fused-norm launch leaves its 16-byte completion counter zero, and
+    launches on one stream are ordered, so they share it."""
+    key = (dev.index, _stream_handle(dev))
+    ws = _L2_WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = _L2_WS[key] = torch.zeros(max(2 * need, 4096), dtype=torch.uint8, device=dev)
+    return ws
 
 
 def split_workspace_bytes(K: int, P: int) -> int:

@@ -82,6 +82,14 @@ enum fjagg_flags {
                                  no FJAGG_NARROW), fjagg_karg_image_words(K, L, nblk) <=
                                  FJAGG_KARG_MAX_WORDS. Anything else returns FJAGG_EUNSUPPORTED
                                  (nothing launched): upload the tables and call without the flag. */
+  FJAGG_ZEROED_WS = 1 << 7,   /* fused-norm calls (fjagg_wsum_l2_*): the workspace's first 16 bytes
+                                 are a completion counter that is zero before the call — zero it
+                                 once when the workspace is allocated; every call leaves it zero —
+                                 and the norm partials follow it. With K <= 128 and a 16-byte
+                                 aligned workspace the fold's last workgroup then adds the
+                                 partials itself, with no second (combine) launch; the norms are
+                                 bitwise the same either way. Without the flag the 16 bytes are
+                                 unused. As always, one workspace serves one call at a time. */
 };
 /* kernel-argument capacity of FJAGG_HOST_TABLES launches */
 #define FJAGG_KARG_MAX_WEIGHTS 1024 /* dense path: 4 KiB of weights */
@@ -174,8 +182,9 @@ int64_t fjagg_karg_image_words(int64_t K, int L, int64_t nblk);
  * fixed order: per lane a packed-FMA sum of its units' squares -> the wave's lanes by
  * v_permlane32_swap / v_permlane16_swap and DPP row rotations (groups of clients at once)
  * -> LDS per wave -> workgroup partials ws[b*K + k] added in workgroup order (XLA's own
- * reduction order is not pinned; the tests bound it against an f64 norm). Float inputs,
- * float fold, K <= 4096; ws_dev of fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk) bytes.
+ * reduction order is not pinned; the tests bound it against an f64 norm) by a second launch,
+ * or by the fold's last workgroup under FJAGG_ZEROED_WS. Float inputs, float fold, K <= 4096;
+ * ws_dev of fjagg_wsum_l2_ptrs_workspace_bytes(K, nblk) bytes.
  * Replaces the per-client tree_l2_norm(delta) of examples/fed_avg.py:79-81
  * (tree_util.py:105-114) next to the tree_mean of the same deltas (:82).
  */

@@ -1044,6 +1044,91 @@ def test_native_fold_table_is_used_and_declines(cuda):
     assert torch.equal(m["a"], tu.tree_mean(zip([{"a": base[k, 1:].clone()} for k in range(5)], w))["a"])
 
 
+@pytest.mark.parametrize("K", [4, 65, 100, 128, 129])
+def test_last_workgroup_combine_matches_two_launches(K, cuda):
+    """FJAGG_ZEROED_WS (include/fjagg.h): the fold's last workgroup adds the norm partials
+    (K <= 128, partial rows padded to 4 floats; above, the flag only moves the partials past
+    the counter). The
+    norms are bitwise those of the two-launch path (k_l2_combine), the means bitwise the plain
+    fold's, the counter is left zero — over calls that alternate two input sets (a stale partial
+    of the previous call would show as that call's norms), with the image in device memory and
+    in the kernel arguments, through fjagg_wsum_l2_ptrs and fjagg_wsum_l2_ptrs_rows."""
+    import ctypes
+    lib = _lib.load()
+    shapes = [(32,), (3, 3, 1, 32), (64,), (3, 3, 32, 64), (128,), (9216, 128), (62,), (128, 62)]
+    L = len(shapes)
+    n = np.array([int(np.prod(s)) for s in shapes], dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum((n + 3) // 4 * 4)])  # every leaf 16-byte aligned
+    sets = []
+    for seed in (5, 6):
+        x = torch.empty(K, int(offs[-1]), device=cuda)
+        kernels.fill_synth(x, seed=seed)
+        sets.append([[x[k, offs[l]:offs[l] + n[l]] for l in range(L)] for k in range(K)])
+    outs = [torch.empty(int(v), device=cuda) for v in n]
+    nb = lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, None, 0)
+    assert nb > 64  # many workgroups: the last-arrival order matters
+    blocks = np.empty(2 * nb, dtype=np.int64)
+    lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, blocks.ctypes.data, nb)
+    wh = np.float32(np.random.RandomState(K).randint(1, 50, size=K))
+    need = lib.fjagg_wsum_l2_ptrs_workspace_bytes(K, nb)
+    ws0, ws1 = torch.zeros(need, dtype=torch.uint8, device=cuda), torch.empty(need, dtype=torch.uint8, device=cuda)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    sc = ctypes.c_float(0.25)
+    karg_ok = lib.fjagg_karg_image_words(K, L, nb) <= 3584  # FJAGG_KARG_MAX_WORDS
+    for call in range(6):
+        leaves = sets[call % 2]
+        karg = karg_ok and call >= 2
+        img = np.concatenate([np.array([[t.data_ptr() for t in r] for r in leaves], dtype=np.int64).ravel(),
+                              np.array([o.data_ptr() for o in outs], dtype=np.int64), n, blocks])
+        if karg:
+            img_p, w_p, flags = img.ctypes.data, wh.ctypes.data, _lib.SCALE | _lib.HOST_TABLES
+        else:
+            img_d, w_d = torch.from_numpy(img).to(cuda), torch.from_numpy(wh).to(cuda)
+            img_p, w_p, flags = img_d.data_ptr(), w_d.data_ptr(), _lib.SCALE
+        _lib.check(lib.fjagg_wsum_ptrs(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p, sc, flags, s), "wsum")
+        mean0 = torch.cat([o.clone() for o in outs])
+        two, last = torch.empty(K, device=cuda), torch.empty(K, device=cuda)
+        _lib.check(lib.fjagg_wsum_l2_ptrs(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p, sc, two.data_ptr(),
+                                          flags, ws1.data_ptr(), need, s), "two launches")
+        _lib.check(lib.fjagg_wsum_l2_ptrs(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p, sc, last.data_ptr(),
+                                          flags | _lib.ZEROED_WS, ws0.data_ptr(), need, s), "last workgroup")
+        rows = torch.full((2, K), -7.0, device=cuda)
+        _lib.check(lib.fjagg_wsum_l2_ptrs_rows(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p, sc,
+                                               rows.data_ptr(), rows.data_ptr() + 4 * K, 1, flags | _lib.ZEROED_WS,
+                                               ws0.data_ptr(), need, s), "rows, last workgroup")
+        torch.cuda.synchronize()
+        assert torch.equal(torch.cat(outs).view(torch.int32), mean0.view(torch.int32))
+        assert torch.equal(last.view(torch.int32), two.view(torch.int32)), f"call {call}"
+        assert torch.equal(rows[0, :K - 1].view(torch.int32), two[1:].view(torch.int32))
+        assert bool((rows[:, K - 1] == -7.0).all())
+        assert int(ws0[:16].count_nonzero()) == 0
+        want = np.array([sum(float((t.double() ** 2).sum()) for t in r) for r in leaves])
+        npt.assert_allclose(last.double().cpu().numpy(), want, rtol=2e-6)
+
+
+@pytest.mark.parametrize("K", [64, 128, 97])
+def test_dense_last_workgroup_combine(K, cuda):
+    """kernels.weighted_sum_l2_dense without a workspace uses the stream's zeroed-counter one
+    (the last workgroup combines); with a caller's workspace, two launches: bitwise the same
+    norms and mean, alternating two slabs."""
+    P = 1206590
+    xs = []
+    for seed in (1, 2):
+        x = torch.empty(K, (P + 3) // 4 * 4, device=cuda)[:, :P]
+        kernels.fill_synth(x, seed=seed)
+        xs.append(x)
+    w = torch.arange(1, K + 1, dtype=torch.float32, device=cuda)
+    ws = torch.empty(int(_lib.load().fjagg_wsum_l2_workspace_bytes(K, P)), dtype=torch.uint8, device=cuda)
+    for call in range(4):
+        x = xs[call % 2]
+        o1, n1 = kernels.weighted_sum_l2_dense(x, w, scale=0.5)
+        o2, n2 = kernels.weighted_sum_l2_dense(x, w, scale=0.5, workspace=ws)
+        torch.cuda.synchronize()
+        assert torch.equal(o1.view(torch.int32), o2.view(torch.int32))
+        assert torch.equal(n1.view(torch.int32), n2.view(torch.int32)), f"call {call}"
+        npt.assert_allclose(n1[:8].double().cpu().numpy(), (x[:8].double() ** 2).sum(1).cpu().numpy(), rtol=2e-6)
+
+
 @pytest.mark.parametrize("karg", [False, True])
 def test_wsum_l2_ptrs_rows_writes_the_norm_rows(karg, cuda):
     """fjagg_wsum_l2_ptrs_rows (the deferred running sum's lazy-norm rows, include/fjagg.h):
