@@ -659,28 +659,43 @@ struct PWalk {
 // same insertion order: a small cache keyed by those key pointers (held by strong
 // references, so a pointer is never a reused address) gives the sorted list without a
 // PyDict_Keys + sort per dict node per call. Guarded by the GIL like every entry point.
-PyObject* sorted_keys(PyObject* x, bool* unorderable) {
+// vals (optional, room for kSortedVals): on a cache hit of a dict of at most kSortedVals
+// entries, x's values in sorted-key order (borrowed), collected by the same insertion-order
+// scan that matched the keys — the walk then does no hash lookups on operand 0; *have_vals
+// says whether they were filled.
+constexpr Py_ssize_t kSortedVals = 32;
+PyObject* sorted_keys(PyObject* x, bool* unorderable, PyObject** vals = nullptr, bool* have_vals = nullptr) {
   struct Entry {
     std::vector<PyObject*> order;  // strong references, insertion order
     PyObject* sorted;              // strong reference
+    std::vector<uint8_t> perm;     // sorted position j -> insertion index (dicts of <= kSortedVals keys)
   };
   static std::vector<Entry> cache;
   static size_t next_slot = 0;
   constexpr size_t kCap = 64;
   *unorderable = false;
+  if (have_vals) *have_vals = false;
   const Py_ssize_t n = PyDict_GET_SIZE(x);
+  PyObject* ins[kSortedVals];
+  const bool collect = vals && n <= kSortedVals;
   for (const Entry& e : cache) {
     if (static_cast<Py_ssize_t>(e.order.size()) != n) continue;
     Py_ssize_t pos = 0, i = 0;
     PyObject *k, *v;
     bool same = true;
     while (PyDict_Next(x, &pos, &k, &v)) {
-      if (k != e.order[i++]) {
+      if (k != e.order[i]) {
         same = false;
         break;
       }
+      if (collect) ins[i] = v;
+      ++i;
     }
     if (same) {
+      if (collect && static_cast<Py_ssize_t>(e.perm.size()) == n) {
+        for (Py_ssize_t j = 0; j < n; ++j) vals[j] = ins[e.perm[j]];
+        *have_vals = true;
+      }
       Py_INCREF(e.sorted);
       return e.sorted;
     }
@@ -699,6 +714,17 @@ PyObject* sorted_keys(PyObject* x, bool* unorderable) {
   while (PyDict_Next(x, &pos, &k, &v)) {
     Py_INCREF(k);
     e.order.push_back(k);
+  }
+  if (n <= kSortedVals && static_cast<Py_ssize_t>(e.order.size()) == n && PyList_GET_SIZE(keys) == n) {
+    for (Py_ssize_t j = 0; j < n; ++j) {
+      Py_ssize_t i = 0;
+      while (i < n && e.order[i] != PyList_GET_ITEM(keys, j)) ++i;
+      if (i == n) {  // (a key compared equal but is another object: no permutation)
+        e.perm.clear();
+        break;
+      }
+      e.perm.push_back(static_cast<uint8_t>(i));
+    }
   }
   Py_INCREF(keys);
   e.sorted = keys;
@@ -740,9 +766,11 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
     const Py_ssize_t n = PyDict_GET_SIZE(x0);
     for (int k = 1; k < K; ++k)
       if (!PyDict_CheckExact(xs[k]) || PyDict_GET_SIZE(xs[k]) != n) return 1;
-    bool unorderable = false;
-    PyObject* keys = sorted_keys(x0, &unorderable);
+    bool unorderable = false, have0 = false;
+    PyObject* v0[kSortedVals];
+    PyObject* keys = sorted_keys(x0, &unorderable, v0, &have0);
     if (!keys) return unorderable ? 1 : -1;  // unorderable keys: the Python path decides
+    if (w.keys.capacity() == 0) w.keys.reserve(8);
     w.keys.push_back(keys);
     if (w.dicts) w.dicts->push_back(x0);
     if (w.sig) {
@@ -753,7 +781,7 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
     for (Py_ssize_t i = 0; i < n; ++i) {
       PyObject* key = PyList_GET_ITEM(keys, i);
       for (int k = 0; k < K; ++k) {
-        vals[k] = PyDict_GetItemWithError(xs[k], key);
+        vals[k] = (k == 0 && have0) ? v0[i] : PyDict_GetItemWithError(xs[k], key);
         if (!vals[k]) {
           if (PyErr_Occurred()) PyErr_Clear();
           return 1;
@@ -899,8 +927,17 @@ struct SigHash {
 int64_t structure_token(const std::vector<int64_t>& sig, const PWalk& w) {
   static auto* table = new std::unordered_map<std::vector<int64_t>, int64_t, SigHash>();
   constexpr size_t kMaxTokens = 4096;
+  // one client pytree after another has the previous one's structure: compare with it first
+  // (its key objects are alive: the table entry of its token holds them)
+  static std::vector<int64_t> last_sig;
+  static int64_t last_tok = -1;
+  if (last_tok >= 0 && sig == last_sig) return last_tok;
   auto it = table->find(sig);
-  if (it != table->end()) return it->second;
+  if (it != table->end()) {
+    last_sig = sig;
+    last_tok = it->second;
+    return it->second;
+  }
   if (table->size() >= kMaxTokens) return -1;
   for (PyObject* kl : w.keys)  // keep the key objects alive for as long as the entry exists
     for (Py_ssize_t i = 0; i < PyList_GET_SIZE(kl); ++i) Py_INCREF(PyList_GET_ITEM(kl, i));
