@@ -971,6 +971,15 @@ inline int64_t captured_ptr(PyObject* cap, Py_ssize_t l) {
   return reinterpret_cast<const int64_t*>(PyBytes_AS_STRING(b))[l];
 }
 
+// All L captured data pointers of a capture (element 4), or nullptr when it has none: the
+// per-leaf loops of the folds read them without re-checking the tuple per leaf.
+inline const int64_t* captured_ptrs(PyObject* cap, Py_ssize_t L) {
+  if (PyTuple_GET_SIZE(cap) < 5) return nullptr;
+  PyObject* b = PyTuple_GET_ITEM(cap, 4);
+  if (!PyBytes_Check(b) || PyBytes_GET_SIZE(b) < 8 * L) return nullptr;
+  return reinterpret_cast<const int64_t*>(PyBytes_AS_STRING(b));
+}
+
 // Capture element 5: the tree's dict nodes in pre-order as int64 pairs (address, CPython
 // dict version tag), bytes — or None when the tree is not dicts over leaves (a list / tuple
 // node, or a leaf at the root). A dict's version tag (PEP 509) changes with every mutation
@@ -1247,12 +1256,12 @@ PyObject* table_from_caps(PyObject*, PyObject* args) {
       PyObject* tup = PyTuple_GET_ITEM(cap, 0);
       if (PyTuple_GET_SIZE(tup) != L) return PyLong_FromSsize_t(k);
       int64_t vs = 0;
+      const int64_t* cps = captured_ptrs(cap, L);
       for (Py_ssize_t l = 0; l < L; ++l) {
         const at::Tensor& t = THPVariable_Unpack(PyTuple_GET_ITEM(tup, l));
         vs += version_of(t);
         out[k * L + l] = reinterpret_cast<int64_t>(t.data_ptr());
-        const int64_t cp = captured_ptr(cap, l);
-        if (cp && cp != out[k * L + l]) return PyLong_FromSsize_t(k);  // storage moved (`.data =`)
+        if (cps && cps[l] != out[k * L + l]) return PyLong_FromSsize_t(k);  // storage moved (`.data =`)
       }
       if (vs != PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1))) return PyLong_FromSsize_t(k);
     }
@@ -1306,6 +1315,7 @@ PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const*
       PyObject* tup = PyTuple_GET_ITEM(cap, 0);
       if (!PyTuple_Check(tup) || PyTuple_GET_SIZE(tup) != L) return PyLong_FromSsize_t(k);
       int64_t vs = 0;
+      const int64_t* cps = captured_ptrs(cap, L);
       for (Py_ssize_t l = 0; l < L; ++l) {
         PyObject* o = PyTuple_GET_ITEM(tup, l);
         if (!THPVariable_Check(o)) Py_RETURN_NONE;
@@ -1324,8 +1334,7 @@ PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const*
         }
         vs += version_of(t);
         ptrs[k * L + l] = reinterpret_cast<int64_t>(t.data_ptr());
-        const int64_t cp = captured_ptr(cap, l);
-        if (cp && cp != ptrs[k * L + l]) return PyLong_FromSsize_t(k);  // storage moved (`.data =`)
+        if (cps && cps[l] != ptrs[k * L + l]) return PyLong_FromSsize_t(k);  // storage moved (`.data =`)
       }
       const long long want = PyLong_AsLongLong(PyTuple_GET_ITEM(cap, 1));
       if (want == -1 && PyErr_Occurred()) return nullptr;

@@ -1,7 +1,8 @@
 """Host cost of the per-client tree_l2_norm in the library loop (fedjax/algorithms/fed_avg.py:
 137-144) at configs[1], split into its parts: the loop with and without the norm call, and the
 pieces the native fast path does per call (the structure walk against the capture, the 0-d view
-TensorImpl, wrapping it as the _NormView subclass, the _ticket attribute). Host time only:
+TensorImpl, wrapping it as the _NormView subclass, the _ticket attribute), and the fold phases of
+each round's final call (fjhost.host_timers: checks, outputs, plan, image, launch, ...). Host time only:
 microseconds per client, median of `reps` rounds of 128 clients. One JSON line.
 usage: python tools/prof_norm_call.py [reps]"""
 import json
@@ -41,6 +42,7 @@ def main(reps=40, K=128):
     res = {}
 
     phases = {}
+    timers = {}  # norm -> fjhost.host_timers() of each round's final call (fold_chain's phases)
 
     def loop(norm):
         torch.cuda.synchronize()
@@ -52,8 +54,10 @@ def main(reps=40, K=128):
             if norm:
                 norms.append(tu.tree_l2_norm(t))
         t1 = pc()
+        host.host_timers()  # reset: the final call's fold phases only
         m = tu.tree_inverse_weight(s, W)
         t2 = pc()
+        timers.setdefault(norm, []).append(host.host_timers())
         torch.cuda.synchronize()
         t3 = pc()
         key = "norms" if norm else "plain"
@@ -94,6 +98,10 @@ def main(reps=40, K=128):
         res[f"round_{key}_us"] = {"zeros": round(a[0], 1), "loop": round(a[1], 1), "final_call": round(a[2], 1),
                                   "sync_wait": round(a[3], 1), "total": round(a[4], 1),
                                   "pool_refill_in_final_call": round(a[5] / 1e6, 1)}
+    for norm, rows in timers.items():
+        keys = [k for k in rows[0] if k != "calls"]
+        res[f"final_call_fold_phases_{'norms' if norm else 'plain'}_us"] = {
+            k: round(float(np.median([r[k] for r in rows[3:]])), 2) for k in keys}
     info = host.pool_info()
     res["pool"] = {"refills_reusing_a_pool": info[4], "refills_building_one": info[5], "retired": info[3]}
     print(json.dumps(res), flush=True)
