@@ -946,8 +946,8 @@ int64_t structure_token(const std::vector<int64_t>& sig, const PWalk& w) {
   return tok;
 }
 
-// capture(tree, dev) -> (leaves_tuple, version_sum, nbytes, token, data_ptrs) | None   (dev = -1: the first
-//     leaf's)
+// capture(tree, dev) -> (leaves_tuple, version_sum, nbytes, token, data_ptrs[+ dict tags], has_tags) | None
+//     (dev = -1: the first leaf's)
 //     tree_weight's lazy result holds its input's leaves (strong references, flatten order)
 //     and their version sum, so the fold can check that nothing changed in between; token
 //     (structure_token) lets tree_add match two captured trees' structures without a walk.
@@ -980,40 +980,49 @@ inline const int64_t* captured_ptrs(PyObject* cap, Py_ssize_t L) {
   return reinterpret_cast<const int64_t*>(PyBytes_AS_STRING(b));
 }
 
-// Capture element 5: the tree's dict nodes in pre-order as int64 pairs (address, CPython
-// dict version tag), bytes — or None when the tree is not dicts over leaves (a list / tuple
-// node, or a leaf at the root). A dict's version tag (PEP 509) changes with every mutation
-// and is never reused, so while the root is the same object and every tag is unchanged,
-// walking the tree again would give the captured leaves: tree_l2_norm of the delta just
-// added checks that instead of re-walking (same_tree). Visiting in pre-order means a dict is
-// dereferenced only after its parent — which still holds it — was found unchanged.
-PyObject* dict_tags(const PWalk& w, PyObject* root) {
+// The dict tags of a capture: its tree's dict nodes in pre-order as int64 pairs (address,
+// CPython dict version tag), appended to element 4 after the L data pointers, element 5 then
+// True (None when the tree is not dicts over leaves: a list / tuple node, or a leaf at the
+// root; one bytes object per capture, not two). A dict's version tag (PEP 509) changes with
+// every mutation and is never reused, so while the root is the same object and every tag is
+// unchanged, walking the tree again would give the captured leaves: tree_l2_norm of the delta
+// just added checks that instead of re-walking (same_tree). Visiting in pre-order means a dict
+// is dereferenced only after its parent — which still holds it — was found unchanged.
+bool has_dict_tags(const PWalk& w, PyObject* root) {
 #if PY_VERSION_HEX < 0x030C0000
-  if (!w.dicts || w.seq_nodes || w.dicts->empty() || (*w.dicts)[0] != root) Py_RETURN_NONE;
-  const size_t n = w.dicts->size();
-  PyObject* b = PyBytes_FromStringAndSize(nullptr, static_cast<Py_ssize_t>(16 * n));
-  if (!b) return nullptr;
-  auto* p = reinterpret_cast<int64_t*>(PyBytes_AS_STRING(b));
-  for (size_t i = 0; i < n; ++i) {
-    PyObject* d = (*w.dicts)[i];
-    p[2 * i] = reinterpret_cast<int64_t>(d);
-    p[2 * i + 1] = static_cast<int64_t>(reinterpret_cast<PyDictObject*>(d)->ma_version_tag);
-  }
-  return b;
+  return w.dicts && !w.seq_nodes && !w.dicts->empty() && (*w.dicts)[0] == root;
 #else
   (void)w, (void)root;
-  Py_RETURN_NONE;
+  return false;
 #endif
 }
 
-// tree is the captured tree, unchanged (capture element 5): true, or false = not known.
+// Element 4 of a capture: the L data pointers, then (with_tags) the dict tags.
+PyObject* ptr_tag_bytes(const PWalk& w, Py_ssize_t L, bool with_tags) {
+  const Py_ssize_t n = with_tags ? static_cast<Py_ssize_t>(w.dicts->size()) : 0;
+  PyObject* b = PyBytes_FromStringAndSize(nullptr, 8 * L + 16 * n);
+  if (!b) return nullptr;
+  auto* p = reinterpret_cast<int64_t*>(PyBytes_AS_STRING(b));
+  for (Py_ssize_t l = 0; l < L; ++l) p[l] = reinterpret_cast<int64_t>(THPVariable_Unpack(w.leaves[0][l]).data_ptr());
+#if PY_VERSION_HEX < 0x030C0000
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* d = (*w.dicts)[i];
+    p[L + 2 * i] = reinterpret_cast<int64_t>(d);
+    p[L + 2 * i + 1] = static_cast<int64_t>(reinterpret_cast<PyDictObject*>(d)->ma_version_tag);
+  }
+#endif
+  return b;
+}
+
+// tree is the captured tree, unchanged (the capture's dict tags): true, or false = not known.
 bool same_tree(PyObject* tree, PyObject* cap) {
 #if PY_VERSION_HEX < 0x030C0000
-  if (PyTuple_GET_SIZE(cap) < 6) return false;
-  PyObject* b = PyTuple_GET_ITEM(cap, 5);
-  if (!PyBytes_CheckExact(b) || PyBytes_GET_SIZE(b) < 16) return false;
-  const auto* p = reinterpret_cast<const int64_t*>(PyBytes_AS_STRING(b));
-  const Py_ssize_t n = PyBytes_GET_SIZE(b) / 16;
+  if (PyTuple_GET_SIZE(cap) < 6 || PyTuple_GET_ITEM(cap, 5) != Py_True) return false;
+  PyObject* b = PyTuple_GET_ITEM(cap, 4);
+  const Py_ssize_t L = PyTuple_GET_SIZE(PyTuple_GET_ITEM(cap, 0));
+  if (!PyBytes_CheckExact(b) || PyBytes_GET_SIZE(b) < 8 * L + 16) return false;
+  const auto* p = reinterpret_cast<const int64_t*>(PyBytes_AS_STRING(b)) + L;
+  const Py_ssize_t n = (PyBytes_GET_SIZE(b) - 8 * L) / 16;
   if (p[0] != reinterpret_cast<int64_t>(tree) || !PyDict_CheckExact(tree)) return false;
   for (Py_ssize_t i = 0; i < n; ++i)
     if (static_cast<int64_t>(reinterpret_cast<PyDictObject*>(p[2 * i])->ma_version_tag) != p[2 * i + 1]) return false;
@@ -1022,6 +1031,24 @@ bool same_tree(PyObject* tree, PyObject* cap) {
   (void)tree, (void)cap;
   return false;
 #endif
+}
+
+// nbytes as a Python int: one client pytree after another has the same size, so the last
+// object is handed out again (ints are immutable).
+PyObject* nbytes_long(int64_t nbytes) {
+  static int64_t last = -1;
+  static PyObject* obj = nullptr;
+  if (obj && nbytes == last) {
+    Py_INCREF(obj);
+    return obj;
+  }
+  PyObject* o = PyLong_FromLongLong(nbytes);
+  if (!o) return nullptr;
+  Py_XDECREF(obj);
+  Py_INCREF(o);
+  obj = o;
+  last = nbytes;
+  return o;
 }
 
 // New reference: the capture tuple, Py_None (not the fast case), or nullptr (Python error).
@@ -1062,14 +1089,16 @@ PyObject* capture_impl(PyObject* tree, int dev) {
       for (int64_t s : t.sizes()) sig.push_back(s);
     }
     const int64_t tok = structure_token(sig, w);
+    const bool tags = has_dict_tags(w, tree);
     PyObject* out = PyTuple_New(6);
     PyObject* a = PyLong_FromLongLong(vs);
-    PyObject* b = PyLong_FromLongLong(nbytes);
+    PyObject* b = nbytes_long(nbytes);
     PyObject* c = PyLong_FromLongLong(tok);
-    PyObject* d = ptr_bytes(w.leaves[0].data(), L);
-    PyObject* e = dict_tags(w, tree);
-    if (!out || !a || !b || !c || !d || !e) {
-      Py_XDECREF(out), Py_XDECREF(a), Py_XDECREF(b), Py_XDECREF(c), Py_XDECREF(d), Py_XDECREF(e), Py_DECREF(tup);
+    PyObject* d = ptr_tag_bytes(w, L, tags);
+    PyObject* e = tags ? Py_True : Py_None;
+    Py_INCREF(e);
+    if (!out || !a || !b || !c || !d) {
+      Py_XDECREF(out), Py_XDECREF(a), Py_XDECREF(b), Py_XDECREF(c), Py_XDECREF(d), Py_DECREF(e), Py_DECREF(tup);
       return nullptr;
     }
     PyTuple_SET_ITEM(out, 0, tup);
