@@ -29,6 +29,16 @@ def test_header_and_binding_agree():
     assert header_symbols() == set(_lib.SYMBOLS)
 
 
+def test_flag_values_match_the_header():
+    """The ctypes layer's flag constants are fjagg.h's `enum fjagg_flags` values."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADERS[0]).read(), flags=re.S)
+    enum = re.search(r"enum fjagg_flags \{(.*?)\};", src, re.S).group(1)
+    values = {name: 1 << int(bit) for name, bit in re.findall(r"FJAGG_(\w+)\s*=\s*1\s*<<\s*(\d+)", enum)}
+    assert values == {n: getattr(_lib, n) for n in values}
+    assert set(values) == {"SCALE", "ACCUMULATE", "NONTEMPORAL", "UNALIGNED", "UNBALANCED", "NARROW", "HOST_TABLES",
+                           "ZEROED_WS"}
+
+
 def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
