@@ -1106,12 +1106,12 @@ def test_last_workgroup_combine_matches_two_launches(K, cuda):
         npt.assert_allclose(last.double().cpu().numpy(), want, rtol=2e-6)
 
 
-@pytest.mark.parametrize("K", [64, 128, 97])
-def test_dense_last_workgroup_combine(K, cuda):
+@pytest.mark.parametrize("K,P", [(64, 1206590), (128, 1206590), (97, 1206590), (8, 1 << 25)])
+def test_dense_last_workgroup_combine(K, P, cuda):
     """kernels.weighted_sum_l2_dense without a workspace uses the stream's zeroed-counter one
-    (the last workgroup combines); with a caller's workspace, two launches: bitwise the same
+    (the last workgroup combines; a grid of more workgroups than CUs falls back to the combine
+    launch with the flag's layout); with a caller's workspace, two launches: bitwise the same
     norms and mean, alternating two slabs."""
-    P = 1206590
     xs = []
     for seed in (1, 2):
         x = torch.empty(K, (P + 3) // 4 * 4, device=cuda)[:, :P]
@@ -1127,6 +1127,42 @@ def test_dense_last_workgroup_combine(K, cuda):
         assert torch.equal(o1.view(torch.int32), o2.view(torch.int32))
         assert torch.equal(n1.view(torch.int32), n2.view(torch.int32)), f"call {call}"
         npt.assert_allclose(n1[:8].double().cpu().numpy(), (x[:8].double() ** 2).sum(1).cpu().numpy(), rtol=2e-6)
+
+
+def test_last_workgroup_combine_many_leaves(cuda):
+    """A plan of more workgroups than CUs (one or more per leaf: 300 leaves) keeps the
+    FJAGG_ZEROED_WS layout but combines in a second launch: norms bitwise the plain two-launch
+    call's, the counter untouched."""
+    import ctypes
+    lib = _lib.load()
+    K, L = 12, 300
+    g = torch.Generator().manual_seed(11)
+    leaves = [[(torch.rand(40 + 8 * l, generator=g) - 0.5).to(cuda) for l in range(L)] for _ in range(K)]
+    n = np.array([40 + 8 * l for l in range(L)], dtype=np.int64)
+    outs = [torch.empty(int(v), device=cuda) for v in n]
+    nb = lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, None, 0)
+    assert nb >= L
+    blocks = np.empty(2 * nb, dtype=np.int64)
+    lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, blocks.ctypes.data, nb)
+    img = torch.from_numpy(np.concatenate([np.array([[x.data_ptr() for x in r] for r in leaves],
+                                                    dtype=np.int64).ravel(),
+                                           np.array([o.data_ptr() for o in outs], dtype=np.int64), n,
+                                           blocks])).to(cuda)
+    w = torch.arange(1, K + 1, dtype=torch.float32, device=cuda)
+    need = lib.fjagg_wsum_l2_ptrs_workspace_bytes(K, nb)
+    ws0, ws1 = torch.zeros(need, dtype=torch.uint8, device=cuda), torch.empty(need, dtype=torch.uint8, device=cuda)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    a, b = torch.empty(K, device=cuda), torch.empty(K, device=cuda)
+    _lib.check(lib.fjagg_wsum_l2_ptrs(_lib.F32, _lib.F32, _lib.F32, img.data_ptr(), L, K, nb, w.data_ptr(),
+                                      ctypes.c_float(1.0), a.data_ptr(), 0, ws1.data_ptr(), need, s), "two launches")
+    _lib.check(lib.fjagg_wsum_l2_ptrs(_lib.F32, _lib.F32, _lib.F32, img.data_ptr(), L, K, nb, w.data_ptr(),
+                                      ctypes.c_float(1.0), b.data_ptr(), _lib.ZEROED_WS, ws0.data_ptr(), need, s),
+               "flag, many workgroups")
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    assert int(ws0[:16].count_nonzero()) == 0
+    want = np.array([sum(float((x.double() ** 2).sum()) for x in r) for r in leaves])
+    npt.assert_allclose(b.double().cpu().numpy(), want, rtol=2e-6)
 
 
 @pytest.mark.parametrize("karg", [False, True])
