@@ -427,7 +427,9 @@ void carve_outputs(const std::vector<at::Tensor>& row0, std::vector<at::Tensor>&
 // back to torch's stream-ordered allocator.
 at::Tensor l2_workspace(int dev, unsigned long long stream, int64_t need) {
   static auto* m = new std::unordered_map<uint64_t, at::Tensor>();
-  at::Tensor& ws = (*m)[static_cast<uint64_t>(stream) ^ (static_cast<uint64_t>(dev) << 56)];
+  const uint64_t key = static_cast<uint64_t>(stream) ^ (static_cast<uint64_t>(dev) << 56);
+  if (m->size() >= 16 && !m->count(key)) m->clear();  // many short-lived streams: keep the map bounded
+  at::Tensor& ws = (*m)[key];
   if (!ws.defined() || ws.numel() < need) {
     ws = at::empty({std::max<int64_t>(need * 2, 4096)},
                    at::TensorOptions().dtype(at::kByte).device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)));

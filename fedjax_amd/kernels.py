@@ -202,6 +202,8 @@ def _l2_workspace(dev: torch.device, need: int) -> torch.Tensor:
     launches on one stream are ordered, so they share it."""
     key = (dev.index, _stream_handle(dev))
     ws = _L2_WS.get(key)
+    if ws is None and len(_L2_WS) >= 16:  # many short-lived streams: keep the cache bounded
+        _L2_WS.clear()
     if ws is None or ws.numel() < need:
         ws = _L2_WS[key] = torch.zeros(max(2 * need, 4096), dtype=torch.uint8, device=dev)
     return ws
