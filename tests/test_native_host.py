@@ -155,3 +155,27 @@ def test_native_whole_call_declines(pairs):
     assert _mean_pairs(pairs) is None
     assert _mean_pairs(tuple(pairs)) is None
     assert _lib.host().server_pairs(pairs, {"w": torch.zeros(5)}, None, None, None, 0, 0.0, 0, 0) is None
+
+
+def test_walk_visits_dict_values_in_sorted_key_order_on_every_call():
+    """The native walk's sorted-key cache also hands out operand 0's dict values in sorted-key
+    order (fjhost sorted_keys: the insertion-order scan that matches the key objects collects
+    them). The same key objects in different insertion orders, dicts up to and past the 32 keys
+    that path serves, the cache-miss walk and the cache-hit ones: every walk visits the leaves in
+    jax's flatten order (fjhost.matches compares them with the flatten-order leaf tuple)."""
+    import random
+    rnd = random.Random(5)
+    for n in (1, 2, 5, 31, 32, 33, 40):
+        names = [f"k{i:02d}" for i in range(n)]  # one set of key objects per size
+        inner = ["w", "b", "a"] if n <= 16 else ["w"]  # (the fast walk takes <= 64 leaves)
+        for _ in range(3):
+            order, inner_order = names[:], inner[:]
+            rnd.shuffle(order)
+            rnd.shuffle(inner_order)
+            tree = {k: {j: torch.zeros(1) for j in inner_order} for k in order}
+            flat = tuple(tree[k][j] for k in sorted(names) for j in sorted(inner))
+            assert flat == tuple(pytree.flatten(tree)[0])
+            vs = sum(x._version for x in flat)
+            for _ in range(3):
+                assert H.matches(tree, flat, vs)
+            assert not H.matches(tree, flat[::-1], vs)
