@@ -523,8 +523,16 @@ int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K,
     return true;
   };
   const bool nt = static_cast<double>(total) * K * 4 >= nt_min_bytes;
+  // FJAGG_L2_COMBINE_LAUNCH=1 keeps the separate norm-combine launch (no FJAGG_ZEROED_WS): the
+  // in-launch hand-off follows the HIP guide's measured recipe for gfx950, which HIP itself does
+  // not promise; the norms are bitwise the same either way
+  static const bool combine_launch = [] {
+    const char* e = getenv("FJAGG_L2_COMBINE_LAUNCH");
+    return e && e[0] == '1';
+  }();
   const int flags = (has_scale ? kScale : 0) | (nt ? kNontemporal : 0) | (accumulate ? kAccumulate : 0) |
-                    (narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0) | (with_l2 ? FJAGG_ZEROED_WS : 0);
+                    (narrow ? (FJAGG_NARROW | FJAGG_VARIANT(svar)) : 0) |
+                    (with_l2 && !combine_launch ? FJAGG_ZEROED_WS : 0);
   at::Tensor ws;  // fused l2 norms: counter header + per-workgroup partials (l2_workspace)
   if (with_l2) {
     const int64_t need = l2ws(K, nblk);

@@ -9,6 +9,7 @@ deltas, an unsupported dtype or a missing library raise.
 
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -180,9 +181,11 @@ def weighted_sum_l2_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[f
     need = int(_lib.load().fjagg_wsum_l2_workspace_bytes(K, P))
     flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
     flags |= _lib.NONTEMPORAL if nontemporal else 0
-    if workspace is None:  # the stream's zeroed-counter workspace: the fold's last workgroup combines
-        workspace = _l2_workspace(dev, need)
+    if workspace is None and not _L2_COMBINE_LAUNCH:  # the stream's zeroed-counter workspace: the
+        workspace = _l2_workspace(dev, need)           # fold's last workgroup combines
         flags |= _lib.ZEROED_WS
+    elif workspace is None:
+        workspace = torch.empty(max(need, 4), dtype=torch.uint8, device=dev)
     elif workspace.numel() * workspace.element_size() < need:  # (a caller's workspace: two launches)
         workspace = torch.empty(max(need, 4), dtype=torch.uint8, device=dev)
     ld = x.stride(0) if K > 1 else P
@@ -194,6 +197,9 @@ def weighted_sum_l2_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[f
 
 
 _L2_WS = {}  # (device index, stream handle) -> fused-norm workspace, counter header zero
+# FJAGG_L2_COMBINE_LAUNCH=1: keep the separate norm-combine launch (as fjhost; include/fjagg.h
+# FJAGG_ZEROED_WS): the in-launch hand-off follows the HIP guide's measured gfx950 recipe
+_L2_COMBINE_LAUNCH = os.environ.get("FJAGG_L2_COMBINE_LAUNCH", "0") == "1"
 
 
 def _l2_workspace(dev: torch.device, need: int) -> torch.Tensor:

@@ -89,7 +89,8 @@ enum fjagg_flags {
                                  aligned workspace the fold's last workgroup then adds the
                                  partials itself, with no second (combine) launch; the norms are
                                  bitwise the same either way. Without the flag the 16 bytes are
-                                 unused. As always, one workspace serves one call at a time. */
+                                 unused. As always, one workspace serves one call at a time.
+                                 (fedjax_amd's callers pass it unless FJAGG_L2_COMBINE_LAUNCH=1.) */
 };
 /* kernel-argument capacity of FJAGG_HOST_TABLES launches */
 #define FJAGG_KARG_MAX_WEIGHTS 1024 /* dense path: 4 KiB of weights */

@@ -1129,6 +1129,21 @@ def test_dense_last_workgroup_combine(K, P, cuda):
         npt.assert_allclose(n1[:8].double().cpu().numpy(), (x[:8].double() ** 2).sum(1).cpu().numpy(), rtol=2e-6)
 
 
+def test_combine_launch_switch(cuda, monkeypatch):
+    """FJAGG_L2_COMBINE_LAUNCH=1 (kernels._L2_COMBINE_LAUNCH) keeps the separate combine launch
+    for weighted_sum_l2_dense's own workspace: the same bits as the in-launch combine."""
+    K, P = 64, 300007
+    x = torch.empty(K, (P + 3) // 4 * 4, device=cuda)[:, :P]
+    kernels.fill_synth(x, seed=4)
+    w = torch.arange(1, K + 1, dtype=torch.float32, device=cuda)
+    o1, n1 = kernels.weighted_sum_l2_dense(x, w, scale=0.25)
+    monkeypatch.setattr(kernels, "_L2_COMBINE_LAUNCH", True)
+    o2, n2 = kernels.weighted_sum_l2_dense(x, w, scale=0.25)
+    torch.cuda.synchronize()
+    assert torch.equal(o1.view(torch.int32), o2.view(torch.int32))
+    assert torch.equal(n1.view(torch.int32), n2.view(torch.int32))
+
+
 def test_last_workgroup_combine_many_leaves(cuda):
     """A plan of more workgroups than CUs (one or more per leaf: 300 leaves) keeps the
     FJAGG_ZEROED_WS layout but combines in a second launch: norms bitwise the plain two-launch
