@@ -1185,8 +1185,9 @@ def test_wsum_l2_ptrs_rows_writes_the_norm_rows(karg, cuda):
     """fjagg_wsum_l2_ptrs_rows (the deferred running sum's lazy-norm rows, include/fjagg.h):
     the mean is bitwise fjagg_wsum_ptrs'; operand k >= first gets fjagg_wsum_l2_ptrs' squared
     norm (bitwise) in sq[k - first] and its correctly rounded sqrt in nrm[k - first]; nothing
-    below `first`, nor past the K - first written entries, is touched. With the plan image in
-    device memory and in the kernel arguments (FJAGG_HOST_TABLES)."""
+    below `first`, nor past the K - first written entries, is touched (first = K: nothing). With
+    the plan image in device memory and in the kernel arguments (FJAGG_HOST_TABLES), the combine
+    in a second launch and in the last workgroup (FJAGG_ZEROED_WS)."""
     import ctypes
     lib = _lib.load()
     shapes = [(37,), (3, 3, 4), (1000,), (61, 13)]
@@ -1215,11 +1216,13 @@ def test_wsum_l2_ptrs_rows_writes_the_norm_rows(karg, cuda):
     l2 = torch.empty(K, device=cuda)
     _lib.check(lib.fjagg_wsum_l2_ptrs(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p, ctypes.c_float(0.04),
                                       l2.data_ptr(), flags, ws.data_ptr(), ws.numel(), s), "l2")
-    for first in (0, 1, 3):
+    wz = torch.zeros_like(ws)  # FJAGG_ZEROED_WS: the last workgroup writes the rows
+    for first, zeroed in ((0, False), (1, False), (3, False), (0, True), (1, True), (K, True), (K, False)):
         rows = torch.full((2, K + 2), -7.0, device=cuda)
+        wsp, fl = (wz.data_ptr(), flags | _lib.ZEROED_WS) if zeroed else (ws.data_ptr(), flags)
         _lib.check(lib.fjagg_wsum_l2_ptrs_rows(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p,
                                                ctypes.c_float(0.04), rows.data_ptr(), rows.data_ptr() + 4 * (K + 2),
-                                               first, flags, ws.data_ptr(), ws.numel(), s), "rows")
+                                               first, fl, wsp, ws.numel(), s), "rows")
         torch.cuda.synchronize()
         assert torch.equal(torch.cat(outs).view(torch.int32), mean0.view(torch.int32))
         m = K - first
@@ -1227,6 +1230,7 @@ def test_wsum_l2_ptrs_rows_writes_the_norm_rows(karg, cuda):
         want_sqrt = np.sqrt(l2[first:].cpu().numpy())  # IEEE binary32 sqrt, correctly rounded
         assert np.array_equal(rows[1, :m].cpu().numpy().view(np.uint32), want_sqrt.view(np.uint32))
         assert bool((rows[:, m:] == -7.0).all())
+        assert int(wz[:16].count_nonzero()) == 0
     want = np.array([sum(float((x.double() ** 2).sum()) for x in r) for r in leaves])
     npt.assert_allclose(l2.double().cpu().numpy(), want, rtol=2e-6)
     bad = lib.fjagg_wsum_l2_ptrs_rows(_lib.F32, _lib.F32, _lib.F32, img_p, L, K, nb, w_p, ctypes.c_float(1.0),
