@@ -214,3 +214,18 @@ def test_server_schedule_and_frozen_mask_host_side():
     assert server._frozen_leaves(server.adam(0.1), params, td).tolist() == [False] * 3
     with pytest.raises(KeyError):
         server._frozen_leaves(server.ignore_grads_haiku(ig, [("linear_3", "w")]), params, td)
+
+
+def test_nontemporal_threshold_setter():
+    """tree_util.set_nontemporal_min_bytes sets the module value the Python folds and fold_chain
+    read, and re-configures the builtin tree_mean with it (fjhost.mean_config), so a runtime
+    change reaches every path; the default is restored after."""
+    old = tu.NONTEMPORAL_MIN_BYTES
+    try:
+        tu.set_nontemporal_min_bytes(12345)
+        assert tu.NONTEMPORAL_MIN_BYTES == 12345 and isinstance(tu.NONTEMPORAL_MIN_BYTES, int)
+        tu.set_nontemporal_min_bytes(float(1 << 20))
+        assert tu.NONTEMPORAL_MIN_BYTES == 1 << 20
+    finally:
+        tu.set_nontemporal_min_bytes(old)
+    assert tu.NONTEMPORAL_MIN_BYTES == old
