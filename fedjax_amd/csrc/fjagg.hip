@@ -435,25 +435,57 @@ __device__ __forceinline__ void combine_last(const float* __restrict__ ws, int64
   if (!*last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below)
   const auto r = row_rsrc(reinterpret_cast<const uint8_t*>(ws), row_range(nb * K4 * 4));
-  for (int64_t p = tid; p < kCombineWaves * q; p += kThreads) {
-    const int64_t wv = p / q, c = p - wv * q;
-    float4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t b0 = wv; b0 < nb; b0 += (int64_t)kCombineWaves * kCombineBatch) {
-      u32x4 a[kCombineBatch];
+  auto add4 = [](float4& s, const u32x4& v) {
+    s.x = __fadd_rn(s.x, __uint_as_float(v[0]));
+    s.y = __fadd_rn(s.y, __uint_as_float(v[1]));
+    s.z = __fadd_rn(s.z, __uint_as_float(v[2]));
+    s.w = __fadd_rn(s.w, __uint_as_float(v[3]));
+  };
+  const int qi = (int)q;
+  if (nb <= kCombineWaves * kCombineBatch) {
+    // the launchers keep nb <= the CU count, so one batch of 16 rows per column: a lane's (at most
+    // two) columns have all their loads in flight together — one memory round trip for any K <= 128
+    constexpr int kCols = (kCombineWaves * kFusedCombineMax / 4 + kThreads - 1) / kThreads;
+    int wv[kCols], c[kCols];
 #pragma unroll
-      for (int i = 0; i < kCombineBatch; ++i) {  // rows past nb lie past the range: zeros
-        const int64_t b = b0 + (int64_t)i * kCombineWaves;
-        a[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)((b * q + c) * 16), 0, 16);  // aux 16 = sc1
-      }
-#pragma unroll
-      for (int i = 0; i < kCombineBatch; ++i) {
-        s.x = __fadd_rn(s.x, __uint_as_float(a[i][0]));
-        s.y = __fadd_rn(s.y, __uint_as_float(a[i][1]));
-        s.z = __fadd_rn(s.z, __uint_as_float(a[i][2]));
-        s.w = __fadd_rn(s.w, __uint_as_float(a[i][3]));
-      }
+    for (int j = 0; j < kCols; ++j) {
+      const int p = tid + j * kThreads;
+      wv[j] = p < kCombineWaves * qi ? p / qi : -1;
+      c[j] = wv[j] >= 0 ? p - wv[j] * qi : 0;
     }
-    reinterpret_cast<float4*>(lds + wv * K4)[c] = s;
+    u32x4 a[kCols][kCombineBatch];
+#pragma unroll
+    for (int j = 0; j < kCols; ++j)
+#pragma unroll
+      for (int i = 0; i < kCombineBatch; ++i) {  // rows past nb, and idle lanes, lie past the range: zeros
+        const int b = wv[j] + i * kCombineWaves;
+        const uint32_t off = wv[j] >= 0 ? (uint32_t)((b * qi + c[j]) * 16) : 0x80000000u;
+        a[j][i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);  // aux 16 = sc1
+      }
+#pragma unroll
+    for (int j = 0; j < kCols; ++j) {
+      if (wv[j] < 0) continue;
+      float4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < kCombineBatch; ++i) add4(s, a[j][i]);
+      reinterpret_cast<float4*>(lds + wv[j] * K4)[c[j]] = s;
+    }
+  } else {
+    for (int p = tid; p < kCombineWaves * qi; p += kThreads) {
+      const int wv = p / qi, c = p - wv * qi;
+      float4 s = {0.f, 0.f, 0.f, 0.f};
+      for (int64_t b0 = wv; b0 < nb; b0 += (int64_t)kCombineWaves * kCombineBatch) {
+        u32x4 a[kCombineBatch];
+#pragma unroll
+        for (int i = 0; i < kCombineBatch; ++i) {
+          const int64_t b = b0 + (int64_t)i * kCombineWaves;
+          a[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)((b * qi + c) * 16), 0, 16);
+        }
+#pragma unroll
+        for (int i = 0; i < kCombineBatch; ++i) add4(s, a[i]);
+      }
+      reinterpret_cast<float4*>(lds + wv * K4)[c] = s;
+    }
   }
   __syncthreads();
   for (int64_t k = tid; k < K; k += kThreads) {
