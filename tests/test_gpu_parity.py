@@ -1129,6 +1129,50 @@ def test_dense_last_workgroup_combine(K, P, cuda):
         npt.assert_allclose(n1[:8].double().cpu().numpy(), (x[:8].double() ** 2).sum(1).cpu().numpy(), rtol=2e-6)
 
 
+@pytest.mark.parametrize("zeroed", [False, True])
+def test_fused_norms_propagate_nan_and_inf(zeroed, cuda):
+    """tree_l2_norm semantics (tree_util.py:105-114: sqrt of a sum of squares) at the edges: a NaN
+    anywhere in a client gives that client a NaN norm, an inf (or a square past f32) an inf one,
+    the other clients' norms are untouched and finite; the mean is the plain fold's, bitwise. Both
+    combine placements (second launch; last workgroup)."""
+    import ctypes
+    lib = _lib.load()
+    shapes = [(37,), (4096,), (61, 13)]
+    K, L = 9, len(shapes)
+    g = torch.Generator().manual_seed(21)
+    leaves = [[(torch.rand(s, generator=g) - 0.5).to(cuda) for s in shapes] for _ in range(K)]
+    leaves[3][1][1000] = float("nan")
+    leaves[5][2][7, 3] = float("inf")
+    leaves[6][0][0] = 3.0e20  # its square overflows f32
+    n = np.array([int(np.prod(sh)) for sh in shapes], dtype=np.int64)
+    outs = [torch.empty(int(v), device=cuda) for v in n]
+    nb = lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, None, 0)
+    blocks = np.empty(2 * nb, dtype=np.int64)
+    lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, blocks.ctypes.data, nb)
+    img = torch.from_numpy(np.concatenate([np.array([[x.data_ptr() for x in r] for r in leaves],
+                                                    dtype=np.int64).ravel(),
+                                           np.array([o.data_ptr() for o in outs], dtype=np.int64), n,
+                                           blocks])).to(cuda)
+    w = torch.arange(1, K + 1, dtype=torch.float32, device=cuda)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(lib.fjagg_wsum_ptrs(_lib.F32, _lib.F32, _lib.F32, img.data_ptr(), L, K, nb, w.data_ptr(),
+                                   ctypes.c_float(0.5), _lib.SCALE, s), "plain")
+    mean0 = torch.cat([o.clone() for o in outs])
+    need = lib.fjagg_wsum_l2_ptrs_workspace_bytes(K, nb)
+    ws = torch.zeros(need, dtype=torch.uint8, device=cuda)
+    l2 = torch.empty(K, device=cuda)
+    _lib.check(lib.fjagg_wsum_l2_ptrs(_lib.F32, _lib.F32, _lib.F32, img.data_ptr(), L, K, nb, w.data_ptr(),
+                                      ctypes.c_float(0.5), l2.data_ptr(),
+                                      _lib.SCALE | (_lib.ZEROED_WS if zeroed else 0), ws.data_ptr(), need, s), "l2")
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs).view(torch.int32), mean0.view(torch.int32))
+    got = l2.cpu().numpy()
+    assert np.isnan(got[3]) and np.isinf(got[5]) and got[5] > 0 and np.isinf(got[6]) and got[6] > 0
+    want = np.array([sum(float((x.double() ** 2).sum()) for x in r) for r in leaves])
+    ok = [k for k in range(K) if k not in (3, 5, 6)]
+    npt.assert_allclose(got[ok].astype(np.float64), want[ok], rtol=2e-6)
+
+
 def test_combine_launch_switch(cuda, monkeypatch):
     """FJAGG_L2_COMBINE_LAUNCH=1 (kernels._L2_COMBINE_LAUNCH) keeps the separate combine launch
     for weighted_sum_l2_dense's own workspace: the same bits as the in-launch combine."""
