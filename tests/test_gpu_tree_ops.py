@@ -651,3 +651,48 @@ def test_tree_zeros_like_one_allocation_own_leaves(cuda, sum_mode):
         base2["z"].add_(1.0)
         with pytest.raises(RuntimeError, match="running sum passed to tree_add was modified"):
             tu.tree_inverse_weight(s2, 3.0)
+
+
+_LOOP_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+from fedjax_amd import kernels, tree_util as tu
+dev = torch.device("cuda:0")
+shapes = {{"a": (300,), "b": (64, 33), "c": (1000,)}}
+deltas = []
+for k in range(80):
+    t = {{}}
+    for i, (name, shp) in enumerate(shapes.items()):
+        x = torch.empty(1, int(np.prod(shp)), device=dev)
+        kernels.fill_synth(x, seed=i + 1, k0=k)
+        t[name] = x.view(shp)
+    deltas.append(t)
+s, norms = tu.tree_zeros_like(deltas[0]), []
+tu.set_deferred_sums(True, max_clients=4095, flush_bytes=1, flush_clients=32)
+for k, d in enumerate(deltas):
+    s = tu.tree_add(s, tu.tree_weight(d, k + 1))
+    norms.append(tu.tree_l2_norm(d))
+m = tu.tree_inverse_weight(s, float(sum(range(1, 81))))
+print(np.array([float(n) for n in norms], dtype=np.float32).view(np.uint32).tolist())
+print(torch.cat([m[k].reshape(-1) for k in sorted(m)]).view(torch.int32).sum().item())
+"""
+
+
+@pytest.mark.deferred_only
+def test_library_loop_norms_with_and_without_the_combine_launch(cuda):
+    """The library loop's lazy norms come from the chain folds' combine, in the fold's last
+    workgroup by default; FJAGG_L2_COMBINE_LAUNCH=1 (read once per process by fjhost) keeps the
+    separate combine launch. A child process with the switch and one without: the same norm bits
+    and the same mean (early flushes every 32 clients, 80 clients)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = _LOOP_SCRIPT.format(root=root)
+    outs = []
+    for switch in ("0", "1"):
+        env = dict(os.environ, FJAGG_L2_COMBINE_LAUNCH=switch)
+        r = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout.strip().splitlines()[-2:])
+    assert outs[0] == outs[1]
