@@ -378,6 +378,40 @@ def dropin_surface(dev, calls=20):
         key = "c1_library_loop_with_norms_round" if with_norms else "c1_library_loop_without_norms_round"
         res[key + "_ms"] = round(ms, 4)
         res[key + "_GBs"] = round(K * P * 4 / ms / 1e6, 1)
+    # examples/fed_avg.py:72-82 as written: per client the (delta, n) pair appended and
+    # tree_l2_norm(delta) kept in client_diagnostics, then tree_mean of the list. The norms are
+    # lazy views the mean's launch fills (tree_util.set_lazy_norms): one pass over the deltas.
+    # Rounds alternate with the same synchronous tree_mean without the norms (same box drift).
+    H = tu._HOST
+    for Kx in (K, 10):
+        sub, sfx = pairs[:Kx], "" if Kx == K else f"_k{Kx}"
+        times, fused0, rounds = {True: [], False: []}, H.solo_info()["fused"], 0
+        for i in range(2 * (calls + 2)):
+            with_norms = i % 2 == 0
+            torch.cuda.synchronize()
+            t0 = pc()
+            if with_norms:
+                client_diagnostics, client_delta_params_weights = {}, []
+                for cid, (delta_params, n_) in enumerate(sub):
+                    client_delta_params_weights.append((delta_params, n_))
+                    client_diagnostics[cid] = {"delta_l2_norm": tu.tree_l2_norm(delta_params)}
+                mean = tu.tree_mean(client_delta_params_weights)
+                rounds += 1
+            else:
+                mean = tu.tree_mean(sub)
+            torch.cuda.synchronize()
+            if i >= 4:
+                times[with_norms].append(pc() - t0)
+        got = torch.stack([client_diagnostics[c]["delta_l2_norm"] for c in range(Kx)])
+        ref = tu.tree_l2_norms([t for t, _ in sub])
+        res[f"c1_example_norms_max_rel_diff{sfx}"] = float(((got - ref).abs() / ref).max())
+        res[f"c1_example_norms_fused_frac{sfx}"] = round((H.solo_info()["fused"] - fused0) / (rounds * Kx), 4)
+        for with_norms in (True, False):
+            ms = float(np.median(times[with_norms])) * 1e3
+            key = "c1_example_round_with_norms" if with_norms else "c1_example_round_mean_only"
+            res[key + sfx + "_ms"] = round(ms, 4)
+            res[key + sfx + "_GBs"] = round(Kx * P * 4 / ms / 1e6, 1)
+        del got, ref, mean, client_diagnostics, client_delta_params_weights
     # the same clients as fedjax_amd produces them under the process-wide switch
     # memory.set_default(True): host deltas copied to the device leaf by leaf
     # (memory.to_device), from the delta pool (include/fjalloc.h) — still one tensor per
@@ -416,6 +450,10 @@ def dropin_surface(dev, calls=20):
                    "timed region; GB/s = K*P*4 client-delta bytes per call (library loop: per round); "
                    "c1_library_loop_with_norms: fed_avg.py:132-146 as written (tree_l2_norm per client into "
                    "client_diagnostics), c1_library_loop_without_norms: the same loop without the norm; "
+                   "c1_example_round_with_norms[_k10]: examples/fed_avg.py:72-82 as written (128 / 10 clients: "
+                   "tree_l2_norm per client into client_diagnostics, then tree_mean of the list; the norms are lazy "
+                   "views the mean's launch fills), c1_example_round_mean_only: the same synchronous tree_mean "
+                   "without the norms, rounds alternating; "
                    "c1_default_pool_*: the same clients produced by fedjax_amd.memory.to_device under "
                    "fedjax_amd.memory.set_default(True) (the delta pool)")
     del pairs

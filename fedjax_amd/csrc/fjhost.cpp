@@ -387,6 +387,8 @@ struct L2Rows {
   float* sq;
   float* nrm;
   int64_t first;
+  bool aligned_only = false;  // fold_core returns 2 (nothing launched) when some leaf would walk element
+                              // units: a standalone lazy norm's value must come from the all-16-byte plan
 };
 constexpr int kF32 = 0, kScale = 1, kAccumulate = 2, kNontemporal = 4;  // fjagg.h enums
 
@@ -418,7 +420,8 @@ void carve_outputs(const std::vector<at::Tensor>& row0, std::vector<at::Tensor>&
 // The launch part of fold_table for a gathered table: K x L pointers `in` (row 0 = row0's
 // leaves), float32 weights wf[K]. outs: empty = fresh outputs shaped like row0 (appended),
 // else the destinations (float32, contiguous, row0's shapes and device). Returns 0 with the
-// library status in *rc (launched), 1 when the case does not hold (nothing launched).
+// library status in *rc (launched), 1 when the case does not hold (nothing launched), 2 when
+// rows->aligned_only and some pointer is off 16 bytes (nothing launched, outs untouched).
 // Throws on torch errors.
 // The fused-norm workspace of (device, stream): FJAGG_ZEROED_WS layout, its 16-byte completion
 // counter zeroed once on the stream when the buffer is (re)allocated and left zero by every
@@ -474,11 +477,15 @@ int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K,
   }
   std::vector<uint8_t> elem(L, 0);
   bool any_elem = false;
+  for (int64_t l = 0; l < L; ++l) any_elem = any_elem || (lbits[l] & 15) != 0;
+  if (any_elem && rows && rows->aligned_only) return 2;
   if (fresh) carve_outputs(row0, outs);
+  any_elem = false;
   for (int64_t l = 0; l < L; ++l) {
     elem[l] = ((lbits[l] | reinterpret_cast<int64_t>(outs[l].data_ptr())) & 15) != 0;
     any_elem = any_elem || elem[l];
   }
+  if (any_elem && rows && rows->aligned_only) return 2;  // (a caller destination off 16 bytes)
   st.lap(kTOutputs);
   // a small delta and many clients: k_ptrs_narrow's LDS-staged stripes (any alignment;
   // the rule of tree_util._narrow), not with fused norms
@@ -1542,6 +1549,500 @@ PyObject* leaf_fold(PyObject*, PyObject* args) {
   }
 }
 
+// ------------------------------------------------------------------ standalone lazy norms
+// examples/fed_avg.py:72-82 takes tree_l2_norm(delta) of every client's delta (:79-81) before
+// the tree_mean of the same deltas (:82). A delta no running sum took gets a lazy norm here: a
+// 0-d view (tree_util._NormView) into a norm buffer whose value the tree_mean launch that folds
+// the delta writes (fjagg_wsum_l2_ptrs_rows, mean_pairs_impl), so the round reads every delta
+// once. The view's ticket is a SoloNorm node: the captured leaves (strong references, their
+// in-place versions and data pointers) and the version tags of the tree's dict nodes (the mean
+// recognises the same, unchanged tree without re-walking it). A view read before a mean folds
+// its delta, a delta no mean folds, and the oldest nodes past the pending budget are computed
+// by their own pytree-kernel launch (solo_resolve) — the same kernel and plan (every leaf in
+// 16-byte units; the per-client reduction order depends on the leaf sizes only), so a norm has
+// the same bits whenever it is computed. A captured leaf updated in place before the value is
+// computed cannot be recovered: the node turns stale and reading its view raises RuntimeError
+// (tree_util.set_lazy_norms(False) opts out, as set_deferred_sums(False) does for the sums).
+constexpr int kSoloMaxDicts = 64;
+constexpr int64_t kSoloCols = 4096;  // columns of a norm buffer (row 0: squared norms, row 1: norms)
+enum { kSoloDone = 0, kSoloPending = 1, kSoloStale = 2 };  // (tp_alloc zeroes: a fresh node is not pending)
+
+struct SoloObject {
+  PyObject_HEAD
+  PyObject* tree;  // the pytree tree_l2_norm was given (the mean matches clients by identity)
+  PyObject* buf;   // float32 [2, kSoloCols] norm buffer
+  long long idx;   // this node's column
+  long long nbytes;
+  int state;
+  int L, ndicts, tagged;
+  long long vsum;  // the leaves' version sum at the call
+  int cap_leaves, cap_dicts;  // capacity of the arrays below (one malloc'd block, kept across reuse)
+  PyObject** leaves;  // [cap_leaves] the captured leaf tensors in the capture walk's order (strong while pending)
+  int64_t* ptrs;      // [cap_leaves] their data pointers at the call
+  int64_t* tags;      // [2 * cap_dicts] (dict node, PEP 509 version tag), pre-order (tagged)
+  PyObject* weakreflist;
+};
+
+struct SoloState {
+  PyTypeObject* type = nullptr;  // _fjhost.SoloNorm
+  bool on = true;                // tree_util.set_lazy_norms
+  long long max_pending = 16383;
+  long long budget = 0;          // bytes of pending deltas; 0: automatic (py_budget(device) once)
+  PyObject* py_budget = nullptr;
+  std::vector<PyObject*> reg;    // weak references to nodes, registration order (pending ones matter)
+  long long pending = 0, pending_bytes = 0;
+  long long recheck = 0;         // pending bytes at which the budget is checked again (solo_evict)
+  PyObject* buf = nullptr;       // the norm buffer new columns come from
+  long long next = 0;
+  unsigned long long rows_fn = 0, l2ws_fn = 0, plan_fn = 0;  // libfjagg entry points (solo_config)
+  long long fused = 0, eager = 0, stale = 0, launches = 0;  // counters (solo_info)
+  // Pool of pre-made (norm view, node) pairs over consecutive columns, built right after a mean
+  // that fused lazy norms has issued its launches (while the GPU folds) and sized to the norms
+  // the round asked for: creating a 0-d tensor subclass and a node on the critical path of the
+  // example's loop costs more than the capture itself. Handed-out pairs stay listed per buffer;
+  // once a buffer is full and the caller has dropped every view of it (nothing but the pool
+  // references them or aliases the storage), its pairs are reused whole on the same stream.
+  std::vector<std::pair<PyObject*, PyObject*>> pool;  // (view of row 1, node), ready, in column order
+  size_t pool_head = 0;
+  struct BufRec {
+    PyObject* buf;
+    unsigned long long stream;
+    std::vector<std::pair<PyObject*, PyObject*>> pairs;  // handed-out pool pairs of this buffer
+  };
+  std::vector<BufRec> bufs;
+  // handed-out pool pairs whose node is pending (strong references): a pair whose view only the
+  // pool still references was dropped by the caller — its node lets its capture go (solo_reap)
+  std::vector<std::pair<PyObject*, PyObject*>> handed;
+  long long want = 0;  // row-1 norms asked for since the last refill
+  long long pool_builds = 0, pool_reuses = 0;
+  double refill_us = 0.0;
+};
+SoloState g_solo;
+
+void solo_release(SoloObject* n, int state) {
+  if (n->state == kSoloPending) {
+    --g_solo.pending;
+    g_solo.pending_bytes -= n->nbytes;
+  }
+  n->state = state;
+  Py_CLEAR(n->tree);
+  for (int l = 0; l < n->L; ++l) Py_CLEAR(n->leaves[l]);
+}
+
+int solo_traverse(PyObject* o, visitproc visit, void* arg) {
+  auto* n = reinterpret_cast<SoloObject*>(o);
+  Py_VISIT(Py_TYPE(o));
+  Py_VISIT(n->tree);
+  Py_VISIT(n->buf);
+  for (int l = 0; l < n->L && n->leaves; ++l) Py_VISIT(n->leaves[l]);
+  return 0;
+}
+int solo_clear(PyObject* o) {
+  auto* n = reinterpret_cast<SoloObject*>(o);
+  if (n->state == kSoloPending) solo_release(n, kSoloDone);  // (dropped unread: nothing to compute)
+  Py_CLEAR(n->tree);
+  Py_CLEAR(n->buf);
+  for (int l = 0; l < n->L && n->leaves; ++l) Py_CLEAR(n->leaves[l]);
+  return 0;
+}
+void solo_dealloc(PyObject* o) {
+  PyTypeObject* tp = Py_TYPE(o);
+  PyObject_GC_UnTrack(o);
+  auto* n = reinterpret_cast<SoloObject*>(o);
+  if (n->weakreflist) PyObject_ClearWeakRefs(o);
+  solo_clear(o);
+  PyMem_Free(n->leaves);
+  tp->tp_free(o);
+  Py_DECREF(tp);
+}
+// `node`: the node itself while its value is not written (flush_views then computes it, or
+// raises for a stale one), None once it is — the protocol of tree_util._Ticket.node
+PyObject* solo_get_node(PyObject* o, void*) {
+  PyObject* r = reinterpret_cast<SoloObject*>(o)->state == kSoloDone ? Py_None : o;
+  Py_INCREF(r);
+  return r;
+}
+PyGetSetDef kSoloGetSet[] = {{const_cast<char*>("node"), solo_get_node, nullptr, nullptr, nullptr},
+                             {nullptr}};
+PyMemberDef kSoloMembers[] = {
+    {const_cast<char*>("_tree"), T_OBJECT, offsetof(SoloObject, tree), READONLY, nullptr},
+    {const_cast<char*>("_buf"), T_OBJECT, offsetof(SoloObject, buf), READONLY, nullptr},
+    {const_cast<char*>("_idx"), T_LONGLONG, offsetof(SoloObject, idx), READONLY, nullptr},
+    {const_cast<char*>("_state"), T_INT, offsetof(SoloObject, state), READONLY, nullptr},
+    {const_cast<char*>("__weaklistoffset__"), T_PYSSIZET, offsetof(SoloObject, weakreflist), READONLY, nullptr},
+    {nullptr}};
+PyType_Slot kSoloSlots[] = {{Py_tp_dealloc, reinterpret_cast<void*>(solo_dealloc)},
+                            {Py_tp_traverse, reinterpret_cast<void*>(solo_traverse)},
+                            {Py_tp_clear, reinterpret_cast<void*>(solo_clear)},
+                            {Py_tp_members, kSoloMembers},
+                            {Py_tp_getset, kSoloGetSet},
+                            {Py_tp_doc, const_cast<char*>("a standalone lazy l2 norm's capture (fjhost.cpp)")},
+                            {0, nullptr}};
+PyType_Spec kSoloSpec = {"_fjhost.SoloNorm", sizeof(SoloObject), 0, Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC,
+                         kSoloSlots};
+
+// room for L leaves and D dict tags in n's arrays (false: out of memory, no error set)
+bool solo_reserve(SoloObject* n, int L, int D) {
+  if (n->leaves && L <= n->cap_leaves && D <= n->cap_dicts) return true;
+  const int cl = std::max(L, 16), cd = std::max(D, 8);
+  void* blk = PyMem_Malloc(sizeof(PyObject*) * cl + sizeof(int64_t) * (cl + 2 * cd));
+  if (!blk) return false;
+  for (int l = 0; l < n->L && n->leaves; ++l) Py_CLEAR(n->leaves[l]);
+  PyMem_Free(n->leaves);
+  n->leaves = static_cast<PyObject**>(blk);
+  n->ptrs = reinterpret_cast<int64_t*>(n->leaves + cl);
+  n->tags = n->ptrs + cl;
+  n->cap_leaves = cl;
+  n->cap_dicts = cd;
+  n->L = 0;
+  std::memset(n->leaves, 0, sizeof(PyObject*) * cl);
+  return true;
+}
+
+// The captured leaves still hold the values of the call: same versions, same storage.
+bool solo_unchanged(const SoloObject* n) {
+  int64_t vs = 0;
+  for (int l = 0; l < n->L; ++l) {
+    const at::Tensor& t = THPVariable_Unpack(n->leaves[l]);
+    vs += static_cast<int64_t>(t._version());
+    if (reinterpret_cast<int64_t>(t.data_ptr()) != n->ptrs[l]) return false;
+  }
+  return vs == n->vsum;
+}
+
+// The capture walk: every dict (pre-order, values in insertion order — no key sort), list / tuple
+// and None node, exact torch.Tensor leaves. 0 walked; 1 not the fast case.
+int solo_walk(PyObject* x, std::vector<PyObject*>& lv, std::vector<PyObject*>& dv, bool& lists, int depth) {
+  if (depth > 64) return 1;
+  if (Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(THPVariableClass)) {
+    lv.push_back(x);
+    return lv.size() > static_cast<size_t>(FJTREE_MAX_LEAVES);
+  }
+  if (x == Py_None) return 0;
+  if (PyDict_CheckExact(x)) {
+    dv.push_back(x);
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    while (PyDict_Next(x, &pos, &k, &v))
+      if (solo_walk(v, lv, dv, lists, depth + 1)) return 1;
+    return 0;
+  }
+  const bool is_list = PyList_CheckExact(x);
+  if (!is_list && !PyTuple_CheckExact(x)) return 1;
+  lists = lists || is_list;
+  for (Py_ssize_t i = 0; i < Py_SIZE(x); ++i)
+    if (solo_walk(is_list ? PyList_GET_ITEM(x, i) : PyTuple_GET_ITEM(x, i), lv, dv, lists, depth + 1)) return 1;
+  return 0;
+}
+
+// The same leaf objects, in any order (L <= FJTREE_MAX_LEAVES).
+bool same_leaf_set(PyObject* const* a, PyObject* const* b, int L) {
+  PyObject* x[FJTREE_MAX_LEAVES];
+  PyObject* y[FJTREE_MAX_LEAVES];
+  std::memcpy(x, a, sizeof(PyObject*) * L);
+  std::memcpy(y, b, sizeof(PyObject*) * L);
+  std::sort(x, x + L);
+  std::sort(y, y + L);
+  return std::equal(x, x + L, y);
+}
+
+// `tree` is the node's tree and still holds exactly the captured leaves: its dict nodes' version
+// tags unchanged (pre-order: a dict is read only after its parent was found unchanged, so it is
+// alive), or for a tree with list nodes a walk finding the same leaf objects.
+bool solo_same_tree(const SoloObject* n, PyObject* tree) {
+  if (n->tree != tree) return false;
+#if PY_VERSION_HEX < 0x030C0000
+  if (n->tagged) {
+    for (int i = 0; i < n->ndicts; ++i)
+      if (static_cast<int64_t>(reinterpret_cast<PyDictObject*>(n->tags[2 * i])->ma_version_tag) != n->tags[2 * i + 1])
+        return false;
+    return true;
+  }
+#endif
+  thread_local std::vector<PyObject*> lv, dv;
+  lv.clear();
+  dv.clear();
+  bool lists = false;
+  if (solo_walk(tree, lv, dv, lists, 0) != 0 || static_cast<int>(lv.size()) != n->L) return false;
+  return same_leaf_set(lv.data(), n->leaves, n->L);
+}
+
+// Captures `tree` into node n (not yet pending). false: not the fast case (float32 CUDA leaves,
+// strided, contiguous, one device, versioned, <= FJTREE_MAX_LEAVES, some element) or no memory.
+bool solo_capture_into(SoloObject* n, PyObject* tree) {
+  thread_local std::vector<PyObject*> lv, dv;
+  lv.clear();
+  dv.clear();
+  bool lists = false;
+  if (solo_walk(tree, lv, dv, lists, 0) != 0 || lv.empty()) return false;
+  const int L = static_cast<int>(lv.size());
+  int dev = -1;
+  int64_t vs = 0, numel = 0;
+  for (PyObject* x : lv) {
+    const at::Tensor& t = THPVariable_Unpack(x);
+    if (t.layout() != c10::kStrided || t.scalar_type() != at::kFloat || !t.is_cuda() || !t.is_contiguous() ||
+        t.is_inference())
+      return false;
+    if (dev < 0) dev = t.get_device();
+    if (t.get_device() != dev) return false;
+    vs += static_cast<int64_t>(t._version());
+    numel += t.numel();
+  }
+  if (numel == 0) return false;  // (the Python path returns a zero)
+  const bool tagged = !lists && dv.size() <= static_cast<size_t>(kSoloMaxDicts);
+  if (!solo_reserve(n, L, tagged ? static_cast<int>(dv.size()) : 0)) return false;
+  n->L = L;
+  n->vsum = vs;
+  n->nbytes = 4 * numel;
+  for (int l = 0; l < L; ++l) {
+    Py_INCREF(lv[l]);
+    n->leaves[l] = lv[l];
+    n->ptrs[l] = reinterpret_cast<int64_t>(THPVariable_Unpack(lv[l]).data_ptr());
+  }
+#if PY_VERSION_HEX < 0x030C0000
+  n->tagged = tagged;
+  n->ndicts = tagged ? static_cast<int>(dv.size()) : 0;
+  for (int i = 0; i < n->ndicts; ++i) {
+    n->tags[2 * i] = reinterpret_cast<int64_t>(dv[i]);
+    n->tags[2 * i + 1] = static_cast<int64_t>(reinterpret_cast<PyDictObject*>(dv[i])->ma_version_tag);
+  }
+#else
+  n->tagged = 0;
+  n->ndicts = 0;
+#endif
+  Py_INCREF(tree);
+  Py_XSETREF(n->tree, tree);
+  return true;
+}
+
+// The leaves of a pending node in flatten order (jax's: dict keys sorted) when its tree still
+// holds them — the order the mean's fused fold reads them in, so a norm computed on its own
+// has the fused value's bits — else in the capture walk's order (the tree changed since the
+// call: no mean can fold this value any more).
+void solo_flatten_order(const SoloObject* n, std::vector<PyObject*>& out) {
+  out.assign(n->leaves, n->leaves + n->L);
+  if (!n->tree || !solo_same_tree(n, n->tree)) return;
+  PWalk w;
+  w.K = 1;
+  PyObject* t = n->tree;
+  if (pwalk(&t, w, 0) != 0) {
+    if (PyErr_Occurred()) PyErr_Clear();
+    return;
+  }
+  if (static_cast<int>(w.leaves[0].size()) == n->L && same_leaf_set(w.leaves[0].data(), n->leaves, n->L))
+    out.assign(w.leaves[0].begin(), w.leaves[0].end());
+}
+
+// every captured pointer 16-byte aligned: the mean's fused plan (no element units) is this node's
+bool solo_aligned(const SoloObject* n) {
+  for (int l = 0; l < n->L; ++l)
+    if (n->ptrs[l] & 15) return false;
+  return true;
+}
+
+// Computes the values of `nodes` (pending ones; others are skipped) by pytree-kernel launches on
+// the current stream, the leaves in flatten order (solo_flatten_order): runs of consecutive
+// columns of one buffer with equal leaf shapes, every pointer aligned, fold together (the fold's
+// outputs are dropped); a misaligned node folds alone (its own element-unit plan, as every
+// computation of it). A node whose leaves changed turns stale. 0, or -1 with a Python error.
+int solo_resolve(std::vector<SoloObject*>& nodes) {
+  std::vector<SoloObject*> todo;
+  for (SoloObject* n : nodes) {
+    if (n->state != kSoloPending) continue;
+    if (!solo_unchanged(n)) {
+      solo_release(n, kSoloStale);
+      ++g_solo.stale;
+      continue;
+    }
+    todo.push_back(n);
+  }
+  if (todo.empty()) return 0;
+  if (!g_solo.rows_fn || !g_solo.l2ws_fn || !g_solo.plan_fn) {
+    PyErr_SetString(PyExc_RuntimeError, "lazy norms: libfjagg entry points not configured (solo_config)");
+    return -1;
+  }
+  std::stable_sort(todo.begin(), todo.end(), [](const SoloObject* a, const SoloObject* b) {
+    return a->buf != b->buf ? a->buf < b->buf : a->idx < b->idx;
+  });
+  for (SoloObject* n : todo) Py_INCREF(n);
+  struct Drop {
+    std::vector<SoloObject*>& v;
+    ~Drop() {
+      for (SoloObject* n : v) Py_DECREF(n);
+    }
+  } drop{todo};
+  try {
+    std::vector<std::vector<PyObject*>> order(todo.size());
+    for (size_t i = 0; i < todo.size(); ++i) solo_flatten_order(todo[i], order[i]);
+    auto same_shape = [&](size_t i, size_t j) {
+      if (order[i].size() != order[j].size()) return false;
+      for (size_t l = 0; l < order[i].size(); ++l)
+        if (THPVariable_Unpack(order[j][l]).sizes() != THPVariable_Unpack(order[i][l]).sizes()) return false;
+      return true;
+    };
+    size_t i = 0;
+    while (i < todo.size()) {
+      SoloObject* a = todo[i];
+      const bool al = solo_aligned(a);
+      const int dev = THPVariable_Unpack(a->leaves[0]).get_device();
+      size_t j = i + 1;
+      while (al && j < todo.size() && j - i < 4096 && todo[j]->buf == a->buf &&
+             todo[j]->idx == a->idx + static_cast<long long>(j - i) && solo_aligned(todo[j]) && same_shape(i, j) &&
+             THPVariable_Unpack(todo[j]->leaves[0]).get_device() == dev)
+        ++j;
+      const int64_t K = static_cast<int64_t>(j - i), L = a->L;
+      std::vector<at::Tensor> row0;
+      row0.reserve(L);
+      for (int64_t l = 0; l < L; ++l) row0.push_back(THPVariable_Unpack(order[i][l]));
+      std::vector<int64_t> ptrs(static_cast<size_t>(K * L));
+      for (int64_t k = 0; k < K; ++k)
+        for (int64_t l = 0; l < L; ++l)
+          ptrs[k * L + l] = reinterpret_cast<int64_t>(THPVariable_Unpack(order[i + k][l]).data_ptr());
+      std::vector<float> wf(static_cast<size_t>(K), 1.0f);
+      const unsigned long long stream = reinterpret_cast<unsigned long long>(
+          c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(dev)).stream());
+      const at::Tensor& b = THPVariable_Unpack(a->buf);
+      if (b.get_device() != dev) {
+        PyErr_SetString(PyExc_RuntimeError, "lazy norms: a norm buffer on another device than its delta");
+        return -1;
+      }
+      float* r0 = b.data_ptr<float>() + a->idx;
+      L2Rows rows{reinterpret_cast<WsumL2RowsFn>(g_solo.rows_fn), r0, r0 + b.stride(0), 0};
+      std::vector<at::Tensor> outs;  // (fresh, dropped: only the norms are wanted)
+      int rc = 0;
+      Stamp st;
+      if (fold_core(row0, ptrs.data(), K, wf.data(), 1.0, false, HUGE_VAL, dev, stream,
+                    reinterpret_cast<PlanFn>(g_solo.plan_fn), nullptr, outs, false, nullptr,
+                    reinterpret_cast<L2WsFn>(g_solo.l2ws_fn), nullptr, &rc, st, &rows) != 0) {
+        PyErr_SetString(PyExc_RuntimeError, "lazy norms: the captured leaves are not a fold's case");
+        return -1;
+      }
+      if (rc != 0) {
+        PyErr_Format(PyExc_RuntimeError, "lazy norms: fjagg_wsum_l2_ptrs_rows failed (%d)", rc);
+        return -1;
+      }
+      ++g_solo.launches;
+      for (size_t q = i; q < j; ++q) {
+        solo_release(todo[q], kSoloDone);
+        ++g_solo.eager;
+      }
+      i = j;
+    }
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return -1;
+  }
+  return 0;
+}
+
+// Pool pairs handed out: drop the done ones from the list, and release the capture of a pending
+// node whose view the caller dropped (only the pool's records hold it: nobody can read it).
+void solo_reap() {
+  size_t o = 0;
+  for (auto& pr : g_solo.handed) {
+    auto* n = reinterpret_cast<SoloObject*>(pr.second);
+    if (n->state == kSoloPending && Py_REFCNT(pr.first) <= 2 && THPVariable_Unpack(pr.first).use_count() == 1)
+      solo_release(n, kSoloDone);
+    if (n->state == kSoloPending) {
+      g_solo.handed[o++] = pr;
+    } else {
+      Py_DECREF(pr.first);
+      Py_DECREF(pr.second);
+    }
+  }
+  g_solo.handed.resize(o);
+}
+
+// drops registry entries whose node is gone or no longer pending
+void solo_compact() {
+  size_t o = 0;
+  for (PyObject* wr : g_solo.reg) {
+    PyObject* n = PyWeakref_GetObject(wr);
+    if (n != Py_None && reinterpret_cast<SoloObject*>(n)->state == kSoloPending) {
+      g_solo.reg[o++] = wr;
+    } else {
+      Py_DECREF(wr);
+    }
+  }
+  g_solo.reg.resize(o);
+  if (g_solo.pending == 0) g_solo.recheck = 0;
+}
+
+// every pending node, oldest first (the budget's eviction and solo_resolve(None))
+int solo_resolve_all() {
+  solo_reap();
+  std::vector<SoloObject*> v;
+  std::vector<PyObject*> held;
+  for (PyObject* wr : g_solo.reg) {
+    PyObject* n = PyWeakref_GetObject(wr);
+    if (n == Py_None || reinterpret_cast<SoloObject*>(n)->state != kSoloPending) continue;
+    Py_INCREF(n);
+    held.push_back(n);
+    v.push_back(reinterpret_cast<SoloObject*>(n));
+  }
+  const int rc = solo_resolve(v);
+  for (PyObject* n : held) Py_DECREF(n);
+  solo_compact();
+  return rc;
+}
+
+// the pending nodes whose pytree only the node holds (the deltas their views alone keep alive)
+int solo_evict() {
+  solo_reap();
+  std::vector<SoloObject*> v;
+  std::vector<PyObject*> held;
+  for (PyObject* wr : g_solo.reg) {
+    PyObject* n = PyWeakref_GetObject(wr);
+    if (n == Py_None) continue;
+    auto* s = reinterpret_cast<SoloObject*>(n);
+    if (s->state != kSoloPending || !s->tree || Py_REFCNT(s->tree) > 1) continue;
+    Py_INCREF(n);
+    held.push_back(n);
+    v.push_back(s);
+  }
+  const int rc = solo_resolve(v);
+  for (PyObject* n : held) Py_DECREF(n);
+  solo_compact();
+  return rc;
+}
+
+// The mean's side: the pending node of a client's tree, checked unchanged, or nullptr. The
+// registry entry after the previous match is tried first (clients in registration order); after
+// a miss, a map of the pending nodes by tree (built once per mean) answers.
+struct SoloMatcher {
+  size_t cursor = 0;
+  bool built = false;
+  std::unordered_map<PyObject*, SoloObject*> by_tree;
+  SoloObject* match(PyObject* tree, int L) {
+    SoloObject* n = nullptr;
+    const size_t R = g_solo.reg.size();
+    for (size_t p = cursor; p < R && p < cursor + 2 && !n; ++p) {
+      PyObject* o = PyWeakref_GetObject(g_solo.reg[p]);
+      auto* c = reinterpret_cast<SoloObject*>(o);
+      if (o != Py_None && c->tree == tree && c->state == kSoloPending) {
+        n = c;
+        cursor = p + 1;
+      }
+    }
+    if (!n) {
+      if (!built) {
+        built = true;
+        for (PyObject* wr : g_solo.reg) {  // (registration order: a tree's earliest pending node)
+          PyObject* o = PyWeakref_GetObject(wr);
+          auto* c = reinterpret_cast<SoloObject*>(o);
+          if (o != Py_None && c->state == kSoloPending && c->tree) by_tree.emplace(c->tree, c);
+        }
+      }
+      auto it = by_tree.find(tree);
+      if (it == by_tree.end() || it->second->state != kSoloPending) return nullptr;
+      n = it->second;
+    }
+    return (n->L == L && solo_same_tree(n, tree) && solo_unchanged(n)) ? n : nullptr;
+  }
+};
+
+int solo_refill(int dev, unsigned long long stream);  // (the lazy-norm pool, below: uses the view type)
+
 // ------------------------------------------------------------------ tree_mean, whole call
 // tree_mean(list of (pytree, weight)) in one native call for the common case: exact dict /
 // list / tuple / None nodes over float32 CUDA tensors (contiguous, client 0's shapes, one
@@ -1767,25 +2268,101 @@ PyObject* mean_pairs_impl(PyObject* pairs, bool triples, int may_pipeline, doubl
     if (with_l2) l2sq = at::empty({K}, row0[0].options());
     int64_t done = 0;
     int rc = 0;
+    // standalone lazy norms of these clients (examples/fed_avg.py:79-81): a chunk whose clients
+    // all have pending nodes in consecutive columns of one buffer folds with the norms written
+    // straight into those columns (fjagg_wsum_l2_ptrs_rows); the nodes are done once every
+    // launch is issued
+    if (!with_l2 && !g_solo.handed.empty()) solo_reap();
+    bool solo = !with_l2 && g_solo.pending > 0 && g_solo.rows_fn && g_solo.l2ws_fn;
+    std::vector<SoloObject*> fused;  // held (new references) until the call returns
+    struct HeldNodes {
+      std::vector<SoloObject*>& v;
+      ~HeldNodes() {
+        for (SoloObject* n : v) Py_DECREF(n);
+      }
+    } held_nodes{fused};
+    SoloMatcher matcher;
+    SoloObject* next_node = nullptr;  // a match found past the end of the previous run (borrowed)
+    bool next_none = false;           // the client past the previous run has no pending node
     for (int64_t k1 : bounds) {
       if (!parse(k1)) Py_RETURN_NONE;
       const int64_t r = gather_clients(spec, trees.data(), std::max<int64_t>(done, 1), k1, dtypes, sizes,
                                        static_cast<c10::DeviceIndex>(dev), ptrs.data());
       if (r < 0) return nullptr;
       if (r > 0) Py_RETURN_NONE;
-      const bool last = k1 == K;  // (then every weight is parsed: W is complete)
-      const double scale = last ? (W > 0.0 ? 1.0 / W : 0.0) : 1.0;  // tree_util.py:37,60
-      if (fold_core(row0, ptrs.data() + done * L, k1 - done, wf.data() + done, scale, last, ntm, dev,
-                    stream, reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs,
-                    !outs.empty(), with_l2 ? reinterpret_cast<WsumL2Fn>(l2_addr) : nullptr,
-                    with_l2 ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr,
-                    with_l2 ? l2sq.data_ptr<float>() + done : nullptr, &rc, st) != 0)
-        Py_RETURN_NONE;
-      if (rc != 0) return Py_BuildValue("(iOdO)", rc, Py_None, job_bytes, Py_None);
-      if (done == 0)
-        g_timers[kTFirstLaunch] +=
-            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_entry).count();
+      // the chunk folds in runs: clients whose pending nodes sit in consecutive columns of one
+      // buffer fold with their norms written there, clients without one fold plainly. Any split
+      // gives the same bits (accumulate mode).
+      for (int64_t a = done; a < k1;) {
+        int64_t b = k1;
+        L2Rows rows{};
+        bool use_rows = false;
+        const size_t f0 = fused.size();
+        if (solo) {
+          SoloObject* n0 = next_node ? next_node : next_none ? nullptr : matcher.match(trees[a], static_cast<int>(L));
+          next_node = nullptr;
+          next_none = false;
+          b = a + 1;
+          if (n0) {
+            Py_INCREF(n0);
+            fused.push_back(n0);
+            while (b < k1 && b - a < 4096) {  // (fjagg_wsum_l2_ptrs: K <= 4096)
+              SoloObject* n = matcher.match(trees[b], static_cast<int>(L));
+              if (!n || n->buf != n0->buf || n->idx != n0->idx + (b - a)) {
+                next_node = n;
+                next_none = !n;
+                break;
+              }
+              Py_INCREF(n);
+              fused.push_back(n);
+              ++b;
+            }
+            const at::Tensor& bt = THPVariable_Unpack(n0->buf);
+            float* r0 = bt.data_ptr<float>() + n0->idx;
+            rows = L2Rows{reinterpret_cast<WsumL2RowsFn>(g_solo.rows_fn), r0, r0 + bt.stride(0), 0, true};
+            use_rows = bt.get_device() == dev;
+          } else {
+            while (b < k1) {  // a run of clients without pending norms: one plain fold
+              SoloObject* n = matcher.match(trees[b], static_cast<int>(L));
+              if (n) {
+                next_node = n;
+                break;
+              }
+              ++b;
+            }
+          }
+        }
+        const bool last = b == K;  // (then every weight is parsed: W is complete)
+        const double scale = last ? (W > 0.0 ? 1.0 / W : 0.0) : 1.0;  // tree_util.py:37,60
+        const bool acc = !outs.empty();
+        int got = 2;
+        if (use_rows)
+          got = fold_core(row0, ptrs.data() + a * L, b - a, wf.data() + a, scale, last, ntm, dev, stream,
+                          reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs, acc,
+                          nullptr, reinterpret_cast<L2WsFn>(g_solo.l2ws_fn), nullptr, &rc, st, &rows);
+        if (got == 2) {  // (no lazy norms here, or a misaligned leaf: the plain fold, the nodes stay pending)
+          for (size_t q = f0; q < fused.size(); ++q) Py_DECREF(fused[q]);
+          fused.resize(f0);
+          got = fold_core(row0, ptrs.data() + a * L, b - a, wf.data() + a, scale, last, ntm, dev, stream,
+                          reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs, acc,
+                          with_l2 ? reinterpret_cast<WsumL2Fn>(l2_addr) : nullptr,
+                          with_l2 ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr,
+                          with_l2 ? l2sq.data_ptr<float>() + a : nullptr, &rc, st);
+        }
+        if (got != 0) Py_RETURN_NONE;
+        if (rc != 0) return Py_BuildValue("(iOdO)", rc, Py_None, job_bytes, Py_None);
+        if (a == 0)
+          g_timers[kTFirstLaunch] +=
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_entry).count();
+        a = b;
+      }
       done = k1;
+    }
+    if (!fused.empty()) {  // every launch is issued: the lazy norms these clients' views read are written
+      for (SoloObject* n : fused) solo_release(n, kSoloDone);
+      g_solo.fused += static_cast<long long>(fused.size());
+      solo_compact();
+      if (g_solo.want > 0 && solo_refill(dev, stream) != 0) return nullptr;  // (while the GPU folds)
     }
     std::vector<PyObject*> wrapped(L);
     for (int64_t l = 0; l < L; ++l) wrapped[l] = THPVariable_Wrap(std::move(outs[l]));
@@ -2465,6 +3042,84 @@ PyObject* fast_install_norms(PyObject*, PyObject* args) {
 // obj.<slot> = v through the slot's descriptor (0, or -1 with a Python error)
 inline int slot_set(PyObject* descr, PyObject* obj, PyObject* v) { return Py_TYPE(descr)->tp_descr_set(descr, obj, v); }
 
+PyObject* solo_stale_error() {
+  PyErr_SetString(PyExc_RuntimeError,
+                  "a client delta passed to tree_l2_norm / tree_l2_squared was modified (a leaf updated in place) "
+                  "before its lazy norm was computed; the reference takes the norm of the value at that call. Add "
+                  "copies, or call fedjax_amd.tree_util.set_lazy_norms(False)");
+  return nullptr;
+}
+
+// solo_config(on, max_pending, budget_bytes, rows_fn, l2ws_fn, plan_fn, py_budget): tree_util's
+// set_lazy_norms and the library's entry points (0: keep the current one)
+PyObject* solo_config(PyObject*, PyObject* args) {
+  int on;
+  long long mp, bb;
+  unsigned long long rf, wf, pf;
+  PyObject* pb;
+  if (!PyArg_ParseTuple(args, "pLLKKKO", &on, &mp, &bb, &rf, &wf, &pf, &pb)) return nullptr;
+  g_solo.on = on != 0;
+  g_solo.max_pending = std::max<long long>(1, std::min<long long>(mp, 1LL << 20));
+  g_solo.budget = std::max<long long>(0, bb);
+  if (rf) g_solo.rows_fn = rf;
+  if (wf) g_solo.l2ws_fn = wf;
+  if (pf) g_solo.plan_fn = pf;
+  if (pb != Py_None) {
+    Py_INCREF(pb);
+    Py_XSETREF(g_solo.py_budget, pb);
+  }
+  Py_RETURN_NONE;
+}
+
+// solo_resolve(nodes | None) -> None: compute these pending standalone norms now (None: every
+// pending one); raises for a stale one among them
+PyObject* solo_resolve_py(PyObject*, PyObject* arg) {
+  if (arg == Py_None) {
+    if (solo_resolve_all() != 0) return nullptr;
+    Py_RETURN_NONE;
+  }
+  PyObject* seq = PySequence_Fast(arg, "solo_resolve: a sequence of SoloNorm nodes or None");
+  if (!seq) return nullptr;
+  std::vector<SoloObject*> v;
+  for (Py_ssize_t i = 0; i < PySequence_Fast_GET_SIZE(seq); ++i) {
+    PyObject* o = PySequence_Fast_GET_ITEM(seq, i);
+    if (Py_TYPE(o) == g_solo.type) v.push_back(reinterpret_cast<SoloObject*>(o));
+  }
+  const int rc = solo_resolve(v);
+  bool stale = false;
+  for (SoloObject* n : v) stale = stale || n->state == kSoloStale;
+  Py_DECREF(seq);
+  if (rc != 0) return nullptr;
+  solo_compact();
+  if (stale) return solo_stale_error();
+  Py_RETURN_NONE;
+}
+
+// solo_info() -> dict: pending nodes and bytes, registry size, norms fused into a mean, computed
+// on their own (and their launches), stale nodes
+PyObject* solo_info(PyObject*, PyObject*) {
+  solo_reap();
+  return Py_BuildValue("{s:L,s:L,s:n,s:L,s:L,s:L,s:L,s:L,s:L,s:n,s:L,s:L,s:d,s:n}", "pending", g_solo.pending,
+                       "pending_bytes", g_solo.pending_bytes, "registry", static_cast<Py_ssize_t>(g_solo.reg.size()),
+                       "fused", g_solo.fused, "eager", g_solo.eager, "eager_launches", g_solo.launches, "stale",
+                       g_solo.stale, "budget", g_solo.budget, "column", g_solo.buf ? g_solo.next : kSoloCols,
+                       "pool_ready", static_cast<Py_ssize_t>(g_solo.pool.size() - g_solo.pool_head), "pool_builds",
+                       g_solo.pool_builds, "pool_reuses", g_solo.pool_reuses, "refill_us", g_solo.refill_us,
+                       "buffers", static_cast<Py_ssize_t>(g_solo.bufs.size()));
+}
+
+// solo_norm_py(tree, which) -> view | None: the standalone lazy norm for tree_util's Python path
+PyObject* solo_norm(PyObject* tree, int which);
+PyObject* solo_norm_py(PyObject*, PyObject* args) {
+  PyObject* tree;
+  int which;
+  if (!PyArg_ParseTuple(args, "Oi", &tree, &which)) return nullptr;
+  if (!g_solo.on || !g_solo.type || !g_solo.rows_fn || !g_fast.norm_view || !g_fast.d_view_ticket ||
+      Py_TYPE(tree) == g_fast.wt || Py_TYPE(tree) == g_fast.ps)
+    Py_RETURN_NONE;
+  return solo_norm(tree, which != 0 ? 1 : 0);
+}
+
 // flush_views(obj): tree_util._flush_views natively — every lazy norm view (tree_util._NormView)
 // in obj (nested lists / tuples / dict values) whose ticket still names an unfolded link gets
 // its chain folded (py_fold_ticket(ticket)), so no torch function reads its buffer early.
@@ -2475,6 +3130,13 @@ PyObject* flush_views(PyObject*, PyObject* arg) {
     return nullptr;
   }
   static PyObject* node_name = PyUnicode_InternFromString("node");
+  std::vector<SoloObject*> solo_wait;  // pending standalone norms met on the way (new references)
+  struct HeldSolo {
+    std::vector<SoloObject*>& v;
+    ~HeldSolo() {
+      for (SoloObject* n : v) Py_DECREF(n);
+    }
+  } held_solo{solo_wait};
   std::vector<std::pair<PyObject*, int>> st;  // (not shared: a fold may run Python code that calls back)
   Py_INCREF(arg);  // (every stacked object is held: folding runs Python code)
   st.emplace_back(arg, 0);
@@ -2507,6 +3169,15 @@ PyObject* flush_views(PyObject*, PyObject* arg) {
         ~DropTk() { Py_DECREF(o); }
       } drop_tk{tk};
       if (tk == Py_None) continue;
+      if (Py_TYPE(tk) == g_solo.type) {  // a standalone lazy norm: computed below, with the others
+        const int stt = reinterpret_cast<SoloObject*>(tk)->state;
+        if (stt == kSoloStale) return solo_stale_error();
+        if (stt == kSoloPending) {
+          Py_INCREF(tk);
+          solo_wait.push_back(reinterpret_cast<SoloObject*>(tk));
+        }
+        continue;
+      }
       PyObject* node = PyObject_GetAttr(tk, node_name);
       if (!node) return nullptr;
       const bool live = node != Py_None;
@@ -2531,6 +3202,12 @@ PyObject* flush_views(PyObject*, PyObject* arg) {
       }
     }
   }
+  if (!solo_wait.empty()) {  // one launch per run of them (solo_resolve)
+    if (solo_resolve(solo_wait) != 0) return nullptr;
+    solo_compact();
+    for (SoloObject* n : solo_wait)
+      if (n->state == kSoloStale) return solo_stale_error();
+  }
   Py_RETURN_NONE;
 }
 
@@ -2541,6 +3218,226 @@ PyObject* new_ticket(PyObject* node) {
   PyObject* t = g_fast.ticket->tp_alloc(g_fast.ticket, 0);
   if (t && slot_set(g_fast.d_ticket_node, t, node) != 0) Py_CLEAR(t);
   return t;
+}
+
+// The device's pending budget (bytes): set_lazy_norms' value, else tree_util's automatic one
+// (min(4 GiB, 1/8 of the free memory), asked once).
+long long solo_budget(int dev) {
+  if (g_solo.budget > 0) return g_solo.budget;
+  static long long autob = 0;
+  if (autob <= 0 && g_solo.py_budget) {
+    PyObject* r = PyObject_CallFunction(g_solo.py_budget, "i", dev);
+    if (r) {
+      autob = PyLong_AsLongLong(r);
+      Py_DECREF(r);
+    }
+    if (PyErr_Occurred()) PyErr_Clear();
+  }
+  return autob > 0 ? autob : (1LL << 30);
+}
+
+// The next free column of the current norm buffer (a new buffer, and its pool record, when it
+// is full or on another device). false: a Python error is set.
+bool solo_column(int dev, PyObject** buf, long long* idx) {
+  if (!g_solo.buf || g_solo.next >= kSoloCols || THPVariable_Unpack(g_solo.buf).get_device() != dev) {
+    at::Tensor b = at::empty({2, kSoloCols}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
+    PyObject* bo = THPVariable_Wrap(std::move(b));
+    if (!bo) return false;
+    Py_XSETREF(g_solo.buf, bo);
+    g_solo.next = 0;
+    Py_INCREF(bo);
+    g_solo.bufs.push_back(SoloState::BufRec{
+        bo, reinterpret_cast<unsigned long long>(c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(dev)).stream()),
+        {}});
+    if (g_solo.bufs.size() > 6) {  // (bounded: the oldest record lets its pairs go)
+      auto& old = g_solo.bufs.front();
+      for (auto& pr : old.pairs) Py_DECREF(pr.first), Py_DECREF(pr.second);
+      Py_DECREF(old.buf);
+      g_solo.bufs.erase(g_solo.bufs.begin());
+    }
+  }
+  *buf = g_solo.buf;
+  *idx = g_solo.next++;
+  return true;
+}
+
+// A view of row `row`, column idx of n's buffer, whose _ticket is n (new reference or nullptr).
+PyObject* solo_view(SoloObject* n, int row) {
+  const at::Tensor& b = THPVariable_Unpack(n->buf);
+  PyObject* v = THPVariable_Wrap(scalar_at(b, b.storage_offset() + row * b.stride(0) + n->idx * b.stride(1)),
+                                 g_fast.norm_view);
+  if (v && slot_set(g_fast.d_view_ticket, v, reinterpret_cast<PyObject*>(n)) != 0) Py_CLEAR(v);
+  return v;
+}
+
+// A full, non-current buffer whose handed-out pool pairs nobody but its record references (the
+// views dropped by the caller, the nodes done, no fresh node on it, no alias of the storage) and
+// whose last norms were written on `stream`: its pairs can take new norms.
+bool solo_recyclable(const SoloState::BufRec& r, unsigned long long stream) {
+  if (r.buf == g_solo.buf || r.stream != stream || r.pairs.empty() ||
+      Py_REFCNT(r.buf) != 1 + static_cast<Py_ssize_t>(r.pairs.size()))
+    return false;
+  const at::Tensor& b = THPVariable_Unpack(r.buf);
+  if (b.use_count() != 1 || static_cast<size_t>(b.storage().use_count()) != r.pairs.size() + 1) return false;
+  for (const auto& pr : r.pairs) {
+    if (Py_REFCNT(pr.first) != 1 || Py_REFCNT(pr.second) != 2 || THPVariable_Unpack(pr.first).use_count() != 1 ||
+        reinterpret_cast<SoloObject*>(pr.second)->state == kSoloPending)
+      return false;
+  }
+  return true;
+}
+
+// Builds the pool for the next round (see SoloState): as many pairs as the last round took,
+// recycled from a buffer nobody reads any more, else new. Runs right after a mean's launches
+// (the GPU folds meanwhile). 0, or -1 with a Python error.
+int solo_refill(int dev, unsigned long long stream) {
+  Stamp clock;
+  const long long m = std::min<long long>(g_solo.want, kSoloCols);
+  g_solo.want = 0;
+  if (m <= 0 || !g_solo.type || !g_fast.norm_view || !g_fast.d_view_ticket) return 0;
+  solo_reap();
+  // pairs handed out since the last refill already moved to their buffers' records; drop the
+  // taken slots, keep the rest when they are enough and on this device
+  g_solo.pool.erase(g_solo.pool.begin(), g_solo.pool.begin() + static_cast<std::ptrdiff_t>(g_solo.pool_head));
+  g_solo.pool_head = 0;
+  if (!g_solo.pool.empty()) {
+    const auto* n0 = reinterpret_cast<SoloObject*>(g_solo.pool.front().second);
+    if (static_cast<long long>(g_solo.pool.size()) >= m && THPVariable_Unpack(n0->buf).get_device() == dev) return 0;
+    for (auto& pr : g_solo.pool) Py_DECREF(pr.first), Py_DECREF(pr.second);
+    g_solo.pool.clear();
+  }
+  for (auto& r : g_solo.bufs) {
+    if (THPVariable_Unpack(r.buf).get_device() != dev || static_cast<long long>(r.pairs.size()) < m ||
+        !solo_recyclable(r, stream))
+      continue;
+    g_solo.pool.swap(r.pairs);  // (column order: handed out in order)
+    ++g_solo.pool_reuses;
+    g_solo.refill_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - clock.t).count();
+    return 0;
+  }
+  g_solo.pool.reserve(static_cast<size_t>(m));
+  for (long long i = 0; i < m; ++i) {
+    PyObject* buf;
+    long long idx;
+    if (!solo_column(dev, &buf, &idx)) return -1;
+    auto* n = reinterpret_cast<SoloObject*>(g_solo.type->tp_alloc(g_solo.type, 0));
+    if (!n) return -1;
+    Py_INCREF(buf);
+    n->buf = buf;
+    n->idx = idx;
+    if (!solo_reserve(n, 16, 8)) {
+      Py_DECREF(n);
+      PyErr_NoMemory();
+      return -1;
+    }
+    PyObject* v = solo_view(n, 1);
+    if (!v) {
+      Py_DECREF(n);
+      return -1;
+    }
+    g_solo.pool.emplace_back(v, reinterpret_cast<PyObject*>(n));
+  }
+  ++g_solo.pool_builds;
+  g_solo.refill_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - clock.t).count();
+  return 0;
+}
+
+// tree_l2_norm / tree_l2_squared (which 1 / 0) of a delta no running sum took: a lazy view of a
+// SoloNorm node (see "standalone lazy norms"). The most recent node answers for its own tree
+// when unchanged (the norm and the squared norm of one delta share a column); a norm takes the
+// pool's next pair. Py_None: not the fast case; nullptr: a Python error.
+PyObject* solo_norm(PyObject* tree, int which) {
+  try {
+    if (!g_solo.reg.empty()) {
+      PyObject* o = PyWeakref_GetObject(g_solo.reg.back());
+      if (o != Py_None) {
+        auto* c = reinterpret_cast<SoloObject*>(o);
+        if (c->state == kSoloPending && c->tree == tree && solo_same_tree(c, tree) && solo_unchanged(c))
+          return solo_view(c, which);
+      }
+    }
+    SoloObject* n = nullptr;   // (a new reference)
+    PyObject* view = nullptr;  // the pool's view for n (a new reference)
+    if (which == 1 && g_solo.pool_head < g_solo.pool.size()) {
+      const auto pr = g_solo.pool[g_solo.pool_head];
+      auto* pn = reinterpret_cast<SoloObject*>(pr.second);
+      if (!solo_capture_into(pn, tree)) {
+        if (PyErr_Occurred()) return nullptr;
+        Py_RETURN_NONE;  // (the pair stays in the pool)
+      }
+      if (THPVariable_Unpack(pn->leaves[0]).get_device() == THPVariable_Unpack(pn->buf).get_device()) {
+        ++g_solo.pool_head;  // the pool's references to the pair move to its buffer's record
+        SoloState::BufRec* rec = nullptr;
+        for (auto& r : g_solo.bufs)
+          if (r.buf == pn->buf) rec = &r;
+        if (rec) {
+          rec->pairs.push_back(pr);
+          Py_INCREF(pr.first);
+          Py_INCREF(pr.second);
+        }
+        Py_INCREF(pr.first);
+        Py_INCREF(pr.second);
+        g_solo.handed.push_back(pr);
+        view = pr.first;
+        n = pn;
+      } else {
+        solo_release(pn, kSoloDone);  // (a pool on another device: this delta takes a fresh node)
+      }
+    }
+    if (!n) {
+      n = reinterpret_cast<SoloObject*>(g_solo.type->tp_alloc(g_solo.type, 0));
+      if (!n) return nullptr;
+      if (!solo_capture_into(n, tree)) {
+        Py_DECREF(n);
+        if (PyErr_Occurred()) return nullptr;
+        Py_RETURN_NONE;
+      }
+    }
+    struct DropN {
+      SoloObject* n;
+      ~DropN() { Py_DECREF(n); }
+    } drop_n{n};
+    const int dev = THPVariable_Unpack(n->leaves[0]).get_device();
+    // the pending limits: past max_pending every pending norm is computed now (one launch per
+    // run); past the byte budget, the ones whose pytree nobody but the node holds any more (the
+    // deltas the views alone keep alive), rechecked after every further quarter budget
+    int er = 0;
+    if (g_solo.pending + 1 > g_solo.max_pending) {
+      er = solo_resolve_all();
+    } else if (g_solo.pending_bytes + n->nbytes > solo_budget(dev) && g_solo.pending_bytes + n->nbytes >= g_solo.recheck) {
+      er = solo_evict();
+      g_solo.recheck = g_solo.pending_bytes + n->nbytes + solo_budget(dev) / 4;
+    }
+    if (er != 0) {
+      Py_XDECREF(view);
+      solo_release(n, kSoloDone);
+      return nullptr;
+    }
+    if (!view) {
+      PyObject* buf;
+      long long idx;
+      if (!solo_column(dev, &buf, &idx)) return nullptr;
+      Py_INCREF(buf);
+      Py_XSETREF(n->buf, buf);
+      n->idx = idx;
+    }
+    PyObject* wr = PyWeakref_NewRef(reinterpret_cast<PyObject*>(n), nullptr);
+    if (!wr) {
+      Py_XDECREF(view);
+      solo_release(n, kSoloDone);
+      return nullptr;
+    }
+    n->state = kSoloPending;
+    ++g_solo.pending;
+    g_solo.pending_bytes += n->nbytes;
+    if (g_solo.reg.size() >= 2 * static_cast<size_t>(g_solo.pending) + 64) solo_compact();
+    g_solo.reg.push_back(wr);
+    if (which == 1) ++g_solo.want;
+    return view ? view : solo_view(n, which);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
 }
 
 // tree_l2_squared / tree_l2_norm (tree_util.py:105-114) of the delta the running sum just
@@ -2557,6 +3454,7 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
     PyErr_SetString(PyExc_RuntimeError, "fedjax_amd.tree_util is not installed (fast_install_norms)");
     return nullptr;
   }
+  bool chain_delta = false;  // the running sum's last delta (its chain's norm, by the Python path)
   if (nargs == 1 && !kwnames && g_fast.defer && g_fast.last && g_fast.norm_view && g_fast.ticket &&
       Py_TYPE(args[0]) != g_fast.wt && Py_TYPE(args[0]) != g_fast.ps) {
     PyObject* no = PyWeakref_GetObject(g_fast.last);
@@ -2597,6 +3495,7 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
           // raises for one modified since tree_weight, so a view is either filled from the
           // values tree_weight saw or never filled)
           if (same) {
+            chain_delta = true;
             if ((!ch->buf || ch->buf == Py_None) && which == 1 && g_fast.pool_buf && g_fast.pool_views) {
               // the chain's first norm: take the pool as the chain's buffer and views (same device,
               // the current chain size)
@@ -2664,6 +3563,12 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
         }
       }
     }
+  }
+  if (!chain_delta && nargs == 1 && !kwnames && g_fast.defer && g_solo.on && g_solo.type && g_solo.rows_fn && g_fast.norm_view &&
+      g_fast.d_view_ticket && Py_TYPE(args[0]) != g_fast.wt && Py_TYPE(args[0]) != g_fast.ps) {
+    PyObject* v = solo_norm(args[0], which);
+    if (v != Py_None) return v;  // (a lazy view, or nullptr with the error set)
+    Py_DECREF(v);
   }
   return PyObject_Vectorcall(py, args, nargs, kwnames);
 }
@@ -3085,6 +3990,10 @@ PyMethodDef kMethods[] = {
     {"flush_views", flush_views, METH_O, "fold the chains lazy norm views in an object still wait on"},
     {"fast_install_norms", fast_install_norms, METH_VARARGS, "register tree_util's lazy norm classes and fallbacks"},
     {"drop_pool", drop_pool, METH_NOARGS, "forget the lazy-norm pool"},
+    {"solo_config", solo_config, METH_VARARGS, "standalone lazy norms: switch, limits, library entry points"},
+    {"solo_resolve", solo_resolve_py, METH_O, "compute pending standalone lazy norms now (None: all)"},
+    {"solo_info", solo_info, METH_NOARGS, "standalone lazy norms: pending, fused, computed alone, stale"},
+    {"solo_norm", solo_norm_py, METH_VARARGS, "the standalone lazy norm view of a tree, or None"},
     {"pool_info", pool_info, METH_NOARGS, "(pool views ready, norms asked for since the last refill)"},
     {"tree_l2_squared", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_tree_l2_squared)),
      METH_FASTCALL | METH_KEYWORDS,
@@ -3134,9 +4043,13 @@ PyMODINIT_FUNC PyInit__fjhost(void) {
     return nullptr;
   }
   const std::pair<const char*, PyType_Spec*> types[] = {
-      {"WeightedBase", &kWTSpec}, {"ChainBase", &kChainSpec}, {"PendingBase", &kPSSpec}};
+      {"WeightedBase", &kWTSpec}, {"ChainBase", &kChainSpec}, {"PendingBase", &kPSSpec}, {"SoloNorm", &kSoloSpec}};
   for (const auto& t : types) {
     PyObject* tp = PyType_FromSpec(t.second);
+    if (tp && t.second == &kSoloSpec) {
+      Py_INCREF(tp);
+      g_solo.type = reinterpret_cast<PyTypeObject*>(tp);
+    }
     if (!tp || PyModule_AddObject(m, t.first, tp) != 0) {
       Py_XDECREF(tp);
       Py_DECREF(m);

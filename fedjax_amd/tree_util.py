@@ -42,7 +42,7 @@ __all__ = [
     "tree_weight", "tree_inverse_weight", "tree_zeros_like", "tree_add", "tree_sum",
     "tree_mean", "tree_size", "tree_l2_squared", "tree_l2_norm", "tree_clip_by_global_norm",
     "tree_l2_norms", "tree_mean_with_l2_norms", "WeightedTree", "PendingSum", "set_deferred_sums",
-    "set_bf16_semantics", "bf16_semantics",
+    "set_lazy_norms", "set_bf16_semantics", "bf16_semantics",
 ]
 
 # Non-temporal loads pay off once the deltas cannot stay in the 256 MiB Infinity
@@ -327,6 +327,7 @@ def _native_fold_addrs() -> None:
     _FILL_ADDR = ctypes.cast(lib.fjtree_norms_fill, ctypes.c_void_p).value
     _ROWS_ADDR = ctypes.cast(lib.fjagg_wsum_l2_ptrs_rows, ctypes.c_void_p).value
     _mean_config()
+    _solo_config()
 
 
 def set_nontemporal_min_bytes(nbytes: int) -> None:
@@ -739,6 +740,55 @@ def set_deferred_sums(enabled: bool = True, *, budget_bytes: Optional[int] = Non
     _HOST.drop_pool()  # (the lazy-norm pool's buffer is sized by max_clients)
 
 
+# Standalone lazy norms (fjhost.cpp "standalone lazy norms"): tree_l2_norm(delta) of a delta no
+# running sum took — examples/fed_avg.py:79-81, before the tree_mean of :82 — is a lazy view
+# whose value the tree_mean launch folding that delta writes. budget_bytes None = automatic (the
+# deferred sums' budget): past it, or past max_pending views, the oldest are computed at once.
+_LAZY = {"enabled": os.environ.get("FJAGG_LAZY_NORMS", "1") != "0", "budget_bytes": None, "max_pending": 16383}
+
+
+def set_lazy_norms(enabled: bool = True, *, budget_bytes: Optional[int] = None,
+                   max_pending: Optional[int] = None) -> None:
+    """Configure ``tree_l2_norm`` / ``tree_l2_squared`` of a float32 device pytree that no
+    deferred running sum just took (examples/fed_avg.py:79-81 takes the norm of each client's
+    delta before the round's ``tree_mean``, :82).
+
+    Enabled (default, with deferred sums on): the call returns a lazy 0-d view and holds the
+    delta's leaves; a later ``tree_mean`` / ``mean_aggregator().apply`` that folds the same,
+    unmodified pytree writes the norm from the same pass over the delta (so the round reads
+    each delta once). Reading the view first (any torch function or method, ``float``,
+    ``print``), or a delta no mean folds, computes it with its own launch of the same kernel:
+    the value does not depend on when it is read (f32 sum of squares in a fixed order,
+    DESIGN.md §4). At most ``max_pending`` norms (default 16383) wait at once, past which all
+    are computed; once the waiting deltas pass ``budget_bytes`` (default: the deferred sums'
+    budget), those whose pytree only the lazy norm still holds are computed (checked again
+    after every further quarter budget), so the views never keep much more than that alive on
+    their own. A delta leaf
+    updated in place before its norm is computed makes reading the view raise RuntimeError
+    (the value at the call is gone); writes that bypass torch's version counter are not
+    detected, as for deferred sums. Disabled (or ``set_deferred_sums(False)``): every call
+    computes at once, as the reference does."""
+    _LAZY["enabled"] = bool(enabled)
+    if budget_bytes is not None:
+        _LAZY["budget_bytes"] = int(budget_bytes) if int(budget_bytes) > 0 else None
+    if max_pending is not None:
+        _LAZY["max_pending"] = max(1, min(1 << 20, int(max_pending)))
+    _solo_config()
+
+
+def _solo_budget(dev: int) -> int:
+    return _defer_budget(torch.device("cuda", dev))
+
+
+def _solo_config() -> None:
+    """set_lazy_norms' settings and the library's entry points, into fjhost (once loaded)."""
+    if _ENTRY_ADDRS is None:
+        _HOST.solo_config(_LAZY["enabled"], _LAZY["max_pending"], _LAZY["budget_bytes"] or 0, 0, 0, 0, _solo_budget)
+        return
+    _HOST.solo_config(_LAZY["enabled"], _LAZY["max_pending"], _LAZY["budget_bytes"] or 0, _ROWS_ADDR,
+                      _ENTRY_ADDRS[3], _ENTRY_ADDRS[0], _solo_budget)
+
+
 def _defer_budget(device: torch.device) -> int:
     """Bytes of deltas one deferred chain may hold on ``device`` (see set_deferred_sums)."""
     b = _DEFER["budget_bytes"]
@@ -796,8 +846,11 @@ class _NormView(torch.Tensor):
 
 
 def _fold_ticket(ticket) -> None:
-    """Fold the chain a waiting lazy norm's ticket names (fjhost.flush_views calls this)."""
-    if ticket.node is not None:
+    """Fold the chain a waiting lazy norm's ticket names (fjhost.flush_views calls this); a
+    standalone norm's ticket (a SoloNorm node) is computed by its own launch."""
+    if type(ticket) is _HOST.SoloNorm:
+        _HOST.solo_resolve([ticket])
+    elif ticket.node is not None:
         ticket.node._chain.tip.materialize()  # folds every pending link of the chain
 
 
@@ -806,7 +859,10 @@ def _flush_views(x) -> None:
     t = type(x)
     if t is _NormView:
         ticket = getattr(x, "_ticket", None)
-        if ticket is not None and ticket.node is not None:
+        if type(ticket) is _HOST.SoloNorm:
+            if ticket.node is not None:
+                _HOST.solo_resolve([ticket])  # (raises for a stale one)
+        elif ticket is not None and ticket.node is not None:
             ticket.node._chain.tip.materialize()  # folds every pending link of the chain
     elif t is list or t is tuple:
         for y in x:
@@ -1578,8 +1634,10 @@ def _l2_rows(rows: List[List[torch.Tensor]], take_sqrt: bool) -> torch.Tensor:
 
 def _l2_fast(pytree_, which: int):
     """(l2sq, l2)[which] of a float32 device pytree: the fused value of a preceding
-    tree_add(s, tree_weight(pytree_, n)) when pytree_ is unchanged since, else one
-    fjtree launch (same reduction order, so the same bits). None: not the fast case."""
+    tree_add(s, tree_weight(pytree_, n)) when pytree_ is unchanged since; with deferral on,
+    else a standalone lazy norm (set_lazy_norms) that the tree_mean folding pytree_ computes;
+    else one fjtree launch (same reduction order as the fused tree_add, so the same bits).
+    None: not the fast case."""
     if _TREE_ADDRS is None:
         _tree_addrs()
     if _DEFER["enabled"]:
@@ -1590,6 +1648,12 @@ def _l2_fast(pytree_, which: int):
     for cap, sq, l2 in _NORMS:
         if host.matches(pytree_, cap[0], cap[1]):
             return sq if which == 0 else l2
+    if _DEFER["enabled"] and _LAZY["enabled"]:
+        if _ENTRY_ADDRS is None:
+            _native_fold_addrs()
+        v = host.solo_norm(pytree_, which)
+        if v is not None:
+            return v
     got = _leaf_fold([pytree_], [1], [None], norm_operand=0, no_out=True)
     return None if got is None else got[1 + which]
 
@@ -1628,6 +1692,7 @@ def _tree_l2_norm_py(pytree_: PyTree) -> torch.Tensor:
 # The per-client delta_l2_norm of the running-sum loops (fed_avg.py:142-144), native: the lazy
 # view of the delta the running sum just took, without a Python frame (fjhost.tree_l2_norm).
 _HOST.fast_install_norms(_Ticket, _NormView, _tree_l2_squared_py, _tree_l2_norm_py, _fold_ticket)
+_solo_config()  # set_lazy_norms' defaults (FJAGG_LAZY_NORMS=0: off); the entry points once the library loads
 tree_l2_squared = _HOST.tree_l2_squared
 tree_l2_norm = _HOST.tree_l2_norm
 

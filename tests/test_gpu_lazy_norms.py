@@ -1,0 +1,276 @@
+"""Standalone lazy norms (fjhost.cpp "standalone lazy norms", tree_util.set_lazy_norms): the
+round of examples/fed_avg.py:72-82 as written —
+
+    for each client: deltas.append((delta, n)); diag[cid] = tree_l2_norm(delta)
+    mean = tree_mean(deltas)
+
+— reads every delta once: each norm is a lazy view that the tree_mean launch folding the same,
+unmodified delta fills (fjagg_wsum_l2_ptrs_rows). The mean stays the oracle's bits; a norm's
+value must not depend on when it is computed (in the mean's launch, read first, past the
+pending budget, with other clients or alone): the same bits every way, within f32 rounding of
+an f64 norm (XLA's own reduction order is not pinned, tree_util.py:105-114). A delta updated in
+place after its norm makes the view raise; a replaced leaf keeps the captured value.
+"""
+import gc
+import weakref
+
+import numpy as np
+import pytest
+import torch
+
+import fedjax_amd
+from fedjax_amd import pytree, tree_util as tu
+from oracle import tree_util_ref as ref
+
+pytestmark = pytest.mark.gpu
+
+EMNIST = {"conv2_d": {"b": (32,), "w": (3, 3, 1, 32)}, "conv2_d_1": {"b": (64,), "w": (3, 3, 32, 64)},
+          "linear": {"b": (128,), "w": (9216, 128)}, "linear_1": {"b": (62,), "w": (128, 62)}}
+SMALL = {"a": (5003,), "b": {"c": (33, 3)}}
+H = tu._HOST
+
+
+@pytest.fixture(autouse=True)
+def lazy_on():
+    tu.set_deferred_sums(True)
+    tu.set_lazy_norms(True, budget_bytes=0)
+    yield
+    H.solo_resolve(None)
+    tu.set_lazy_norms(True, budget_bytes=0, max_pending=16383)
+
+
+def tmap(fn, t):
+    return {k: tmap(fn, v) for k, v in t.items()} if isinstance(t, dict) else fn(t)
+
+
+def make_deltas(shapes, K, seed, dev):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    return [tmap(lambda s: (torch.rand(s, device=dev, generator=g) - 0.5) * 0.02, shapes) for _ in range(K)]
+
+
+def bits(t):
+    return t.detach().reshape(-1).view(torch.int32).cpu()
+
+
+def f64norm(t):
+    x = np.concatenate([v.detach().cpu().numpy().astype(np.float64).reshape(-1) for v in pytree.leaves_of(t)])
+    return float(np.sqrt((x * x).sum()))
+
+
+def example_round(deltas, weights, read_at=()):
+    """examples/fed_avg.py:72-82 with the clients' updates already made."""
+    client_diagnostics = {}
+    client_delta_params_weights = []
+    for cid, (delta_params, n) in enumerate(zip(deltas, weights)):
+        client_delta_params_weights.append((delta_params, n))
+        client_diagnostics[cid] = {"delta_l2_norm": tu.tree_l2_norm(delta_params)}
+        if cid in read_at:
+            float(client_diagnostics[cid]["delta_l2_norm"])  # a read before the mean
+    mean = tu.tree_mean(client_delta_params_weights)
+    return mean, [client_diagnostics[c]["delta_l2_norm"] for c in range(len(deltas))]
+
+
+def want_mean(deltas, weights):
+    return ref.tree_mean([(tmap(lambda x: x.cpu().numpy(), d), n) for d, n in zip(deltas, weights)])
+
+
+def same_mean(got, want):
+    return all(np.array_equal(a.cpu().numpy().reshape(-1).view(np.uint32), np.asarray(b).reshape(-1).view(np.uint32))
+               for a, b in zip(pytree.leaves_of(got), pytree.leaves_of(want)))
+
+
+@pytest.mark.parametrize("K", [10, 128])
+def test_example_round_fuses_the_norms_into_the_mean(cuda, K):
+    deltas = make_deltas(EMNIST, K, 1, cuda)
+    weights = [int(v) for v in ref.fedavg_weights(K, seed=2)]
+    before = H.solo_info()
+    mean, norms = example_round(deltas, weights)
+    info = H.solo_info()
+    assert info["fused"] - before["fused"] == K  # every norm came from the mean's launches
+    assert info["eager"] == before["eager"] and info["pending"] == 0
+    assert all(type(v) is tu._NormView and v._ticket.node is None for v in norms)
+    assert same_mean(mean, want_mean(deltas, weights))
+    np.testing.assert_allclose([float(v) for v in norms], [f64norm(d) for d in deltas], rtol=2e-6)
+    # each norm computed on its own (read before any mean): the same bits
+    alone = []
+    for d in deltas:
+        v = tu.tree_l2_norm(d)
+        assert type(v._ticket) is H.SoloNorm and v._ticket.node is not None
+        alone.append(bits(v).clone())  # (the read computes it: one launch)
+    assert H.solo_info()["eager"] - info["eager"] == K
+    for v, a in zip(norms, alone):
+        assert torch.equal(bits(v), a)
+    # squared norms share the node of the norm taken just before
+    d = deltas[0]
+    n, q = tu.tree_l2_norm(d), tu.tree_l2_squared(d)
+    assert n._ticket is q._ticket
+    tu.tree_mean([(d, 1), (deltas[1], 2)])
+    assert float(q) == pytest.approx(float(n) ** 2, rel=1e-6)
+
+
+def test_read_before_mean_and_partial_rounds(cuda):
+    """Reading some norms mid-loop computes just those; the rest fuse into the mean. Values
+    equal the all-fused round's bits; the mean is unchanged."""
+    K = 40
+    deltas = make_deltas(SMALL, K, 3, cuda)
+    weights = [k % 7 + 1 for k in range(K)]
+    mean0, norms0 = example_round(deltas, weights)
+    ref0 = [bits(v).clone() for v in norms0]
+    before = H.solo_info()
+    mean1, norms1 = example_round(deltas, weights, read_at=(0, 3, 17, 39))
+    info = H.solo_info()
+    assert info["eager"] - before["eager"] == 4 and info["fused"] - before["fused"] == K - 4
+    assert all(torch.equal(bits(v), r) for v, r in zip(norms1, ref0))
+    assert all(torch.equal(a, b) for a, b in zip(pytree.leaves_of(mean0), pytree.leaves_of(mean1)))
+    # norms of a subset of the mean's clients: a run of matched clients, then plain folds
+    norms2 = [tu.tree_l2_norm(d) for d in deltas[:5]]
+    mean2 = tu.tree_mean(list(zip(deltas, weights)))
+    assert all(v._ticket.node is None for v in norms2)
+    assert all(torch.equal(bits(v), r) for v, r in zip(norms2, ref0[:5]))
+    assert all(torch.equal(a, b) for a, b in zip(pytree.leaves_of(mean0), pytree.leaves_of(mean2)))
+
+
+def test_modified_and_replaced_leaves(cuda):
+    deltas = make_deltas(SMALL, 6, 4, cuda)
+    want = [f64norm(d) for d in deltas]
+    norms = [tu.tree_l2_norm(d) for d in deltas]
+    deltas[2]["a"].mul_(2.0)  # in place after the norm: the value at the call is gone
+    deltas[4]["b"] = {"c": torch.zeros(33, 3, device=cuda)}  # replaced: the captured leaves hold the value
+    mean = tu.tree_mean([(d, 1) for d in deltas])  # (the mean folds the current values, as always)
+    assert same_mean(mean, want_mean(deltas, [1] * 6))
+    with pytest.raises(RuntimeError, match="modified"):
+        float(norms[2])
+    with pytest.raises(RuntimeError, match="modified"):
+        torch.stack(norms)
+    ok = [0, 1, 3, 4, 5]
+    np.testing.assert_allclose([float(norms[k]) for k in ok], [want[k] for k in ok], rtol=2e-6)
+    assert norms[4]._ticket.node is None
+
+
+@pytest.mark.parametrize("form", ["iterator", "generator", "aggregator"])
+def test_one_shot_iterables_fuse(cuda, form):
+    K = 12
+    deltas = make_deltas(SMALL, K, 5, cuda)
+    weights = [k + 1 for k in range(K)]
+    norms = [tu.tree_l2_norm(d) for d in deltas]
+    before = H.solo_info()
+    if form == "iterator":
+        mean = tu.tree_mean(iter(list(zip(deltas, weights))))
+    elif form == "generator":
+        mean = tu.tree_mean((d, w) for d, w in zip(deltas, weights))
+    else:
+        agg = fedjax_amd.aggregators.mean_aggregator()
+        state = agg.init()
+        mean, _ = agg.apply(iter([(str(k), d, w) for k, (d, w) in enumerate(zip(deltas, weights))]), state)
+    assert H.solo_info()["fused"] - before["fused"] == K
+    assert same_mean(mean, want_mean(deltas, weights))
+    np.testing.assert_allclose([float(v) for v in norms], [f64norm(d) for d in deltas], rtol=2e-6)
+
+
+def test_dropped_views_release_the_deltas(cuda):
+    d = make_deltas(SMALL, 1, 6, cuda)[0]
+    leaf = weakref.ref(d["a"])
+    v = tu.tree_l2_norm(d)
+    node = weakref.ref(v._ticket)
+    assert H.solo_info()["pending"] == 1
+    del d
+    gc.collect()
+    assert leaf() is not None  # the pending view holds the captured leaves
+    del v
+    gc.collect()
+    # (a pool view's node lets its capture go when the pool next looks: any mean, the budget, solo_info)
+    assert H.solo_info()["pending"] == 0
+    gc.collect()
+    assert leaf() is None
+
+
+def test_budget_computes_the_deltas_only_views_hold(cuda):
+    """Past the byte budget the norms whose pytree nobody else holds are computed; the ones
+    whose pytree the caller still holds wait for the mean. Same bits either way."""
+    deltas = make_deltas(SMALL, 8, 7, cuda)
+    ref_bits = [bits(tu.tree_l2_norm(d)).clone() for d in deltas]
+    per = 4 * (5003 + 99)
+    tu.set_lazy_norms(True, budget_bytes=3 * per)
+    before = H.solo_info()
+    held = [tu.tree_l2_norm(d) for d in deltas]  # the caller holds every delta: all wait
+    assert H.solo_info()["pending"] == 8
+    tu.tree_mean([(d, 1) for d in deltas])
+    assert H.solo_info()["fused"] - before["fused"] == 8
+    orphans = []
+    src = make_deltas(SMALL, 8, 7, cuda)
+    for k in range(8):  # copies of the same values; nobody else keeps these trees
+        orphans.append(tu.tree_l2_norm(tmap(lambda x: x.clone(), src[k])))
+    assert H.solo_info()["pending"] <= 4 and H.solo_info()["eager"] > before["eager"]
+    for v, r in zip(held + orphans, ref_bits + ref_bits):
+        assert torch.equal(bits(v), r)
+    tu.set_lazy_norms(True, max_pending=3)
+    vs = [tu.tree_l2_norm(d) for d in deltas]
+    assert H.solo_info()["pending"] <= 3
+    assert all(torch.equal(bits(v), r) for v, r in zip(vs, ref_bits))
+
+
+def test_misaligned_delta_is_computed_alone(cuda):
+    """A leaf off 16 bytes walks element units: its client's chunk folds plainly and every
+    norm of it is computed by its own launch (its own plan); the aligned clients' norms keep
+    the all-16-byte plan's bits."""
+    deltas = make_deltas(SMALL, 5, 8, cuda)
+    ref_bits = [bits(tu.tree_l2_norm(d)).clone() for d in deltas]
+    base = torch.empty(5004, device=cuda)
+    odd = {"a": base[1:], "b": {"c": deltas[2]["b"]["c"]}}
+    odd["a"].copy_(deltas[2]["a"])
+    trees = deltas[:2] + [odd] + deltas[3:]
+    norms = [tu.tree_l2_norm(d) for d in trees]
+    mean = tu.tree_mean([(d, 3) for d in trees])
+    assert same_mean(mean, want_mean(trees, [3] * 5))
+    for k in (0, 1, 3, 4):
+        assert torch.equal(bits(norms[k]), ref_bits[k])
+    assert float(norms[2]) == pytest.approx(f64norm(odd), rel=2e-6)
+
+
+def test_buffer_boundary_splits_the_run(cuda):
+    """Norms of one round that straddle two norm buffers fold in two runs, all fused."""
+    deltas = make_deltas(SMALL, 16, 9, cuda)
+    col = H.solo_info()["column"] % 4096
+    junk = [tu.tree_l2_norm({"a": torch.ones(4, device=cuda)}) for _ in range((4090 - col) % 4096)]
+    del junk
+    gc.collect()
+    assert H.solo_info()["column"] == 4090
+    before = H.solo_info()
+    mean, norms = example_round(deltas, list(range(1, 17)))
+    assert H.solo_info()["fused"] - before["fused"] == 16
+    np.testing.assert_allclose([float(v) for v in norms], [f64norm(d) for d in deltas], rtol=2e-6)
+    assert same_mean(mean, want_mean(deltas, list(range(1, 17))))
+
+
+def test_switch_off_is_eager(cuda):
+    d = make_deltas(SMALL, 1, 10, cuda)[0]
+    tu.set_lazy_norms(False)
+    v = tu.tree_l2_norm(d)
+    assert type(v) is not tu._NormView
+    tu.set_lazy_norms(True)
+    tu.set_deferred_sums(False)
+    try:
+        assert type(tu.tree_l2_norm(d)) is not tu._NormView
+    finally:
+        tu.set_deferred_sums(True)
+    assert float(v) == pytest.approx(f64norm(d), rel=2e-6)
+
+
+def test_pool_pairs_are_reused_once_dropped(cuda):
+    """After a mean that fused lazy norms, the next round's (view, node) pairs are pre-made; a
+    full buffer whose views the caller dropped is reused whole; values stay the fused bits."""
+    deltas = make_deltas(SMALL, 64, 11, cuda)
+    ref_bits = [bits(tu.tree_l2_norm(d)).clone() for d in deltas]
+    example_round(deltas, list(range(1, 65)))  # asks for 64 norms: the pool is sized to that
+    assert H.solo_info()["pool_ready"] >= 64
+    kept = None
+    for rnd in range(80):  # > 4096 columns: buffers fill, the dropped ones come back
+        mean, norms = example_round(deltas, list(range(1, 65)))
+        if rnd == 3:
+            kept = norms  # held: that buffer is never reused
+        if rnd % 20 == 0:
+            assert all(torch.equal(bits(v), r) for v, r in zip(norms, ref_bits))
+    info = H.solo_info()
+    assert info["pool_reuses"] >= 1
+    assert all(torch.equal(bits(v), r) for v, r in zip(kept, ref_bits))
+    assert all(torch.equal(bits(v), r) for v, r in zip(norms, ref_bits))

@@ -341,10 +341,12 @@ def test_lazy_norms_of_a_deferred_sum(cuda, sum_mode):
     want = ref.tree_inverse_weight(want, 12.0)
     for a, b in zip(leaves_np(mean), pytree.leaves_of(want)):
         assert np.array_equal(bits(a), bits(b.reshape(-1)))
-    # a norm of a delta that is not the last one added is computed at once (not lazy)
+    # a norm of a delta that is not the last one added is not the chain's: a standalone lazy norm
     s = tu.tree_add(tu.tree_zeros_like(xs[0]), tu.tree_weight(xs[0], 1))
     s = tu.tree_add(s, tu.tree_weight(xs[1], 1))
-    assert type(tu.tree_l2_norm(xs[0])) is not tu._NormView
+    v = tu.tree_l2_norm(xs[0])
+    assert type(v._ticket) is tu._HOST.SoloNorm
+    np.testing.assert_allclose(float(v), f64norm(xs[0]), rtol=2e-6)
 
 
 @pytest.mark.deferred_only
@@ -395,7 +397,7 @@ def test_lazy_norm_pool_across_rounds(cuda, sum_mode):
     s = tu.tree_add(tu.tree_zeros_like(t), tu.tree_weight(t, 1))
     t["b"] = {"c": xs[1]["b"]["c"]}  # a new inner dict: the root's version tag moved
     v = tu.tree_l2_norm(t)
-    assert type(v) is not tu._NormView
+    assert type(v._ticket) is H.SoloNorm  # not the chain's: a standalone lazy norm of the new contents
     np.testing.assert_allclose(float(v), f64norm({"a": xs[0]["a"], "b": {"c": xs[1]["b"]["c"]}}), rtol=2e-6)
     tu.tree_inverse_weight(s, 1.0)
     # the same dict with a leaf updated in place after tree_weight: the view is lazy, and the
