@@ -462,6 +462,60 @@ def dropin_surface(dev, calls=20):
     return res
 
 
+def drain_stream(stream, seconds: float) -> bool:
+    """Wait (polling) until `stream` has no pending work, at most `seconds`."""
+    done = torch.cuda.Event()
+    done.record(stream)
+    t0 = time.perf_counter()
+    while not done.query():
+        if time.perf_counter() - t0 > seconds:
+            return False
+        time.sleep(0.001)
+    return True
+
+
+def autotune_exchange(cands, measure, abort_native, dev, rank):
+    """Time every exchange candidate (engine, collective, buckets) on every rank and agree on
+    each outcome over the process group: ({candidate: ms, max over ranks}, {candidate: why
+    dropped}). ``measure(cand)`` returns this rank's ms per step, None past its host deadline,
+    or raises. A candidate that failed or missed its deadline on ANY rank is dropped on every
+    rank; a missed deadline on the library's own communicator ("native" engine) makes every
+    rank call ``abort_native()`` (fjcomm_abort) and skip the remaining native candidates, so one
+    hung collective costs one deadline instead of the run (reference analogue: the pmap
+    gather of fedjax/core/for_each_client.py:266-357, which has no such bound)."""
+    import torch.distributed as dist
+    tune, dropped, native_dead = {}, {}, False
+    for cand in cands:
+        if cand[0] == "native" and native_dead:
+            dropped[cand] = "skipped: communicator aborted"
+            continue
+        status, ms = 0.0, 0.0  # 0 ok, 1 raised, 2 missed the deadline
+        try:
+            got = measure(cand)
+            if got is None:
+                status = 2.0
+                log(f"[bench rank {rank}] auto-tune candidate {cand[0]}/{cand[1]}/{cand[2]} missed its deadline")
+            else:
+                ms = float(got)
+        except Exception as e:  # noqa: BLE001
+            status = 1.0
+            log(f"[bench rank {rank}] auto-tune candidate {cand[0]}/{cand[1]}/{cand[2]} failed: {e}")
+        if status == 2.0 and cand[0] == "native":
+            abort_native()  # before the agreement: its collective may hold the GPU until then
+        flag = torch.tensor([status, ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        worst, slowest = float(flag[0].item()), float(flag[1].item())
+        if worst == 0.0:
+            tune[cand] = slowest
+            continue
+        dropped[cand] = "dropped: missed the deadline" if worst == 2.0 else "dropped: raised"
+        if worst == 2.0 and cand[0] == "native":
+            if status != 2.0:
+                abort_native()  # (another rank missed it: this rank stops using the communicator too)
+            native_dead = True
+    return tune, dropped
+
+
 def rank_timeout(args) -> float:
     """Seconds a spawned N-rank run may take before spawn_ranks kills it: process start,
     rendezvous and communicator init (300 s), plus every step the ranks run — warmup,
@@ -472,7 +526,8 @@ def rank_timeout(args) -> float:
     esize = torch.empty((), dtype=dtype).element_size()
     per_rank_s = (K + args.gpus - 1) // args.gpus * P * esize / 0.5e12
     steps = args.warmup + args.steps + 24 * 7 + 6
-    return 300.0 + 4.0 * steps * per_rank_s
+    # (+ one missed auto-tune deadline, the abort's stream drain and the communicator's teardown)
+    return 300.0 + 4.0 * steps * per_rank_s + 2.0 * args.candidate_deadline + 70.0
 
 
 def start_rank_watchdog(rank: int, seconds: float):
@@ -722,6 +777,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--candidate-deadline", type=float, default=60.0,
+                    help="host seconds one exchange auto-tune measurement may take before the library's own "
+                         "communicator is aborted and its candidates dropped (torch-engine candidates run first)")
     ap.add_argument("--buckets", default="0",
                     help="N>1: parameter buckets of the fold/reduce pipeline, a count or relative sizes "
                          "like 4:2:1; 0 = pick the fastest of BUCKET_CANDIDATES during warmup (max over ranks)")
@@ -937,40 +995,64 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def wall_local(nsteps, deadline_s):
+        """This rank's wall time of nsteps steps, or None when they have not completed within
+        deadline_s (polled: no blocking wait on a collective that may never end). No
+        collective runs after the steps: the ranks compare results in autotune_exchange."""
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(nsteps):
+            step()
+        done = torch.cuda.Event()
+        done.record(stream)  # (the steps end on `stream`: the last bucket reduces there)
+        while not done.query():
+            if time.perf_counter() - t0 > deadline_s:
+                return None
+            time.sleep(0.0002)
+        return time.perf_counter() - t0
+
     tune = {}
     if sharded and args.buckets == "0":
-        # every rank measures every candidate and sees the same max-over-ranks times,
-        # so all ranks pick the same (engine, collective, buckets) without another exchange.
-        # The mean is needed on rank 0 only, so all_reduce is a candidate next to reduce:
-        # RCCL may run it faster (its all-reduce algorithms are the most tuned), and it
-        # leaves the same mean on rank 0 (within the tolerance of DESIGN.md §4).
-        engines = ["native", "torch"] if comm is not None and args.engine == "auto" else [engine]
+        # every rank measures every candidate and the ranks agree on each result (max over
+        # ranks), so all pick the same (engine, collective, buckets). The mean is needed on rank
+        # 0 only, so all_reduce is a candidate next to reduce: RCCL may run it faster (its
+        # all-reduce algorithms are the most tuned), and it leaves the same mean on rank 0
+        # (within the tolerance of DESIGN.md §4). The torch engine's candidates run first; the
+        # library's own communicator's run under a host deadline — past it every rank aborts
+        # that communicator (fjcomm_abort) and its remaining candidates are skipped.
+        engines = ["torch", "native"] if comm is not None and args.engine == "auto" else [engine]
         colls = ["all_reduce"] if args.all_ranks else ["reduce", "all_reduce"]
-        for eng in engines:
-            for col in colls:
-                for b in BUCKET_CANDIDATES:
-                    if len(fd.bucket_edges(P, b)) < (b if isinstance(b, int) else len(b)):
-                        continue  # P too small for that many aligned buckets
-                    engine, collective, buckets = eng, col, b
-                    phase(rank, f"auto-tune candidate {eng}/{col}/{fd.bucket_name(b)}")
-                    # a candidate that raises on every rank (e.g. an RCCL error from the
-                    # library's own communicator) is dropped and the others still run; the
-                    # ranks agree on that over the process group before going on
-                    ok, t = 1.0, float("inf")
-                    try:
-                        wall(2)
-                        t = wall(5) / 5 * 1e3
-                    except Exception as e:  # noqa: BLE001
-                        ok = 0.0
-                        log(f"[bench rank {rank}] auto-tune candidate {eng}/{col}/{fd.bucket_name(b)} failed: {e}")
-                    flag = torch.tensor([ok], dtype=torch.float32, device=dev)
-                    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-                    if float(flag.item()) == 1.0:
-                        tune[(eng, col, b)] = t
+        cands = [(eng, col, b) for eng in engines for col in colls for b in BUCKET_CANDIDATES
+                 if len(fd.bucket_edges(P, b)) >= (b if isinstance(b, int) else len(b))]
+        deadline_s = args.candidate_deadline
+
+        def measure(cand):
+            nonlocal engine, collective, buckets
+            engine, collective, buckets = cand
+            phase(rank, f"auto-tune candidate {cand[0]}/{cand[1]}/{fd.bucket_name(cand[2])}")
+            if wall_local(2, deadline_s) is None:
+                return None
+            t = wall_local(5, deadline_s)
+            return None if t is None else t / 5 * 1e3
+
+        def abort_native():
+            if comm is not None:
+                try:
+                    comm.abort()
+                except Exception as e:  # noqa: BLE001
+                    log(f"[bench rank {rank}] fjcomm_abort: {e}")
+            if not drain_stream(stream, 60.0):
+                log(f"[bench rank {rank}] the stream did not drain within 60 s after fjcomm_abort")
+                sys.stdout.flush()
+                os._exit(124)
+
+        tune, dropped = autotune_exchange(cands, measure, abort_native, dev, rank)
         if not tune:
             raise SystemExit("every exchange candidate failed (see the auto-tune lines above)")
         engine, collective, buckets = min(tune, key=tune.get)
-        tune = {f"{e}/{c}/{fd.bucket_name(b)}": t for (e, c, b), t in tune.items()}
+        tune = {f"{e}/{c}/{fd.bucket_name(b)}": round(t, 4) for (e, c, b), t in tune.items()}
+        tune.update({f"{e}/{c}/{fd.bucket_name(b)}": why for (e, c, b), why in dropped.items()})
         log(f"exchange auto-tune (ms/step, max over ranks): {tune} -> "
             f"{engine}/{collective}/{fd.bucket_name(buckets)}")
     phase(rank, f"warmup ({args.warmup} steps)")

@@ -94,6 +94,8 @@ _SIGNATURES = {
     "fjcomm_unique_id": (_i32, [_vp]),
     "fjcomm_init": (_i32, [_vp, _vp, _i32, _i32]),
     "fjcomm_destroy": (_i32, [_vp]),
+    "fjcomm_abort": (_i32, [_vp]),
+    "fjcomm_test_block": (_i32, [_i64, _vp]),
     "fjcomm_sharded_wsum_dense": (_i32, [_vp, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _i32, _i32, _i32, _vp,
                                          _vp]),
     "fjcomm_sharded_wsum_dense_edges": (_i32, [_vp, _i32, _vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i32, _i32,

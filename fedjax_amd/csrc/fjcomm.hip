@@ -13,6 +13,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
+#include <thread>
+
 #include "fjagg.h"
 #include "fjcomm.h"
 
@@ -52,6 +55,7 @@ struct Rccl {
   int (*group_start)() = nullptr;
   int (*group_end)() = nullptr;
   int (*comm_destroy)(NcclComm) = nullptr;
+  int (*comm_abort)(NcclComm) = nullptr;  // (optional: fjcomm_abort)
   int (*reduce)(const void*, void*, size_t, int, int, int, NcclComm, hipStream_t) = nullptr;
   int (*all_reduce)(const void*, void*, size_t, int, int, NcclComm, hipStream_t) = nullptr;
   const char* (*error_string)(int) = nullptr;
@@ -69,6 +73,7 @@ const Rccl& rccl() {
     t.get_unique_id = reinterpret_cast<decltype(t.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
     t.comm_init_rank = reinterpret_cast<decltype(t.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
     t.comm_destroy = reinterpret_cast<decltype(t.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    t.comm_abort = reinterpret_cast<decltype(t.comm_abort)>(dlsym(h, "ncclCommAbort"));
     t.comm_init_all = reinterpret_cast<decltype(t.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
     t.group_start = reinterpret_cast<decltype(t.group_start)>(dlsym(h, "ncclGroupStart"));
     t.group_end = reinterpret_cast<decltype(t.group_end)>(dlsym(h, "ncclGroupEnd"));
@@ -94,6 +99,7 @@ int need_rccl() {
 struct Comm {
   NcclComm nc = nullptr;
   int nranks = 0, rank = 0, device = 0;
+  bool aborted = false;  // fjcomm_abort ran: every later step is refused
   hipStream_t cs = nullptr;
   hipEvent_t ready[FJCOMM_MAX_BUCKETS] = {};
   hipEvent_t done = nullptr;
@@ -191,13 +197,63 @@ int fjcomm_destroy(void* comm) {
   if (!c) return FJAGG_OK;
   DeviceGuard guard;  // the communicator's resources live on its device
   (void)hipSetDevice(c->device);
-  if (c->cs) (void)hipStreamSynchronize(c->cs);
+  if (c->aborted && c->cs) {
+    // after an abort the stream may still hold work that never ends: wait a bounded time, and
+    // past it leave the stream and its events alive (leaked) rather than block the caller
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hipStreamQuery(c->cs) == hipErrorNotReady) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+        delete c;
+        return fail(FJAGG_EHIP, "fjcomm_destroy: the aborted communicator's stream did not drain in 10 s (leaked)");
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+  } else if (c->cs) {
+    (void)hipStreamSynchronize(c->cs);
+  }
   if (c->nc && rccl().ok) rccl().comm_destroy(c->nc);
   for (hipEvent_t& e : c->ready)
     if (e) (void)hipEventDestroy(e);
   if (c->done) (void)hipEventDestroy(c->done);
   if (c->cs) (void)hipStreamDestroy(c->cs);
   delete c;
+  return FJAGG_OK;
+}
+
+int fjcomm_abort(void* comm) {
+  fjagg_g_err[0] = 0;
+  Comm* c = reinterpret_cast<Comm*>(comm);
+  if (!c) return fail(FJAGG_EINVAL, "null communicator");
+  if (c->aborted) return FJAGG_OK;
+  if (!rccl().comm_abort) return fail(FJAGG_EUNSUPPORTED, "librccl.so.1 has no ncclCommAbort");
+  DeviceGuard guard;
+  (void)hipSetDevice(c->device);
+  c->aborted = true;
+  NcclComm nc = c->nc;
+  c->nc = nullptr;
+  if (nc) {
+    if (int rc = rccl().comm_abort(nc)) return nccl_fail(rc, "ncclCommAbort");
+  }
+  return FJAGG_OK;
+}
+
+namespace {
+// a bounded spin on the real-time counter (read-only; no memory is touched): one wave
+__global__ void k_block(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+}  // namespace
+
+int fjcomm_test_block(int64_t us, void* stream) {
+  fjagg_g_err[0] = 0;
+  if (us < 0 || us > 60LL * 1000 * 1000) return fail(FJAGG_EINVAL, "us must be in [0, 60 s]");
+  int dev = 0, khz = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return hip_fail(e, "hipGetDevice");
+  if (hipError_t e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) return hip_fail(e, "wall clock rate");
+  if (khz <= 0) khz = 100000;  // (gfx9's s_memrealtime: 100 MHz)
+  hipLaunchKernelGGL(k_block, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), (long long)(us * khz / 1000));
+  if (hipError_t e = hipGetLastError()) return hip_fail(e, "k_block launch");
   return FJAGG_OK;
 }
 
@@ -227,6 +283,7 @@ int fjcomm_sharded_wsum_dense_edges(void* comm, int in_dtype, const void* x_dev,
                                     void* const* fold_events) {
   fjagg_g_err[0] = 0;
   Comm* c = reinterpret_cast<Comm*>(comm);
+  if (c && c->aborted) return fail(FJAGG_EINVAL, "the communicator was aborted (fjcomm_abort)");
   if (!c || !c->nc) return fail(FJAGG_EINVAL, "not an initialised communicator");
   if (in_dtype != FJAGG_F32 && in_dtype != FJAGG_BF16) return fail(FJAGG_EINVAL, "in_dtype must be F32 or BF16");
   if (K < 0 || P < 0 || ld < P) return fail(FJAGG_EINVAL, "need K >= 0 and 0 <= P <= ld");
@@ -341,6 +398,7 @@ int fjcomm_multi_wsum_dense(void* const* comms, int ndev, int in_dtype, const vo
   Comm* cs[FJCOMM_MAX_DEVICES];
   for (int d = 0; d < ndev; ++d) {
     cs[d] = reinterpret_cast<Comm*>(comms[d]);
+    if (cs[d] && cs[d]->aborted) return fail(FJAGG_EINVAL, "comms[%d] was aborted (fjcomm_abort)", d);
     if (!cs[d] || !cs[d]->nc) return fail(FJAGG_EINVAL, "comms[%d] is not an initialised communicator", d);
     if (cs[d]->rank != d || cs[d]->nranks != ndev)
       return fail(FJAGG_EINVAL, "comms[%d] is rank %d of %d, not %d of %d (pass fjcomm_init_all's handles in order)",

@@ -126,6 +126,14 @@ class RcclCommunicator:
         self.handle = handle
         self.device = dev
 
+    def abort(self) -> None:
+        """``fjcomm_abort``: end this communicator's outstanding collectives without waiting for
+        the other ranks (after a collective missed its deadline). The communicator refuses every
+        later step; every rank must stop using it (agree over another group first)."""
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            _lib.check(_lib.load().fjcomm_abort(self.handle), "fjcomm_abort")
+            self.aborted = True
+
     def close(self) -> None:
         if getattr(self, "handle", None) is not None and self.handle.value:
             _lib.load().fjcomm_destroy(self.handle)

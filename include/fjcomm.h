@@ -47,6 +47,19 @@ int fjcomm_unique_id(uint8_t* id /* FJCOMM_ID_BYTES */);
 int fjcomm_init(void** comm, const uint8_t* id, int nranks, int rank);
 int fjcomm_destroy(void* comm);
 
+/* ncclCommAbort: ends the communicator's outstanding collectives without waiting for the other
+ * ranks (a rank that missed a deadline on a collective that never completes calls it; every
+ * rank must then stop using this communicator). Every later step on it returns FJAGG_EINVAL;
+ * fjcomm_destroy still frees it (waiting at most 10 s for its stream). Non-blocking on the
+ * collective; no other rank's participation is needed. FJAGG_EUNSUPPORTED when the loaded RCCL
+ * has no ncclCommAbort. Replaces nothing in the reference (jax's pmap has no such control,
+ * fedjax/core/for_each_client.py:266-357): it bounds the bench's exchange auto-tune. */
+int fjcomm_abort(void* comm);
+
+/* Test support: one wave that spins on the real-time counter for `us` microseconds (<= 60 s)
+ * on `stream` (reads no memory), so tests can enqueue a collective behind running work. */
+int fjcomm_test_block(int64_t us, void* stream);
+
 /*
  * One round of the sharded weighted mean on this rank:
  *   out_dev[p] = fl(sum_{k<K} fl(x_k[p] * w_k)) * scale        (this rank's partial,

@@ -135,9 +135,10 @@ def test_spawn_timeout_names_the_stalled_rank(tmp_path, capfd):
 def test_rank_timeout_scales_with_the_workload():
     import argparse
 
-    a = argparse.Namespace(workload="c3", clients=0, gpus=8, warmup=5, steps=20)
-    c5 = argparse.Namespace(workload="c5", clients=0, gpus=8, warmup=5, steps=20)
-    assert 300 < bench.rank_timeout(a) < 400  # configs[3]: 2.1 GB per rank
+    a = argparse.Namespace(workload="c3", clients=0, gpus=8, warmup=5, steps=20, candidate_deadline=60.0)
+    c5 = argparse.Namespace(workload="c5", clients=0, gpus=8, warmup=5, steps=20, candidate_deadline=60.0)
+    # configs[3]: 2.1 GB per rank, plus one missed auto-tune deadline (2 x 60 s) and the abort's 70 s
+    assert 300 + 190 < bench.rank_timeout(a) < 400 + 190
     assert bench.rank_timeout(c5) > bench.rank_timeout(a) + 300  # configs[4]: 256 GB per rank
 
 

@@ -233,3 +233,56 @@ def test_single_process_multi_device_ndev1(cuda, coracle):
         assert np.array_equal(y.view(np.uint32), want.astype(np.float32).view(np.uint32)), key
     assert np.all(z == 0)
     assert errs == ["ValueError", "ValueError", "ValueError"]
+
+
+def _abort_worker(q):
+    """A world-1 RCCL communicator with a sharded step enqueued behind 1.5 s of other work on the
+    stream: fjcomm_abort with the step still queued returns (RCCL's teardown waits for the work
+    already on the device: about the blocker's 1.5 s here), the stream drains, and the aborted
+    communicator refuses the next step (include/fjcomm.h)."""
+    import time
+    init_world1("gloo")
+    try:
+        import bench
+        from fedjax_amd import _lib, distributed as fd, kernels
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        comm = fd.RcclCommunicator(device=dev)
+        x = torch.empty(K, P, dtype=torch.float32, device=dev)
+        kernels.fill_synth(x, seed=9)
+        wl = torch.tensor(np.float32(ref.fedavg_weights(K, seed=3)), device=dev)
+        W = float(wl.double().sum())
+        fd.sharded_weighted_mean(x, wl, W, buckets=2, comm=comm)  # a healthy step first
+        stream = torch.cuda.current_stream(dev)
+        torch.cuda.synchronize()
+        _lib.check(_lib.load().fjcomm_test_block(1_500_000, stream.cuda_stream), "fjcomm_test_block")
+        fd.sharded_weighted_mean(x, wl, W, buckets=2, comm=comm)  # queued behind the blocker
+        queued = not stream.query()
+        t0 = time.perf_counter()
+        comm.abort()
+        t_abort = time.perf_counter() - t0
+        drained = bench.drain_stream(stream, 30.0)
+        t_drain = time.perf_counter() - t0
+        try:
+            fd.sharded_weighted_mean(x, wl, W, buckets=2, comm=comm)
+            refused = None
+        except Exception as e:  # noqa: BLE001
+            refused = str(e)
+        comm.abort()  # (idempotent)
+        comm.close()
+        q.put({"queued": queued, "t_abort": t_abort, "drained": drained, "t_drain": t_drain, "refused": refused})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fjcomm_abort_with_a_queued_step(cuda):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_abort_worker, args=(q,))
+    p.start()
+    got = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert got["queued"], got  # the step was still behind the blocker when abort was called
+    assert got["t_abort"] < 30.0 and got["drained"] and got["t_drain"] < 30.0, got
+    assert got["refused"] and "aborted" in got["refused"], got
