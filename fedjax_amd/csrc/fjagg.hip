@@ -92,6 +92,7 @@ struct LdsNorm {
   // clients k .. k+N-1 (N = 1, 2, 4 or 8): lane partials -> the wave's LDS slots
   template <int N>
   __device__ __forceinline__ void commit(const f32x2 (&q2)[N], int64_t k) {
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8, "LdsNorm::commit reduces groups of 1, 2, 4 or 8 clients");
     const int lane = threadIdx.x & 63;
     if constexpr (N == 8) {
       const f32x2 a[4] = {q2[0], q2[1], q2[2], q2[3]}, b[4] = {q2[4], q2[5], q2[6], q2[7]};
@@ -418,8 +419,10 @@ __device__ __forceinline__ void write_norm(const L2Out& out, int64_t k, float t)
 // write-through (sc1, 4 B per lane), every storing wave drains its stores, the workgroup
 // barrier, then ONE lane adds 1 to the agent-scope counter; the workgroup whose add returns
 // nb - 1 is last, and reads every row with sc1 loads only (they bypass this CU's L1, so no
-// acquire is needed), adds them and re-arms the counter at 0. Placement-independent for one
-// workgroup per CU, which the launchers ensure (grid <= CUs). lds: 16 x K4 floats + the flag.
+// acquire is needed), adds them and re-arms the counter at 0. That is the guide's measured form for
+// one workgroup of the launch per CU (not an architectural guarantee): the launchers keep the grid
+// to one wave of workgroups and reserve more than half a CU's LDS per workgroup (l2_smem), so two
+// cannot share a CU. lds: 16 x K4 floats + the flag.
 // The sum order is k_l2_combine's exactly (column wv of 16 adds partials b = wv, wv+16, ... in
 // order from +0, then the 16 column sums in wv order): bitwise the two-launch norms.
 __device__ __forceinline__ void combine_last(const float* __restrict__ ws, int64_t K, const L2Out& out,
@@ -429,8 +432,13 @@ __device__ __forceinline__ void combine_last(const float* __restrict__ ws, int64
   unsigned* last = reinterpret_cast<unsigned*>(lds + kCombineWaves * K4);  // in the one dynamic LDS array
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 partials are out
   __syncthreads();
-  if (tid == 0)
-    *last = __hip_atomic_fetch_add(out.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nb - 1);
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(out.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a counter that was not zero at the call (a caller that did not zero it, fjagg.h): the word
+    // after it records that this call's norms are not valid (sticky; the caller clears it)
+    if (old >= (unsigned)nb) __hip_atomic_fetch_or(out.done + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last = old == (unsigned)(nb - 1);
+  }
   __syncthreads();
   if (!*last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below)
@@ -615,9 +623,44 @@ int launch_l2_combine(const float* ws, int64_t nb, int64_t K, L2Out out, hipStre
   return check_launch("k_l2_combine");
 }
 
-// dynamic LDS of a fused-norm fold: the wave rows, or combine_last's 16 columns
-inline size_t l2_smem(int64_t K, const L2Out& out) {
-  return out.done ? (size_t)(kCombineWaves * round4(K) + 4) * sizeof(float) : (size_t)(kThreads / 64) * K * sizeof(float);
+// combine_last's hand-off is the guide's measured form for ONE workgroup of the launch per CU
+// (MI355X_MICROARCH.md, "Valid forms", first row). A grid of at most as many workgroups as CUs
+// does not make the dispatcher place them so: two may share a CU. A fold that combines in its
+// last workgroup therefore reserves more than half of the CU's 160 KiB of LDS per workgroup, so
+// two of its workgroups cannot share a CU whatever the placement (the plan has one wave of
+// workgroups anyway). FJAGG_L2_ONE_PER_CU=0 drops the reservation (A/B runs only).
+constexpr size_t kOnePerCuLds = 80 * 1024 + 16;
+inline bool one_per_cu_lds() {
+  static const bool on = [] {
+    const char* e = getenv("FJAGG_L2_ONE_PER_CU");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// dynamic LDS of a fused-norm fold: the wave rows, or combine_last's 16 columns (and the
+// one-workgroup-per-CU reservation). reserve = false: the bytes the code uses, which size the
+// dense path's balanced grid — the reservation must not change the partition (the norms' order).
+inline size_t l2_smem(int64_t K, const L2Out& out, bool reserve = true) {
+  if (!out.done) return (size_t)(kThreads / 64) * K * sizeof(float);
+  const size_t need = (size_t)(kCombineWaves * round4(K) + 4) * sizeof(float);
+  return reserve && one_per_cu_lds() && need < kOnePerCuLds ? kOnePerCuLds : need;
+}
+
+// Lets `kern` launch with `bytes` of dynamic LDS (above the default 64 KiB: once per kernel).
+int allow_lds(const void* kern, size_t bytes) {
+  if (bytes <= 64 * 1024) return FJAGG_OK;
+  static std::mutex mu;
+  static std::unordered_map<const void*, size_t> done;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = done.find(kern);
+  if (it != done.end() && it->second >= bytes) return FJAGG_OK;
+  if (hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes)) {
+    (void)hipGetLastError();
+    return fail(FJAGG_EHIP, "hipFuncSetAttribute(max dynamic LDS %zu): %s", bytes, hipGetErrorString(e));
+  }
+  done[kern] = bytes;
+  return FJAGG_OK;
 }
 
 // Exact fold of the slab + the server optimizer step in the epilogue (no mean
@@ -1514,8 +1557,11 @@ int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, c
   const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
   if constexpr (std::is_same<ACC, AccF>::value) {
     if (ws) {  // fused per-client squared l2 norms: block partials, then ordered combine
-      if (nblk > cu_count()) l2.done = nullptr;  // combine_last's hand-off: one workgroup per CU
+      if (nblk > cu_count()) l2.done = nullptr;  // combine_last: a grid of one wave of workgroups
       const size_t smem = l2_smem(K, l2);
+      const void* kf = nt ? reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true, true>)
+                          : reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, false, true>);
+      if (int rc = allow_lds(kf, smem)) return rc;
       if (nt)
         hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true>), dim3((unsigned)nblk), dim3(kThreads), smem, s,
                            img, L, K, wt, scale, do_scale, accumulate, ws, l2, KargWords<1>{});
@@ -1575,12 +1621,13 @@ template <int IN, int OUT, int V, int E, int U, bool NT>
 int launch_dense_l2_t(const DenseArgs& a, float* ws, int64_t ws_floats, L2Out l2, hipStream_t s) {
   auto kern = k_dense_l2<IN, OUT, V, E, U, NT>;
   size_t smem = l2_smem(a.K, l2);
+  if (int rc = allow_lds(reinterpret_cast<const void*>(kern), smem)) return rc;
   int64_t S = (int64_t)kThreads * E, nblk = 0;
-  balanced_grid(residency(reinterpret_cast<const void*>(kern), smem), a.nunits, (int64_t)kThreads * E,
-                1, &S, &nblk);
+  balanced_grid(residency(reinterpret_cast<const void*>(kern), l2_smem(a.K, l2, false)), a.nunits,
+                (int64_t)kThreads * E, 1, &S, &nblk);
   if (a.nunits == 0) nblk = 0;
   const int64_t grid = nblk + (a.tail_n > 0 ? 1 : 0);
-  if (l2.done && grid > cu_count()) {  // combine_last's hand-off: one workgroup per CU
+  if (l2.done && grid > cu_count()) {  // combine_last: a grid of one wave of workgroups
     l2.done = nullptr;
     smem = l2_smem(a.K, l2);
   }
@@ -1822,8 +1869,11 @@ int launch_ptrs_karg_n(bool nt, const int64_t* img, int L, int64_t K, int64_t nb
   std::memcpy(ki.w + nimg, w, sizeof(float) * (size_t)K);
   const dim3 grid((unsigned)nblk), block(kThreads);
   if (ws) {
-    if (nblk > cu_count()) l2.done = nullptr;  // combine_last's hand-off: one workgroup per CU
+    if (nblk > cu_count()) l2.done = nullptr;  // combine_last: a grid of one wave of workgroups
     const size_t smem = l2_smem(K, l2);
+    const void* kf = nt ? reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, true, true, true, NW>)
+                        : reinterpret_cast<const void*>(k_ptrs<IN, ACC, OUT, V, false, true, true, NW>);
+    if (int rc = allow_lds(kf, smem)) return rc;
     if (nt)
       hipLaunchKernelGGL((k_ptrs<IN, ACC, OUT, V, true, true, true, NW>), grid, block, smem, s, nullptr, L,
                          K, nullptr, scale, ds, ac, ws, l2, ki);

@@ -2860,6 +2860,8 @@ struct FastState {
   // pools a chain took: (buf, all pairs). Once the caller has dropped every view of one and
   // nothing else holds its buffer, the next refill reuses it whole (no new objects).
   std::vector<std::pair<PyObject*, PyObject*>> retired;
+  std::vector<unsigned long long> retired_stream;  // the stream each retired pool's norms were written on
+  unsigned long long pool_stream = 0;              // the stream the current pool was built on
   PyObject* d_view_ticket = nullptr;  // _NormView._ticket and _Ticket.node slot descriptors
   PyObject* d_ticket_node = nullptr;
   long long pool_want = 0;  // norms (row 1) the current round's chains asked for: the next pool's size
@@ -3579,16 +3581,19 @@ void clear_pool() {
   Py_CLEAR(g_fast.pool_all);
 }
 
-// a chain took (buf, all): keep them (new references) for reuse, at most 4 (the oldest goes)
+// a chain took (buf, all): keep them (new references) for reuse, at most 4 (the oldest goes),
+// with the stream the pool was built on (its norms are written and read there)
 void retire_pool(PyObject* buf, PyObject* all) {
   if (!buf || !all) return;
   Py_INCREF(buf);
   Py_INCREF(all);
   g_fast.retired.emplace_back(buf, all);
+  g_fast.retired_stream.push_back(g_fast.pool_stream);
   if (g_fast.retired.size() > 4) {
     Py_DECREF(g_fast.retired.front().first);
     Py_DECREF(g_fast.retired.front().second);
     g_fast.retired.erase(g_fast.retired.begin());
+    g_fast.retired_stream.erase(g_fast.retired_stream.begin());
   }
 }
 
@@ -3629,14 +3634,20 @@ int refill_pool(c10::DeviceIndex dev) {
       return 0;
     clear_pool();
   }
+  const unsigned long long stream =
+      reinterpret_cast<unsigned long long>(c10::hip::getCurrentHIPStream(dev).stream());
   for (size_t r = 0; r < g_fast.retired.size(); ++r) {
     auto [buf, all] = g_fast.retired[r];
-    if (!reusable(buf, all, dev, m)) continue;
+    // (only on the stream its earlier norms were written on: a kernel on another stream that
+    // reads a dropped view may not have run yet, and the new norms must not overtake it)
+    if (g_fast.retired_stream[r] != stream || !reusable(buf, all, dev, m)) continue;
     for (Py_ssize_t i = 0; i < PyList_GET_SIZE(all); ++i)
       if (slot_set(g_fast.d_ticket_node, PyTuple_GET_ITEM(PyList_GET_ITEM(all, i), 1), Py_None) != 0) return -1;
     PyObject* views = PyList_GetSlice(all, 0, PyList_GET_SIZE(all));
     if (!views) return -1;
     g_fast.retired.erase(g_fast.retired.begin() + static_cast<std::ptrdiff_t>(r));
+    g_fast.retired_stream.erase(g_fast.retired_stream.begin() + static_cast<std::ptrdiff_t>(r));
+    g_fast.pool_stream = stream;
     g_fast.pool_buf = buf;  // (the retired entry's references move to the pool)
     g_fast.pool_all = all;
     g_fast.pool_views = views;
@@ -3670,6 +3681,7 @@ int refill_pool(c10::DeviceIndex dev) {
     return -1;
   }
   g_fast.pool_all = views;
+  g_fast.pool_stream = stream;
   ++g_fast.pool_builds;
   g_fast.refill_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - clock.t).count();
   return 0;
@@ -3683,6 +3695,7 @@ PyObject* drop_pool(PyObject*, PyObject*) {
     Py_DECREF(e.second);
   }
   g_fast.retired.clear();
+  g_fast.retired_stream.clear();
   g_fast.pool_want = 0;
   Py_RETURN_NONE;
 }
@@ -3839,8 +3852,14 @@ PyObject* fold_chain(PyObject*, PyObject* args) {
       if (buf && THPVariable_Check(buf)) {
         const at::Tensor& b = THPVariable_Unpack(buf);
         const int64_t i0 = links[0]->idx, n = static_cast<int64_t>(links.size());
+        // (the fold's device: its base capture's first leaf; a buffer elsewhere takes the fill path)
+        PyObject* bt0 = PyTuple_Check(bcap) && PyTuple_GET_SIZE(bcap) > 0 ? PyTuple_GET_ITEM(bcap, 0) : nullptr;
+        const int fold_dev = bt0 && PyTuple_Check(bt0) && PyTuple_GET_SIZE(bt0) > 0 &&
+                                     THPVariable_Check(PyTuple_GET_ITEM(bt0, 0))
+                                 ? THPVariable_Unpack(PyTuple_GET_ITEM(bt0, 0)).get_device()
+                                 : -2;
         if (b.dim() == 2 && b.size(0) == 2 && b.is_contiguous() && b.scalar_type() == at::kFloat && b.is_cuda() &&
-            i0 >= 0 && i0 + n <= b.size(1)) {
+            b.get_device() == fold_dev && i0 >= 0 && i0 + n <= b.size(1)) {
           float* row0 = b.data_ptr<float>() + i0;
           rows = L2Rows{reinterpret_cast<WsumL2RowsFn>(rows_addr), row0, row0 + b.size(1), 1};
           use_rows = true;

@@ -90,6 +90,9 @@ enum fjagg_flags {
                                  partials itself, with no second (combine) launch; the norms are
                                  bitwise the same either way. Without the flag the 16 bytes are
                                  unused. As always, one workspace serves one call at a time.
+                                 Bytes 4..7 are an error word: a call that finds the counter
+                                 non-zero sets it to 1 (sticky: that call's norms are not valid;
+                                 zero both words to recover).
                                  (fedjax_amd's callers pass it unless FJAGG_L2_COMBINE_LAUNCH=1.) */
 };
 /* kernel-argument capacity of FJAGG_HOST_TABLES launches */

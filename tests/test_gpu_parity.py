@@ -1173,6 +1173,47 @@ def test_fused_norms_propagate_nan_and_inf(zeroed, cuda):
     npt.assert_allclose(got[ok].astype(np.float64), want[ok], rtol=2e-6)
 
 
+@pytest.mark.parametrize("start", [5, 1000])
+def test_nonzero_completion_counter_is_flagged(start, cuda):
+    """FJAGG_ZEROED_WS with a counter that was NOT zero at the call (a caller that did not zero
+    it, include/fjagg.h): the call sets the workspace's error word (bytes 4..7), so the invalid
+    norms are detectable; zeroing both words restores the bitwise norms."""
+    import ctypes
+    lib = _lib.load()
+    shapes = [(37,), (40960,), (61, 13)]
+    K, L = 12, len(shapes)
+    g = torch.Generator().manual_seed(23)
+    leaves = [[(torch.rand(sh, generator=g) - 0.5).to(cuda) for sh in shapes] for _ in range(K)]
+    n = np.array([int(np.prod(sh)) for sh in shapes], dtype=np.int64)
+    outs = [torch.empty(int(v), device=cuda) for v in n]
+    nb = lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, None, 0)
+    blocks = np.empty(2 * nb, dtype=np.int64)
+    lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, n.ctypes.data, None, L, blocks.ctypes.data, nb)
+    img = torch.from_numpy(np.concatenate([np.array([[x.data_ptr() for x in r] for r in leaves],
+                                                    dtype=np.int64).ravel(),
+                                           np.array([o.data_ptr() for o in outs], dtype=np.int64), n,
+                                           blocks])).to(cuda)
+    w = torch.arange(1, K + 1, dtype=torch.float32, device=cuda)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    need = lib.fjagg_wsum_l2_ptrs_workspace_bytes(K, nb)
+    ws = torch.zeros(need, dtype=torch.uint8, device=cuda)
+    l2, l2ok = torch.empty(K, device=cuda), torch.empty(K, device=cuda)
+
+    def call(out):
+        _lib.check(lib.fjagg_wsum_l2_ptrs(_lib.F32, _lib.F32, _lib.F32, img.data_ptr(), L, K, nb, w.data_ptr(),
+                                          ctypes.c_float(0.5), out.data_ptr(), _lib.SCALE | _lib.ZEROED_WS,
+                                          ws.data_ptr(), need, st), "l2")
+        torch.cuda.synchronize()
+        return ws[:8].view(torch.int32).cpu().tolist()
+    assert call(l2ok) == [0, 0]  # a zeroed counter: left zero, no error
+    ws[:4].view(torch.int32).fill_(start)
+    hdr = call(l2)
+    assert hdr[1] == 1, hdr  # flagged
+    ws[:8].zero_()
+    assert call(l2) == [0, 0]
+    assert torch.equal(l2.view(torch.int32), l2ok.view(torch.int32))
+
+
 def test_combine_launch_switch(cuda, monkeypatch):
     """FJAGG_L2_COMBINE_LAUNCH=1 (kernels._L2_COMBINE_LAUNCH) keeps the separate combine launch
     for weighted_sum_l2_dense's own workspace: the same bits as the in-launch combine."""
