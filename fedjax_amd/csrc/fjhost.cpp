@@ -658,10 +658,51 @@ PyObject* fold_table(PyObject*, PyObject* args) {
 // exact dict (keys sorted, as jax flattens) / list / tuple / None nodes, exact
 // torch.Tensor leaves. Anything else is "not the fast case" (None to the caller).
 
+// A vector of pointers with room for N inline: the per-call walks below (one client pytree of a
+// few leaves and dicts per call) then allocate nothing on the heap.
+template <class T, size_t N>
+struct SmallVec {
+  T inl[N];
+  T* p = inl;
+  size_t n = 0, cap = N;
+  SmallVec() = default;
+  SmallVec(const SmallVec&) = delete;
+  SmallVec& operator=(const SmallVec&) = delete;
+  ~SmallVec() {
+    if (p != inl) std::free(p);
+  }
+  void grow() {
+    const size_t c = cap * 2;
+    T* q = static_cast<T*>(std::malloc(sizeof(T) * c));
+    if (!q) throw std::bad_alloc();
+    std::memcpy(q, p, sizeof(T) * n);
+    if (p != inl) std::free(p);
+    p = q;
+    cap = c;
+  }
+  void push_back(T v) {
+    if (n == cap) grow();
+    p[n++] = v;
+  }
+  void reserve(size_t) {}
+  size_t size() const { return n; }
+  size_t capacity() const { return cap; }
+  bool empty() const { return n == 0; }
+  void clear() { n = 0; }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+  T* data() { return p; }
+  const T* data() const { return p; }
+  T* begin() { return p; }
+  T* end() { return p + n; }
+  const T* begin() const { return p; }
+  const T* end() const { return p + n; }
+};
+
 struct PWalk {
   int K = 0;
-  std::vector<PyObject*> leaves[FJTREE_MAX_OPERANDS];  // borrowed, flatten order
-  std::vector<PyObject*> keys;                         // owned sorted key lists, pre-order
+  SmallVec<PyObject*, 16> leaves[FJTREE_MAX_OPERANDS];  // borrowed, flatten order
+  SmallVec<PyObject*, 8> keys;                          // owned sorted key lists, pre-order
   std::vector<int64_t>* sig = nullptr;  // optional: operand 0's structure (kinds, lengths, key objects)
   std::vector<PyObject*>* dicts = nullptr;  // optional: operand 0's dict nodes, pre-order (borrowed)
   bool seq_nodes = false;                   // operand 0 has a list / tuple node
@@ -787,7 +828,6 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
     PyObject* v0[kSortedVals];
     PyObject* keys = sorted_keys(x0, &unorderable, v0, &have0);
     if (!keys) return unorderable ? 1 : -1;  // unorderable keys: the Python path decides
-    if (w.keys.capacity() == 0) w.keys.reserve(8);
     w.keys.push_back(keys);
     if (w.dicts) w.dicts->push_back(x0);
     if (w.sig) {
@@ -827,7 +867,7 @@ int pwalk(PyObject* const* xs, PWalk& w, int depth) {
 
 // A new tree shaped like x0 whose leaves are outs[i++] (stolen references), dict keys
 // in sorted order (jax's unflatten of a dict); key lists from the walk, in pre-order.
-PyObject* rebuild(PyObject* x0, PyObject** outs, size_t& i, const std::vector<PyObject*>& keys, size_t& ki) {
+PyObject* rebuild(PyObject* x0, PyObject** outs, size_t& i, PyObject* const* keys, size_t& ki) {
   if (Py_TYPE(x0) == reinterpret_cast<PyTypeObject*>(THPVariableClass)) {
     PyObject* o = outs[i];
     outs[i++] = nullptr;
@@ -1408,7 +1448,7 @@ PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const*
     std::vector<PyObject*> wrapped(L);
     for (Py_ssize_t l = 0; l < L; ++l) wrapped[l] = THPVariable_Wrap(std::move(outs[l]));
     size_t i = 0, ki = 0;
-    PyObject* tree = rebuild(base, wrapped.data(), i, w.keys, ki);
+    PyObject* tree = rebuild(base, wrapped.data(), i, w.keys.data(), ki);
     for (PyObject* o : wrapped) Py_XDECREF(o);  // (rebuild took the ones it used)
     if (!tree) return nullptr;
     st.lap(kTWrap);
@@ -1525,7 +1565,7 @@ PyObject* leaf_fold(PyObject*, PyObject* args) {
       std::vector<PyObject*> objs(L);
       for (int l = 0; l < L; ++l) objs[l] = THPVariable_Wrap(std::move(outs[l]));
       size_t i = 0, ki = 0;
-      PyObject* r = rebuild(xs[0], objs.data(), i, w.keys, ki);
+      PyObject* r = rebuild(xs[0], objs.data(), i, w.keys.data(), ki);
       for (PyObject* o : objs) Py_XDECREF(o);
       if (!r) {
         Py_DECREF(Py_None);
@@ -1589,13 +1629,23 @@ struct SoloState {
   long long max_pending = 16383;
   long long budget = 0;          // bytes of pending deltas; 0: automatic (py_budget(device) once)
   PyObject* py_budget = nullptr;
-  std::vector<PyObject*> reg;    // weak references to nodes, registration order (pending ones matter)
+  // every node registered since the last compaction, in registration order, with the view handed
+  // out for it (strong references both; pooled: the buffer's record holds the view too). A pending
+  // node whose view nobody else references any more was dropped by the caller: its capture goes
+  // (solo_compact) — the views, not the registry, decide how long a capture lives.
+  struct Entry {
+    PyObject* view;
+    SoloObject* node;
+    bool pooled;
+  };
+  std::vector<Entry> reg;
   long long pending = 0, pending_bytes = 0;
   long long recheck = 0;         // pending bytes at which the budget is checked again (solo_evict)
   PyObject* buf = nullptr;       // the norm buffer new columns come from
   long long next = 0;
   unsigned long long rows_fn = 0, l2ws_fn = 0, plan_fn = 0;  // libfjagg entry points (solo_config)
   long long fused = 0, eager = 0, stale = 0, launches = 0;  // counters (solo_info)
+  double t_release = 0, t_compact = 0, t_refill = 0;  // host us spent after the mean's launches (solo_info)
   // Pool of pre-made (norm view, node) pairs over consecutive columns, built right after a mean
   // that fused lazy norms has issued its launches (while the GPU folds) and sized to the norms
   // the round asked for: creating a 0-d tensor subclass and a node on the critical path of the
@@ -1610,9 +1660,6 @@ struct SoloState {
     std::vector<std::pair<PyObject*, PyObject*>> pairs;  // handed-out pool pairs of this buffer
   };
   std::vector<BufRec> bufs;
-  // handed-out pool pairs whose node is pending (strong references): a pair whose view only the
-  // pool still references was dropped by the caller — its node lets its capture go (solo_reap)
-  std::vector<std::pair<PyObject*, PyObject*>> handed;
   long long want = 0;  // row-1 norms asked for since the last refill
   long long pool_builds = 0, pool_reuses = 0;
   double refill_us = 0.0;
@@ -1935,33 +1982,23 @@ int solo_resolve(std::vector<SoloObject*>& nodes) {
   return 0;
 }
 
-// Pool pairs handed out: drop the done ones from the list, and release the capture of a pending
-// node whose view the caller dropped (only the pool's records hold it: nobody can read it).
-void solo_reap() {
-  size_t o = 0;
-  for (auto& pr : g_solo.handed) {
-    auto* n = reinterpret_cast<SoloObject*>(pr.second);
-    if (n->state == kSoloPending && Py_REFCNT(pr.first) <= 2 && THPVariable_Unpack(pr.first).use_count() == 1)
-      solo_release(n, kSoloDone);
-    if (n->state == kSoloPending) {
-      g_solo.handed[o++] = pr;
-    } else {
-      Py_DECREF(pr.first);
-      Py_DECREF(pr.second);
-    }
-  }
-  g_solo.handed.resize(o);
-}
-
-// drops registry entries whose node is gone or no longer pending
+// Drops the registry entries of nodes that are no longer pending, after releasing the capture of a
+// pending node whose view only the registry (and its buffer's record) still references: the caller
+// dropped it, nobody can read the value.
 void solo_compact() {
   size_t o = 0;
-  for (PyObject* wr : g_solo.reg) {
-    PyObject* n = PyWeakref_GetObject(wr);
-    if (n != Py_None && reinterpret_cast<SoloObject*>(n)->state == kSoloPending) {
-      g_solo.reg[o++] = wr;
+  for (auto& e : g_solo.reg) {
+    // (no view of the node left outside: the registry's view and node references, the record's
+    // pair when pooled, and that view's _ticket are all that hold them)
+    if (e.node->state == kSoloPending && Py_REFCNT(e.view) <= (e.pooled ? 2 : 1) &&
+        Py_REFCNT(reinterpret_cast<PyObject*>(e.node)) <= (e.pooled ? 3 : 2) &&
+        THPVariable_Unpack(e.view).use_count() == 1)
+      solo_release(e.node, kSoloDone);
+    if (e.node->state == kSoloPending) {
+      g_solo.reg[o++] = e;
     } else {
-      Py_DECREF(wr);
+      Py_DECREF(e.view);
+      Py_DECREF(reinterpret_cast<PyObject*>(e.node));
     }
   }
   g_solo.reg.resize(o);
@@ -1970,38 +2007,22 @@ void solo_compact() {
 
 // every pending node, oldest first (the budget's eviction and solo_resolve(None))
 int solo_resolve_all() {
-  solo_reap();
+  solo_compact();
   std::vector<SoloObject*> v;
-  std::vector<PyObject*> held;
-  for (PyObject* wr : g_solo.reg) {
-    PyObject* n = PyWeakref_GetObject(wr);
-    if (n == Py_None || reinterpret_cast<SoloObject*>(n)->state != kSoloPending) continue;
-    Py_INCREF(n);
-    held.push_back(n);
-    v.push_back(reinterpret_cast<SoloObject*>(n));
-  }
+  for (auto& e : g_solo.reg)
+    if (e.node->state == kSoloPending) v.push_back(e.node);  // (the registry holds them)
   const int rc = solo_resolve(v);
-  for (PyObject* n : held) Py_DECREF(n);
   solo_compact();
   return rc;
 }
 
 // the pending nodes whose pytree only the node holds (the deltas their views alone keep alive)
 int solo_evict() {
-  solo_reap();
+  solo_compact();
   std::vector<SoloObject*> v;
-  std::vector<PyObject*> held;
-  for (PyObject* wr : g_solo.reg) {
-    PyObject* n = PyWeakref_GetObject(wr);
-    if (n == Py_None) continue;
-    auto* s = reinterpret_cast<SoloObject*>(n);
-    if (s->state != kSoloPending || !s->tree || Py_REFCNT(s->tree) > 1) continue;
-    Py_INCREF(n);
-    held.push_back(n);
-    v.push_back(s);
-  }
+  for (auto& e : g_solo.reg)
+    if (e.node->state == kSoloPending && e.node->tree && Py_REFCNT(e.node->tree) <= 1) v.push_back(e.node);
   const int rc = solo_resolve(v);
-  for (PyObject* n : held) Py_DECREF(n);
   solo_compact();
   return rc;
 }
@@ -2017,9 +2038,8 @@ struct SoloMatcher {
     SoloObject* n = nullptr;
     const size_t R = g_solo.reg.size();
     for (size_t p = cursor; p < R && p < cursor + 2 && !n; ++p) {
-      PyObject* o = PyWeakref_GetObject(g_solo.reg[p]);
-      auto* c = reinterpret_cast<SoloObject*>(o);
-      if (o != Py_None && c->tree == tree && c->state == kSoloPending) {
+      SoloObject* c = g_solo.reg[p].node;
+      if (c->tree == tree && c->state == kSoloPending) {
         n = c;
         cursor = p + 1;
       }
@@ -2027,11 +2047,8 @@ struct SoloMatcher {
     if (!n) {
       if (!built) {
         built = true;
-        for (PyObject* wr : g_solo.reg) {  // (registration order: a tree's earliest pending node)
-          PyObject* o = PyWeakref_GetObject(wr);
-          auto* c = reinterpret_cast<SoloObject*>(o);
-          if (o != Py_None && c->state == kSoloPending && c->tree) by_tree.emplace(c->tree, c);
-        }
+        for (auto& e : g_solo.reg)  // (registration order: a tree's earliest pending node)
+          if (e.node->state == kSoloPending && e.node->tree) by_tree.emplace(e.node->tree, e.node);
       }
       auto it = by_tree.find(tree);
       if (it == by_tree.end() || it->second->state != kSoloPending) return nullptr;
@@ -2272,7 +2289,7 @@ PyObject* mean_pairs_impl(PyObject* pairs, bool triples, int may_pipeline, doubl
     // all have pending nodes in consecutive columns of one buffer folds with the norms written
     // straight into those columns (fjagg_wsum_l2_ptrs_rows); the nodes are done once every
     // launch is issued
-    if (!with_l2 && !g_solo.handed.empty()) solo_reap();
+    if (!with_l2 && !g_solo.reg.empty()) solo_compact();
     bool solo = !with_l2 && g_solo.pending > 0 && g_solo.rows_fn && g_solo.l2ws_fn;
     std::vector<SoloObject*> fused;  // held (new references) until the call returns
     struct HeldNodes {
@@ -2359,15 +2376,20 @@ PyObject* mean_pairs_impl(PyObject* pairs, bool triples, int may_pipeline, doubl
       done = k1;
     }
     if (!fused.empty()) {  // every launch is issued: the lazy norms these clients' views read are written
+      Stamp sw;
       for (SoloObject* n : fused) solo_release(n, kSoloDone);
       g_solo.fused += static_cast<long long>(fused.size());
+      const double t_rel = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - sw.t).count();
       solo_compact();
+      const double t_cmp = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - sw.t).count();
       if (g_solo.want > 0 && solo_refill(dev, stream) != 0) return nullptr;  // (while the GPU folds)
+      const double t_ref = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - sw.t).count();
+      g_solo.t_release += t_rel, g_solo.t_compact += t_cmp - t_rel, g_solo.t_refill += t_ref - t_cmp;
     }
     std::vector<PyObject*> wrapped(L);
     for (int64_t l = 0; l < L; ++l) wrapped[l] = THPVariable_Wrap(std::move(outs[l]));
     size_t i = 0, ki = 0;
-    PyObject* tree = rebuild(trees[0], wrapped.data(), i, sb.keys, ki);
+    PyObject* tree = rebuild(trees[0], wrapped.data(), i, sb.keys.data(), ki);
     for (PyObject* o : wrapped) Py_XDECREF(o);  // (rebuild took the ones it used)
     if (!tree) return nullptr;
     st.lap(kTWrap);
@@ -3100,7 +3122,7 @@ PyObject* solo_resolve_py(PyObject*, PyObject* arg) {
 // solo_info() -> dict: pending nodes and bytes, registry size, norms fused into a mean, computed
 // on their own (and their launches), stale nodes
 PyObject* solo_info(PyObject*, PyObject*) {
-  solo_reap();
+  solo_compact();
   return Py_BuildValue("{s:L,s:L,s:n,s:L,s:L,s:L,s:L,s:L,s:L,s:n,s:L,s:L,s:d,s:n}", "pending", g_solo.pending,
                        "pending_bytes", g_solo.pending_bytes, "registry", static_cast<Py_ssize_t>(g_solo.reg.size()),
                        "fused", g_solo.fused, "eager", g_solo.eager, "eager_launches", g_solo.launches, "stale",
@@ -3108,6 +3130,12 @@ PyObject* solo_info(PyObject*, PyObject*) {
                        "pool_ready", static_cast<Py_ssize_t>(g_solo.pool.size() - g_solo.pool_head), "pool_builds",
                        g_solo.pool_builds, "pool_reuses", g_solo.pool_reuses, "refill_us", g_solo.refill_us,
                        "buffers", static_cast<Py_ssize_t>(g_solo.bufs.size()));
+}
+PyObject* solo_times(PyObject*, PyObject*) {
+  PyObject* r = Py_BuildValue("{s:d,s:d,s:d}", "release_us", g_solo.t_release, "compact_us", g_solo.t_compact,
+                              "refill_us", g_solo.t_refill);
+  g_solo.t_release = g_solo.t_compact = g_solo.t_refill = 0;
+  return r;
 }
 
 // solo_norm_py(tree, which) -> view | None: the standalone lazy norm for tree_util's Python path
@@ -3297,7 +3325,7 @@ int solo_refill(int dev, unsigned long long stream) {
   const long long m = std::min<long long>(g_solo.want, kSoloCols);
   g_solo.want = 0;
   if (m <= 0 || !g_solo.type || !g_fast.norm_view || !g_fast.d_view_ticket) return 0;
-  solo_reap();
+  solo_compact();
   // pairs handed out since the last refill already moved to their buffers' records; drop the
   // taken slots, keep the rest when they are enough and on this device
   g_solo.pool.erase(g_solo.pool.begin(), g_solo.pool.begin() + static_cast<std::ptrdiff_t>(g_solo.pool_head));
@@ -3351,15 +3379,13 @@ int solo_refill(int dev, unsigned long long stream) {
 PyObject* solo_norm(PyObject* tree, int which) {
   try {
     if (!g_solo.reg.empty()) {
-      PyObject* o = PyWeakref_GetObject(g_solo.reg.back());
-      if (o != Py_None) {
-        auto* c = reinterpret_cast<SoloObject*>(o);
-        if (c->state == kSoloPending && c->tree == tree && solo_same_tree(c, tree) && solo_unchanged(c))
-          return solo_view(c, which);
-      }
+      SoloObject* c = g_solo.reg.back().node;
+      if (c->state == kSoloPending && c->tree == tree && solo_same_tree(c, tree) && solo_unchanged(c))
+        return solo_view(c, which);
     }
     SoloObject* n = nullptr;   // (a new reference)
     PyObject* view = nullptr;  // the pool's view for n (a new reference)
+    bool pooled = false;       // (its buffer's record holds the view too)
     if (which == 1 && g_solo.pool_head < g_solo.pool.size()) {
       const auto pr = g_solo.pool[g_solo.pool_head];
       auto* pn = reinterpret_cast<SoloObject*>(pr.second);
@@ -3377,11 +3403,9 @@ PyObject* solo_norm(PyObject* tree, int which) {
           Py_INCREF(pr.first);
           Py_INCREF(pr.second);
         }
-        Py_INCREF(pr.first);
-        Py_INCREF(pr.second);
-        g_solo.handed.push_back(pr);
         view = pr.first;
         n = pn;
+        pooled = rec != nullptr;
       } else {
         solo_release(pn, kSoloDone);  // (a pool on another device: this delta takes a fresh node)
       }
@@ -3423,19 +3447,22 @@ PyObject* solo_norm(PyObject* tree, int which) {
       Py_XSETREF(n->buf, buf);
       n->idx = idx;
     }
-    PyObject* wr = PyWeakref_NewRef(reinterpret_cast<PyObject*>(n), nullptr);
-    if (!wr) {
-      Py_XDECREF(view);
-      solo_release(n, kSoloDone);
-      return nullptr;
+    if (!view) {
+      view = solo_view(n, which);
+      if (!view) {
+        solo_release(n, kSoloDone);
+        return nullptr;
+      }
     }
     n->state = kSoloPending;
     ++g_solo.pending;
     g_solo.pending_bytes += n->nbytes;
     if (g_solo.reg.size() >= 2 * static_cast<size_t>(g_solo.pending) + 64) solo_compact();
-    g_solo.reg.push_back(wr);
+    Py_INCREF(view);  // (the registry's references: the view and the node)
+    Py_INCREF(reinterpret_cast<PyObject*>(n));
+    g_solo.reg.push_back(SoloState::Entry{view, n, pooled});
     if (which == 1) ++g_solo.want;
-    return view ? view : solo_view(n, which);
+    return view;
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
@@ -3763,7 +3790,7 @@ PyObject* zeros_like(PyObject*, PyObject* tree) {
       if (!wrapped[l]) return nullptr;
     }
     size_t i = 0, ki = 0;
-    return rebuild(tree, wrapped.data(), i, w.keys, ki);
+    return rebuild(tree, wrapped.data(), i, w.keys.data(), ki);
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
@@ -4013,6 +4040,7 @@ PyMethodDef kMethods[] = {
     {"solo_resolve", solo_resolve_py, METH_O, "compute pending standalone lazy norms now (None: all)"},
     {"solo_info", solo_info, METH_NOARGS, "standalone lazy norms: pending, fused, computed alone, stale"},
     {"solo_norm", solo_norm_py, METH_VARARGS, "the standalone lazy norm view of a tree, or None"},
+    {"solo_times", solo_times, METH_NOARGS, "host us the means spent releasing, compacting, refilling (resets)"},
     {"pool_info", pool_info, METH_NOARGS, "(pool views ready, norms asked for since the last refill)"},
     {"tree_l2_squared", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_tree_l2_squared)),
      METH_FASTCALL | METH_KEYWORDS,

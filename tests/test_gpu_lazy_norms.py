@@ -274,3 +274,18 @@ def test_pool_pairs_are_reused_once_dropped(cuda):
     assert info["pool_reuses"] >= 1
     assert all(torch.equal(bits(v), r) for v, r in zip(kept, ref_bits))
     assert all(torch.equal(bits(v), r) for v, r in zip(norms, ref_bits))
+
+
+def test_a_second_view_keeps_the_capture(cuda):
+    """tree_l2_norm and tree_l2_squared of one delta share a node: dropping the first view while
+    the second is held keeps the capture, and the second reads the right value."""
+    d = make_deltas(SMALL, 1, 12, cuda)[0]
+    want = f64norm(d)
+    n = tu.tree_l2_norm(d)
+    q = tu.tree_l2_squared(d)
+    assert n._ticket is q._ticket
+    del n
+    gc.collect()
+    H.solo_info()  # (the registry looks at the views)
+    assert q._ticket.node is not None and H.solo_info()["pending"] == 1
+    assert float(q) == pytest.approx(want ** 2, rel=4e-6)

@@ -55,6 +55,8 @@ def main():
         t0 = pc()
         if m == "mean_only":
             tu.tree_mean(pairs)
+            t1 = t0
+            t2 = pc()
         else:
             diag, lst = {}, []
             for cid, (d, n) in enumerate(pairs):
@@ -71,6 +73,9 @@ def main():
                 parts["loop"].append(t1 - t0)
                 parts["mean_call"].append(t2 - t1)
                 parts["wait"].append(t3 - t2)
+            elif m == "mean_only":
+                parts.setdefault("plain_mean_call", []).append(t2 - t1)
+                parts.setdefault("plain_wait", []).append(t3 - t2)
     tu.set_lazy_norms(True)
     for m in modes:
         res[m + "_ms"] = round(float(np.median(t[m])) * 1e3, 4)
