@@ -508,7 +508,8 @@ __device__ __forceinline__ void combine_last(const float* __restrict__ ws, int64
 // A fused-norm workgroup's epilogue: its (kThreads/64) wave rows of LDS norms -> the partial
 // row ws[b*ld + k] (ld = K; with a completion counter ld = round4(K), sc1 stores, then the
 // last-workgroup combine).
-__device__ __forceinline__ void l2_epilogue(float* l2lds, float* __restrict__ ws, int64_t K, const L2Out& out) {
+__device__ __forceinline__ void l2_epilogue(float* l2lds, float* __restrict__ ws, int64_t K, const L2Out& out,
+                                            int64_t row) {
   __syncthreads();
   if (out.done) {
     const int64_t ld = round4(K);
@@ -516,7 +517,7 @@ __device__ __forceinline__ void l2_epilogue(float* l2lds, float* __restrict__ ws
       float t = l2lds[k];
 #pragma unroll
       for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, l2lds[i * K + k]);
-      __hip_atomic_store(reinterpret_cast<unsigned*>(ws) + (int64_t)blockIdx.x * ld + k, __float_as_uint(t),
+      __hip_atomic_store(reinterpret_cast<unsigned*>(ws) + row * ld + k, __float_as_uint(t),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through (sc1)
     }
     combine_last(ws, K, out, l2lds);  // (its first barrier also ends the reads of l2lds above)
@@ -526,7 +527,7 @@ __device__ __forceinline__ void l2_epilogue(float* l2lds, float* __restrict__ ws
     float t = l2lds[k];
 #pragma unroll
     for (int i = 1; i < kThreads / 64; ++i) t = __fadd_rn(t, l2lds[i * K + k]);
-    ws[(int64_t)blockIdx.x * K + k] = t;
+    ws[row * K + k] = t;
   }
 }
 
@@ -578,7 +579,7 @@ __global__ __launch_bounds__(kThreads) void k_dense_l2(
                                        scale, accumulate != 0, nrm);
     }
   }
-  l2_epilogue(l2lds, ws, K, l2out);
+  l2_epilogue(l2lds, ws, K, l2out, blockIdx.x);
 }
 
 // out[k] = sum over b of ws[b*K + k]. Workgroup = 64 clients x 16 waves: wave w sums
@@ -737,6 +738,13 @@ __device__ __forceinline__ void walk_units(RowFn row, uint32_t row_bytes, int64_
   }
 }
 
+// The plan entry of hardware workgroup h of nb when XCD x (= h % 8) takes the consecutive
+// entries [x*q + min(x, r), +q + (x < r)), q = nb / 8, r = nb % 8: a permutation of [0, nb).
+__device__ __forceinline__ int64_t xcd_plan_index(int64_t h, int64_t nb) {
+  const int64_t q = nb >> 3, r = nb & 7, x = h & 7, i = h >> 3;
+  return x * q + (x < r ? x : r) + i;
+}
+
 // Pytree path. image = in_ptrs[K*L] | out_ptrs[L] | leaf_n[L] | blocks[2*nblk].
 // Block b: word 0 = first unit (bits 0..39) | leaf (40..61) | tail flag (62) |
 // element flag (63); word 1 = end unit (exclusive). A workgroup walks its unit range
@@ -761,7 +769,12 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   const int64_t* in_ptrs = img;
   const int64_t* out_ptrs = img + K * L;
   const int64_t* leaf_n = out_ptrs + L;
-  const int64_t bid = blockIdx.x;
+  // accumulate bit 1 (FJAGG_XCD_REMAP, the launchers): workgroups are dealt round-robin over the
+  // 8 XCDs, so hardware workgroup h runs on XCD h % 8; plan entry bid = xcd_plan_index(h) gives
+  // each XCD a run of consecutive plan entries (neighbouring unit ranges of one leaf: the same
+  // pages of every client's row in that XCD's L2 and translation caches). Each entry is folded
+  // exactly as without it, and its norm partial keeps its row: the same bits.
+  const int64_t bid = (accumulate & 2) ? xcd_plan_index(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   const int64_t* blk = leaf_n + L + 2 * bid;
   const int64_t be = blk[0];
   const int leaf = (int)((be >> 40) & 0x3fffff);
@@ -777,7 +790,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   uint8_t* ob = reinterpret_cast<uint8_t*>(out_ptrs[leaf]) + e_base * Elem<OUT>::B;
   auto row = [=](int64_t k) { return reinterpret_cast<const uint8_t*>(in_ptrs[k * L + leaf]) + e_base * IB; };
   const uint32_t row_bytes = row_range((n - e_base) * IB);
-  const bool dsc = do_scale != 0, acm = accumulate != 0;
+  const bool dsc = do_scale != 0, acm = (accumulate & 1) != 0;
   // L2: per-client squared norms of this block's units, (kThreads/64) x K floats in LDS
   extern __shared__ __attribute__((aligned(16))) float l2lds[];
   using Norm = typename std::conditional<L2, LdsNorm, NoNorm>::type;
@@ -800,7 +813,7 @@ __global__ __launch_bounds__(kThreads) void k_ptrs(const int64_t* __restrict__ i
   } else {
     walk_units<IN, ACC, OUT, V, NT, BURST>(row, row_bytes, K, 0, u1 - u0, ob, w, dsc, scale, acm, nrm, PlainEpi());
   }
-  if constexpr (L2) l2_epilogue(l2lds, ws, K, l2out);
+  if constexpr (L2) l2_epilogue(l2lds, ws, K, l2out, bid);
 }
 
 // Pytree path + server optimizer step in the epilogue (fjagg_server_update_ptrs): the
@@ -1551,10 +1564,21 @@ int dense_exact_chunked(int in, int acc, int out, const uint8_t* x, int64_t ld_b
   return FJAGG_OK;
 }
 
+// k_ptrs' XCD-aware plan order (xcd_plan_index), carried in bit 1 of its accumulate argument.
+// FJAGG_XCD_REMAP=1 turns it on (A/B runs).
+inline int xcd_remap_bit() {
+  static const int on = [] {
+    const char* e = getenv("FJAGG_XCD_REMAP");
+    return (e && e[0] == '1') ? 2 : 0;
+  }();
+  return on;
+}
+
 template <int IN, class ACC, int OUT, int V>
 int launch_ptrs_t(bool nt, const int64_t* img, int L, int64_t K, int64_t nblk, const void* w,
                   float scale, int do_scale, int accumulate, float* ws, L2Out l2, hipStream_t s) {
   const auto* wt = reinterpret_cast<const typename ACC::T*>(w);
+  accumulate = (accumulate ? 1 : 0) | xcd_remap_bit();
   if constexpr (std::is_same<ACC, AccF>::value) {
     if (ws) {  // fused per-client squared l2 norms: block partials, then ordered combine
       if (nblk > cu_count()) l2.done = nullptr;  // combine_last: a grid of one wave of workgroups
@@ -1862,6 +1886,7 @@ int launch_ptrs_karg_n(bool nt, const int64_t* img, int L, int64_t K, int64_t nb
                        int ds, int ac, float* ws, L2Out l2, hipStream_t s) {
   constexpr int IN = FJAGG_F32, OUT = FJAGG_F32, V = 4;
   using ACC = AccF;
+  ac = (ac ? 1 : 0) | xcd_remap_bit();
   KargWords<NW> ki;
   const int64_t nimg = K * L + 2 * (int64_t)L + 2 * nblk;
   std::memcpy(ki.w, img, sizeof(int64_t) * (size_t)nimg);
