@@ -60,6 +60,8 @@
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <unordered_map>
 #include <vector>
 
@@ -1617,6 +1619,7 @@ struct SoloObject {
   int L, ndicts, tagged;
   long long vsum;  // the leaves' version sum at the call
   int cap_leaves, cap_dicts;  // capacity of the arrays below (one malloc'd block, kept across reuse)
+  const void* order;          // the structure's flatten permutation (solo_structure), or nullptr
   PyObject** leaves;  // [cap_leaves] the captured leaf tensors in the capture walk's order (strong while pending)
   int64_t* ptrs;      // [cap_leaves] their data pointers at the call
   int64_t* tags;      // [2 * cap_dicts] (dict node, PEP 509 version tag), pre-order (tagged)
@@ -1759,27 +1762,123 @@ bool solo_unchanged(const SoloObject* n) {
 
 // The capture walk: every dict (pre-order, values in insertion order — no key sort), list / tuple
 // and None node, exact torch.Tensor leaves. 0 walked; 1 not the fast case.
-int solo_walk(PyObject* x, std::vector<PyObject*>& lv, std::vector<PyObject*>& dv, bool& lists, int depth) {
+// sig (optional): the walked structure in walk order — kLeaf, kNone, (kList | kTuple, n, children),
+// (kDict, n, then per item its key object and the child's entries) — for solo_structure.
+int solo_walk(PyObject* x, std::vector<PyObject*>& lv, std::vector<PyObject*>& dv, bool& lists, int depth,
+              std::vector<int64_t>* sig = nullptr) {
   if (depth > 64) return 1;
   if (Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(THPVariableClass)) {
     lv.push_back(x);
+    if (sig) sig->push_back(kLeaf);
     return lv.size() > static_cast<size_t>(FJTREE_MAX_LEAVES);
   }
-  if (x == Py_None) return 0;
+  if (x == Py_None) {
+    if (sig) sig->push_back(kNone);
+    return 0;
+  }
   if (PyDict_CheckExact(x)) {
     dv.push_back(x);
+    if (sig) sig->push_back(kDict), sig->push_back(PyDict_GET_SIZE(x));
     Py_ssize_t pos = 0;
     PyObject *k, *v;
-    while (PyDict_Next(x, &pos, &k, &v))
-      if (solo_walk(v, lv, dv, lists, depth + 1)) return 1;
+    while (PyDict_Next(x, &pos, &k, &v)) {
+      if (sig) sig->push_back(reinterpret_cast<int64_t>(k));
+      if (solo_walk(v, lv, dv, lists, depth + 1, sig)) return 1;
+    }
     return 0;
   }
   const bool is_list = PyList_CheckExact(x);
   if (!is_list && !PyTuple_CheckExact(x)) return 1;
   lists = lists || is_list;
+  if (sig) sig->push_back(is_list ? kList : kTuple), sig->push_back(Py_SIZE(x));
   for (Py_ssize_t i = 0; i < Py_SIZE(x); ++i)
-    if (solo_walk(is_list ? PyList_GET_ITEM(x, i) : PyTuple_GET_ITEM(x, i), lv, dv, lists, depth + 1)) return 1;
+    if (solo_walk(is_list ? PyList_GET_ITEM(x, i) : PyTuple_GET_ITEM(x, i), lv, dv, lists, depth + 1, sig))
+      return 1;
   return 0;
+}
+
+// The flatten order (jax's: dict keys sorted) of the capture walk's leaf order, per structure:
+// structures are interned by their walk signature (the table keeps their key objects alive, so a
+// key's address is never reused while its entry exists), the permutation computed once, when a
+// structure is first seen (perm[f] = the walk-order index of flatten leaf f). -1: no order (keys
+// that do not sort, or the table is full): not the fast case.
+struct SoloStruct {
+  std::vector<int32_t> perm;
+};
+int solo_sort_walk(const std::vector<int64_t>& sig, size_t& i, int& leaf, std::vector<int32_t>& out) {
+  const int64_t kind = sig[i++];
+  if (kind == kLeaf) {
+    out.push_back(leaf++);
+    return 0;
+  }
+  if (kind == kNone) return 0;
+  const int64_t n = sig[i++];
+  if (kind == kList || kind == kTuple) {
+    for (int64_t c = 0; c < n; ++c)
+      if (solo_sort_walk(sig, i, leaf, out)) return 1;
+    return 0;
+  }
+  // a dict: its children's flatten orders, concatenated in key order
+  std::vector<std::pair<PyObject*, std::vector<int32_t>>> kids(static_cast<size_t>(n));
+  for (int64_t c = 0; c < n; ++c) {
+    kids[c].first = reinterpret_cast<PyObject*>(sig[i++]);
+    if (solo_sort_walk(sig, i, leaf, kids[c].second)) return 1;
+  }
+  bool bad = false;
+  std::stable_sort(kids.begin(), kids.end(), [&](const auto& a, const auto& b) {
+    if (bad) return false;
+    const int r = PyObject_RichCompareBool(a.first, b.first, Py_LT);
+    if (r < 0) {
+      PyErr_Clear();
+      bad = true;
+      return false;
+    }
+    return r == 1;
+  });
+  if (bad) return 1;
+  for (auto& k : kids) out.insert(out.end(), k.second.begin(), k.second.end());
+  return 0;
+}
+const SoloStruct* solo_structure(const std::vector<int64_t>& sig) {
+  static auto* table = new std::unordered_map<std::vector<int64_t>, int64_t, SigHash>();
+  static auto* structs = new std::deque<SoloStruct>();  // (stable addresses: nodes point at entries)
+  static std::vector<int64_t> last_sig;
+  static int64_t last = -1;
+  if (last >= 0 && sig == last_sig) return &(*structs)[last];
+  auto it = table->find(sig);
+  if (it != table->end()) {
+    last_sig = sig;
+    last = it->second;
+    return it->second >= 0 ? &(*structs)[it->second] : nullptr;
+  }
+  if (table->size() >= 4096) return nullptr;
+  SoloStruct st;
+  size_t i = 0;
+  int leaf = 0;
+  const bool ok = solo_sort_walk(sig, i, leaf, st.perm) == 0 && i == sig.size();
+  int64_t id = -1;
+  if (ok) {
+    id = static_cast<int64_t>(structs->size());
+    structs->push_back(std::move(st));
+  }
+  // keep the key objects alive for as long as the entry exists (their addresses are in the sig)
+  {
+    size_t j = 0;
+    std::function<void()> walk = [&]() {
+      const int64_t kind = sig[j++];
+      if (kind == kLeaf || kind == kNone) return;
+      const int64_t n = sig[j++];
+      for (int64_t c = 0; c < n; ++c) {
+        if (kind == kDict) Py_INCREF(reinterpret_cast<PyObject*>(sig[j++]));
+        walk();
+      }
+    };
+    walk();
+  }
+  table->emplace(sig, id);
+  last_sig = sig;
+  last = id;
+  return id >= 0 ? &(*structs)[id] : nullptr;
 }
 
 // The same leaf objects, in any order (L <= FJTREE_MAX_LEAVES).
@@ -1818,10 +1917,14 @@ bool solo_same_tree(const SoloObject* n, PyObject* tree) {
 // strided, contiguous, one device, versioned, <= FJTREE_MAX_LEAVES, some element) or no memory.
 bool solo_capture_into(SoloObject* n, PyObject* tree) {
   thread_local std::vector<PyObject*> lv, dv;
+  thread_local std::vector<int64_t> sig;
   lv.clear();
   dv.clear();
+  sig.clear();
   bool lists = false;
-  if (solo_walk(tree, lv, dv, lists, 0) != 0 || lv.empty()) return false;
+  if (solo_walk(tree, lv, dv, lists, 0, &sig) != 0 || lv.empty()) return false;
+  const SoloStruct* order = solo_structure(sig);
+  if (!order || order->perm.size() != lv.size()) return false;  // (keys that do not sort: the Python path)
   const int L = static_cast<int>(lv.size());
   int dev = -1;
   int64_t vs = 0, numel = 0;
@@ -1841,6 +1944,7 @@ bool solo_capture_into(SoloObject* n, PyObject* tree) {
   n->L = L;
   n->vsum = vs;
   n->nbytes = 4 * numel;
+  n->order = order;
   for (int l = 0; l < L; ++l) {
     Py_INCREF(lv[l]);
     n->leaves[l] = lv[l];
@@ -1862,22 +1966,13 @@ bool solo_capture_into(SoloObject* n, PyObject* tree) {
   return true;
 }
 
-// The leaves of a pending node in flatten order (jax's: dict keys sorted) when its tree still
-// holds them — the order the mean's fused fold reads them in, so a norm computed on its own
-// has the fused value's bits — else in the capture walk's order (the tree changed since the
-// call: no mean can fold this value any more).
+// The captured leaves of a node in flatten order (jax's: dict keys sorted) — the order the mean's
+// fused fold reads them in, so a norm computed on its own has the fused value's bits, whether
+// or not the tree has changed since the call (the permutation is the captured structure's).
 void solo_flatten_order(const SoloObject* n, std::vector<PyObject*>& out) {
-  out.assign(n->leaves, n->leaves + n->L);
-  if (!n->tree || !solo_same_tree(n, n->tree)) return;
-  PWalk w;
-  w.K = 1;
-  PyObject* t = n->tree;
-  if (pwalk(&t, w, 0) != 0) {
-    if (PyErr_Occurred()) PyErr_Clear();
-    return;
-  }
-  if (static_cast<int>(w.leaves[0].size()) == n->L && same_leaf_set(w.leaves[0].data(), n->leaves, n->L))
-    out.assign(w.leaves[0].begin(), w.leaves[0].end());
+  const auto* st = static_cast<const SoloStruct*>(n->order);
+  out.resize(static_cast<size_t>(n->L));
+  for (int f = 0; f < n->L; ++f) out[f] = n->leaves[st->perm[f]];
 }
 
 // every captured pointer 16-byte aligned: the mean's fused plan (no element units) is this node's

@@ -228,17 +228,21 @@ def test_misaligned_delta_is_computed_alone(cuda):
 
 
 def test_buffer_boundary_splits_the_run(cuda):
-    """Norms of one round that straddle two norm buffers fold in two runs, all fused."""
+    """Norms of one round that straddle two norm buffers fold in two runs, all fused. (Squared
+    norms take fresh columns in call order; the norms' pre-made pool pairs come in runs of their
+    own, tested above.)"""
     deltas = make_deltas(SMALL, 16, 9, cuda)
     col = H.solo_info()["column"] % 4096
-    junk = [tu.tree_l2_norm({"a": torch.ones(4, device=cuda)}) for _ in range((4090 - col) % 4096)]
+    junk = [tu.tree_l2_squared({"a": torch.ones(4, device=cuda)}) for _ in range((4090 - col) % 4096)]
     del junk
     gc.collect()
     assert H.solo_info()["column"] == 4090
     before = H.solo_info()
-    mean, norms = example_round(deltas, list(range(1, 17)))
+    sq = [tu.tree_l2_squared(d) for d in deltas]
+    mean = tu.tree_mean([(d, k + 1) for k, d in enumerate(deltas)])
     assert H.solo_info()["fused"] - before["fused"] == 16
-    np.testing.assert_allclose([float(v) for v in norms], [f64norm(d) for d in deltas], rtol=2e-6)
+    assert len({v._ticket._buf.data_ptr() for v in sq}) == 2  # the run crossed into a new buffer
+    np.testing.assert_allclose([float(v) for v in sq], [f64norm(d) ** 2 for d in deltas], rtol=4e-6)
     assert same_mean(mean, want_mean(deltas, list(range(1, 17))))
 
 
