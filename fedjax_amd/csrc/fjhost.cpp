@@ -1180,6 +1180,80 @@ PyObject* capture(PyObject*, PyObject* args) {
   return capture_impl(tree, dev);
 }
 
+// capture_probe(tree, reps) -> dict: ns per call of the parts of capture_impl over `reps` calls
+// (tools/prof_capture_parts.py): the sorted walk, the leaf checks, the signature + structure
+// token, the capture objects, and the whole capture.
+PyObject* capture_probe(PyObject*, PyObject* args) {
+  PyObject* tree;
+  long long reps;
+  if (!PyArg_ParseTuple(args, "OL", &tree, &reps)) return nullptr;
+  using clk = std::chrono::steady_clock;
+  auto ns = [&](clk::time_point t0) {
+    return std::chrono::duration<double, std::nano>(clk::now() - t0).count() / static_cast<double>(reps);
+  };
+  try {
+    double t_walk, t_check, t_sig, t_full;
+    {
+      auto t0 = clk::now();
+      for (long long r = 0; r < reps; ++r) {
+        thread_local std::vector<int64_t> sig;
+        thread_local std::vector<PyObject*> dicts;
+        sig.clear(), dicts.clear();
+        PWalk w;
+        w.K = 1;
+        w.sig = &sig;
+        w.dicts = &dicts;
+        if (pwalk(&tree, w, 0) != 0) Py_RETURN_NONE;
+      }
+      t_walk = ns(t0);
+    }
+    PWalk w;
+    w.K = 1;
+    std::vector<int64_t> sig;
+    std::vector<PyObject*> dicts;
+    w.sig = &sig;
+    w.dicts = &dicts;
+    if (pwalk(&tree, w, 0) != 0 || w.leaves[0].empty()) Py_RETURN_NONE;
+    const int dev = THPVariable_Unpack(w.leaves[0][0]).get_device();
+    {
+      auto t0 = clk::now();
+      int64_t vs = 0;
+      bool unv = false;
+      for (long long r = 0; r < reps; ++r)
+        if (!check_leaves(w, 0, static_cast<c10::DeviceIndex>(dev), &vs, &unv)) Py_RETURN_NONE;
+      t_check = ns(t0);
+    }
+    {
+      auto t0 = clk::now();
+      for (long long r = 0; r < reps; ++r) {
+        std::vector<int64_t> s2(sig);
+        s2.push_back(dev);
+        for (size_t l = 0; l < w.leaves[0].size(); ++l) {
+          const at::Tensor& t = THPVariable_Unpack(w.leaves[0][l]);
+          s2.push_back(t.dim());
+          for (int64_t z : t.sizes()) s2.push_back(z);
+        }
+        (void)structure_token(s2, w);
+      }
+      t_sig = ns(t0);
+    }
+    {
+      auto t0 = clk::now();
+      for (long long r = 0; r < reps; ++r) {
+        PyObject* c = capture_impl(tree, -1);
+        if (!c) return nullptr;
+        Py_DECREF(c);
+      }
+      t_full = ns(t0);
+    }
+    return Py_BuildValue("{s:d,s:d,s:d,s:d}", "walk_ns", t_walk, "check_ns", t_check, "sig_token_ns", t_sig,
+                         "capture_ns", t_full);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 // matches(tree, leaves_tuple, version_sum) -> bool: the same leaf objects, unmodified.
 PyObject* matches(PyObject*, PyObject* args) {
   PyObject *tree, *tup;
@@ -4105,6 +4179,7 @@ PyMethodDef kMethods[] = {
     {"leaf_versions", leaf_versions, METH_VARARGS, "torch in-place version counters of K pytrees' leaves"},
     {"fold_weights", fold_weights, METH_VARARGS, "f32/i32 weights and W of Python-number weights"},
     {"capture", capture, METH_VARARGS, "leaves + version sum of a tree for a lazy tree_weight"},
+    {"capture_probe", capture_probe, METH_VARARGS, "ns per call of capture's parts (profiling)"},
     {"matches", matches, METH_VARARGS, "tree holds exactly the captured leaves, unmodified"},
     {"compatible", compatible, METH_VARARGS, "tree_add(a, b) is the fast case (structure, float32 leaves)"},
     {"append_check", append_check, METH_VARARGS, "deferred tree_add: structure + capture check in one walk"},
