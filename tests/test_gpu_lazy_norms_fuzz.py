@@ -5,6 +5,8 @@ generator), leaves replaced after a norm, pending limits and buffer boundaries c
 read value must be the bits of that delta's norm computed alone (the value does not depend on
 when or how it is computed) and every mean the oracle's bits (oracle/tree_util_ref.py restates
 tree_util.py:76-96)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -88,11 +90,17 @@ def run_program(seed, cuda):
     np.testing.assert_allclose([np.float32(np.array(c[0], np.int32).view(np.float32)) for c in canon], x64, rtol=2e-6)
 
 
-@pytest.mark.parametrize("block", range(4))
+# FJ_FUZZ_CASES / FJ_FUZZ_SEED0: a longer campaign over other seeds (the suite runs the defaults)
+NCASES = int(os.environ.get("FJ_FUZZ_CASES", "200"))
+SEED0 = int(os.environ.get("FJ_FUZZ_SEED0", "0"))
+BLOCK = 50
+
+
+@pytest.mark.parametrize("block", range((NCASES + BLOCK - 1) // BLOCK))
 def test_lazy_norm_programs(block, cuda):
     tu.set_deferred_sums(True)
     try:
-        for seed in range(block * 50, block * 50 + 50):
+        for seed in range(SEED0 + block * BLOCK, SEED0 + min(NCASES, (block + 1) * BLOCK)):
             run_program(seed, cuda)
             tu.set_lazy_norms(True, max_pending=16383)
     finally:
