@@ -32,6 +32,8 @@ def tree(k):
 pairs = [(tree(k), 1 + (k * 37) % 500) for k in range(128)]
 H = tu._HOST
 SCHEDULES = [[], [0.06, 0.2], [0.08, 0.25, 0.6], [0.05, 0.15, 0.4], [0.1, 0.35], [0.04, 0.12, 0.32, 0.7]]
+if len(sys.argv) > 1:  # e.g. '[[], [0.1], [0.15], [0.3]]': single first chunks of other sizes
+    SCHEDULES = json.loads(sys.argv[1])
 ref = [x.clone() for x in pytree.leaves_of(tu.tree_mean(pairs))]
 times = {str(s): [] for s in SCHEDULES}
 pc = time.perf_counter
