@@ -94,6 +94,28 @@ def main():
         torch.cuda.synchronize()
         only.append(pc() - t0)
     res["norms_only_rounds_ms"] = round(float(np.median(only)) * 1e3, 4)
+    # the example's loop without the norm call (its own Python: enumerate, append, the dict), and the
+    # same loop calling the native tree_l2_norm, back to back with nothing on the GPU: the norm's share
+    floor, calls = [], []
+    for i in range(2 * a.rounds):
+        diag = lst = None
+        torch.cuda.synchronize()
+        t0 = pc()
+        diag, lst = {}, []
+        if i % 2 == 0:
+            for cid, (d, n) in enumerate(pairs):
+                lst.append((d, n))
+                diag[cid] = {"delta_l2_norm": d}
+        else:
+            for cid, (d, n) in enumerate(pairs):
+                lst.append((d, n))
+                diag[cid] = {"delta_l2_norm": tu.tree_l2_norm(d)}
+        (floor if i % 2 == 0 else calls).append(pc() - t0)
+        if i % 2:
+            tu.tree_mean(lst)  # (fills the views: the registry does not grow)
+            torch.cuda.synchronize()
+    res["example_loop_without_norm_call_us"] = round(float(np.median(floor)) * 1e6, 1)
+    res["example_loop_with_norm_call_us"] = round(float(np.median(calls)) * 1e6, 1)
     res["ratio_norms_vs_mean_only"] = round(res["norms_ms"] / res["mean_only_ms"], 4)
     res["solo_info"] = H.solo_info()
     print(json.dumps(res))
