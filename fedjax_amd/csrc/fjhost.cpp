@@ -3541,6 +3541,73 @@ int solo_refill(int dev, unsigned long long stream) {
   return 0;
 }
 
+// solo_probe(tree, reps) -> dict: ns per call of the standalone lazy norm's capture steps on one
+// tree, repeated (caches warm): the walk with its signature, the structure lookup, the leaf checks,
+// the data-pointer reads (data_ptr / const_data_ptr) and the whole capture into a scratch node.
+// (tools/prof_capture_parts.py; profiling only)
+PyObject* solo_probe(PyObject*, PyObject* args) {
+  PyObject* tree;
+  long long reps;
+  if (!PyArg_ParseTuple(args, "OL", &tree, &reps)) return nullptr;
+  if (!g_solo.type) Py_RETURN_NONE;
+  using clk = std::chrono::steady_clock;
+  auto ns = [&](clk::time_point t0) {
+    return std::chrono::duration<double, std::nano>(clk::now() - t0).count() / static_cast<double>(reps);
+  };
+  try {
+    std::vector<PyObject*> lv, dv;
+    std::vector<int64_t> sig;
+    bool lists = false;
+    auto t0 = clk::now();
+    for (long long r = 0; r < reps; ++r) {
+      lv.clear(), dv.clear(), sig.clear();
+      if (solo_walk(tree, lv, dv, lists, 0, &sig) != 0) Py_RETURN_NONE;
+    }
+    const double t_walk = ns(t0);
+    t0 = clk::now();
+    const SoloStruct* st = nullptr;
+    for (long long r = 0; r < reps; ++r) st = solo_structure(sig);
+    const double t_struct = ns(t0);
+    if (!st || lv.empty()) Py_RETURN_NONE;
+    t0 = clk::now();
+    int64_t acc = 0;
+    for (long long r = 0; r < reps; ++r)
+      for (PyObject* x : lv) {
+        const at::Tensor& t = THPVariable_Unpack(x);
+        acc += t.layout() == c10::kStrided && t.scalar_type() == at::kFloat && t.is_cuda() && t.is_contiguous() &&
+               !t.is_inference();
+        acc += t.get_device() + static_cast<int64_t>(t._version()) + t.numel();
+      }
+    const double t_check = ns(t0);
+    t0 = clk::now();
+    for (long long r = 0; r < reps; ++r)
+      for (PyObject* x : lv) acc += reinterpret_cast<int64_t>(THPVariable_Unpack(x).data_ptr());
+    const double t_ptr = ns(t0);
+    t0 = clk::now();
+    for (long long r = 0; r < reps; ++r)
+      for (PyObject* x : lv) acc += reinterpret_cast<int64_t>(THPVariable_Unpack(x).const_data_ptr());
+    const double t_cptr = ns(t0);
+    auto* n = reinterpret_cast<SoloObject*>(g_solo.type->tp_alloc(g_solo.type, 0));
+    if (!n) return nullptr;
+    t0 = clk::now();
+    for (long long r = 0; r < reps; ++r) {
+      if (!solo_capture_into(n, tree)) {
+        Py_DECREF(n);
+        Py_RETURN_NONE;
+      }
+      solo_release(n, kSoloDone);
+    }
+    const double t_cap = ns(t0);
+    Py_DECREF(n);
+    return Py_BuildValue("{s:d,s:d,s:d,s:d,s:d,s:d,s:L}", "walk_sig_ns", t_walk, "structure_ns", t_struct,
+                         "leaf_checks_ns", t_check, "data_ptr_ns", t_ptr, "const_data_ptr_ns", t_cptr,
+                         "capture_into_ns", t_cap, "_", static_cast<long long>(acc & 1));
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 // tree_l2_norm / tree_l2_squared (which 1 / 0) of a delta no running sum took: a lazy view of a
 // SoloNorm node (see "standalone lazy norms"). The most recent node answers for its own tree
 // when unchanged (the norm and the squared norm of one delta share a column); a norm takes the
@@ -4180,6 +4247,7 @@ PyMethodDef kMethods[] = {
     {"fold_weights", fold_weights, METH_VARARGS, "f32/i32 weights and W of Python-number weights"},
     {"capture", capture, METH_VARARGS, "leaves + version sum of a tree for a lazy tree_weight"},
     {"capture_probe", capture_probe, METH_VARARGS, "ns per call of capture's parts (profiling)"},
+    {"solo_probe", solo_probe, METH_VARARGS, "ns per call of the lazy norm capture's parts (profiling)"},
     {"matches", matches, METH_VARARGS, "tree holds exactly the captured leaves, unmodified"},
     {"compatible", compatible, METH_VARARGS, "tree_add(a, b) is the fast case (structure, float32 leaves)"},
     {"append_check", append_check, METH_VARARGS, "deferred tree_add: structure + capture check in one walk"},

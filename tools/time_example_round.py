@@ -114,6 +114,20 @@ def main():
         if i % 2:
             tu.tree_mean(lst)  # (fills the views: the registry does not grow)
             torch.cuda.synchronize()
+    # the same 128 calls on two trees in turn (their metadata stays in cache): the call's own work
+    warm = []
+    two = [pairs[0][0], pairs[1][0]]
+    for i in range(a.rounds):
+        diag = None
+        torch.cuda.synchronize()
+        t0 = pc()
+        diag = {}
+        for cid in range(K):
+            diag[cid] = {"delta_l2_norm": tu.tree_l2_norm(two[cid & 1])}
+        warm.append(pc() - t0)
+        tu.tree_mean([(t, 1) for t in two])
+        torch.cuda.synchronize()
+    res["example_loop_norm_calls_on_two_warm_trees_us"] = round(float(np.median(warm)) * 1e6, 1)
     res["example_loop_without_norm_call_us"] = round(float(np.median(floor)) * 1e6, 1)
     res["example_loop_with_norm_call_us"] = round(float(np.median(calls)) * 1e6, 1)
     res["ratio_norms_vs_mean_only"] = round(res["norms_ms"] / res["mean_only_ms"], 4)
