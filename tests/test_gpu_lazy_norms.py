@@ -293,3 +293,34 @@ def test_a_second_view_keeps_the_capture(cuda):
     H.solo_info()  # (the registry looks at the views)
     assert q._ticket.node is not None and H.solo_info()["pending"] == 1
     assert float(q) == pytest.approx(want ** 2, rel=4e-6)
+
+
+def test_deltas_with_autograd_history(cuda):
+    """Deltas computed from trained parameters outside torch.no_grad carry autograd history
+    (requires_grad, a grad_fn), as `server_p - client_p` of nn.Parameters does. The example
+    round (fed_avg.py:72-82), the library's running sum (algorithms/fed_avg.py:132-146) and the
+    aggregator read their values: the oracle's mean bits and the f64 norms, as for plain deltas.
+    Results carry no autograd history: the server never differentiates its aggregation."""
+    K = 6
+    base = make_deltas(SMALL, K, 7, cuda)
+    deltas = [tmap(lambda x: x.clone().requires_grad_(True) * 1.0, d) for d in base]  # same values
+    assert all(x.requires_grad and x.grad_fn is not None for d in deltas for x in pytree.leaves_of(d))
+    weights = [3, 1, 4, 1, 5, 9]
+    want = want_mean(base, weights)
+    before = H.solo_info()["fused"]
+    mean, norms = example_round(deltas, weights)
+    assert H.solo_info()["fused"] - before == K
+    assert same_mean(mean, want)  # (.numpy() would raise on a result that requires grad)
+    np.testing.assert_allclose([float(v) for v in norms], [f64norm(d) for d in base], rtol=2e-6)
+    s = tu.tree_zeros_like(deltas[0])
+    for d, n in zip(deltas, weights):
+        s = tu.tree_add(s, tu.tree_weight(d, n))
+    got = tu.tree_inverse_weight(s, float(sum(weights)))
+    s_ref = ref.tree_zeros_like(tmap(lambda x: x.cpu().numpy(), base[0]))
+    for d, n in zip(base, weights):
+        s_ref = ref.tree_add(s_ref, ref.tree_weight(tmap(lambda x: x.cpu().numpy(), d), n))
+    assert same_mean(got, ref.tree_inverse_weight(s_ref, float(sum(weights))))
+    agg = fedjax_amd.aggregators.mean_aggregator()
+    m2, _ = agg.apply([(str(i), d, w) for i, (d, w) in enumerate(zip(deltas, weights))], agg.init())
+    assert same_mean(m2, want)
+    assert not any(x.requires_grad for t in (mean, got, m2) for x in pytree.leaves_of(t))
