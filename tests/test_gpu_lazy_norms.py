@@ -324,3 +324,25 @@ def test_deltas_with_autograd_history(cuda):
     m2, _ = agg.apply([(str(i), d, w) for i, (d, w) in enumerate(zip(deltas, weights))], agg.init())
     assert same_mean(m2, want)
     assert not any(x.requires_grad for t in (mean, got, m2) for x in pytree.leaves_of(t))
+
+
+def test_a_delta_twice_in_one_mean_and_two_views_of_one_tree(cuda):
+    """A client delta listed twice in one tree_mean (a client sampled twice), and a tree normed
+    twice with another norm in between (two pending nodes of one tree): the mean is the oracle's
+    bits and every view the bits of its delta's norm computed alone, whichever node the mean
+    fills and whichever is computed on its own."""
+    d = make_deltas(SMALL, 3, 11, cuda)
+    alone = []
+    for x in d:
+        alone.append(bits(tu.tree_l2_norm(x)).clone())
+        tu.tree_mean([(x, 1)])  # (computes it; the mean does not change the value)
+    v0 = tu.tree_l2_norm(d[0])
+    v1 = tu.tree_l2_norm(d[1])
+    v0b = tu.tree_l2_norm(d[0])  # a second node of d[0] (v1's node sits in between)
+    v2 = tu.tree_l2_norm(d[2])
+    pairs = [(d[0], 2), (d[1], 3), (d[0], 5), (d[2], 7), (d[1], 1)]
+    mean = tu.tree_mean(pairs)
+    assert same_mean(mean, ref.tree_mean([(tmap(lambda x: x.cpu().numpy(), t), w) for t, w in pairs]))
+    for v, i in ((v0, 0), (v1, 1), (v0b, 0), (v2, 2)):
+        assert torch.equal(bits(v), alone[i]), i
+    assert H.solo_info()["pending"] == 0

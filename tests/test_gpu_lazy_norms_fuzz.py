@@ -1,7 +1,7 @@
 """Random programs over standalone lazy norms (fjhost.cpp "standalone lazy norms"): norms and
 squared norms taken in any order, views read early or late or dropped, tree_mean /
-mean_aggregator().apply over random subsets, orders and container kinds (list, tuple,
-generator), leaves replaced after a norm, pending limits and buffer boundaries crossed. Every
+mean_aggregator().apply over random subsets (some with a delta listed twice), orders and
+container kinds (list, tuple, generator), leaves replaced after a norm, pending limits and buffer boundaries crossed. Every
 read value must be the bits of that delta's norm computed alone (the value does not depend on
 when or how it is computed) and every mean the oracle's bits (oracle/tree_util_ref.py restates
 tree_util.py:76-96)."""
@@ -53,7 +53,9 @@ def run_program(seed, cuda):
         elif op == 3 and views:  # drop one
             views.pop(rng.randint(len(views)))
         elif op == 4:  # a mean over a random subset, order and container
-            idx = list(rng.permutation(n)[: int(rng.randint(1, n + 1))])
+            m = int(rng.randint(1, n + 1))
+            # (sometimes with replacement: a client sampled twice lists its delta twice)
+            idx = list(rng.randint(n, size=m)) if rng.rand() < 0.3 else list(rng.permutation(n)[:m])
             ws = [int(rng.randint(1, 9)) if rng.rand() < 0.7 else float(rng.rand() + 0.1) for _ in idx]
             pairs = [(deltas[i], w) for i, w in zip(idx, ws)]
             kind = rng.randint(4)
