@@ -346,3 +346,24 @@ def test_a_delta_twice_in_one_mean_and_two_views_of_one_tree(cuda):
     for v, i in ((v0, 0), (v1, 1), (v0b, 0), (v2, 2)):
         assert torch.equal(bits(v), alone[i]), i
     assert H.solo_info()["pending"] == 0
+
+
+def test_many_rounds_hold_no_growing_state(cuda):
+    """300 example rounds of 10 clients, each round's diagnostics dropped when the next one
+    starts, as a training loop does: the registry keeps nothing pending, the norm buffers stay
+    within their bound and the device memory in use returns to where it started."""
+    deltas = make_deltas(SMALL, 10, 13, cuda)
+    weights = list(range(1, 11))
+    mean, norms = example_round(deltas, weights)  # (the first round builds the pool and its buffers)
+    del mean, norms
+    torch.cuda.synchronize()
+    start = torch.cuda.memory_allocated(cuda)
+    for _ in range(300):
+        mean, norms = example_round(deltas, weights)
+        float(norms[-1])
+    del mean, norms
+    torch.cuda.synchronize()
+    info = H.solo_info()
+    assert info["pending"] == 0 and info["registry"] <= 64
+    assert info["buffers"] <= 6
+    assert torch.cuda.memory_allocated(cuda) <= start + 2 * 2 * 4096 * 4  # (at most the next buffers' columns)
