@@ -367,3 +367,30 @@ def test_many_rounds_hold_no_growing_state(cuda):
     assert info["pending"] == 0 and info["registry"] <= 64
     assert info["buffers"] <= 6
     assert torch.cuda.memory_allocated(cuda) <= start + 2 * 2 * 4096 * 4  # (at most the next buffers' columns)
+
+
+def test_rounds_on_alternating_streams(cuda):
+    """Example rounds that alternate between the default stream and a side stream (the mean and
+    its norms run on the current stream; a pooled buffer is reused only on the stream it was
+    written on): after a synchronize every view holds the bits of its delta's norm alone and
+    every mean the oracle's."""
+    deltas = make_deltas(SMALL, 8, 17, cuda)
+    weights = [2, 7, 1, 8, 2, 8, 1, 8]
+    alone = [bits(tu.tree_l2_norm(d)).clone() for d in deltas]
+    want = want_mean(deltas, weights)
+    side = torch.cuda.Stream(cuda)
+    kept = []
+    for r in range(12):
+        stream = side if r % 2 else torch.cuda.current_stream(cuda)
+        with torch.cuda.stream(stream):
+            mean, norms = example_round(deltas, weights)
+        stream.synchronize()
+        assert same_mean(mean, want), r
+        for v, a in zip(norms, alone):
+            assert torch.equal(bits(v), a), r
+        if r % 3 == 0:
+            kept.append(norms)  # (some rounds' views stay alive: their buffers cannot be reused)
+    torch.cuda.synchronize()
+    for norms in kept:
+        for v, a in zip(norms, alone):
+            assert torch.equal(bits(v), a)
