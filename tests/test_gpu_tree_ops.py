@@ -411,6 +411,46 @@ def test_lazy_norm_pool_across_rounds(cuda, sum_mode):
     H.drop_pool()
 
 
+def test_library_loop_on_alternating_streams(cuda, sum_mode):
+    """The library loop with its per-client norms (fed_avg.py:132-146), rounds alternating between
+    the default stream and a side stream (the folds run on the current stream; a retired norm pool
+    is reused only on the stream it was built on): after a synchronize every mean is the
+    reference's bits and every norm the first round's bits (within 2e-6 of f64), including the
+    views kept from earlier rounds."""
+    g = torch.Generator().manual_seed(43)
+    shapes = {"a": (5000,), "b": {"c": (33, 3)}}
+    xs = [to_dev(rand_tree(shapes, g), cuda) for _ in range(8)]
+    W = float(sum(range(1, 9)))
+    want = ref.tree_zeros_like(to_np(xs[0]))
+    for k, x in enumerate(xs):
+        want = ref.tree_add(want, ref.tree_weight(to_np(x), k + 1))
+    want = ref.tree_inverse_weight(want, W)
+    f64 = [np.sqrt(sum((v.astype(np.float64) ** 2).sum() for v in leaves_np(x))) for x in xs]
+    side = torch.cuda.Stream(cuda)
+    first, kept = None, []
+    for r in range(10):
+        st = side if r % 2 else torch.cuda.current_stream(cuda)
+        with torch.cuda.stream(st):
+            s, norms = tu.tree_zeros_like(xs[0]), []
+            for k, x in enumerate(xs):
+                s = tu.tree_add(s, tu.tree_weight(x, k + 1))
+                norms.append(tu.tree_l2_norm(x))
+            mean = tu.tree_inverse_weight(s, W)
+        st.synchronize()
+        for a, b in zip(leaves_np(mean), pytree.leaves_of(want)):
+            assert np.array_equal(bits(a), bits(b.reshape(-1))), r
+        got = [bits(v.detach().cpu().numpy().reshape(-1)).copy() for v in norms]
+        if first is None:
+            first = got
+            np.testing.assert_allclose([float(v) for v in norms], f64, rtol=2e-6)
+        assert all(np.array_equal(a, b) for a, b in zip(got, first)), r
+        if r % 3 == 0:
+            kept.append(norms)
+    torch.cuda.synchronize()
+    for norms in kept:
+        assert all(np.array_equal(bits(v.detach().cpu().numpy().reshape(-1)), b) for v, b in zip(norms, first))
+
+
 def test_norm_combine_orders_give_the_same_bits(cuda):
     """The per-call fused norm with its workgroup partials handed off by the gfx950
     write-through + drain form (default) and by release/acquire atomics (FJTREE_ORDERED,
