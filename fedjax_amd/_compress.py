@@ -72,7 +72,7 @@ class Upload:
         host = np.zeros(max(self._size, 16), dtype=np.uint8)
         for off, b in self._parts:
             host[off:off + b.size] = b
-        self.dev = torch.from_numpy(host).pin_memory().to(device, non_blocking=True)
+        self.dev = _lib.upload(torch.from_numpy(host), device)
         return self.dev.data_ptr()
 
 
@@ -393,7 +393,7 @@ def drive_mean(rows: List[List[torch.Tensor]], client_keys: np.ndarray, w: np.nd
     Z = torch.empty((B, Pp), dtype=torch.float32, device=device)
     # pinned + non_blocking: a pageable copy would make the host wait for the previous
     # round to drain and then leave the GPU idle while this round's tables are built
-    w_dev = torch.from_numpy(np.ascontiguousarray(w, dtype=np.float32)).pin_memory().to(device, non_blocking=True)
+    w_dev = _lib.upload(torch.from_numpy(np.ascontiguousarray(w, dtype=np.float32)), device)
     leaf_n = np.asarray(leaf_n, dtype=np.int64)
     leaf_d = np.asarray(ds, dtype=np.int64)
     yoff = 4 * offs[:-1].astype(np.uint64)

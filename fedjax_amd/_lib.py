@@ -280,3 +280,15 @@ def call(name: str, *args):
     rc = getattr(load(), name)(*args)
     check(rc, name)
     return rc
+
+
+def upload(host: "torch.Tensor", device) -> "torch.Tensor":
+    """``host`` on ``device`` through pinned memory, ordered on the current stream (the plan images
+    and weights the kernels read). Refused while that stream is being captured into a graph: once
+    the copy is recorded, the pinned staging tensor goes back to torch's host allocator, which hands
+    the block out again, and a replay would copy whatever it then holds (kernel pointers, weights)."""
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("fedjax_amd: this call uploads a host table through a pinned staging buffer, "
+                           "which a graph replay cannot reuse safely; not capturable (the dense fold with "
+                           "device weights and the kernel-argument paths are)")
+    return host.pin_memory().to(device, non_blocking=True)

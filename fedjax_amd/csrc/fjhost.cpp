@@ -444,6 +444,23 @@ at::Tensor l2_workspace(int dev, unsigned long long stream, int64_t need) {
   return ws;
 }
 
+// An upload from a pinned staging tensor cannot be replayed from a graph: once the copy is recorded
+// the tensor goes back to torch's host allocator, which hands the block out again, and a replay
+// copies whatever the block then holds (as kernel pointers, here). While `stream` is being captured
+// such an upload is refused: true with a Python error set. (Images in the kernel arguments are
+// part of the recorded launch and replay as captured.)
+bool upload_refused_in_capture(unsigned long long stream, const char* what) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(reinterpret_cast<hipStream_t>(stream), &cs) != hipSuccess || cs == hipStreamCaptureStatusNone)
+    return false;
+  PyErr_Format(PyExc_RuntimeError,
+               "%s: its plan image is too large for the kernel arguments and would be uploaded from a pinned "
+               "staging buffer, which a graph replay cannot reuse safely; not capturable (fewer clients or "
+               "leaves per call keep the image in the kernel arguments)",
+               what);
+  return true;
+}
+
 int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K, const float* wf, double scale,
               bool has_scale, double nt_min_bytes, int dev, unsigned long long stream, PlanFn plan, WsumFn wsum,
               std::vector<at::Tensor>& outs, bool accumulate, WsumL2Fn l2fn, L2WsFn l2ws, float* l2p, int* rc,
@@ -570,6 +587,7 @@ int fold_core(const std::vector<at::Tensor>& row0, const int64_t* in, int64_t K,
     if (*rc != FJAGG_EUNSUPPORTED) ++g_image_karg;
   }
   if (*rc == FJAGG_EUNSUPPORTED) {  // too large for the kernel arguments: pinned image + stream-ordered upload
+    if (upload_refused_in_capture(stream, "a pytree fold")) return 3;
     at::Tensor img = at::empty({n}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
     if (!fill(img.data_ptr<int64_t>())) return 1;
     st.lap(kTImage);
@@ -642,8 +660,10 @@ PyObject* fold_table(PyObject*, PyObject* args) {
     if (fold_core(r0, static_cast<const int64_t*>(bp.buf), K, static_cast<const float*>(bw.buf), scale,
                   has_scale != 0, nt_min_bytes, dev, stream, reinterpret_cast<PlanFn>(plan_addr),
                   reinterpret_cast<WsumFn>(wsum_addr), outs, accumulate != 0, reinterpret_cast<WsumL2Fn>(l2_addr),
-                  reinterpret_cast<L2WsFn>(l2ws_addr), l2p, &rc, st) != 0)
+                  reinterpret_cast<L2WsFn>(l2ws_addr), l2p, &rc, st) != 0) {
+      if (PyErr_Occurred()) return nullptr;
       Py_RETURN_NONE;
+    }
     PyObject* list = PyList_New(L);
     if (!list) return nullptr;
     for (Py_ssize_t l = 0; l < L; ++l) PyList_SET_ITEM(list, l, THPVariable_Wrap(std::move(outs[l])));
@@ -1518,8 +1538,10 @@ PyObject* fold_caps_impl(PyObject* base, PyObject* const* caps, PyObject* const*
     if (fold_core(row0, ptrs.data(), K, wf.data(), scale, has_scale, nt_min, dev, stream,
                   reinterpret_cast<PlanFn>(plan_addr), reinterpret_cast<WsumFn>(wsum_addr), outs, false,
                   l2p ? reinterpret_cast<WsumL2Fn>(l2_addr) : nullptr,
-                  (l2p || rows) ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr, l2p, &rc, st, rows) != 0)
+                  (l2p || rows) ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr, l2p, &rc, st, rows) != 0) {
+      if (PyErr_Occurred()) return nullptr;
       Py_RETURN_NONE;
+    }
     if (rc != 0) return Py_BuildValue("(iO)", rc, Py_None);
     std::vector<PyObject*> wrapped(L);
     for (Py_ssize_t l = 0; l < L; ++l) wrapped[l] = THPVariable_Wrap(std::move(outs[l]));
@@ -2130,6 +2152,7 @@ int solo_resolve(std::vector<SoloObject*>& nodes) {
       if (fold_core(row0, ptrs.data(), K, wf.data(), 1.0, false, HUGE_VAL, dev, stream,
                     reinterpret_cast<PlanFn>(g_solo.plan_fn), nullptr, outs, false, nullptr,
                     reinterpret_cast<L2WsFn>(g_solo.l2ws_fn), nullptr, &rc, st, &rows) != 0) {
+        if (PyErr_Occurred()) return -1;
         PyErr_SetString(PyExc_RuntimeError, "lazy norms: the captured leaves are not a fold's case");
         return -1;
       }
@@ -2535,7 +2558,10 @@ PyObject* mean_pairs_impl(PyObject* pairs, bool triples, int may_pipeline, doubl
                           with_l2 ? reinterpret_cast<L2WsFn>(l2ws_addr) : nullptr,
                           with_l2 ? l2sq.data_ptr<float>() + a : nullptr, &rc, st);
         }
-        if (got != 0) Py_RETURN_NONE;
+        if (got != 0) {
+          if (PyErr_Occurred()) return nullptr;
+          Py_RETURN_NONE;
+        }
         if (rc != 0) return Py_BuildValue("(iOdO)", rc, Py_None, job_bytes, Py_None);
         if (a == 0)
           g_timers[kTFirstLaunch] +=
@@ -2823,6 +2849,10 @@ PyObject* server_pairs(PyObject*, PyObject* args) {
     const int64_t nblk = plan(kF32, 0, leaf_n.data(), mask, static_cast<int>(L), nullptr, 0);
     if (nblk < 1) Py_RETURN_NONE;
     const int64_t nw = (K + 1) / 2, n = K * L + 2 * L + 2 * nblk + nw + 3 * L;
+    if (upload_refused_in_capture(reinterpret_cast<unsigned long long>(
+                                      c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(dev)).stream()),
+                                  "the server step's pytree fold"))
+      return nullptr;
     at::Tensor img = at::empty({n}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
     int64_t* p = img.data_ptr<int64_t>();
     std::memcpy(p, ptrs.data(), sizeof(int64_t) * K * L);

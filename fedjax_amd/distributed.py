@@ -181,7 +181,7 @@ def _native_sharded(comm: RcclCommunicator, x_local: torch.Tensor, w_local: torc
             _lib.check(rc, "fjcomm_sharded_wsum_dense_edges")
             kernels.HOST_WEIGHT_PATHS["kernel_args"] += 1
             return
-        w_local = w_local.pin_memory().to(out.device, non_blocking=True)
+        w_local = _lib.upload(w_local, out.device)
         kernels.HOST_WEIGHT_PATHS["uploaded"] += 1
     _lib.call("fjcomm_sharded_wsum_dense_edges", comm.handle, kernels.dtype_code(x_local.dtype),
               x_local.data_ptr() if K else None, x_local.stride(0) if K else P, K, P,
@@ -430,7 +430,7 @@ def multi_device_weighted_mean(xs: Sequence[torch.Tensor], ws: Sequence[torch.Te
             _lib.check(rc, "fjcomm_multi_wsum_dense")
             kernels.HOST_WEIGHT_PATHS["kernel_args"] += 1
             return list(outs)
-        ws = [w.pin_memory().to(dev, non_blocking=True) for w, dev in zip(ws, comm.devices)]
+        ws = [_lib.upload(w, dev) for w, dev in zip(ws, comm.devices)]
         kernels.HOST_WEIGHT_PATHS["uploaded"] += 1
     _lib.check(issue(ws, flags), "fjcomm_multi_wsum_dense")
     return list(outs)

@@ -148,7 +148,7 @@ def weighted_sum_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[floa
                 _lib.check(rc, "fjagg_wsum_dense")
                 HOST_WEIGHT_PATHS["kernel_args"] += 1
                 return out
-        w = w.pin_memory().to(dev, non_blocking=True)  # not built with kernel-argument weights
+        w = _lib.upload(w, dev)  # not built with kernel-argument weights
         HOST_WEIGHT_PATHS["uploaded"] += 1
     ws_ptr, ws_bytes = None, 0
     if m == _lib.MODE_SPLIT:

@@ -333,7 +333,7 @@ def fused_tree_mean_update(pytrees_and_weights, opt: ServerOptimizer, params, st
     w_words = np.zeros((K + 1) // 2, dtype=np.int64)
     w_words.view(np.uint8)[:4 * K] = w32.view(np.uint8)
     image = np.concatenate([in_ptrs.ravel(), out_ptrs, leaf_n, blocks, w_words, st])
-    image_dev = torch.from_numpy(image).pin_memory().to(device, non_blocking=True)
+    image_dev = _lib.upload(torch.from_numpy(image), device)
     base = image_dev.data_ptr()
     w_ptr = base + 8 * (K * L + 2 * L + blocks.size)
     st_ptr = w_ptr + 8 * w_words.size
@@ -537,7 +537,7 @@ class Adafactor:
                 words = int(lib.fjopt_adafactor_plan(arr, len(recs), ctypes.byref(hp), plan[1].ctypes.data,
                                                      plan[1].size, ctypes.byref(ws_bytes)))
                 _lib.check(min(words, 0), "fjopt_adafactor_plan")
-                plan[2].copy_(torch.from_numpy(plan[1]).pin_memory(), non_blocking=True)
+                plan[2].copy_(_lib.upload(torch.from_numpy(plan[1]), plan[2].device), non_blocking=True)
                 plan[0] = ptr_key
             _, table, table_dev, ws = plan
             _lib.call("fjopt_adafactor_step", table.ctypes.data, table_dev.data_ptr(), ctypes.byref(hp),

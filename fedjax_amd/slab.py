@@ -23,7 +23,7 @@ from typing import Optional, Sequence
 import numpy as np
 import torch
 
-from fedjax_amd import kernels, pytree, tree_util
+from fedjax_amd import _lib, kernels, pytree, tree_util
 from fedjax_amd.typing import PyTree
 
 
@@ -85,7 +85,7 @@ class ClientDeltaSlab:
 
     def weight_vector(self, weights: Sequence) -> torch.Tensor:
         """float32 weights f32(w_k) on the device (pinned H2D, stream-ordered)."""
-        return torch.from_numpy(self.host_weights(weights)).pin_memory().to(self.device, non_blocking=True)
+        return _lib.upload(torch.from_numpy(self.host_weights(weights)), self.device)
 
     def weighted_sum_flat(self, w_dev: torch.Tensor, *, scale=None, out: Optional[torch.Tensor] = None,
                           accumulate: bool = False, mode: str = "exact",

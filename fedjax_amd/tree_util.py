@@ -290,7 +290,7 @@ def _fold(rows, weights, *, scale=None,
         w_words = np.zeros((K + 1) // 2, dtype=np.int64)
         w_words.view(np.uint8)[: 4 * K] = w_host.view(np.uint8)
         image = np.concatenate([in_ptrs.ravel(), out_ptrs, leaf_n, blocks, w_words])
-        image_dev = torch.from_numpy(image).pin_memory().to(device, non_blocking=True)
+        image_dev = _lib.upload(torch.from_numpy(image), device)
         w_dev_ptr = image_dev.data_ptr() + 8 * (image.size - w_words.size)
         total_bytes = int(leaf_n.sum()) * K * (2 if in_c == _lib.BF16 else 4)
         nt = (total_bytes >= NONTEMPORAL_MIN_BYTES) if nontemporal is None else nontemporal
@@ -1622,7 +1622,7 @@ def _l2_rows(rows: List[List[torch.Tensor]], take_sqrt: bool) -> torch.Tensor:
         raise TypeError("l2 norms need one leaf dtype across the tree")
     ptrs = np.array([x.data_ptr() for row in rows for x in row], dtype=np.int64)
     ns = np.array([x.numel() for row in rows for x in row], dtype=np.int64)
-    image_dev = torch.from_numpy(np.concatenate([ptrs, ns])).pin_memory().to(device, non_blocking=True)
+    image_dev = _lib.upload(torch.from_numpy(np.concatenate([ptrs, ns])), device)
     max_n = int(ns.max()) if ns.size else 0
     need = int(_lib.load().fjagg_l2sq_rows_workspace_bytes(K * L, max_n))
     ws = torch.empty(max(need, 4), dtype=torch.uint8, device=device)

@@ -3,9 +3,10 @@ arguments (no allocation or synchronisation inside the library).
 
 A server that runs the same round shape every round can capture the aggregation once
 and replay it (torch.cuda.CUDAGraph = hipGraph on ROCm): the dense slab fold (weights on
-the device) and the per-call tree ops (fjtree: the leaf table is in the kernel arguments)
-are capturable. The pytree fold of tree_mean uploads a fresh plan image from pinned host
-memory per call, so it is not (replaying it would read a freed staging buffer).
+the device), the per-call tree ops (fjtree: the leaf table is in the kernel arguments), and
+the pytree folds of tree_mean and the deferred running sum while their plan image fits the
+kernel arguments. A plan image too large for them would be uploaded from a pinned staging
+buffer that torch hands out again after the capture: such a capture is refused with an error.
 Replays must give the eager launch's bits on the new contents of the same buffers.
 """
 import numpy as np
@@ -73,3 +74,61 @@ def test_per_call_tree_ops_replay_bitwise(cuda):
             assert torch.equal(nrm.view(torch.int32), want_n.view(torch.int32))
     finally:
         tu.set_deferred_sums(True)
+
+
+def test_default_settings_capture_replays_or_refuses(cuda):
+    """With the defaults (deferred running sums, lazy norms) a captured library-loop round and a
+    small tree_mean record their launches with the plan images in the kernel arguments and replay
+    bitwise on new contents. A tree_mean whose image is too large for the kernel arguments would
+    upload it through a pinned staging buffer, which torch's host allocator hands out again after
+    the capture: that capture is refused with an error (nothing is recorded that a replay could
+    not reuse), and the stream works normally afterwards."""
+    g0 = torch.Generator(device=cuda).manual_seed(5)
+    xs = [{"u": torch.rand(5000, device=cuda, generator=g0), "v": torch.rand(33, 9, device=cuda, generator=g0)}
+          for _ in range(6)]
+    W = float(sum(range(1, 7)))
+
+    def loop():
+        s = tu.tree_zeros_like(xs[0])
+        for k, x in enumerate(xs):
+            s = tu.tree_add(s, tu.tree_weight(x, k + 1))
+        return tu.tree_inverse_weight(s, W)
+
+    def mean():
+        return tu.tree_mean([(x, k + 1) for k, x in enumerate(xs)])
+
+    for fn in (loop, mean):
+        fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            fn()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                out = fn()
+        for _ in range(2):
+            with torch.no_grad():
+                for x in xs:
+                    for leaf in pytree.leaves_of(x):
+                        leaf.copy_(torch.rand(leaf.shape, device=cuda, generator=g0))
+            g.replay()
+            torch.cuda.synchronize()
+            want = fn()
+            for a, b in zip(pytree.leaves_of(out), pytree.leaves_of(want)):
+                assert torch.equal(a.view(torch.int32), b.view(torch.int32)), fn.__name__
+    big = [{"u": torch.rand(64, device=cuda, generator=g0), "v": torch.rand(8, device=cuda, generator=g0)}
+           for _ in range(2000)]
+    pairs = [(t, 1 + k % 7) for k, t in enumerate(big)]
+    want = tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with pytest.raises(RuntimeError, match="not capturable"):
+            with torch.cuda.graph(g, stream=s):
+                tu.tree_mean(pairs)
+    torch.cuda.synchronize()
+    again = tu.tree_mean(pairs)
+    for a, b in zip(pytree.leaves_of(again), pytree.leaves_of(want)):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
