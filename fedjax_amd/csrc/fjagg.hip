@@ -1731,6 +1731,14 @@ __attribute__((visibility("hidden"))) int fjagg_host_weights_check(int in_dtype,
   return FJAGG_OK;
 }
 
+namespace {
+// n words of v at p (split mode's unit weights): a kernel, not hipMemsetD32Async, whose node in a
+// captured graph takes effect on the first replay only (measured: tools/probe_memset_node.py)
+__global__ __launch_bounds__(256) void k_fill_u32(unsigned* __restrict__ p, unsigned v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = v;
+}
+}  // namespace
+
 // ====================================================================== C ABI
 extern "C" {
 
@@ -1787,8 +1795,9 @@ int fjagg_wsum_dense(int in_dtype, int acc_dtype, int out_dtype, const void* x_d
   if (rc) return rc;
   // 2) ordered combine of the gy partials = unit-weight fold (x*1 is exact)
   const unsigned one_bits = acc_dtype == FJAGG_F32 ? 0x3f800000u : 1u;
-  if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws), (int)one_bits, kSplitMax, s) != hipSuccess)
-    return check_launch("hipMemsetD32Async");
+  hipLaunchKernelGGL(k_fill_u32, dim3((unsigned)((kSplitMax + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<unsigned*>(ws), one_bits, (int64_t)kSplitMax);
+  if (int rc2 = check_launch("k_fill_u32")) return rc2;
   const int flags2 = flags & (FJAGG_SCALE | FJAGG_ACCUMULATE);
   return dense_exact_chunked(acc_dtype, acc_dtype, out_dtype, ws + kSplitHeader, pstride, gy, P,
                              ws, scale, y, flags2, s, gy, 1, 0);

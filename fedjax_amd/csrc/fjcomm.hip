@@ -238,6 +238,19 @@ int fjcomm_abort(void* comm) {
 }
 
 namespace {
+// n zero floats at p (a shard without clients): a kernel, not hipMemsetAsync, whose node in a
+// captured graph takes effect on the first replay only (measured: tools/probe_memset_node.py)
+__global__ __launch_bounds__(256) void k_zero_f32(float* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.0f;
+}
+int zero_f32(float* p, int64_t n, hipStream_t s) {
+  if (n <= 0) return FJAGG_OK;
+  const int64_t g = (n + 255) / 256;
+  hipLaunchKernelGGL(k_zero_f32, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, p, n);
+  if (hipError_t e = hipGetLastError()) return hip_fail(e, "k_zero_f32 launch");
+  return FJAGG_OK;
+}
+
 // a bounded spin on the real-time counter (read-only; no memory is touched): one wave
 __global__ void k_block(long long ticks) {
   const long long t0 = wall_clock64();
@@ -315,8 +328,8 @@ int fjcomm_sharded_wsum_dense_edges(void* comm, int in_dtype, const void* x_dev,
       if (int rc = fjagg_wsum_dense(in_dtype, FJAGG_F32, FJAGG_F32, xb, ld, K, n, w_dev, scale, seg,
                                     flags | FJAGG_SCALE, FJAGG_MODE_EXACT, nullptr, 0, stream))
         return rc;
-    } else if (hipError_t e = hipMemsetAsync(seg, 0, n * sizeof(float), s)) {
-      return hip_fail(e, "hipMemsetAsync");
+    } else if (int rc = zero_f32(seg, n, s)) {
+      return rc;
     }
     if (fold_events) {
       if (hipError_t e = hipEventRecord(reinterpret_cast<hipEvent_t>(fold_events[2 * b + 1]), s))
@@ -430,8 +443,8 @@ int fjcomm_multi_wsum_dense(void* const* comms, int ndev, int in_dtype, const vo
         if (int rc = fjagg_wsum_dense(in_dtype, FJAGG_F32, FJAGG_F32, xb, ld[d], K[d], n, w_dev[d], scale, seg,
                                       flags | FJAGG_SCALE, FJAGG_MODE_EXACT, nullptr, 0, s))
           return rc;
-      } else if (hipError_t e = hipMemsetAsync(seg, 0, n * sizeof(float), s)) {
-        return hip_fail(e, "hipMemsetAsync");
+      } else if (int rc = zero_f32(seg, n, s)) {
+        return rc;
       }
       if (b + 1 < nb) {
         if (hipError_t e = hipEventRecord(c->ready[b], s)) return hip_fail(e, "hipEventRecord");

@@ -430,7 +430,23 @@ void carve_outputs(const std::vector<at::Tensor>& row0, std::vector<at::Tensor>&
 // launch, so the fold's last workgroup adds the norm partials (no combine launch, fjagg.h).
 // Launches on one stream are ordered, so they share it; a grown buffer's predecessor goes
 // back to torch's stream-ordered allocator.
+// `stream` is being captured into a graph (hipStreamIsCapturing: a runtime call, ~0.1 us — asked
+// once per fold or per round, never per client)
+bool stream_capturing(unsigned long long stream) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(reinterpret_cast<hipStream_t>(stream), &cs) == hipSuccess &&
+         cs != hipStreamCaptureStatusNone;
+}
+
 at::Tensor l2_workspace(int dev, unsigned long long stream, int64_t need) {
+  if (stream_capturing(stream)) {
+    // a capture records the zeroing instead of running it: a cached workspace would then reach
+    // later launches with its counter unset. A workspace of the capture's own, not cached, zeroed
+    // by a fill kernel every replay runs in front of the fold (a recorded hipMemsetAsync node takes
+    // effect on the first replay only: measured, tools/probe_memset_node.py)
+    return at::zeros({std::max<int64_t>(need, 4096)},
+                     at::TensorOptions().dtype(at::kByte).device(at::kCUDA, static_cast<c10::DeviceIndex>(dev)));
+  }
   static auto* m = new std::unordered_map<uint64_t, at::Tensor>();
   const uint64_t key = static_cast<uint64_t>(stream) ^ (static_cast<uint64_t>(dev) << 56);
   if (m->size() >= 16 && !m->count(key)) m->clear();  // many short-lived streams: keep the map bounded
@@ -450,9 +466,7 @@ at::Tensor l2_workspace(int dev, unsigned long long stream, int64_t need) {
 // such an upload is refused: true with a Python error set. (Images in the kernel arguments are
 // part of the recorded launch and replay as captured.)
 bool upload_refused_in_capture(unsigned long long stream, const char* what) {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(reinterpret_cast<hipStream_t>(stream), &cs) != hipSuccess || cs == hipStreamCaptureStatusNone)
-    return false;
+  if (!stream_capturing(stream)) return false;
   PyErr_Format(PyExc_RuntimeError,
                "%s: its plan image is too large for the kernel arguments and would be uploaded from a pinned "
                "staging buffer, which a graph replay cannot reuse safely; not capturable (fewer clients or "
@@ -1650,11 +1664,19 @@ PyObject* leaf_fold(PyObject*, PyObject* args) {
       nrm = at::empty({2}, THPVariable_Unpack(w.leaves[0][0]).options());
       t.norm_out = nrm.data_ptr<float>();
       const int64_t need = reinterpret_cast<TreeWsFn>(ws_addr)(&t);
-      at::Tensor& ws = workspaces()[WsKey{dev, stream}];
-      if (!ws.defined() || ws.numel() < need)
-        ws = at::zeros({need > 4096 ? need * 2 : 8192}, nrm.options().dtype(at::kByte));
-      t.ws = ws.data_ptr();
-      t.ws_bytes = ws.numel();
+      // (under a graph capture a workspace of the capture's own: its zeroing fill is recorded, not
+      // run, so a cached one would reach later launches with its counter unset)
+      at::Tensor own;
+      at::Tensor* wsp = &own;
+      if (stream_capturing(stream)) {
+        own = at::zeros({need > 4096 ? need : 4096}, nrm.options().dtype(at::kByte));
+      } else {
+        wsp = &workspaces()[WsKey{dev, stream}];
+        if (!wsp->defined() || wsp->numel() < need)
+          *wsp = at::zeros({need > 4096 ? need * 2 : 8192}, nrm.options().dtype(at::kByte));
+      }
+      t.ws = wsp->data_ptr();
+      t.ws_bytes = wsp->numel();
     }
     rc = reinterpret_cast<TreeFoldFn>(fold_addr)(&t, reinterpret_cast<void*>(stream));
     PyObject* tree_out = Py_None;
@@ -2482,7 +2504,9 @@ PyObject* mean_pairs_impl(PyObject* pairs, bool triples, int may_pipeline, doubl
     // straight into those columns (fjagg_wsum_l2_ptrs_rows); the nodes are done once every
     // launch is issued
     if (!with_l2 && !g_solo.reg.empty()) solo_compact();
-    bool solo = !with_l2 && g_solo.pending > 0 && g_solo.rows_fn && g_solo.l2ws_fn;
+    // (not under a graph capture: a replay would write those columns again, and a column is handed
+    // out again once its view is dropped; the pending norms are computed on their own when read)
+    bool solo = !with_l2 && g_solo.pending > 0 && g_solo.rows_fn && g_solo.l2ws_fn && !stream_capturing(stream);
     std::vector<SoloObject*> fused;  // held (new references) until the call returns
     struct HeldNodes {
       std::vector<SoloObject*>& v;
@@ -3644,6 +3668,42 @@ PyObject* solo_probe(PyObject*, PyObject* args) {
 // pool's next pair. Py_None: not the fast case; nullptr: a Python error.
 PyObject* solo_norm(PyObject* tree, int which) {
   try {
+    // Under a graph capture the norm is computed now, by the launch that computes it whenever it is
+    // read alone (solo_resolve: the same kernel and plan, so the same bits), which the graph records:
+    // a node with a column of its own (a direct column is never handed out again, a pooled one is
+    // once its view is dropped, and every replay writes the column). Asked at the first norm of a
+    // round (nothing pending), not per client.
+    if (g_solo.pending == 0 &&
+        stream_capturing(reinterpret_cast<unsigned long long>(c10::hip::getCurrentHIPStream().stream()))) {
+      auto* c = reinterpret_cast<SoloObject*>(g_solo.type->tp_alloc(g_solo.type, 0));
+      if (!c) return nullptr;
+      struct DropC {
+        SoloObject* n;
+        ~DropC() { Py_DECREF(n); }
+      } drop_c{c};
+      if (!solo_capture_into(c, tree)) {
+        if (PyErr_Occurred()) return nullptr;
+        Py_RETURN_NONE;
+      }
+      PyObject* buf;
+      long long idx;
+      if (!solo_column(THPVariable_Unpack(c->leaves[0]).get_device(), &buf, &idx)) return nullptr;
+      Py_INCREF(buf);
+      Py_XSETREF(c->buf, buf);
+      c->idx = idx;
+      PyObject* v = solo_view(c, which);
+      if (!v) return nullptr;
+      c->state = kSoloPending;
+      ++g_solo.pending;
+      g_solo.pending_bytes += c->nbytes;
+      std::vector<SoloObject*> one{c};
+      if (solo_resolve(one) != 0) {
+        solo_release(c, kSoloDone);
+        Py_DECREF(v);
+        return nullptr;
+      }
+      return v;
+    }
     if (!g_solo.reg.empty()) {
       SoloObject* c = g_solo.reg.back().node;
       if (c->state == kSoloPending && c->tree == tree && solo_same_tree(c, tree) && solo_unchanged(c))
@@ -3791,7 +3851,10 @@ PyObject* fast_l2(PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames, in
           // values tree_weight saw or never filled)
           if (same) {
             chain_delta = true;
-            if ((!ch->buf || ch->buf == Py_None) && which == 1 && g_fast.pool_buf && g_fast.pool_views) {
+            if ((!ch->buf || ch->buf == Py_None) && which == 1 && g_fast.pool_buf && g_fast.pool_views &&
+                !stream_capturing(reinterpret_cast<unsigned long long>(c10::hip::getCurrentHIPStream().stream()))) {
+              // (not under a graph capture: replays would write the pool's columns, which are handed
+              // out again once their views are dropped; the chain then takes a buffer of its own)
               // the chain's first norm: take the pool as the chain's buffer and views (same device,
               // the current chain size)
               const at::Tensor& pb = THPVariable_Unpack(g_fast.pool_buf);
@@ -4033,10 +4096,14 @@ PyObject* zeros_like(PyObject*, PyObject* tree) {
       offs[l + 1] = offs[l] + (t.numel() + 63) / 64 * 64;
     }
     const at::Tensor& t0 = THPVariable_Unpack(w.leaves[0][0]);
-    // zeroed by one hipMemsetAsync on the current stream (at::zeros would add a dispatched fill)
+    // zeroed by one hipMemsetAsync on the current stream (at::zeros would add a dispatched fill);
+    // under a graph capture by a fill kernel: a recorded memset node takes effect on the graph's
+    // first replay only (measured, tools/probe_memset_node.py)
     at::Tensor flat = at::empty({std::max<int64_t>(offs[L], 1)}, t0.options());
     const hipStream_t zs = c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(dev)).stream();
-    if (hipMemsetAsync(flat.data_ptr(), 0, static_cast<size_t>(flat.numel()) * 4, zs) != hipSuccess) {
+    if (stream_capturing(reinterpret_cast<unsigned long long>(zs))) {
+      flat.zero_();
+    } else if (hipMemsetAsync(flat.data_ptr(), 0, static_cast<size_t>(flat.numel()) * 4, zs) != hipSuccess) {
       PyErr_SetString(PyExc_RuntimeError, "tree_zeros_like: hipMemsetAsync failed");
       return nullptr;
     }

@@ -132,3 +132,116 @@ def test_default_settings_capture_replays_or_refuses(cuda):
     again = tu.tree_mean(pairs)
     for a, b in zip(pytree.leaves_of(again), pytree.leaves_of(want)):
         assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+def test_captured_rounds_with_norms_replay(cuda):
+    """examples/fed_avg.py's round (tree_l2_norm per client, then tree_mean) and the library loop
+    with its per-client norms (fed_avg.py:132-146), captured with the default settings. Under a
+    capture the norms come from launches recorded in the graph (no pooled norm columns, which a
+    replay would overwrite after they are handed out again; fjhost stream_capturing), so every
+    replay refreshes the mean and the norms: the bits of an eager round on the new contents.
+    Eager rounds on the capture stream afterwards keep their own bits."""
+    g0 = torch.Generator(device=cuda).manual_seed(9)
+    xs = [{"u": torch.rand(5000, device=cuda, generator=g0), "v": torch.rand(33, 9, device=cuda, generator=g0)}
+          for _ in range(6)]
+    ws = [3, 1, 4, 1, 5, 9]
+
+    def example():
+        norms = [tu.tree_l2_norm(x) for x in xs]
+        return tu.tree_mean(list(zip(xs, ws))), norms
+
+    def library():
+        s, norms = tu.tree_zeros_like(xs[0]), []
+        for x, w in zip(xs, ws):
+            s = tu.tree_add(s, tu.tree_weight(x, w))
+            norms.append(tu.tree_l2_norm(x))
+        return tu.tree_inverse_weight(s, float(sum(ws))), norms
+
+    def same(a, b):
+        return all(torch.equal(x.reshape(-1).view(torch.int32), y.reshape(-1).view(torch.int32))
+                   for x, y in zip(pytree.leaves_of(a), pytree.leaves_of(b)))
+
+    for fn in (example, library):
+        fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            fn()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=st):
+                mean, norms = fn()
+        for _ in range(2):
+            with torch.no_grad():
+                for x in xs:
+                    for leaf in pytree.leaves_of(x):
+                        leaf.copy_(torch.rand(leaf.shape, device=cuda, generator=g0))
+            g.replay()
+            torch.cuda.synchronize()
+            want, want_norms = fn()
+            assert same(mean, want), fn.__name__
+            assert same(norms, want_norms), fn.__name__
+        with torch.cuda.stream(st):
+            again, again_norms = fn()
+        st.synchronize()
+        assert same(again, want) and same(again_norms, want_norms), fn.__name__
+
+
+def test_recorded_zeroing_runs_on_every_replay(cuda):
+    """On this ROCm a hipMemsetAsync recorded into a graph takes effect on the first replay only
+    (tools/probe_memset_node.py), so what the captured calls zero, they zero with a kernel:
+    tree_zeros_like's running-sum base (eager mode: one fused fjtree launch per tree_add, which
+    reads it) and the split-mode dense fold's unit weights. Both replay bitwise three times on
+    new contents."""
+    g0 = torch.Generator(device=cuda).manual_seed(13)
+    xs = [{"u": torch.rand(5000, device=cuda, generator=g0), "v": torch.rand(33, 9, device=cuda, generator=g0)}
+          for _ in range(6)]
+    tu.set_deferred_sums(False)
+    try:
+        def loop():
+            s = tu.tree_zeros_like(xs[0])
+            for k, x in enumerate(xs):
+                s = tu.tree_add(s, tu.tree_weight(x, k + 1))
+            return s
+        loop()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            loop()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=st):
+                out = loop()
+        for _ in range(3):
+            with torch.no_grad():
+                for x in xs:
+                    for leaf in pytree.leaves_of(x):
+                        leaf.copy_(torch.rand(leaf.shape, device=cuda, generator=g0))
+            g.replay()
+            torch.cuda.synchronize()
+            want = loop()
+            for a, b in zip(pytree.leaves_of(out), pytree.leaves_of(want)):
+                assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    finally:
+        tu.set_deferred_sums(True)
+    K, P = next((k, p) for k, p in ((4096, 2048), (8192, 1024), (16384, 512), (2048, 4096))
+                if kernels.split_workspace_bytes(k, p) > 0)
+    x = torch.empty(K, P, device=cuda)
+    w = torch.tensor(np.float32(np.random.RandomState(3).randint(1, 501, size=K)), device=cuda)
+    scale = float(np.float32(1.0 / float(w.double().sum())))
+    ws = torch.empty(kernels.split_workspace_bytes(K, P), dtype=torch.uint8, device=cuda)
+    out = torch.empty(P, device=cuda)
+    kernels.fill_synth(x, seed=1)
+    kernels.weighted_sum_dense(x, w, scale=scale, out=out, mode="split", workspace=ws)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(g, stream=st):
+            kernels.weighted_sum_dense(x, w, scale=scale, out=out, mode="split", workspace=ws)
+    for seed in (2, 3, 4):
+        kernels.fill_synth(x, seed=seed)
+        g.replay()
+        torch.cuda.synchronize()
+        want = kernels.weighted_sum_dense(x, w, scale=scale, mode="split")
+        assert torch.equal(out.view(torch.int32), want.view(torch.int32)), seed
