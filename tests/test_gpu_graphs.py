@@ -245,3 +245,40 @@ def test_recorded_zeroing_runs_on_every_replay(cuda):
         torch.cuda.synchronize()
         want = kernels.weighted_sum_dense(x, w, scale=scale, mode="split")
         assert torch.equal(out.view(torch.int32), want.view(torch.int32)), seed
+
+
+def test_dense_fused_norms_capture_on_a_fresh_stream(cuda):
+    """kernels.weighted_sum_l2_dense without a workspace uses the stream's cached zeroed-counter
+    workspace; first used inside a capture, that workspace would be zeroed by a recorded fill that
+    has not run yet. The capture gets a workspace of its own: replays give the eager bits, and eager
+    calls on the capture stream afterwards (before and after a replay) do too."""
+    K, P = 64, 100_003
+    x = torch.empty(K, P + 1, device=cuda)[:, :P]
+    w = torch.tensor(np.float32(np.random.RandomState(5).randint(1, 501, size=K)), device=cuda)
+    scale = float(np.float32(1.0 / float(w.double().sum())))
+    out = torch.empty(P, device=cuda)
+    l2 = torch.empty(K, device=cuda)
+    kernels.fill_synth(x, seed=1)
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()  # (a stream no fused-norm call has used yet)
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(g, stream=st):
+            kernels.weighted_sum_l2_dense(x, w, scale=scale, out=out, l2sq=l2)
+
+    def eager_on(stream):
+        with torch.cuda.stream(stream):
+            o, n = kernels.weighted_sum_l2_dense(x, w, scale=scale)
+        stream.synchronize()
+        return o, n
+
+    o0, n0 = eager_on(st)  # before any replay
+    o1, n1 = kernels.weighted_sum_l2_dense(x, w, scale=scale, workspace=torch.empty(1, dtype=torch.uint8, device=cuda))
+    torch.cuda.synchronize()  # (a caller's workspace: two launches, the same bits)
+    assert torch.equal(o0.view(torch.int32), o1.view(torch.int32)) and torch.equal(n0.view(torch.int32), n1.view(torch.int32))
+    for seed in (2, 3, 4):
+        kernels.fill_synth(x, seed=seed)
+        g.replay()
+        torch.cuda.synchronize()
+        want_o, want_n = eager_on(st)
+        assert torch.equal(out.view(torch.int32), want_o.view(torch.int32)), seed
+        assert torch.equal(l2.view(torch.int32), want_n.view(torch.int32)), seed
