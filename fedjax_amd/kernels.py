@@ -181,13 +181,12 @@ def weighted_sum_l2_dense(x: torch.Tensor, w: torch.Tensor, *, scale: Optional[f
     need = int(_lib.load().fjagg_wsum_l2_workspace_bytes(K, P))
     flags = (_lib.SCALE if scale is not None else 0) | (_lib.ACCUMULATE if accumulate else 0)
     flags |= _lib.NONTEMPORAL if nontemporal else 0
-    if workspace is None and torch.cuda.is_current_stream_capturing():
-        # a graph capture records the zeroing instead of running it: a workspace of its own (zeroed
-        # by a fill kernel every replay runs; a recorded memset acts on the first replay only)
-        workspace = torch.zeros(max(need, 4096), dtype=torch.uint8, device=dev)
-        flags |= _lib.ZEROED_WS
-    elif workspace is None and not _L2_COMBINE_LAUNCH:  # the stream's zeroed-counter workspace: the
-        workspace = _l2_workspace(dev, need)             # fold's last workgroup combines
+    if workspace is None and not _L2_COMBINE_LAUNCH:  # a zeroed-counter workspace: the fold's last
+        # workgroup combines. The stream's cached one, or under a graph capture one of the capture's
+        # own: a capture records the zeroing instead of running it (torch.zeros: a fill kernel every
+        # replay runs; a recorded memset acts on the first replay only)
+        workspace = (torch.zeros(max(need, 4096), dtype=torch.uint8, device=dev)
+                     if torch.cuda.is_current_stream_capturing() else _l2_workspace(dev, need))
         flags |= _lib.ZEROED_WS
     elif workspace is None:
         workspace = torch.empty(max(need, 4), dtype=torch.uint8, device=dev)
