@@ -844,6 +844,21 @@ class _NormView(torch.Tensor):
         with torch._C.DisableTorchFunctionSubclass():
             return self.item().__format__(spec) if self.dim() == 0 else torch.Tensor.__format__(self, spec)
 
+    def _value(self) -> torch.Tensor:
+        """The value as a plain tensor of its own (computed first if pending): no ticket and no
+        view of the norm buffer."""
+        _HOST.flush_views(self)
+        with torch._C.DisableTorchFunctionSubclass():
+            return self.detach().clone()
+
+    def __reduce_ex__(self, proto):
+        # pickled (torch.save, multiprocessing, copy.copy) as its value, as the reference's jnp
+        # scalar is: a capture's node cannot travel, and the view would carry the whole buffer
+        return torch.Tensor.__reduce_ex__(self._value(), proto)
+
+    def __deepcopy__(self, memo):
+        return self._value()
+
 
 def _fold_ticket(ticket) -> None:
     """Fold the chain a waiting lazy norm's ticket names (fjhost.flush_views calls this); a

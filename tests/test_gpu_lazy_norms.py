@@ -394,3 +394,37 @@ def test_rounds_on_alternating_streams(cuda):
     for norms in kept:
         for v, a in zip(norms, alone):
             assert torch.equal(bits(v), a)
+
+
+@pytest.mark.parametrize("kind", ["example", "library"])
+def test_norm_views_pickle_and_copy_as_values(cuda, kind):
+    """Client diagnostics travel (pickle to a logging process, torch.save with a checkpoint,
+    copy.deepcopy): a lazy norm view pickles and copies as its value, a plain 0-d float32
+    tensor of its own, as the reference's jnp scalar does (computed first when still pending).
+    Both the standalone norms of examples/fed_avg.py and the running sum's norms."""
+    import copy
+    import io
+    import pickle
+    xs = make_deltas(SMALL, 4, 19, cuda)
+    if kind == "example":
+        diag = {i: {"delta_l2_norm": tu.tree_l2_norm(x)} for i, x in enumerate(xs)}
+        pending = copy.deepcopy(diag[3])  # (before any mean: computed on its own)
+        tu.tree_mean([(x, 1) for x in xs])
+    else:
+        s, diag = tu.tree_zeros_like(xs[0]), {}
+        for i, x in enumerate(xs):
+            s = tu.tree_add(s, tu.tree_weight(x, i + 1))
+            diag[i] = {"delta_l2_norm": tu.tree_l2_norm(x)}
+        pending = copy.deepcopy(diag[3])  # (before the fold: the chain folds first)
+        tu.tree_inverse_weight(s, 10.0)
+    want = [bits(diag[i]["delta_l2_norm"]) for i in range(4)]
+    buf = io.BytesIO()
+    torch.save(diag, buf)
+    for got in (pickle.loads(pickle.dumps(diag)), torch.load(io.BytesIO(buf.getvalue()), weights_only=True),
+                copy.deepcopy(diag), {k: copy.copy(v["delta_l2_norm"]) for k, v in diag.items()}):
+        for i in range(4):
+            v = got[i]["delta_l2_norm"] if isinstance(got[i], dict) else got[i]
+            assert type(v) is torch.Tensor and v.dim() == 0 and v.dtype == torch.float32
+            assert v.untyped_storage().nbytes() == 4  # (its own value, not the norm buffer)
+            assert torch.equal(bits(v), want[i])
+    assert type(pending["delta_l2_norm"]) is torch.Tensor and torch.equal(bits(pending["delta_l2_norm"]), want[3])
