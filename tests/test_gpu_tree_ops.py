@@ -738,3 +738,31 @@ def test_library_loop_norms_with_and_without_the_combine_launch(cuda):
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(r.stdout.strip().splitlines()[-2:])
     assert outs[0] == outs[1]
+
+
+def test_lazy_sums_pickle_and_copy_as_pytrees(cuda, sum_mode):
+    """tree_weight's result and a running sum mid-loop pickle, deepcopy and copy as the pytrees
+    they stand for (plain dicts of tensors, the reference's values); the loop then goes on from
+    the original and ends with the reference's bits."""
+    import copy
+    import pickle
+    g = torch.Generator().manual_seed(47)
+    shapes = {"a": (5000,), "b": {"c": (33, 3)}}
+    xs = [to_dev(rand_tree(shapes, g), cuda) for _ in range(3)]
+    wt = tu.tree_weight(xs[0], 3)
+    s = tu.tree_zeros_like(xs[0])
+    s = tu.tree_add(s, tu.tree_weight(xs[0], 1))
+    s = tu.tree_add(s, tu.tree_weight(xs[1], 2))
+    want_w = ref.tree_weight(to_np(xs[0]), 3)
+    want_s = ref.tree_add(ref.tree_add(ref.tree_zeros_like(to_np(xs[0])), ref.tree_weight(to_np(xs[0]), 1)),
+                          ref.tree_weight(to_np(xs[1]), 2))
+    for obj, want in ((wt, want_w), (s, want_s)):
+        for got in (pickle.loads(pickle.dumps(obj)), copy.deepcopy(obj), copy.copy(obj)):
+            assert type(got) is dict
+            for a, b in zip(leaves_np(got), pytree.leaves_of(want)):
+                assert np.array_equal(bits(a), bits(b.reshape(-1)))
+    s = tu.tree_add(s, tu.tree_weight(xs[2], 3))
+    mean = tu.tree_inverse_weight(s, 6.0)
+    want = ref.tree_inverse_weight(ref.tree_add(want_s, ref.tree_weight(to_np(xs[2]), 3)), 6.0)
+    for a, b in zip(leaves_np(mean), pytree.leaves_of(want)):
+        assert np.array_equal(bits(a), bits(b.reshape(-1)))
