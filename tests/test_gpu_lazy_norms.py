@@ -428,3 +428,31 @@ def test_norm_views_pickle_and_copy_as_values(cuda, kind):
             assert v.untyped_storage().nbytes() == 4  # (its own value, not the norm buffer)
             assert torch.equal(bits(v), want[i])
     assert type(pending["delta_l2_norm"]) is torch.Tensor and torch.equal(bits(pending["delta_l2_norm"]), want[3])
+
+
+def test_a_generator_that_raises_mid_mean(cuda):
+    """tree_mean over a one-shot iterable that raises partway (a client's data failed to load):
+    the caller gets the generator's exception; every norm view taken before still reads its
+    delta's bits (the launched chunk's clients stay pending and are computed alone on read), and
+    the next round fuses as usual."""
+    deltas = make_deltas(EMNIST, 40, 23, cuda)
+    alone = [bits(tu.tree_l2_norm(d)).clone() for d in deltas]
+    views = [tu.tree_l2_norm(d) for d in deltas]
+
+    def pairs():
+        for i, d in enumerate(deltas):
+            if i == 30:
+                raise ValueError("client 30 failed")
+            yield d, i + 1
+
+    with pytest.raises(ValueError, match="client 30 failed"):
+        tu.tree_mean(pairs())
+    for v, a in zip(views, alone):
+        assert torch.equal(bits(v), a)
+    before = H.solo_info()["fused"]
+    weights = list(range(1, 41))
+    mean, norms = example_round(deltas, weights)
+    assert H.solo_info()["fused"] - before == 40
+    assert same_mean(mean, want_mean(deltas, weights))
+    for v, a in zip(norms, alone):
+        assert torch.equal(bits(v), a)
