@@ -93,6 +93,10 @@ enum fjagg_flags {
                                  Bytes 4..7 are an error word: a call that finds the counter
                                  non-zero sets it to 1 (sticky: that call's norms are not valid;
                                  zero both words to recover).
+                                 Graph capture: zero it before the capture (every replayed call
+                                 leaves it zero) or with a kernel inside it; a hipMemsetAsync
+                                 recorded into a graph acts on the first replay only (ROCm 7,
+                                 measured: tools/probe_memset_node.py).
                                  (fedjax_amd's callers pass it unless FJAGG_L2_COMBINE_LAUNCH=1.) */
 };
 /* kernel-argument capacity of FJAGG_HOST_TABLES launches */
