@@ -79,7 +79,9 @@ typedef struct fjtree_leaves {
   float* norm_out;   /* device float[2] (FJTREE_NORM) */
   void* ws;          /* device, fjtree_workspace_bytes(table) bytes (FJTREE_NORM); its first
                         4 bytes are a completion counter that must be 0 before the first use
-                        (the kernel leaves it 0: reuse the workspace on the same stream) */
+                        (the kernel leaves it 0: reuse the workspace on the same stream). Under
+                        graph capture zero it before the capture or with a kernel: a recorded
+                        hipMemsetAsync acts on the first replay only (ROCm 7, measured) */
   int64_t ws_bytes;
 } fjtree_leaves;
 
