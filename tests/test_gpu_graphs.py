@@ -282,3 +282,53 @@ def test_dense_fused_norms_capture_on_a_fresh_stream(cuda):
         want_o, want_n = eager_on(st)
         assert torch.equal(out.view(torch.int32), want_o.view(torch.int32)), seed
         assert torch.equal(l2.view(torch.int32), want_n.view(torch.int32)), seed
+
+
+def test_c_abi_zeroed_counter_captured_after_zeroing(cuda):
+    """The FJAGG_ZEROED_WS contract for a C caller (include/fjagg.h): a workspace whose counter was
+    zeroed before the capture stays zero across replays (every launch leaves it zero), so a
+    captured fjagg_wsum_l2_ptrs with its norm combine in the last workgroup replays the eager
+    two-launch call's mean and norms bitwise, three times, on new contents."""
+    import ctypes
+
+    from fedjax_amd import _lib
+    lib = _lib.load()
+    shapes = [(32,), (3, 3, 1, 32), (9216, 16), (62,)]
+    K, L = 24, 4
+    rows = [[torch.empty(int(np.prod(s)), device=cuda) for s in shapes] for _ in range(K)]
+    leaf_n = np.array([int(np.prod(s)) for s in shapes], dtype=np.int64)
+    outs = [torch.empty(int(n), device=cuda) for n in leaf_n]
+    nb = lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, leaf_n.ctypes.data, None, L, None, 0)
+    blocks = np.empty(2 * nb, dtype=np.int64)
+    lib.fjagg_ptrs_plan_leaves(_lib.F32, 0, leaf_n.ctypes.data, None, L, blocks.ctypes.data, nb)
+    img = torch.from_numpy(np.concatenate([np.array([[x.data_ptr() for x in r] for r in rows], np.int64).ravel(),
+                                           np.array([o.data_ptr() for o in outs], np.int64), leaf_n, blocks])).to(cuda)
+    w = torch.tensor(np.float32(np.arange(1, K + 1)), device=cuda)
+    l2 = torch.empty(K, device=cuda)
+    need = max(16, int(lib.fjagg_wsum_l2_ptrs_workspace_bytes(K, nb)))
+    ws = torch.zeros(need, dtype=torch.uint8, device=cuda)  # zeroed before the capture
+    torch.cuda.synchronize()
+
+    def call(l2_out, flags, work, stream):
+        _lib.check(lib.fjagg_wsum_l2_ptrs(_lib.F32, _lib.F32, _lib.F32, img.data_ptr(), L, K, nb, w.data_ptr(),
+                                          ctypes.c_float(0.01), l2_out.data_ptr(), flags, work.data_ptr(),
+                                          work.numel(), ctypes.c_void_p(stream.cuda_stream)), "fjagg_wsum_l2_ptrs")
+
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(g, stream=st):
+            call(l2, _lib.SCALE | _lib.ZEROED_WS, ws, st)
+    for seed in (1, 2, 3):
+        for k, r in enumerate(rows):
+            for x in r:
+                kernels.fill_synth(x.view(1, -1), seed=seed, k0=k)
+        g.replay()
+        torch.cuda.synchronize()
+        got_mean = torch.cat([o.clone() for o in outs])
+        want_l2 = torch.empty(K, device=cuda)
+        call(want_l2, _lib.SCALE, torch.empty(need, dtype=torch.uint8, device=cuda), torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        assert torch.equal(l2.view(torch.int32), want_l2.view(torch.int32)), seed
+        assert torch.equal(got_mean.view(torch.int32), torch.cat(outs).view(torch.int32)), seed
+        assert int(ws[:8].view(torch.int32)[0]) == 0 and int(ws[:8].view(torch.int32)[1]) == 0  # counter, error word
